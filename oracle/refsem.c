@@ -1,0 +1,641 @@
+/*
+ * refsem.c -- TEST INFRASTRUCTURE ONLY: CPU restatement of the reference
+ * Keto Check/Expand engines, used as the parity oracle and as bench.py's
+ * cpu_baseline ("port").  Never linked by the product.
+ *
+ * Schedule: the reference evaluates sub-checks through checkgroup with one
+ * reservation per group (internal/check/checkgroup/concurrent_checkgroup.go:
+ * 66-138), i.e. sequentially in add order.  This restatement fixes the
+ * "one-worker sequential order" (SURVEY.md section 8.0 H3): every sub-check
+ * completes before the next one is constructed.  Where the reference is
+ * schedule-dependent (visited-set pruning interacting with truncation) this
+ * is the canonical legal order both the oracle and the GPU engine follow.
+ */
+#include "refsem.h"
+
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MAX_RECURSION 4096
+
+typedef struct {
+    uint32_t ns, obj, rel, kind, sid, sns, srel;
+} key7;
+
+struct rs_db {
+    rs_tuple *t;       /* sorted by (ns, obj, rel, shard) */
+    size_t n;
+    key7 *ex;          /* sorted exact keys for EXISTS */
+    size_t n_ex;
+    rs_ns *ns;
+    rs_rel *rels;
+    rs_ast *ast;
+    int32_t *children;
+    uint32_t *vclass;
+    uint32_t n_ns, n_relnames, empty_rel, n_rels, n_ast, n_children;
+    int32_t strict, max_depth, max_width;
+};
+
+/* ------------------------------------------------------------------ */
+/* indexes                                                             */
+
+static int cmp_u32(uint32_t a, uint32_t b) { return a < b ? -1 : a > b; }
+static int cmp_u64(uint64_t a, uint64_t b) { return a < b ? -1 : a > b; }
+
+static int cmp_tuple(const void *pa, const void *pb) {
+    const rs_tuple *a = pa, *b = pb;
+    int c;
+    if ((c = cmp_u32(a->ns, b->ns))) return c;
+    if ((c = cmp_u32(a->obj, b->obj))) return c;
+    if ((c = cmp_u32(a->rel, b->rel))) return c;
+    /* ORDER BY nid, shard_id  (traverser.go:88, relationtuples.go:216) */
+    if ((c = cmp_u64(a->shard_hi, b->shard_hi))) return c;
+    return cmp_u64(a->shard_lo, b->shard_lo);
+}
+
+static int cmp_key7(const void *pa, const void *pb) {
+    const uint32_t *a = pa, *b = pb;
+    for (int i = 0; i < 7; i++) {
+        int c = cmp_u32(a[i], b[i]);
+        if (c) return c;
+    }
+    return 0;
+}
+
+static key7 mk_key(const rs_tuple *t) {
+    key7 k = {t->ns, t->obj, t->rel, t->kind, t->sid, 0, 0};
+    if (t->kind == 1) {
+        k.sns = t->sns;
+        k.srel = t->srel;
+    }
+    return k;
+}
+
+rs_db *rs_build(const rs_tuple *tuples, size_t n, const rs_config *cfg) {
+    rs_db *db = calloc(1, sizeof *db);
+    db->n = n;
+    db->t = malloc((n ? n : 1) * sizeof *db->t);
+    memcpy(db->t, tuples, n * sizeof *db->t);
+    qsort(db->t, n, sizeof *db->t, cmp_tuple);
+    db->ex = malloc((n ? n : 1) * sizeof *db->ex);
+    for (size_t i = 0; i < n; i++) db->ex[i] = mk_key(&tuples[i]);
+    qsort(db->ex, n, sizeof *db->ex, cmp_key7);
+    db->n_ex = n;
+
+    db->n_ns = cfg->n_ns;
+    db->n_relnames = cfg->n_relnames;
+    db->empty_rel = cfg->empty_rel;
+    db->n_rels = cfg->n_rels;
+    db->n_ast = cfg->n_ast;
+    db->n_children = cfg->n_children;
+#define DUP(field, cnt)                                                  \
+    do {                                                                 \
+        size_t sz = (size_t)(cnt) * sizeof *cfg->field;                  \
+        db->field = malloc(sz ? sz : 1);                                 \
+        if (sz) memcpy(db->field, cfg->field, sz);                       \
+    } while (0)
+    DUP(ns, cfg->n_ns);
+    DUP(rels, cfg->n_rels);
+    DUP(ast, cfg->n_ast);
+    DUP(children, cfg->n_children);
+    DUP(vclass, (size_t)cfg->n_ns * cfg->n_relnames);
+#undef DUP
+    db->strict = cfg->strict;
+    db->max_depth = cfg->max_depth;
+    db->max_width = cfg->max_width;
+    return db;
+}
+
+void rs_free(rs_db *db) {
+    if (!db) return;
+    free(db->t);
+    free(db->ex);
+    free(db->ns);
+    free(db->rels);
+    free(db->ast);
+    free(db->children);
+    free(db->vclass);
+    free(db);
+}
+
+void rs_set_limits(rs_db *db, int32_t max_depth, int32_t max_width) {
+    db->max_depth = max_depth;
+    db->max_width = max_width;
+}
+
+/* rows of (ns,obj,rel): [lo, hi) in shard order */
+static void node_rows(const rs_db *db, uint32_t ns, uint32_t obj, uint32_t rel, size_t *lo,
+                      size_t *hi) {
+    rs_tuple probe = {ns, obj, rel, 0, 0, 0, 0, 0, 0, 0};
+    size_t a = 0, b = db->n;
+    while (a < b) {
+        size_t m = (a + b) / 2;
+        const rs_tuple *t = &db->t[m];
+        int c = cmp_u32(t->ns, probe.ns);
+        if (!c) c = cmp_u32(t->obj, probe.obj);
+        if (!c) c = cmp_u32(t->rel, probe.rel);
+        if (c < 0) a = m + 1;
+        else b = m;
+    }
+    *lo = a;
+    b = db->n;
+    size_t e = a;
+    while (a < b) {
+        size_t m = (a + b) / 2;
+        const rs_tuple *t = &db->t[m];
+        int c = cmp_u32(t->ns, probe.ns);
+        if (!c) c = cmp_u32(t->obj, probe.obj);
+        if (!c) c = cmp_u32(t->rel, probe.rel);
+        if (c <= 0) a = m + 1;
+        else b = m;
+    }
+    *hi = a;
+    (void)e;
+}
+
+/* ------------------------------------------------------------------ */
+/* per-query evaluation context                                         */
+
+typedef struct {
+    uint64_t *slot;
+    size_t cap, cnt;
+} vset;
+
+typedef struct {
+    const rs_db *db;
+    uint32_t kind, sid, sns, srel; /* the query subject: never changes (traverser.go:102) */
+    rs_stats *st;
+    int depth_guard;
+} qctx;
+
+typedef struct {
+    int m;
+    int err;
+} res;
+
+static const res R_UNK = {RS_UNKNOWN, 0};
+static const res R_IS = {RS_IS_MEMBER, 0};
+static const res R_NOT = {RS_NOT_MEMBER, 0};
+
+static int decisive(res r) { return r.err != 0 || r.m == RS_IS_MEMBER; }
+
+static vset *vset_new(void) {
+    vset *v = calloc(1, sizeof *v);
+    v->cap = 64;
+    v->slot = calloc(v->cap, sizeof *v->slot);
+    return v;
+}
+static void vset_free(vset *v) {
+    if (v) {
+        free(v->slot);
+        free(v);
+    }
+}
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+/* stringSet.addNoDuplicate (x/graph/graph_utils.go:27-36): returns 1 if present */
+static int vset_add(vset *v, uint64_t key) {
+    key += 1; /* 0 = empty slot */
+    if (2 * (v->cnt + 1) > v->cap) {
+        size_t nc = v->cap * 2;
+        uint64_t *ns = calloc(nc, sizeof *ns);
+        for (size_t i = 0; i < v->cap; i++) {
+            uint64_t k = v->slot[i];
+            if (!k) continue;
+            size_t h = mix64(k) & (nc - 1);
+            while (ns[h]) h = (h + 1) & (nc - 1);
+            ns[h] = k;
+        }
+        free(v->slot);
+        v->slot = ns;
+        v->cap = nc;
+    }
+    size_t h = mix64(key) & (v->cap - 1);
+    while (v->slot[h]) {
+        if (v->slot[h] == key) return 1;
+        h = (h + 1) & (v->cap - 1);
+    }
+    v->slot[h] = key;
+    v->cnt++;
+    return 0;
+}
+
+/* SubjectSet.UniqueID = UUIDv5(obj, ns+"-"+rel) (relationtuple/definitions.go:114-116) */
+static uint64_t vkey(const rs_db *db, uint32_t ns, uint32_t obj, uint32_t rel) {
+    uint32_t cls = db->vclass[(size_t)ns * db->n_relnames + rel];
+    return ((uint64_t)obj << 32) | cls;
+}
+
+/* ExistsRelationTuples (persistence/sql/relationtuples.go:249-261) for the query subject */
+static int exists(const qctx *c, uint32_t ns, uint32_t obj, uint32_t rel) {
+    key7 k = {ns, obj, rel, c->kind, c->sid, 0, 0};
+    if (c->kind == 1) {
+        k.sns = c->sns;
+        k.srel = c->srel;
+    }
+    c->st->probes++;
+    return bsearch(&k, c->db->ex, c->db->n_ex, sizeof k, cmp_key7) != NULL;
+}
+
+/* namespace.ASTRelationFor (internal/namespace/definitions.go:37-62).
+ * Returns relation index or -1 (nil relation); *err on "does not exist". */
+static int ast_relation_for(const rs_db *db, uint32_t ns, uint32_t rel, int *err) {
+    *err = 0;
+    if (rel == db->empty_rel) return -1;                   /* :40-42 */
+    if (ns >= db->n_ns || !db->ns[ns].configured) return -1; /* :43-48 */
+    if (db->ns[ns].rel_count == 0) return -1;              /* :52-54 */
+    for (int i = 0; i < db->ns[ns].rel_count; i++) {
+        int ri = db->ns[ns].rel_begin + i;
+        if (db->rels[ri].name == rel) return ri;           /* :56-60 */
+    }
+    *err = RS_ERR_NO_RELATION;                             /* :61 */
+    return -1;
+}
+
+static res check_is_allowed(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip_direct,
+                            vset *vs);
+static res check_rewrite(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs);
+static res check_inverted(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs);
+
+/* checkDirect (internal/check/engine.go:167-208) */
+static res check_direct(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d) {
+    if (d <= 0) return R_UNK; /* :168-173 */
+    return exists(c, ns, obj, rel) ? R_IS : R_NOT;
+}
+
+/* checkExpandSubject (engine.go:102-164) + TraverseSubjectSetExpansion (traverser.go:53-121) */
+static res check_expand_subject(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, vset *vs) {
+    if (d <= 0) return R_UNK; /* :103-108 */
+    const rs_db *db = c->db;
+    vset *own = NULL;
+    if (!vs) vs = own = vset_new(); /* graph.InitVisited (graph_utils.go:38-43) */
+    size_t lo, hi;
+    node_rows(db, ns, obj, rel, &lo, &hi);
+    c->st->rows++;
+    /* subject-set rows in shard order, each with EXISTS(found) lookahead; stop at first found */
+    size_t nres = 0;
+    for (size_t i = lo; i < hi; i++) {
+        const rs_tuple *t = &db->t[i];
+        if (t->kind != 1) continue; /* current.subject_id IS NULL (traverser.go:87) */
+        c->st->edges++;
+        nres++;
+        if (exists(c, t->sns, t->sid, t->srel)) { /* :109-111, engine.go:133-138 */
+            vset_free(own);
+            return R_IS;
+        }
+    }
+    /* width truncation: results[:maxWidth-1] (engine.go:141-150) */
+    size_t keep = nres;
+    if ((long)nres > (long)db->max_width) keep = db->max_width > 0 ? (size_t)(db->max_width - 1) : 0;
+    size_t seen = 0;
+    for (size_t i = lo; i < hi && seen < keep; i++) {
+        const rs_tuple *t = &db->t[i];
+        if (t->kind != 1) continue;
+        seen++;
+        /* CheckAndAddVisited (engine.go:157-160) */
+        if (vset_add(vs, vkey(db, t->sns, t->sid, t->srel))) continue;
+        res r = check_is_allowed(c, t->sns, t->sid, t->srel, d, 1, vs); /* :161 */
+        if (decisive(r)) {
+            vset_free(own);
+            return r;
+        }
+    }
+    vset_free(own);
+    return R_NOT;
+}
+
+/* checkComputedSubjectSet (rewrites.go:208-230) */
+static res check_css(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, vset *vs) {
+    if (d < 0) return R_UNK; /* :214-217 */
+    return check_is_allowed(c, ns, obj, rel, d, 0, vs);
+}
+
+/* checkTupleToSubjectSet (rewrites.go:242-293) + GetRelationTuples (relationtuples.go:207-247) */
+static res check_ttu(qctx *c, uint32_t ns, uint32_t obj, const rs_ast *a, int d, vset *vs) {
+    if (d < 0) return R_UNK; /* :247-250 */
+    const rs_db *db = c->db;
+    size_t lo, hi;
+    node_rows(db, ns, obj, a->rel, &lo, &hi);
+    c->st->rows++;
+    for (size_t i = lo; i < hi; i++) {
+        const rs_tuple *t = &db->t[i];
+        if (t->kind != 1) continue; /* subject IDs are skipped (:280) */
+        c->st->edges++;
+        res r = check_is_allowed(c, t->sns, t->sid, a->computed, d - 1, 0, vs); /* :281-286 */
+        if (decisive(r)) return r;
+    }
+    return R_NOT;
+}
+
+/* OR computed-userset shortcut: rewrites.go:62-92 + TraverseSubjectSetRewrite (traverser.go:123-191) */
+static res check_shortcut(qctx *c, uint32_t ns, uint32_t obj, const rs_ast *a, int d, vset *vs) {
+    const rs_db *db = c->db;
+    int any_probe = 0, found = 0;
+    for (int k = 0; k < a->child_count; k++) {
+        const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+        if (ch->type != RS_CSS) continue;
+        int err;
+        int ri = ast_relation_for(db, ns, ch->rel, &err); /* error ignored (:134) */
+        if (db->strict && ri >= 0 && db->rels[ri].rewrite >= 0) continue; /* :137-139 */
+        any_probe = 1;
+        if (!found && exists(c, ns, obj, ch->rel)) found = 1; /* relation IN (...) LIMIT 1 */
+    }
+    (void)any_probe;
+    if (found) return R_IS; /* :160-172, rewrites.go:81-86 */
+    for (int k = 0; k < a->child_count; k++) {
+        const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+        if (ch->type != RS_CSS) continue;
+        res r = check_is_allowed(c, ns, obj, ch->rel, d - 1, 1, vs); /* rewrites.go:88-90 */
+        if (decisive(r)) return r;
+    }
+    return R_NOT;
+}
+
+/* dispatch of one rewrite child (rewrites.go:100-125 / 153-178) */
+static res check_child(qctx *c, uint32_t ns, uint32_t obj, int ci, int d, int nested_cost, vset *vs) {
+    const rs_ast *ch = &c->db->ast[ci];
+    switch (ch->type) {
+    case RS_TTU:
+        return check_ttu(c, ns, obj, ch, d, vs);
+    case RS_CSS:
+        return check_css(c, ns, obj, ch->rel, d, vs);
+    case RS_REWRITE:
+        return check_rewrite(c, ns, obj, ci, d - nested_cost, vs);
+    case RS_INVERT:
+        return check_inverted(c, ns, obj, ci, d, vs);
+    default: {
+        res r = {RS_UNKNOWN, RS_ERR_NOT_IMPLEMENTED};
+        return r;
+    }
+    }
+}
+
+/* checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73) */
+static res check_rewrite(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs) {
+    if (d <= 0) return R_UNK; /* :39-42 */
+    const rs_db *db = c->db;
+    const rs_ast *a = &db->ast[ai];
+    if (a->op != RS_OP_OR && a->op != RS_OP_AND) {
+        res r = {RS_UNKNOWN, RS_ERR_NOT_IMPLEMENTED}; /* :58-59 */
+        return r;
+    }
+    if (++c->depth_guard > MAX_RECURSION) {
+        c->depth_guard--;
+        res r = {RS_UNKNOWN, RS_ERR_INTERNAL};
+        return r;
+    }
+    int nchecks = 0;
+    res out = R_NOT;
+    if (a->op == RS_OP_OR) {
+        int has_css = 0;
+        for (int k = 0; k < a->child_count; k++)
+            if (db->ast[db->children[a->child_begin + k]].type == RS_CSS) has_css = 1;
+        if (has_css) {
+            nchecks++;
+            res r = check_shortcut(c, ns, obj, a, d, vs);
+            if (decisive(r)) {
+                out = r;
+                goto done;
+            }
+        }
+    }
+    for (int k = 0; k < a->child_count; k++) {
+        int ci = db->children[a->child_begin + k];
+        if (a->op == RS_OP_OR && db->ast[ci].type == RS_CSS) continue; /* handled (:95-98) */
+        nchecks++;
+        res r = check_child(c, ns, obj, ci, d, 1, vs); /* nested rewrite: restDepth-1 (:118) */
+        if (a->op == RS_OP_OR) {
+            if (decisive(r)) { /* binop.go:23-26 */
+                out = r;
+                goto done;
+            }
+        } else if (r.err || r.m != RS_IS_MEMBER) { /* binop.go:52-54 */
+            out.m = RS_NOT_MEMBER;
+            out.err = r.err;
+            goto done;
+        }
+    }
+    if (a->op == RS_OP_AND) out = nchecks ? R_IS : R_NOT; /* binop.go:42-44, 62-65 */
+    else out = R_NOT;                                     /* binop.go:19-21, 38 */
+done:
+    c->depth_guard--;
+    return out;
+}
+
+/* checkInverted (rewrites.go:136-200) */
+static res check_inverted(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs) {
+    if (d < 0) return R_UNK; /* :142-145 */
+    const rs_ast *a = &c->db->ast[ai];
+    if (a->child_count != 1) {
+        res r = {RS_UNKNOWN, RS_ERR_NOT_IMPLEMENTED};
+        return r;
+    }
+    if (++c->depth_guard > MAX_RECURSION) {
+        c->depth_guard--;
+        res r = {RS_UNKNOWN, RS_ERR_INTERNAL};
+        return r;
+    }
+    /* nested rewrite under NOT keeps restDepth (:171) */
+    res r = check_child(c, ns, obj, c->db->children[a->child_begin], d, 0, vs);
+    c->depth_guard--;
+    if (r.m == RS_IS_MEMBER) r.m = RS_NOT_MEMBER; /* :189-194 */
+    else if (r.m == RS_NOT_MEMBER) r.m = RS_IS_MEMBER;
+    return r;
+}
+
+/* checkIsAllowed (engine.go:214-249) */
+static res check_is_allowed(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip_direct,
+                            vset *vs) {
+    if (d <= 0) return R_UNK; /* :215-220 */
+    const rs_db *db = c->db;
+    if (++c->depth_guard > MAX_RECURSION) {
+        c->depth_guard--;
+        res r = {RS_UNKNOWN, RS_ERR_INTERNAL};
+        return r;
+    }
+    int err;
+    int ri = ast_relation_for(db, ns, rel, &err); /* :228-232 */
+    res out = R_NOT;
+    if (err) {
+        out.m = RS_UNKNOWN;
+        out.err = err;
+        goto done;
+    }
+    int has_rewrite = ri >= 0 && db->rels[ri].rewrite >= 0;                 /* :233 */
+    int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;        /* :235 */
+    if (has_rewrite) {                                                      /* :236-238 */
+        res r = check_rewrite(c, ns, obj, db->rels[ri].rewrite, d, vs);
+        if (decisive(r)) {
+            out = r;
+            goto done;
+        }
+    }
+    if ((!db->strict || !has_rewrite) && !skip_direct) { /* :239-243 */
+        res r = check_direct(c, ns, obj, rel, d - 1);
+        if (decisive(r)) {
+            out = r;
+            goto done;
+        }
+    }
+    if (can_ss) { /* :244-246 */
+        res r = check_expand_subject(c, ns, obj, rel, d - 1, vs);
+        if (decisive(r)) {
+            out = r;
+            goto done;
+        }
+    }
+done:
+    c->depth_guard--;
+    return out;
+}
+
+/* Engine.CheckRelationTuple (engine.go:76-95) */
+int rs_check(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st) {
+    rs_stats dummy = {0, 0, 0, 0};
+    qctx c = {db, q->kind, q->sid, q->kind == 1 ? q->sns : 0, q->kind == 1 ? q->srel : 0,
+              st ? st : &dummy, 0};
+    int d = q->depth;
+    if (d <= 0 || db->max_depth < d) d = db->max_depth; /* :82-84 */
+    res r = check_is_allowed(&c, q->ns, q->obj, q->rel, d, 0, NULL);
+    if (err) *err = r.err;
+    return r.m;
+}
+
+/* ------------------------------------------------------------------ */
+/* batch (CPU baseline)                                                  */
+
+typedef struct {
+    rs_db *db;
+    const rs_query *q;
+    size_t n;
+    uint8_t *decision;
+    int32_t *err;
+    atomic_size_t next;
+    pthread_mutex_t mu;
+    rs_stats total;
+} batch_job;
+
+static void *batch_worker(void *arg) {
+    batch_job *j = arg;
+    rs_stats st = {0, 0, 0, 0};
+    for (;;) {
+        size_t i = atomic_fetch_add(&j->next, 64);
+        if (i >= j->n) break;
+        size_t e = i + 64 < j->n ? i + 64 : j->n;
+        for (; i < e; i++) {
+            int32_t er = 0;
+            int m = rs_check(j->db, &j->q[i], &er, &st);
+            j->decision[i] = (er == 0 && m == RS_IS_MEMBER); /* engine.go:65-71 */
+            j->err[i] = er;
+        }
+    }
+    pthread_mutex_lock(&j->mu);
+    j->total.rows += st.rows;
+    j->total.edges += st.edges;
+    j->total.probes += st.probes;
+    pthread_mutex_unlock(&j->mu);
+    return NULL;
+}
+
+void rs_check_batch(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t *decision,
+                    int32_t *err, rs_stats *st) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    batch_job j;
+    j.db = db;
+    j.q = q;
+    j.n = n;
+    j.decision = decision;
+    j.err = err;
+    atomic_init(&j.next, 0);
+    pthread_mutex_init(&j.mu, NULL);
+    memset(&j.total, 0, sizeof j.total);
+    pthread_t th[256];
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, batch_worker, &j);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&j.mu);
+    if (st) {
+        st->rows += j.total.rows;
+        st->edges += j.total.edges;
+        st->probes += j.total.probes;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Expand (internal/expand/engine.go:43-124)                            */
+
+typedef struct {
+    const rs_db *db;
+    rs_tree_node *out;
+    size_t cap, len;
+    int overflow;
+    vset *vs;
+    rs_stats *st;
+} xctx;
+
+static void emit(xctx *x, uint32_t type, uint32_t kind, uint32_t sid, uint32_t sns, uint32_t srel) {
+    if (x->len >= x->cap) {
+        x->overflow = 1;
+        x->len++;
+        return;
+    }
+    rs_tree_node *n = &x->out[x->len++];
+    n->type = type;
+    n->kind = kind;
+    n->sid = sid;
+    n->sns = kind ? sns : 0;
+    n->srel = kind ? srel : 0;
+    n->n_children = 0;
+}
+
+/* returns 1 if a node was written, 0 for nil */
+static int build_tree(xctx *x, uint32_t kind, uint32_t sid, uint32_t sns, uint32_t srel, int d) {
+    const rs_db *db = x->db;
+    if (d <= 0 || db->max_depth < d) d = db->max_depth; /* :56-58 */
+    if (kind == 0) {                                     /* :60-67 */
+        emit(x, 4, 0, sid, 0, 0);
+        x->st->out_nodes++;
+        return 1;
+    }
+    if (vset_add(x->vs, vkey(db, sns, sid, srel))) return 0; /* :69-72 (root included) */
+    size_t lo, hi;
+    node_rows(db, sns, sid, srel, &lo, &hi);
+    x->st->rows++;
+    if (lo == hi) return 0; /* :97-99 */
+    size_t me = x->len;
+    if (d <= 1) { /* :101-104 */
+        emit(x, 4, 1, sid, sns, srel);
+        x->st->out_nodes++;
+        return 1;
+    }
+    emit(x, 1, 1, sid, sns, srel);
+    x->st->out_nodes++;
+    for (size_t i = lo; i < hi; i++) { /* :106-119 */
+        const rs_tuple *t = &db->t[i];
+        x->st->edges++;
+        if (!build_tree(x, t->kind, t->sid, t->sns, t->srel, d - 1)) {
+            emit(x, 4, t->kind, t->sid, t->sns, t->srel); /* nil child -> leaf (:112-117) */
+            x->st->out_nodes++;
+        }
+        if (me < x->cap) x->out[me].n_children++;
+    }
+    return 1;
+}
+
+long rs_expand(rs_db *db, uint32_t kind, uint32_t sid, uint32_t sns, uint32_t srel, int32_t depth,
+               rs_tree_node *out, size_t cap, rs_stats *st) {
+    rs_stats dummy = {0, 0, 0, 0};
+    xctx x = {db, out, cap, 0, 0, vset_new(), st ? st : &dummy};
+    int wrote = build_tree(&x, kind, sid, sns, srel, depth);
+    vset_free(x.vs);
+    if (x.overflow) return -1;
+    return wrote ? (long)x.len : 0;
+}
