@@ -1,0 +1,329 @@
+// extern "C" boundary (include/keto_mi355x.h): plain pointers and sizes, status codes,
+// thread-local error text.  No CPU evaluation path exists behind it: every Check and
+// Expand runs on the gfx950 kernels, and a missing/failed device is an error.
+#include <cstring>
+#include <memory>
+#include <new>
+#include <numeric>
+
+#include "engine.hpp"
+
+using keto::Error;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+template <class F>
+int guarded(F &&f) {
+    try {
+        f();
+        return KETO_OK;
+    } catch (const Error &e) {
+        return fail(e.code, e.what());
+    } catch (const std::bad_alloc &) {
+        return fail(KETO_E_LIMIT, "host allocation failed");
+    } catch (const std::exception &e) {
+        return fail(KETO_E_INVALID, e.what());
+    }
+}
+
+void grow(void *&p, size_t &cap, size_t need) {
+    if (cap >= need) return;
+    if (p) KETO_HIP(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    KETO_HIP(hipMalloc(&p, need));
+    cap = need;
+}
+
+}  // namespace
+
+namespace keto {
+Stream::~Stream() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (check_scratch.mem) (void)hipFree(check_scratch.mem);
+    if (expand_scratch.mem) (void)hipFree(expand_scratch.mem);
+    if (lists) (void)hipFree(lists);
+    if (qbuf) (void)hipFree(qbuf);
+    if (obuf) (void)hipFree(obuf);
+    if (counters) (void)hipFree(counters);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+}  // namespace keto
+
+// the opaque ABI handles are the internal objects themselves
+static keto::Snapshot *SN(keto_snapshot *p) { return reinterpret_cast<keto::Snapshot *>(p); }
+static const keto::Snapshot *SN(const keto_snapshot *p) { return reinterpret_cast<const keto::Snapshot *>(p); }
+static keto::Stream *ST(keto_stream *p) { return reinterpret_cast<keto::Stream *>(p); }
+
+extern "C" {
+
+int keto_abi_version(void) { return KETO_ABI_VERSION; }
+
+size_t keto_last_error(char *buf, size_t len) {
+    if (buf && len) {
+        size_t n = std::min(len - 1, g_err.size());
+        std::memcpy(buf, g_err.data(), n);
+        buf[n] = 0;
+    }
+    return g_err.size();
+}
+
+int keto_device_count(int32_t *out) {
+    return guarded([&] {
+        int n = 0;
+        KETO_HIP(hipGetDeviceCount(&n));
+        if (out) *out = n;
+    });
+}
+
+int keto_snapshot_build(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, keto_snapshot **out) {
+    if (!out) return fail(KETO_E_INVALID, "null output pointer");
+    *out = nullptr;
+    return guarded([&] {
+        *out = reinterpret_cast<keto_snapshot *>(keto::build_snapshot(cfg, tuples, n));
+    });
+}
+
+int keto_snapshot_free(keto_snapshot *snap) {
+    delete SN(snap);
+    return KETO_OK;
+}
+
+int keto_snapshot_info_get(const keto_snapshot *snap, keto_snapshot_info *out) {
+    if (!snap || !out) return fail(KETO_E_INVALID, "null argument");
+    *out = SN(snap)->info;
+    return KETO_OK;
+}
+
+int keto_stream_create(int32_t device, keto_stream **out) {
+    if (!out) return fail(KETO_E_INVALID, "null output pointer");
+    *out = nullptr;
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(device));
+        auto s = std::make_unique<keto::Stream>();
+        s->device = device;
+        KETO_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        KETO_HIP(hipEventCreate(&s->ev0));
+        KETO_HIP(hipEventCreate(&s->ev1));
+        KETO_HIP(hipMalloc(&s->counters, 24 * sizeof(unsigned long long)));
+        KETO_HIP(hipMemset(s->counters, 0, 24 * sizeof(unsigned long long)));
+        *out = reinterpret_cast<keto_stream *>(s.release());
+    });
+}
+
+int keto_stream_destroy(keto_stream *s) {
+    delete ST(s);
+    return KETO_OK;
+}
+
+int keto_stream_sync(keto_stream *hs) {
+    keto::Stream *s = ST(hs);
+    if (!s) return fail(KETO_E_INVALID, "null stream");
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        KETO_HIP(hipStreamSynchronize(s->stream));
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, s->ev0, s->ev1) == hipSuccess) s->last_kernel_ms = ms;
+    });
+}
+
+int keto_stream_counters(keto_stream *hs, keto_work_counters *out, int32_t reset) {
+    keto::Stream *s = ST(hs);
+    if (!s) return fail(KETO_E_INVALID, "null stream");
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        unsigned long long c[24];
+        KETO_HIP(hipStreamSynchronize(s->stream));
+        KETO_HIP(hipMemcpy(c, s->counters, sizeof c, hipMemcpyDeviceToHost));
+        if (out)
+            for (int t = 0; t < 3; t++) {
+                out->rows[t] = c[8 * t + 0];
+                out->edges[t] = c[8 * t + 1];
+                out->probes[t] = c[8 * t + 2];
+                out->out_nodes[t] = c[8 * t + 3];
+                out->queries[t] = c[8 * t + 4];
+            }
+        if (reset) KETO_HIP(hipMemset(s->counters, 0, sizeof c));
+    });
+}
+
+int keto_stream_last_kernel_ms(keto_stream *hs, double *ms) {
+    keto::Stream *s = ST(hs);
+    if (!s || !ms) return fail(KETO_E_INVALID, "null argument");
+    *ms = s->last_kernel_ms;
+    return KETO_OK;
+}
+
+int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *queries, uint64_t n,
+                     const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags) {
+    keto::Snapshot *snap = SN(hsnap);
+    keto::Stream *s = ST(hs);
+    if (!snap || !s) return fail(KETO_E_INVALID, "null snapshot or stream");
+    if (n && (!queries || !out_allowed || !out_err)) return fail(KETO_E_INVALID, "null buffer");
+    keto_limits lim = limits ? *limits : keto_limits{5, 100};
+    if (lim.max_read_depth < 1 || lim.max_read_depth > 65535 || lim.max_read_width < 1 || lim.max_read_width > 65535)
+        return fail(KETO_E_INVALID, "limits out of range (embedx/config.schema.json:368-383: 1..65535)");
+    if (s->device != snap->device) return fail(KETO_E_INVALID, "stream and snapshot are on different devices");
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        keto::CheckLaunch L{};
+        L.n = n;
+        L.max_depth = lim.max_read_depth;
+        L.max_width = lim.max_read_width;
+        L.count = (flags & KETO_F_COUNT_WORK) != 0;
+        if (flags & KETO_F_DEVICE_PTRS) {
+            L.queries = queries;
+            L.out_allowed = out_allowed;
+            L.out_err = out_err;
+            keto::run_check(*snap, *s, L);
+            if (!(flags & KETO_F_ASYNC)) {
+                KETO_HIP(hipStreamSynchronize(s->stream));
+                float ms = 0;
+                if (n && hipEventElapsedTime(&ms, s->ev0, s->ev1) == hipSuccess) s->last_kernel_ms = ms;
+            }
+            return;
+        }
+        // host buffers: stage through device memory owned by the stream
+        const size_t qb = n * sizeof(keto_query), ob = n * (1 + sizeof(int32_t));
+        grow(s->qbuf, s->qbuf_bytes, std::max<size_t>(qb, 64));
+        grow(s->obuf, s->obuf_bytes, std::max<size_t>(ob + 64, 64));
+        auto *d_allowed = static_cast<uint8_t *>(s->obuf);
+        auto *d_err = reinterpret_cast<int32_t *>(static_cast<char *>(s->obuf) + ((n + 63) / 64) * 64);
+        KETO_HIP(hipMemcpyAsync(s->qbuf, queries, qb, hipMemcpyHostToDevice, s->stream));
+        L.queries = static_cast<const keto_query *>(s->qbuf);
+        L.out_allowed = d_allowed;
+        L.out_err = d_err;
+        keto::run_check(*snap, *s, L);
+        KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->stream));
+        KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+        KETO_HIP(hipStreamSynchronize(s->stream));
+        float ms = 0;
+        if (n && hipEventElapsedTime(&ms, s->ev0, s->ev1) == hipSuccess) s->last_kernel_ms = ms;
+    });
+}
+
+int keto_expand_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_set *roots, uint64_t n,
+                      const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets,
+                      int32_t *out_err) {
+    keto::Snapshot *snap = SN(hsnap);
+    keto::Stream *s = ST(hs);
+    if (!snap || !s) return fail(KETO_E_INVALID, "null snapshot or stream");
+    if (n && (!roots || !out_offsets || !out_err)) return fail(KETO_E_INVALID, "null buffer");
+    keto_limits lim = limits ? *limits : keto_limits{5, 100};
+    if (lim.max_read_depth < 1 || lim.max_read_depth > 65535) return fail(KETO_E_INVALID, "max_read_depth out of range");
+    if (s->device != snap->device) return fail(KETO_E_INVALID, "stream and snapshot are on different devices");
+    int rc = KETO_OK;
+    int g = guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        out_offsets[0] = 0;
+        if (n == 0) return;
+        // device buffers: roots | sizes | offsets | err
+        const size_t rb = (n * sizeof(keto_subject_set) + 255) / 256 * 256;
+        const size_t sb = (n * 8 + 255) / 256 * 256;
+        const size_t eb = (n * 4 + 255) / 256 * 256;
+        grow(s->qbuf, s->qbuf_bytes, rb + 2 * sb + eb);
+        char *base = static_cast<char *>(s->qbuf);
+        auto *d_roots = reinterpret_cast<keto_subject_set *>(base);
+        auto *d_sizes = reinterpret_cast<uint64_t *>(base + rb);
+        auto *d_offs = reinterpret_cast<uint64_t *>(base + rb + sb);
+        auto *d_err = reinterpret_cast<int32_t *>(base + rb + 2 * sb);
+        KETO_HIP(hipMemcpyAsync(d_roots, roots, n * sizeof(keto_subject_set), hipMemcpyHostToDevice, s->stream));
+        keto::ExpandLaunch L{};
+        L.roots = d_roots;
+        L.n = n;
+        L.max_depth = lim.max_read_depth;
+        L.sizes = d_sizes;
+        L.offsets = d_offs;
+        L.err = d_err;
+        L.emit = false;
+        keto::run_expand(*snap, *s, L);  // pass 1: count nodes per tree
+        std::vector<uint64_t> sizes(n);
+        KETO_HIP(hipMemcpyAsync(sizes.data(), d_sizes, n * 8, hipMemcpyDeviceToHost, s->stream));
+        KETO_HIP(hipMemcpyAsync(out_err, d_err, n * 4, hipMemcpyDeviceToHost, s->stream));
+        KETO_HIP(hipStreamSynchronize(s->stream));
+        for (uint64_t i = 0; i < n; i++) out_offsets[i + 1] = out_offsets[i] + (out_err[i] ? 0 : sizes[i]);
+        const uint64_t total = out_offsets[n];
+        if (total > out_cap || (total && !out_nodes)) {
+            rc = fail(KETO_E_CAPACITY, "expand output needs " + std::to_string(total) + " nodes");
+            return;
+        }
+        if (total == 0) return;
+        void *d_out = nullptr;
+        grow(s->obuf, s->obuf_bytes, total * 12);
+        d_out = s->obuf;
+        KETO_HIP(hipMemcpyAsync(d_offs, out_offsets, n * 8, hipMemcpyHostToDevice, s->stream));
+        L.emit = true;
+        L.out = static_cast<uint32_t *>(d_out);
+        keto::run_expand(*snap, *s, L);  // pass 2: emit pre-order nodes
+        std::vector<uint32_t> raw(total * 3);
+        KETO_HIP(hipMemcpyAsync(raw.data(), d_out, total * 12, hipMemcpyDeviceToHost, s->stream));
+        KETO_HIP(hipStreamSynchronize(s->stream));
+        const keto::Snapshot &S = *snap;
+        for (uint64_t i = 0; i < total; i++) {
+            keto_tree_node &o = out_nodes[i];
+            o.type = raw[3 * i];
+            o.n_children = raw[3 * i + 2];
+            uint32_t sk = raw[3 * i + 1];
+            if (sk & keto::SKEY_SET) {
+                uint32_t node = sk & ~keto::SKEY_SET;
+                uint32_t ns = S.ns_of(node);
+                const keto::NsDev &nd = S.ns[ns];
+                uint32_t e = nd.ent_base + (node - nd.node_base) / nd.n_slots;
+                uint32_t slot = (node - nd.node_base) % nd.n_slots;
+                o.subj_kind = 1;
+                o.s_obj = S.ent_obj[e];
+                o.s_ns = ns;
+                o.s_rel = S.slot_rel[nd.slot_base + slot];
+            } else {
+                o.subj_kind = 0;
+                o.s_obj = sk;
+                o.s_ns = 0;
+                o.s_rel = 0;
+            }
+        }
+    });
+    return g != KETO_OK ? g : rc;
+}
+
+int keto_device_alloc(int32_t device, uint64_t bytes, void **out) {
+    if (!out) return fail(KETO_E_INVALID, "null output pointer");
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(device));
+        KETO_HIP(hipMalloc(out, bytes ? bytes : 1));
+    });
+}
+
+int keto_device_free(void *p) {
+    return guarded([&] { KETO_HIP(hipFree(p)); });
+}
+
+int keto_memcpy_h2d(keto_stream *hs, void *dst, const void *src, uint64_t bytes) {
+    keto::Stream *s = ST(hs);
+    if (!s) return fail(KETO_E_INVALID, "null stream");
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        KETO_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s->stream));
+        KETO_HIP(hipStreamSynchronize(s->stream));
+    });
+}
+
+int keto_memcpy_d2h(keto_stream *hs, void *dst, const void *src, uint64_t bytes) {
+    keto::Stream *s = ST(hs);
+    if (!s) return fail(KETO_E_INVALID, "null stream");
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        KETO_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream));
+        KETO_HIP(hipStreamSynchronize(s->stream));
+    });
+}
+
+}  // extern "C"

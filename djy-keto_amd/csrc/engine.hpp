@@ -1,0 +1,107 @@
+// Internal host-side types of libketo_mi355x (behind the C ABI in include/keto_mi355x.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/keto_mi355x.h"
+#include "layout.hpp"
+
+namespace keto {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define KETO_HIP(expr)                                                                              \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess)                                                                       \
+            throw ::keto::Error(KETO_E_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// Host mirror of the snapshot + its device buffers.
+struct Snapshot {
+    int device = 0;
+    uint32_t n_ns = 0, n_rel = 0, n_rel_caller = 0, n_uuids = 0;
+    bool strict = false;
+    std::vector<std::string> ns_names, rel_names;
+    std::vector<NsDev> ns;          // [n_ns+1]
+    std::vector<uint32_t> ent_obj;  // entity -> uuid id (NONE32 for phantoms)
+    std::vector<uint32_t> slot_rel; // global slot -> relname
+    std::vector<uint32_t> relinfo, nsrel;
+    std::vector<Op> ops;
+    std::vector<uint32_t> op_children;
+    DevSnapshot dev{};
+    std::vector<void *> allocs;
+    keto_snapshot_info info{};
+
+    ~Snapshot();
+    // node -> (ns, entity, slot) on the host (for Expand output conversion)
+    uint32_t ns_of(uint32_t node) const;
+};
+
+Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n);
+
+// scratch tier: per-lane visited capacity (slots, pow2) and stack frames
+struct Tier {
+    uint32_t lanes, vcap, scap;
+};
+
+// per-stream device scratch for one kernel family: disjoint per-tier regions so an
+// epoch-tagged visited slot can only ever be read back by the lane that wrote it
+struct Scratch {
+    void *mem = nullptr;
+    size_t bytes = 0;
+    Tier t[3]{};
+    uint32_t *ctrl = nullptr;
+    uint32_t *epochs[3]{};
+    unsigned long long *vis[3]{};
+    uint4 *stack[3]{};
+};
+
+struct Stream {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // device workspace (allocated on first use, never inside a launch sequence)
+    Scratch check_scratch, expand_scratch;
+    uint32_t *lists = nullptr;  // two overflow hand-off lists of list_cap entries
+    uint64_t list_cap = 0;
+    void *qbuf = nullptr, *obuf = nullptr;  // staging for host-pointer batches
+    size_t qbuf_bytes = 0, obuf_bytes = 0;
+    unsigned long long *counters = nullptr;  // device [3 tiers][8]
+    keto_work_counters host_counters{};
+    double last_kernel_ms = 0;
+    ~Stream();
+};
+
+// kernels.hip
+struct CheckLaunch {
+    const keto_query *queries;
+    uint64_t n;
+    uint8_t *out_allowed;
+    int32_t *out_err;
+    int32_t max_depth, max_width;
+    bool count;
+};
+void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);
+
+struct ExpandLaunch {
+    const keto_subject_set *roots;  // device
+    uint64_t n;
+    int32_t max_depth;
+    uint64_t *sizes;    // device [n] (count pass output)
+    const uint64_t *offsets; // device [n] (emit pass input)
+    uint32_t *out;      // device nodes: 3 x u32 each {type, skey, n_children}
+    int32_t *err;       // device [n]
+    bool emit;
+};
+void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L);
+
+}  // namespace keto

@@ -1,0 +1,81 @@
+// Device-resident snapshot layout shared by the host builder and the gfx950 kernels.
+//
+// Node space ("dense arithmetic layout"): every namespace ns owns a contiguous
+// entity range [ent_base, ent_base + n_ent) (real objects sorted by uuid id,
+// plus one phantom entity standing for every object the snapshot has never seen)
+// and a fixed relation-slot count n_slots.  The node for (entity e, slot s) is
+//     node = node_base[ns] + (e - ent_base[ns]) * n_slots[ns] + s
+// so computed-userset and tuple-to-userset hops are pure arithmetic on the node id
+// (rewrites.go:208-230, 242-293) and no per-node metadata is ever fetched.
+// (ns, relname) pairs that own no slot are "virtual" nodes: they have no tuples,
+// only a relation status (NIL / ERR), and are encoded as VIRT_BIT|ns<<16|relname.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace keto {
+
+constexpr uint32_t VIRT_BIT = 0x80000000u;  // frame node id: virtual node
+constexpr uint32_t EDGE_ALIAS = 0x80000000u; // set_dst entry: visited key != node id
+constexpr uint32_t SKEY_SET = 0x80000000u;   // all-row entry: subject set (else subject id)
+constexpr uint32_t NO_SLOT = 0xFFFFu;
+constexpr uint32_t NO_OP = 0xFFFFu;
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+
+// relation status of (ns, relname) per namespace.ASTRelationFor
+// (internal/namespace/definitions.go:37-62)
+enum RelStatus : uint32_t { REL_NIL = 0, REL_DECLARED = 1, REL_ERROR = 2 };
+
+// relinfo word (per (ns, slot)):  bits 0-15 rewrite op (NO_OP = none)
+//   bit 16 has_rewrite, bit 17 can_have_subject_sets (engine.go:233-235), bits 18-19 status
+//   bit 20 shared visited class (vkey array must be consulted)
+__host__ __device__ inline uint32_t ri_op(uint32_t ri) { return ri & 0xFFFFu; }
+__host__ __device__ inline bool ri_rw(uint32_t ri) { return (ri >> 16) & 1u; }
+__host__ __device__ inline bool ri_ss(uint32_t ri) { return (ri >> 17) & 1u; }
+__host__ __device__ inline uint32_t ri_status(uint32_t ri) { return (ri >> 18) & 3u; }
+__host__ __device__ inline bool ri_shared(uint32_t ri) { return (ri >> 20) & 1u; }
+__host__ __device__ inline uint32_t make_ri(uint32_t op, bool rw, bool ss, uint32_t status, bool shared) {
+    return (op & 0xFFFFu) | (uint32_t(rw) << 16) | (uint32_t(ss) << 17) | (status << 18) | (uint32_t(shared) << 20);
+}
+// nsrel word (per (ns, relname)): bits 0-15 slot (NO_SLOT = virtual), bits 16-17 status
+__host__ __device__ inline uint32_t nr_slot(uint32_t w) { return w & 0xFFFFu; }
+__host__ __device__ inline uint32_t nr_status(uint32_t w) { return (w >> 16) & 3u; }
+
+// rewrite program op (flattened ast.SubjectSetRewrite / Child, ast_definitions.go:8-72)
+enum OpType : uint32_t { OP_REWRITE = 0, OP_CSS = 1, OP_TTU = 2, OP_INVERT = 3 };
+enum OpKind : uint32_t { OPK_OR = 0, OPK_AND = 1, OPK_BAD = 2 };
+struct alignas(16) Op {
+    uint32_t type_kind;    // type | kind << 8 | has_css << 16
+    uint32_t child_begin;  // into op_children
+    uint32_t child_count;
+    uint32_t rel_computed; // CSS: rel | 0 ; TTU: tupleset rel | computed << 16
+};
+
+struct alignas(16) NsDev {
+    uint32_t ent_base, node_base, n_slots, slot_base;
+};
+
+// Device view (all pointers device memory).  Passed by value to kernels.
+struct DevSnapshot {
+    const uint32_t *set_off;   // [n_nodes+1]  subject-set rows, shard order (ES + TTU)
+    const uint32_t *set_dst;   // node | EDGE_ALIAS
+    const uint32_t *vkey;      // [n_nodes] visited representative (only read for aliased nodes)
+    const uint32_t *all_off;   // [n_nodes+1]  every tuple of a node, shard order (Expand)
+    const uint32_t *all_subj;  // subject id, or SKEY_SET|node
+    const uint32_t *rev_off;   // [n_uuids + n_nodes + 1]  subject -> sorted nodes containing it
+    const uint32_t *rev_nodes;
+    const NsDev *ns;           // [n_ns + 1] (sentinel: node_base = n_nodes)
+    const uint32_t *relinfo;   // [total slots]
+    const uint32_t *nsrel;     // [n_ns * n_rel]
+    const Op *ops;
+    const uint32_t *op_children;
+    const unsigned long long *ent_keys; // open addressing: ((ns<<32)|obj)+1, 0 = empty
+    const uint32_t *ent_vals;
+    uint32_t ent_mask;
+    uint32_t n_ns, n_rel, n_nodes, n_uuids;
+    int32_t strict;
+};
+
+}  // namespace keto

@@ -1,0 +1,108 @@
+"""ctypes declarations of include/keto_mi355x.h (the C ABI of libketo_mi355x.so)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_NAME = "libketo_mi355x.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+KETO_OK = 0
+KETO_E_INVALID, KETO_E_DEVICE, KETO_E_CAPACITY, KETO_E_LIMIT = -1, -2, -3, -4
+F_DEVICE_PTRS, F_ASYNC, F_COUNT_WORK = 0x1, 0x2, 0x4
+QERR_NONE, QERR_NO_RELATION, QERR_INTERNAL, QERR_NOT_IMPLEMENTED = 0, 1, 2, 3
+
+TUPLE_DT = np.dtype([("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"), ("subj_kind", "<u4"), ("s_obj", "<u4"),
+                     ("s_ns", "<u4"), ("s_rel", "<u4"), ("reserved", "<u4"), ("shard_id", "u1", (16,))])
+QUERY_DT = np.dtype([("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"), ("subj_kind", "<u4"), ("s_obj", "<u4"),
+                     ("s_ns", "<u4"), ("s_rel", "<u4"), ("max_depth", "<i4")])
+SUBJSET_DT = np.dtype([("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"), ("max_depth", "<i4")])
+TREE_DT = np.dtype([("type", "<u4"), ("subj_kind", "<u4"), ("s_obj", "<u4"), ("s_ns", "<u4"), ("s_rel", "<u4"),
+                    ("n_children", "<u4")])
+assert TUPLE_DT.itemsize == 48 and QUERY_DT.itemsize == 32 and TREE_DT.itemsize == 24
+
+
+class SnapshotConfig(ctypes.Structure):
+    _fields_ = [("n_namespaces", ctypes.c_uint32), ("namespace_names", ctypes.POINTER(ctypes.c_char_p)),
+                ("n_relations", ctypes.c_uint32), ("relation_names", ctypes.POINTER(ctypes.c_char_p)),
+                ("n_uuids", ctypes.c_uint32), ("namespaces_json", ctypes.c_char_p),
+                ("strict_mode", ctypes.c_int32), ("device", ctypes.c_int32)]
+
+
+class SnapshotInfo(ctypes.Structure):
+    _fields_ = [("n_tuples", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64), ("n_entities", ctypes.c_uint64),
+                ("n_set_edges", ctypes.c_uint64), ("n_rev_entries", ctypes.c_uint64),
+                ("device_bytes", ctypes.c_uint64), ("build_seconds", ctypes.c_double)]
+
+
+class Limits(ctypes.Structure):
+    _fields_ = [("max_read_depth", ctypes.c_int32), ("max_read_width", ctypes.c_int32)]
+
+
+class WorkCounters(ctypes.Structure):
+    _fields_ = [("rows", ctypes.c_uint64 * 3), ("edges", ctypes.c_uint64 * 3), ("probes", ctypes.c_uint64 * 3),
+                ("out_nodes", ctypes.c_uint64 * 3), ("queries", ctypes.c_uint64 * 3)]
+
+
+# symbol -> (restype, argtypes); the header's complete export list
+_VP, _U32, _I32, _U64, _SZ = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
+SIGNATURES = {
+    "keto_abi_version": (ctypes.c_int, []),
+    "keto_last_error": (_SZ, [ctypes.c_char_p, _SZ]),
+    "keto_snapshot_build": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, ctypes.POINTER(_VP)]),
+    "keto_snapshot_free": (ctypes.c_int, [_VP]),
+    "keto_snapshot_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(SnapshotInfo)]),
+    "keto_stream_create": (ctypes.c_int, [_I32, ctypes.POINTER(_VP)]),
+    "keto_stream_destroy": (ctypes.c_int, [_VP]),
+    "keto_stream_sync": (ctypes.c_int, [_VP]),
+    "keto_stream_counters": (ctypes.c_int, [_VP, ctypes.POINTER(WorkCounters), _I32]),
+    "keto_stream_last_kernel_ms": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double)]),
+    "keto_check_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),
+    "keto_expand_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _U64, _VP, _VP]),
+    "keto_device_alloc": (ctypes.c_int, [_I32, _U64, ctypes.POINTER(_VP)]),
+    "keto_device_free": (ctypes.c_int, [_VP]),
+    "keto_memcpy_h2d": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
+    "keto_memcpy_d2h": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
+    "keto_device_count": (ctypes.c_int, [ctypes.POINTER(_I32)]),
+}
+
+
+class KetoError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"keto error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP engine.  There is no fallback: a missing library is an error."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C djy-keto_amd` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.keto_abi_version() != 1:
+            raise RuntimeError("libketo_mi355x ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(4096)
+    lib().keto_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int):
+    if rc != KETO_OK:
+        raise KetoError(rc, last_error())
+    return rc

@@ -1,0 +1,211 @@
+"""Host-side mirror of the reference engine API over the C ABI.
+
+  CheckEngine.check_is_member(tuple, rest_depth)  ~ check.Engine.CheckIsMember   (internal/check/engine.go:65-71)
+  CheckEngine.check_relation_tuple(...)            ~ check.Engine.CheckRelationTuple (engine.go:76-95)
+  CheckEngine.check_batch(queries)                 ~ the batched form the Go shim's dispatcher uses
+  ExpandEngine.build_tree(subject, rest_depth)     ~ expand.Engine.BuildTree       (internal/expand/engine.go:43-52)
+
+Every evaluation runs in libketo_mi355x's gfx950 kernels; this module only
+interns strings (the Mapper role, internal/relationtuple/uuid_mapping.go) and
+moves buffers.  A missing library or device raises -- there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi
+from ._abi import KetoError, check, lib
+
+IS_MEMBER, NOT_MEMBER = 1, 2
+
+
+def shard_bytes(hi: np.ndarray, lo: np.ndarray) -> np.ndarray:
+    """(hi, lo) uint64 halves -> big-endian 16-byte UUIDs (ORDER BY shard_id byte order)."""
+    out = np.empty((len(hi), 16), dtype=np.uint8)
+    out[:, :8] = hi.astype(">u8").view(np.uint8).reshape(-1, 8)
+    out[:, 8:] = lo.astype(">u8").view(np.uint8).reshape(-1, 8)
+    return out
+
+
+class Interner:
+    def __init__(self, names=()):
+        self.ids: dict[str, int] = {}
+        self.names: list[str] = []
+        for n in names:
+            self(n)
+
+    def __call__(self, s: str) -> int:
+        i = self.ids.get(s)
+        if i is None:
+            i = len(self.names)
+            self.ids[s] = i
+            self.names.append(s)
+        return i
+
+
+@dataclass
+class Mapper:
+    """String <-> dense id tables (the Go shim's job; uuid_mapping.go:199-399)."""
+    namespaces: Interner = field(default_factory=Interner)
+    relations: Interner = field(default_factory=Interner)
+    uuids: Interner = field(default_factory=Interner)
+
+
+class Snapshot:
+    """Immutable device-resident snapshot (CSR rows + compiled rewrite program)."""
+
+    def __init__(self, namespaces_json: str | dict, tuples: np.ndarray, ns_names: list, rel_names: list,
+                 n_uuids: int, strict: bool = False, device: int = 0):
+        if isinstance(namespaces_json, dict):
+            namespaces_json = json.dumps(namespaces_json)
+        tuples = np.ascontiguousarray(tuples, dtype=_abi.TUPLE_DT)
+        self._ns = (ctypes.c_char_p * max(1, len(ns_names)))(*[n.encode() for n in ns_names])
+        self._rel = (ctypes.c_char_p * max(1, len(rel_names)))(*[r.encode() for r in rel_names])
+        self._json = namespaces_json.encode()
+        cfg = _abi.SnapshotConfig(len(ns_names), self._ns, len(rel_names), self._rel, n_uuids, self._json,
+                                  int(strict), device)
+        h = ctypes.c_void_p()
+        check(lib().keto_snapshot_build(ctypes.byref(cfg), tuples.ctypes.data, len(tuples), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+        self.ns_names, self.rel_names = list(ns_names), list(rel_names)
+
+    def info(self) -> dict:
+        inf = _abi.SnapshotInfo()
+        check(lib().keto_snapshot_info_get(self.handle, ctypes.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in inf._fields_}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().keto_snapshot_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+class Stream:
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        check(lib().keto_stream_create(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def sync(self):
+        check(lib().keto_stream_sync(self.handle))
+
+    def counters(self, reset: bool = False) -> dict:
+        """{'rows': total, ..., 'per_tier': {'rows': [t0, t1, t2], ...}}"""
+        c = _abi.WorkCounters()
+        check(lib().keto_stream_counters(self.handle, ctypes.byref(c), int(reset)))
+        per = {k: list(getattr(c, k)) for k, _ in c._fields_}
+        out = {k: sum(v) for k, v in per.items()}
+        out["per_tier"] = per
+        return out
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_double()
+        check(lib().keto_stream_last_kernel_ms(self.handle, ctypes.byref(ms)))
+        return ms.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().keto_stream_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+class DeviceBuffer:
+    """Raw device allocation (keto_device_alloc) for HBM-resident batches."""
+
+    def __init__(self, device: int, nbytes: int):
+        p = ctypes.c_void_p()
+        check(lib().keto_device_alloc(device, max(1, nbytes), ctypes.byref(p)))
+        self.ptr, self.nbytes = p, nbytes
+
+    def upload(self, stream: Stream, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        check(lib().keto_memcpy_h2d(stream.handle, self.ptr, arr.ctypes.data, arr.nbytes))
+
+    def download(self, stream: Stream, arr: np.ndarray):
+        check(lib().keto_memcpy_d2h(stream.handle, arr.ctypes.data, self.ptr, arr.nbytes))
+        return arr
+
+    def free(self):
+        if self.ptr:
+            lib().keto_device_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+class CheckEngine:
+    """check.Engine over the GPU snapshot (limits = limit.max_read_depth/max_read_width)."""
+
+    def __init__(self, snapshot: Snapshot, stream: Stream | None = None, max_read_depth: int = 5,
+                 max_read_width: int = 100):
+        self.snapshot = snapshot
+        self.stream = stream or Stream(snapshot.device)
+        self.limits = _abi.Limits(max_read_depth, max_read_width)
+
+    def check_batch(self, queries: np.ndarray, count_work: bool = False):
+        """queries: QUERY_DT array (host).  Returns (allowed uint8[n], err int32[n])."""
+        q = np.ascontiguousarray(queries, dtype=_abi.QUERY_DT)
+        allowed = np.zeros(len(q), dtype=np.uint8)
+        err = np.zeros(len(q), dtype=np.int32)
+        flags = _abi.F_COUNT_WORK if count_work else 0
+        check(lib().keto_check_batch(self.snapshot.handle, self.stream.handle, q.ctypes.data, len(q),
+                                     ctypes.byref(self.limits), allowed.ctypes.data, err.ctypes.data, flags))
+        return allowed, err
+
+    def check_batch_device(self, d_queries: DeviceBuffer, n: int, d_allowed: DeviceBuffer, d_err: DeviceBuffer,
+                           sync: bool = True, count_work: bool = False):
+        flags = _abi.F_DEVICE_PTRS | (0 if sync else _abi.F_ASYNC) | (_abi.F_COUNT_WORK if count_work else 0)
+        check(lib().keto_check_batch(self.snapshot.handle, self.stream.handle, d_queries.ptr, n,
+                                     ctypes.byref(self.limits), d_allowed.ptr, d_err.ptr, flags))
+
+    def check_relation_tuple(self, query_rec: np.ndarray):
+        """-> (membership-as-bool, error code) for one QUERY_DT record."""
+        a, e = self.check_batch(np.atleast_1d(query_rec))
+        return bool(a[0]), int(e[0])
+
+    def check_is_member(self, query_rec: np.ndarray) -> bool:
+        a, e = self.check_relation_tuple(query_rec)
+        if e:
+            raise KetoError(e, "relation does not exist" if e == _abi.QERR_NO_RELATION else "check failed")
+        return a
+
+
+class ExpandEngine:
+    """expand.Engine.BuildTree over the GPU snapshot."""
+
+    def __init__(self, snapshot: Snapshot, stream: Stream | None = None, max_read_depth: int = 5):
+        self.snapshot = snapshot
+        self.stream = stream or Stream(snapshot.device)
+        self.limits = _abi.Limits(max_read_depth, 100)
+
+    def build_trees(self, roots: np.ndarray):
+        """roots: SUBJSET_DT array -> (nodes TREE_DT, offsets uint64[n+1], err int32[n])."""
+        r = np.ascontiguousarray(roots, dtype=_abi.SUBJSET_DT)
+        n = len(r)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        err = np.zeros(max(1, n), dtype=np.int32)
+        cap = max(64, 16 * n)
+        while True:
+            nodes = np.zeros(cap, dtype=_abi.TREE_DT)
+            rc = lib().keto_expand_batch(self.snapshot.handle, self.stream.handle, r.ctypes.data, n,
+                                         ctypes.byref(self.limits), nodes.ctypes.data, cap, offs.ctypes.data,
+                                         err.ctypes.data)
+            if rc == _abi.KETO_E_CAPACITY:
+                cap = int(offs[n]) + 1
+                continue
+            check(rc)
+            return nodes[: int(offs[n])], offs, err[:n]

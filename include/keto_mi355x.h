@@ -1,0 +1,178 @@
+/*
+ * keto_mi355x.h -- C ABI of the MI355X batched Check / Expand engine.
+ *
+ * This is the drop-in boundary for Keto's permission hot path.  It replaces
+ * everything BELOW these reference entry points (paths relative to the
+ * reference repository):
+ *
+ *   check.Engine.CheckIsMember / CheckRelationTuple   internal/check/engine.go:65-95
+ *   expand.Engine.BuildTree                            internal/expand/engine.go:43-52
+ *   relationtuple.Traverser / Manager read ops          internal/relationtuple/definitions.go:22-33
+ *     (TraverseSubjectSetExpansion   persistence/sql/traverser.go:53-121,
+ *      TraverseSubjectSetRewrite     persistence/sql/traverser.go:123-191,
+ *      GetRelationTuples             persistence/sql/relationtuples.go:207-247,
+ *      ExistsRelationTuples          persistence/sql/relationtuples.go:249-261)
+ *
+ * A Go cgo shim keeps the check.Engine / expand.Engine API
+ * and does the Mapper work on the host (internal/relationtuple/uuid_mapping.go):
+ * strings/UUIDs are interned to dense uint32 ids before they cross this ABI.
+ *
+ * Conventions: every entry point returns KETO_OK (0) or a negative KETO_E_*
+ * status; keto_last_error() gives the message (thread-local).  Plain pointers
+ * and sizes only.  The caller owns every buffer it passes; the library owns
+ * device memory of snapshots and streams.  A snapshot is immutable after build
+ * and may be shared by many streams/threads; a stream is used by one thread
+ * at a time.
+ */
+#ifndef KETO_MI355X_H
+#define KETO_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KETO_ABI_VERSION 1
+
+/* status codes */
+#define KETO_OK 0
+#define KETO_E_INVALID (-1)   /* bad argument / malformed namespace JSON */
+#define KETO_E_DEVICE (-2)    /* HIP runtime error */
+#define KETO_E_CAPACITY (-3)  /* output buffer too small (required size reported) */
+#define KETO_E_LIMIT (-4)     /* id space exceeds the snapshot format */
+
+/* per-query error codes (out_err[i]); 0 = no error.
+ * 1 -> herodot.ErrBadRequest "relation %q does not exist"
+ *      (internal/namespace/definitions.go:61, surfaced by engine.go:228-232)
+ * 2 -> internal: evaluation exceeded every scratch tier (only reachable with a
+ *      cyclic zero-depth-cost rewrite, on which the reference never returns)
+ * 3 -> "not implemented" rewrite operator (internal/check/rewrites.go:18-20) */
+#define KETO_QERR_NONE 0
+#define KETO_QERR_NO_RELATION 1
+#define KETO_QERR_INTERNAL 2
+#define KETO_QERR_NOT_IMPLEMENTED 3
+
+/* Relation tuple as stored in keto_relation_tuples (schema:
+ * persistence/sql/migrations/sql/20230228091200000000_add-on-delete-cascade-to-relationship.sqlite.up.sql:14-49).
+ * ns/rel index the name tables of keto_snapshot_config; obj/s_obj are interned
+ * UUIDs (< n_uuids).  subj_kind 0 = SubjectID(s_obj); 1 = SubjectSet(s_ns:s_obj#s_rel).
+ * shard_id = the tuple's shard_id UUID bytes: it defines every iteration order
+ * (ORDER BY shard_id, traverser.go:88 / relationtuples.go:216). */
+typedef struct keto_tuple {
+    uint32_t ns, obj, rel;
+    uint32_t subj_kind;
+    uint32_t s_obj, s_ns, s_rel;
+    uint32_t reserved;
+    uint8_t shard_id[16];
+} keto_tuple;
+
+/* One Check: ns:obj#rel@subject; max_depth = request max-depth
+ * (<= 0 or > global -> global, engine.go:82-84). */
+typedef struct keto_query {
+    uint32_t ns, obj, rel;
+    uint32_t subj_kind;
+    uint32_t s_obj, s_ns, s_rel;
+    int32_t max_depth;
+} keto_query;
+
+/* Expand root: a subject set ns:obj#rel (a SubjectID root is answered by the
+ * shim itself as a leaf, expand/handler.go:119-126 / expand/engine.go:60-67). */
+typedef struct keto_subject_set {
+    uint32_t ns, obj, rel;
+    int32_t max_depth;
+} keto_subject_set;
+
+/* Expand output, pre-order.  type: 1 = union, 4 = leaf (ketoapi/enc_proto.go:164-176
+ * numbering).  Each node's tuple carries only its subject (uuid_mapping.go:356-385). */
+typedef struct keto_tree_node {
+    uint32_t type;
+    uint32_t subj_kind;
+    uint32_t s_obj, s_ns, s_rel;
+    uint32_t n_children;
+} keto_tree_node;
+
+typedef struct keto_snapshot_config {
+    uint32_t n_namespaces;
+    const char *const *namespace_names; /* id -> name */
+    uint32_t n_relations;
+    const char *const *relation_names;  /* id -> name ("" allowed) */
+    uint32_t n_uuids;                   /* every obj / s_obj is < n_uuids */
+    /* Namespace configuration as AST JSON, the format of
+     * internal/schema/.snapshots/TestParser-*.json: {"Ns": [relation, ...]} with
+     * relation = {"name", "types": [{"namespace", "relation"?}], "rewrite"?}.
+     * A namespace mapped to [] is a legacy namespace without relation config. */
+    const char *namespaces_json;
+    int32_t strict_mode;                /* namespaces.experimental_strict_mode */
+    int32_t device;                     /* HIP device ordinal */
+} keto_snapshot_config;
+
+typedef struct keto_snapshot_info {
+    uint64_t n_tuples, n_nodes, n_entities, n_set_edges, n_rev_entries;
+    uint64_t device_bytes;
+    double build_seconds;
+} keto_snapshot_info;
+
+/* limit.max_read_depth / limit.max_read_width (internal/driver/config/provider.go:180-185) */
+typedef struct keto_limits {
+    int32_t max_read_depth; /* default 5 */
+    int32_t max_read_width; /* default 100 */
+} keto_limits;
+
+/* Algorithmic work counters (BASELINE.md byte model), per scratch tier t = 0..2:
+ * rows opened, subject-set edges read, membership probes, Expand nodes emitted and
+ * queries completed by the kernels of tier t. */
+typedef struct keto_work_counters {
+    uint64_t rows[3], edges[3], probes[3], out_nodes[3], queries[3];
+} keto_work_counters;
+
+typedef struct keto_snapshot keto_snapshot;
+typedef struct keto_stream keto_stream;
+
+/* flags for keto_check_batch / keto_expand_batch */
+#define KETO_F_DEVICE_PTRS 0x1u  /* query / output pointers are device memory */
+#define KETO_F_ASYNC 0x2u        /* enqueue only; pair with keto_stream_sync */
+#define KETO_F_COUNT_WORK 0x4u   /* accumulate keto_work_counters on the stream */
+
+int keto_abi_version(void);
+/* copies the thread's last error message; returns its full length */
+size_t keto_last_error(char *buf, size_t len);
+
+int keto_snapshot_build(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n_tuples,
+                        keto_snapshot **out);
+int keto_snapshot_free(keto_snapshot *snap);
+int keto_snapshot_info_get(const keto_snapshot *snap, keto_snapshot_info *out);
+
+int keto_stream_create(int32_t device, keto_stream **out);
+int keto_stream_destroy(keto_stream *s);
+int keto_stream_sync(keto_stream *s);
+int keto_stream_counters(keto_stream *s, keto_work_counters *out, int32_t reset);
+/* average device time (ms) of the last batch's main check kernel, measured with
+ * HIP events on the stream the kernel ran on */
+int keto_stream_last_kernel_ms(keto_stream *s, double *ms);
+
+/* Check n queries: out_allowed[i] = CheckIsMember's bool, out_err[i] = error code.
+ * Replaces check.Engine.CheckIsMember (engine.go:65-71) for a whole batch. */
+int keto_check_batch(keto_snapshot *snap, keto_stream *s, const keto_query *queries, uint64_t n,
+                     const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags);
+
+/* Expand n roots into one pre-order node buffer; out_offsets[i]..out_offsets[i+1]
+ * delimit root i's tree (empty range = nil tree, expand/handler.go:141-143).
+ * If out_cap is too small returns KETO_E_CAPACITY with out_offsets[n] = required.
+ * Replaces expand.Engine.BuildTree (expand/engine.go:43-124). */
+int keto_expand_batch(keto_snapshot *snap, keto_stream *s, const keto_subject_set *roots, uint64_t n,
+                      const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap,
+                      uint64_t *out_offsets, int32_t *out_err);
+
+/* device memory helpers (for callers without their own allocator) */
+int keto_device_alloc(int32_t device, uint64_t bytes, void **out);
+int keto_device_free(void *p);
+int keto_memcpy_h2d(keto_stream *s, void *dst, const void *src, uint64_t bytes);
+int keto_memcpy_d2h(keto_stream *s, void *dst, const void *src, uint64_t bytes);
+int keto_device_count(int32_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's known answers
+and against the oracle on the same seeded inputs.  Integer/boolean work: bit-exact."""
+import numpy as np
+import pytest
+
+import keto_mi355x as km
+import refsem
+from fixtures import fixture_names, load, world_for
+from product_helpers import product_snapshot, product_tree_to_nested, queries_to_product
+from randworld import random_world
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def stream():
+    s = km.Stream(0)
+    yield s
+    s.close()
+
+
+def _oracle_decisions(orc, q, max_depth, max_width):
+    orc.set_limits(max_depth, max_width)
+    mem, err, st = orc.check(q)
+    return ((err == 0) & (mem == refsem.IS_MEMBER)).astype(np.uint8), err, st
+
+
+@pytest.mark.parametrize("name", [n for n in fixture_names() if load(n).get("checks")])
+def test_golden_checks(stream, name):
+    fx = load(name)
+    w, t, q = world_for(fx)
+    snap = product_snapshot(w, t)
+    for i, c in enumerate(fx["checks"]):
+        eng = km.CheckEngine(snap, stream, max_read_depth=c.get("global", fx.get("global", 5)),
+                             max_read_width=fx.get("max_width", 100))
+        allowed, err = eng.check_batch(queries_to_product(q[i:i + 1]))
+        assert int(err[0]) == c.get("err", 0), (name, c)
+        assert bool(allowed[0]) == c["allowed"], (name, c)
+
+
+@pytest.mark.parametrize("name", [n for n in fixture_names() if load(n).get("expands")])
+def test_golden_expands(stream, name):
+    fx = load(name)
+    w, t, _ = world_for(fx)
+    snap = product_snapshot(w, t)
+    eng = km.ExpandEngine(snap, stream, max_read_depth=fx.get("global", 5))
+    cases = [e for e in fx["expands"] if "subject" in e]
+    roots = np.zeros(len(cases), dtype=km.SUBJSET_DT)
+    for i, e in enumerate(cases):
+        ns, obj, rel = refsem.parse_subject_set(e["subject"])
+        roots[i] = (w.ns_names.ids[ns], w.uuids.ids[obj], w.rel_names.ids[rel], e["depth"])
+    nodes, offs, err = eng.build_trees(roots)
+    assert (err == 0).all()
+    for i, e in enumerate(cases):
+        got = product_tree_to_nested(w, nodes[int(offs[i]):int(offs[i + 1])])
+        if e.get("exact"):
+            assert got == e["tree"], (name, e["src"])
+        assert refsem.trees_equal_unordered(got, e["tree"]), (name, e["src"], got)
+
+
+@pytest.mark.parametrize("seed", list(range(60)))
+def test_random_worlds_vs_oracle(stream, seed):
+    w, t, q, expands = random_world(seed)
+    orc = refsem.Oracle(w, t)
+    snap = product_snapshot(w, t)
+    dec, err, st = _oracle_decisions(orc, q, w.max_depth, w.max_width)
+    eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+    stream.counters(reset=True)
+    allowed, gerr = eng.check_batch(queries_to_product(q), count_work=True)
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    c = stream.counters(reset=True)
+    if (err == 0).all():  # work counters of completed queries: identical traversal
+        assert (c["rows"], c["edges"], c["probes"]) == (st.rows, st.edges, st.probes)
+    # expand trees: exact, including child order
+    xe = km.ExpandEngine(snap, stream, max_read_depth=w.max_depth)
+    roots = np.array([(w.ns_names.ids[a], w.uuids.ids[b], w.rel_names.ids[r], d) for a, b, r, d in expands],
+                     dtype=km.SUBJSET_DT)
+    nodes, offs, xerr = xe.build_trees(roots)
+    assert (xerr == 0).all()
+    orc.set_limits(w.max_depth, w.max_width)
+    for i, (a, b, r, d) in enumerate(expands):
+        on, _ = orc.expand(1, w.uuids.ids[b], w.ns_names.ids[a], w.rel_names.ids[r], d)
+        assert product_tree_to_nested(w, nodes[int(offs[i]):int(offs[i + 1])]) == refsem.tree_to_nested(w, on)
+
+
+def _world_from_workload(wl):
+    """oracle World over a synth Workload (same ids as the product snapshot)"""
+    w = refsem.World(namespaces=wl.namespaces, strict=wl.strict, max_depth=wl.max_depth, max_width=wl.max_width)
+    w.ns_names = refsem.Interner()
+    w.rel_names = refsem.Interner()
+    w.uuids = refsem.Interner()
+    for n in wl.ns_names:
+        w.ns_names(n)
+    for r in wl.rel_names:
+        w.rel_names(r)
+    w._walk_names()
+    t = np.zeros(len(wl.tuples), dtype=refsem.TUPLE_DT)
+    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
+                 ("sns", "s_ns"), ("srel", "s_rel")):
+        t[a] = wl.tuples[b]
+    sb = wl.tuples["shard_id"]
+    t["shard_hi"] = sb[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+    t["shard_lo"] = sb[:, 8:].copy().view(">u8").reshape(-1).astype(np.uint64)
+    return w, t
+
+
+def _q_to_oracle(q):
+    o = np.zeros(len(q), dtype=refsem.QUERY_DT)
+    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
+                 ("sns", "s_ns"), ("srel", "s_rel"), ("depth", "max_depth")):
+        o[a] = q[b]
+    return o
+
+
+@pytest.mark.parametrize("wl_name", ["nested_groups", "drive"])
+def test_synthetic_small_vs_oracle(stream, wl_name):
+    from keto_mi355x import synth
+    if wl_name == "nested_groups":
+        wl = synth.nested_groups(200_000, seed=5)
+        q = synth.nested_groups_queries(wl, 20_000, seed=9, trunc_frac=0.05)
+    else:
+        wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=4)
+        q = synth.drive_queries(wl, 20_000, seed=3)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    w, t = _world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    dec, err, st = orc.check_batch(_q_to_oracle(q), threads=8)
+    eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    stream.counters(reset=True)
+    allowed, gerr = eng.check_batch(q, count_work=True)
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    c = stream.counters(reset=True)
+    assert (c["rows"], c["edges"], c["probes"]) == (st.rows, st.edges, st.probes)
+    assert 0.05 < allowed.mean() < 0.95
+
+
+def test_nested_groups_full_size_properties(stream):
+    """BASELINE config 2 at full size (10M tuples): size-independent properties."""
+    from keto_mi355x import synth
+    wl = synth.nested_groups(10_000_000, seed=1)
+    q = synth.nested_groups_queries(wl, 1 << 20, seed=7)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth)
+    a1, e1 = eng.check_batch(q)
+    assert (e1 == 0).all()
+    # determinism and batch-split invariance (queries are independent units)
+    a2, _ = eng.check_batch(q)
+    np.testing.assert_array_equal(a1, a2)
+    h = len(q) // 3
+    parts = [eng.check_batch(q[i:j])[0] for i, j in ((0, h), (h, 2 * h), (2 * h, len(q)))]
+    np.testing.assert_array_equal(np.concatenate(parts), a1)
+    # random-walk positives at full request depth are members (union-only, no truncation)
+    rng = np.random.Generator(np.random.PCG64(7))
+    # regenerate which queries were positives: they are the ones whose subject is a real member
+    full = q["max_depth"] == 0
+    assert a1[full].mean() > 0.45
+    # a sample of 4096 checked exactly against the oracle
+    w, t = _world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    idx = rng.choice(len(q), size=4096, replace=False)
+    dec, err, _ = orc.check_batch(_q_to_oracle(q[idx]), threads=8)
+    np.testing.assert_array_equal(a1[idx], dec)
+
+
+def test_device_pointer_path(stream):
+    w, t, q, _ = random_world(3)
+    snap = product_snapshot(w, t)
+    eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+    host_a, host_e = eng.check_batch(queries_to_product(q))
+    pq = queries_to_product(q)
+    dq = km.DeviceBuffer(0, pq.nbytes)
+    da = km.DeviceBuffer(0, len(pq))
+    de = km.DeviceBuffer(0, 4 * len(pq))
+    dq.upload(stream, pq)
+    eng.check_batch_device(dq, len(pq), da, de, sync=False)
+    stream.sync()
+    a = da.download(stream, np.zeros(len(pq), np.uint8))
+    e = de.download(stream, np.zeros(len(pq), np.int32))
+    np.testing.assert_array_equal(a, host_a)
+    np.testing.assert_array_equal(e, host_e)
+    assert stream.last_kernel_ms() > 0
+
+
+def test_scratch_tiers(stream):
+    """A query whose visited set (200 subgroups) and stack (deep chain) outgrow tier 1."""
+    ns = {"g": []}
+    tuples = [f"g:root#m@g:s{i}#m" for i in range(300)] + [f"g:s{i}#m@g:t{i}#m" for i in range(300)]
+    tuples += [f"g:c{i}#m@g:c{i + 1}#m" for i in range(120)] + ["g:c120#m@deep_user", "g:t299#m@wide_user"]
+    w = refsem.World(namespaces=ns, max_depth=200, max_width=1000)
+    t = w.tuple_array(tuples)
+    q = w.query_array([("g:root#m@wide_user", 0), ("g:root#m@nobody", 0), ("g:c0#m@deep_user", 0),
+                       ("g:c0#m@nobody", 0), ("g:c0#m@deep_user", 50)])
+    orc = refsem.Oracle(w, t)
+    dec, err, _ = _oracle_decisions(orc, q, 200, 1000)
+    snap = product_snapshot(w, t)
+    eng = km.CheckEngine(snap, stream, max_read_depth=200, max_read_width=1000)
+    a, e = eng.check_batch(queries_to_product(q))
+    np.testing.assert_array_equal(e, err)
+    np.testing.assert_array_equal(a, dec)
+    assert list(dec) == [1, 0, 1, 0, 0]
