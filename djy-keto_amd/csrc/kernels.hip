@@ -877,7 +877,9 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         P.last_tier = tier == 2;
         uint32_t lanes = t[tier].lanes;
         if (tier == 0) lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + BLOCK - 1) / BLOCK) * BLOCK);
-        dim3 grid(lanes / BLOCK), block(BLOCK);
+        // every launched lane owns scratch: lanes is a multiple of the block size
+        const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);
+        dim3 grid(lanes / bs), block(bs);
         if (tier == 0) KETO_HIP(hipEventRecord(st.ev0, st.stream));
         // one instantiation per tier so profiles attribute time per tier
 #define KETO_LAUNCH_CHECK(T)                                                                              \
@@ -929,7 +931,8 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
         P.counters = L.emit ? nullptr : st.counters + 8 * tier;
         uint32_t lanes = t[tier].lanes;
         if (tier == 0) lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + BLOCK - 1) / BLOCK) * BLOCK);
-        hipLaunchKernelGGL(expand_kernel, dim3((lanes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st.stream, P);
+        const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);  // every launched lane owns scratch
+        hipLaunchKernelGGL(expand_kernel, dim3(lanes / bs), dim3(bs), 0, st.stream, P);
         KETO_HIP(hipGetLastError());
     }
 }
