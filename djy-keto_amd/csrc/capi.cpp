@@ -49,6 +49,7 @@ Stream::~Stream() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (check_scratch.mem) (void)hipFree(check_scratch.mem);
     if (expand_scratch.mem) (void)hipFree(expand_scratch.mem);
+    if (union_scratch.mem) (void)hipFree(union_scratch.mem);
     if (lists) (void)hipFree(lists);
     if (qbuf) (void)hipFree(qbuf);
     if (obuf) (void)hipFree(obuf);
@@ -184,7 +185,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
             L.queries = queries;
             L.out_allowed = out_allowed;
             L.out_err = out_err;
-            keto::run_check(*snap, *s, L);
+            (snap->ops.empty() ? keto::run_check_union : keto::run_check)(*snap, *s, L);
             if (!(flags & KETO_F_ASYNC)) {
                 KETO_HIP(hipStreamSynchronize(s->stream));
                 float ms = 0;
@@ -202,7 +203,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         L.queries = static_cast<const keto_query *>(s->qbuf);
         L.out_allowed = d_allowed;
         L.out_err = d_err;
-        keto::run_check(*snap, *s, L);
+        (snap->ops.empty() ? keto::run_check_union : keto::run_check)(*snap, *s, L);
         KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipStreamSynchronize(s->stream));

@@ -1,0 +1,629 @@
+// gfx950 batched Check for rewrite-free namespace configs (legacy / union-only Zanzibar).
+//
+// Without userset rewrites the reference recursion (engine.go:102-249) collapses to:
+//   checkIsAllowed(n, d)  = [direct(n, d-1)] || expandSubject(n, d-1)
+//   expandSubject(n, d)   = found-lookahead over n's subject-set row, then for each child c
+//                           (visited-pruned, width-truncated) checkIsAllowed(c, d, skipDirect)
+// Every group is an OR whose first IsMember/Err ends the WHOLE query, there is exactly one
+// visited scope per query (opened by the root's expandSubject), and the only frames are
+// expand-subject frames.  That makes a compact lane-per-query state machine: few states,
+// small live state (<= 64 VGPRs target: 8 waves/SIMD), two independent 16-byte loads per
+// step issued by every lane in the same instructions, frames of 32 B that carry the parent's
+// edge window so returning from a child needs no edge reload.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device_common.hpp"
+
+namespace keto {
+namespace {
+
+enum UState : uint32_t {
+    U_IDLE = 0,
+    U_QREC,    // query record
+    U_ENT,     // entity hash slot (root / subject set)
+    U_REVOFF,  // subject reverse-row offsets
+    U_REVREG,  // reverse-row entries -> VGPRs
+    U_DPROBE,  // checkDirect of the root via the probe hash
+    U_ROWOFF,  // set-row offsets of the current node
+    U_SCAN,    // edge window of the found-lookahead
+    U_SPROBE,  // hash probes of the lookahead (2 per step)
+    U_CEDGE,   // edge window of the child loop
+    U_VKEY,    // visited alias key
+    U_VIS,     // visited slot pair
+    U_POP,     // parent frame (2 x 16 B)
+};
+
+struct UParams {
+    DevSnapshot s;
+    const keto_query *queries;
+    const uint32_t *qlist;
+    const uint32_t *qlist_count;
+    uint32_t n;
+    uint8_t *out_allowed;
+    int32_t *out_err;
+    uint32_t *next;
+    uint32_t *ovf_list;
+    uint32_t *ovf_count;
+    unsigned long long *vis;
+    uint4 *stack;  // 2 x uint4 per frame
+    uint32_t *epochs;
+    uint32_t vcap, scap;
+    int32_t max_depth, max_width;
+    unsigned long long *counters;
+    uint32_t last_tier;
+};
+
+// word j (0..7) of the two consecutive windows v0, v1 -- selects, no scratch
+__device__ __forceinline__ uint32_t w8(const uint4 &v0, const uint4 &v1, uint32_t j) {
+    return j < 4 ? wword(v0, j) : wword(v1, j - 4);
+}
+
+__device__ __forceinline__ uint32_t probe_check(const uint4 &b, uint64_t key) {
+    const uint64_t k0 = (uint64_t)b.x | ((uint64_t)b.y << 32), k1 = (uint64_t)b.z | ((uint64_t)b.w << 32);
+    if (k0 == key || k1 == key) return 1;
+    if (k0 == 0 || k1 == 0) return 0;
+    return 2;
+}
+
+template <bool COUNT, bool LDS_TABLES>
+__global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const DevSnapshot &s = P.s;
+    const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
+    const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long *vis = P.vis + (size_t)gl * P.vcap;
+    uint4 *stk = P.stack + (size_t)gl * 2 * P.scap;
+    uint32_t epoch = P.epochs[gl];
+    const uint32_t nq = P.qlist ? *P.qlist_count : P.n;
+    const uint32_t pmask = (P.vcap >> 1) - 1;
+    const uint32_t W = (uint32_t)P.max_width;
+    const uint32_t lane = __lane_id();
+
+    uint32_t q = 0, st = U_IDLE;
+    bool exhausted = false;
+    // query + subject
+    uint32_t qns = 0, qobj = 0, qrel = 0, qkind = 0, qsobj = 0, qsns = 0, qsrel = 0;
+    uint32_t sidx = NONE32, rb = 0, re = 0;
+    bool heavy = false;
+    uint32_t R0 = NONE32, R1 = NONE32, R2 = NONE32, R3 = NONE32;
+    // current expand-subject frame: node, cursor, end, depth, row begin; edge window
+    uint32_t node = 0, cur = 0, end = 0, d = 0, rbeg = 0;
+    uint4 ew = make_uint4(0, 0, 0, 0);
+    uint32_t ew_lo = 1, ew_hi = 0;
+    uint32_t sp = 0, vcount = 0, aux = 0, aux2 = 0;  // aux: entity slot / probe bucket / visited pair
+    uint32_t vk = 0;                                  // visited key of the child being inserted
+    bool resolving_subject = false, root_ss = false;
+    const uint4 *la0 = nullptr, *la1 = nullptr;
+    uint32_t ln = 0;
+    uint32_t q_rows = 0, q_edges = 0, q_probes = 0;
+    unsigned long long c_rows = 0, c_edges = 0, c_probes = 0, c_q = 0;
+
+    while (true) {
+        const bool need = (st == U_IDLE) && !exhausted;
+        const unsigned long long mask = __ballot(need);
+        if (mask) {
+            const int leader = __ffsll((long long)mask) - 1;
+            uint32_t base = 0;
+            if ((int)lane == leader) base = atomicAdd(P.next, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t my = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                if (my >= nq) exhausted = true;
+                else {
+                    q = P.qlist ? P.qlist[my] : my;
+                    st = U_QREC;
+                    la0 = reinterpret_cast<const uint4 *>(P.queries + q);
+                    la1 = la0 + 1;
+                    ln = 2;
+                    q_rows = q_edges = q_probes = 0;
+                }
+            }
+        }
+        if (__ballot(st != U_IDLE) == 0) break;
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+        if (ln > 0) v0 = *la0;
+        if (ln > 1) v1 = *la1;
+        ln = 0;
+        if (st == U_IDLE) continue;
+
+        // result: 0 = keep going, 1 = allowed, 2 = denied, 3 = relation error, 4 = overflow
+        uint32_t fin = 0;
+        for (int guard = 0; guard < 8 && ln == 0 && fin == 0; guard++) {
+            switch (st) {
+            case U_QREC: {
+                qns = v0.x;
+                qobj = v0.y;
+                qrel = v0.z;
+                qkind = v0.w;
+                qsobj = v1.x;
+                qsns = v1.y;
+                qsrel = v1.z;
+                int32_t d0 = (int32_t)v1.w;
+                if (d0 <= 0 || P.max_depth < d0) d0 = P.max_depth;  // engine.go:82-84
+                d = (uint32_t)d0;
+                sidx = NONE32;
+                if (qns < s.n_ns) {  // resolve the root entity
+                    resolving_subject = false;
+                    aux = (uint32_t)mix64((((uint64_t)qns << 32) | qobj) + 1) & s.ent_mask;
+                    la0 = s.ent_table + aux;
+                    ln = 1;
+                    st = U_ENT;
+                    break;
+                }
+                node = VIRT_BIT | (0x7FFFu << 16) | 0xFFFFu;  // unknown namespace
+                st = U_ENT + 100;
+                break;
+            }
+            case U_ENT: {
+                const uint32_t ns = resolving_subject ? qsns : qns, obj = resolving_subject ? qsobj : qobj;
+                const uint64_t key = (((uint64_t)ns << 32) | obj) + 1;
+                const uint64_t k = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
+                if (k != key && k != 0) {  // keep probing
+                    aux = (aux + 1) & s.ent_mask;
+                    la0 = s.ent_table + aux;
+                    ln = 1;
+                    break;
+                }
+                uint32_t e = k == key ? v0.z : NONE32;
+                if (!resolving_subject) {
+                    if (e == NONE32) e = T.ns[qns + 1].ent_base - 1;  // phantom entity: no tuples
+                    node = t_node(T, qns, e, qrel);
+                    st = U_ENT + 100;
+                } else {
+                    if (e != NONE32) {
+                        const uint32_t sn = t_node(T, qsns, e, qsrel);
+                        if (!(sn & VIRT_BIT)) sidx = s.n_uuids + sn;
+                    }
+                    st = U_REVOFF + 100;
+                }
+                break;
+            }
+            case U_ENT + 100:  // subject: id, or subject set to resolve
+                if (qkind == 1) {
+                    if (qsns < s.n_ns) {
+                        resolving_subject = true;
+                        aux = (uint32_t)mix64((((uint64_t)qsns << 32) | qsobj) + 1) & s.ent_mask;
+                        la0 = s.ent_table + aux;
+                        ln = 1;
+                        st = U_ENT;
+                        break;
+                    }
+                } else if (qsobj < s.n_uuids) {
+                    sidx = qsobj;
+                }
+                st = U_REVOFF + 100;
+                break;
+            case U_REVOFF + 100:
+                heavy = false;
+                if (sidx == NONE32) {  // subject held by no tuple
+                    rb = re = 0;
+                    st = U_REVREG;
+                    break;
+                }
+                la0 = win(s.rev_off, sidx);
+                la1 = win(s.rev_off, sidx + 1);
+                ln = 2;
+                st = U_REVOFF;
+                break;
+            case U_REVOFF:
+                rb = pick(s.rev_off, sidx, v0);
+                re = pick(s.rev_off, sidx + 1, v1);
+                heavy = (re - rb) > PROBE_K;
+                if (heavy || re == rb) {
+                    v0 = v1 = make_uint4(NONE32, NONE32, NONE32, NONE32);
+                    rb = re;  // no register entries
+                    st = U_REVREG;
+                    break;
+                }
+                la0 = win(s.rev_nodes, rb);
+                la1 = la0 + 1;
+                ln = 2;
+                st = U_REVREG;
+                break;
+            case U_REVREG: {
+                // up to PROBE_K (=4) entries starting at rb, spread over the two windows
+                const uint32_t o = (uint32_t)((reinterpret_cast<uintptr_t>(s.rev_nodes + rb) >> 2) & 3);
+                const uint32_t cnt = re - rb;
+                R0 = cnt > 0 ? w8(v0, v1, o) : NONE32;
+                R1 = cnt > 1 ? w8(v0, v1, o + 1) : NONE32;
+                R2 = cnt > 2 ? w8(v0, v1, o + 2) : NONE32;
+                R3 = cnt > 3 ? w8(v0, v1, o + 3) : NONE32;
+                // root checkIsAllowed(node, d, false) (engine.go:214-249)
+                const NodeInfo ni = t_node_info(T, node);
+                if (ri_status(ni.ri) == REL_ERROR) {
+                    fin = 3;
+                    break;
+                }
+                root_ss = ri_ss(ni.ri);
+                if (d > 1) {  // checkDirect(d-1) (engine.go:167-208)
+                    if (COUNT) q_probes++;
+                    if (!(node & VIRT_BIT)) {
+                        if (!heavy) {
+                            if (R0 == node || R1 == node || R2 == node || R3 == node) {
+                                fin = 1;
+                                break;
+                            }
+                        } else {
+                            aux = (uint32_t)mix64((((uint64_t)sidx << 32) | node) + 1) & s.probe_mask;
+                            la0 = s.probe + aux;
+                            ln = 1;
+                            st = U_DPROBE;
+                            break;
+                        }
+                    }
+                }
+                if (!root_ss || d <= 1) {
+                    fin = 2;
+                    break;
+                }
+                d -= 1;  // checkExpandSubject(root, d-1)
+                epoch++;  // the query's one visited scope (graph_utils.go:38-43)
+                vcount = 0;
+                sp = 0;
+                st = U_ROWOFF + 100;
+                break;
+            }
+            case U_DPROBE: {
+                const uint32_t r = probe_check(v0, (((uint64_t)sidx << 32) | node) + 1);
+                if (r == 2) {
+                    aux = (aux + 1) & s.probe_mask;
+                    la0 = s.probe + aux;
+                    ln = 1;
+                    break;
+                }
+                if (r == 1) {
+                    fin = 1;
+                    break;
+                }
+                if (!root_ss || d <= 1) {
+                    fin = 2;
+                    break;
+                }
+                d -= 1;
+                epoch++;
+                vcount = 0;
+                sp = 0;
+                st = U_ROWOFF + 100;
+                break;
+            }
+            case U_ROWOFF + 100:  // enter expand-subject(node, d): rows (traverser.go:53-121)
+                if (COUNT) q_rows++;
+                if (node & VIRT_BIT) {
+                    st = U_POP + 100;  // empty row: not a member, return
+                    break;
+                }
+                la0 = win(s.set_off, node);
+                la1 = win(s.set_off, node + 1);
+                ln = 2;
+                st = U_ROWOFF;
+                break;
+            case U_ROWOFF:
+                rbeg = pick(s.set_off, node, v0);
+                end = pick(s.set_off, node + 1, v1);
+                cur = rbeg;
+                if (rbeg == end) {
+                    st = U_POP + 100;
+                    break;
+                }
+                la0 = win(s.set_dst, cur);
+                ln = 1;
+                st = U_SCAN;
+                break;
+            case U_SCAN: {  // found-lookahead over one window (traverser.go:73-80, 109-111)
+                ew = v0;
+                ew_lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + cur) >> 2) & 3);
+                ew_hi = ew_lo + 4;
+                if (!heavy) {
+                    bool found = false;
+                    while (cur < end && cur < ew_hi) {
+                        const uint32_t c = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
+                        cur++;
+                        if (COUNT) {
+                            q_edges++;
+                            q_probes++;
+                        }
+                        if (R0 == c || R1 == c || R2 == c || R3 == c) {
+                            found = true;
+                            break;
+                        }
+                    }
+                    if (found) {
+                        fin = 1;
+                        break;
+                    }
+                } else if (cur < end) {  // two probes per step, in edge order
+                    const uint32_t c0 = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
+                    aux = (uint32_t)mix64((((uint64_t)sidx << 32) | c0) + 1) & s.probe_mask;
+                    la0 = s.probe + aux;
+                    ln = 1;
+                    if (cur + 1 < end && cur + 1 < ew_hi) {
+                        const uint32_t c1 = wword(ew, cur + 1 - ew_lo) & ~EDGE_ALIAS;
+                        aux2 = (uint32_t)mix64((((uint64_t)sidx << 32) | c1) + 1) & s.probe_mask;
+                        la1 = s.probe + aux2;
+                        ln = 2;
+                    }
+                    st = U_SPROBE;
+                    break;
+                }
+                if (cur < end) {
+                    la0 = win(s.set_dst, cur);
+                    ln = 1;
+                    break;
+                }
+                // lookahead done: width truncation, then the child loop (engine.go:141-162)
+                if (end - rbeg > W) end = rbeg + (W > 0 ? W - 1 : 0);
+                cur = rbeg;
+                st = U_CEDGE + 100;
+                break;
+            }
+            case U_SPROBE: {
+                const uint32_t c0 = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
+                uint32_t r0 = probe_check(v0, (((uint64_t)sidx << 32) | c0) + 1);
+                uint32_t r1 = 0;
+                const bool two = cur + 1 < end && cur + 1 < ew_hi;
+                uint32_t c1 = 0;
+                if (two) {
+                    c1 = wword(ew, cur + 1 - ew_lo) & ~EDGE_ALIAS;
+                    r1 = probe_check(v1, (((uint64_t)sidx << 32) | c1) + 1);
+                }
+                if (r0 == 2 || r1 == 2) {  // full buckets: continue those probes (rare)
+                    if (r0 == 2) aux = (aux + 1) & s.probe_mask;
+                    la0 = s.probe + aux;
+                    ln = 1;
+                    if (two) {
+                        if (r1 == 2) aux2 = (aux2 + 1) & s.probe_mask;
+                        la1 = s.probe + aux2;
+                        ln = 2;
+                    }
+                    break;
+                }
+                if (COUNT) {
+                    q_edges++;
+                    q_probes++;
+                }
+                if (r0 == 1) {
+                    fin = 1;
+                    break;
+                }
+                cur++;
+                if (two) {
+                    if (COUNT) {
+                        q_edges++;
+                        q_probes++;
+                    }
+                    if (r1 == 1) {
+                        fin = 1;
+                        break;
+                    }
+                    cur++;
+                }
+                if (cur < end && cur < ew_hi) {  // rest of the cached window
+                    v0 = ew;
+                    st = U_SCAN;
+                    break;
+                }
+                if (cur < end) {
+                    la0 = win(s.set_dst, cur);
+                    ln = 1;
+                    st = U_SCAN;
+                    break;
+                }
+                if (end - rbeg > W) end = rbeg + (W > 0 ? W - 1 : 0);
+                cur = rbeg;
+                st = U_CEDGE + 100;
+                break;
+            }
+            case U_CEDGE + 100: {  // next child (engine.go:151-162)
+                if (cur >= end) {
+                    st = U_POP + 100;
+                    break;
+                }
+                if (cur < ew_lo || cur >= ew_hi) {
+                    la0 = win(s.set_dst, cur);
+                    ln = 1;
+                    st = U_CEDGE;
+                    break;
+                }
+                const uint32_t raw = wword(ew, cur - ew_lo);
+                cur++;
+                aux2 = raw & ~EDGE_ALIAS;  // child node
+                if (raw & EDGE_ALIAS) {
+                    la0 = win(s.vkey, aux2);
+                    ln = 1;
+                    st = U_VKEY;
+                    break;
+                }
+                vk = aux2;
+                aux = (uint32_t)mix64(vk) & pmask;
+                la0 = reinterpret_cast<const uint4 *>(vis + 2 * aux);
+                ln = 1;
+                st = U_VIS;
+                break;
+            }
+            case U_CEDGE:
+                ew = v0;
+                ew_lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + cur) >> 2) & 3);
+                ew_hi = ew_lo + 4;
+                st = U_CEDGE + 100;
+                break;
+            case U_VKEY:
+                vk = pick(s.vkey, aux2, v0);
+                aux = (uint32_t)mix64(vk) & pmask;
+                la0 = reinterpret_cast<const uint4 *>(vis + 2 * aux);
+                ln = 1;
+                st = U_VIS;
+                break;
+            case U_VIS: {  // CheckAndAddVisited (graph_utils.go:45-53), epoch-tagged
+                const unsigned long long tag = ((unsigned long long)epoch << 32) | vk;
+                const unsigned long long s0 = (unsigned long long)v0.x | ((unsigned long long)v0.y << 32);
+                const unsigned long long s1 = (unsigned long long)v0.z | ((unsigned long long)v0.w << 32);
+                const bool e0 = (uint32_t)(s0 >> 32) != epoch, e1 = (uint32_t)(s1 >> 32) != epoch;
+                if (s0 == tag || (!e0 && s1 == tag)) {
+                    st = U_CEDGE + 100;  // already visited
+                    break;
+                }
+                if (!e0 && !e1) {
+                    aux = (aux + 1) & pmask;
+                    la0 = reinterpret_cast<const uint4 *>(vis + 2 * aux);
+                    ln = 1;
+                    break;
+                }
+                if (2 * (vcount + 1) > P.vcap) {
+                    fin = 4;
+                    break;
+                }
+                vis[2 * aux + (e0 ? 0 : 1)] = tag;
+                vcount++;
+                // child checkIsAllowed(c, d, skipDirect=true) -> expandSubject(c, d-1)
+                const NodeInfo ni = t_node_info(T, aux2);
+                if (ri_status(ni.ri) == REL_ERROR) {
+                    fin = 3;
+                    break;
+                }
+                if (!ri_ss(ni.ri) || d <= 1) {
+                    st = U_CEDGE + 100;
+                    break;
+                }
+                if (sp + 1 >= P.scap) {
+                    fin = 4;
+                    break;
+                }
+                // push the parent (cursor, end, depth, row begin | window)
+                stk[2 * sp] = make_uint4(cur, end, d, rbeg);
+                stk[2 * sp + 1] = ew;
+                sp++;
+                node = aux2;
+                d -= 1;
+                st = U_ROWOFF + 100;
+                break;
+            }
+            case U_POP + 100:  // expand-subject returned NotMember
+                if (sp == 0) {
+                    fin = 2;
+                    break;
+                }
+                sp--;
+                la0 = stk + 2 * sp;
+                la1 = la0 + 1;
+                ln = 2;
+                st = U_POP;
+                break;
+            case U_POP:
+                cur = v0.x;
+                end = v0.y;
+                d = v0.z;
+                rbeg = v0.w;
+                ew = v1;
+                {
+                    const uint32_t pc = cur > rbeg ? cur - 1 : cur;  // the window held edge cur-1
+                    ew_lo = pc - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + pc) >> 2) & 3);
+                    ew_hi = ew_lo + 4;
+                }
+                st = U_CEDGE + 100;
+                break;
+            default:
+                fin = 4;
+            }
+        }
+        if (fin) {
+            if (fin == 4) {
+                if (P.last_tier) {
+                    P.out_allowed[q] = 0;
+                    P.out_err[q] = KETO_QERR_INTERNAL;
+                } else {
+                    P.ovf_list[atomicAdd(P.ovf_count, 1u)] = q;
+                }
+            } else {
+                P.out_allowed[q] = fin == 1 ? 1 : 0;
+                P.out_err[q] = fin == 3 ? KETO_QERR_NO_RELATION : 0;
+                if (COUNT) {
+                    c_rows += q_rows;
+                    c_edges += q_edges;
+                    c_probes += q_probes;
+                    c_q++;
+                }
+            }
+            st = U_IDLE;
+            ln = 0;
+        }
+    }
+    P.epochs[gl] = epoch;
+    if (COUNT) {
+        for (int off = 32; off > 0; off >>= 1) {
+            c_rows += __shfl_down(c_rows, off);
+            c_edges += __shfl_down(c_edges, off);
+            c_probes += __shfl_down(c_probes, off);
+            c_q += __shfl_down(c_q, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&P.counters[0], c_rows);
+            atomicAdd(&P.counters[1], c_edges);
+            atomicAdd(&P.counters[2], c_probes);
+            atomicAdd(&P.counters[4], c_q);
+        }
+    }
+}
+
+}  // namespace
+
+void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
+    constexpr uint32_t BLOCK = 256;
+    const uint32_t cus = (uint32_t)num_cus(s.device);
+    const Tier t[3] = {Tier{cus * 32 * 64, 256, 32},   // 32 waves / CU
+                       Tier{cus * 64, 1u << 13, 512},
+                       Tier{64, 1u << 20, 1u << 14}};
+    ensure_scratch(st.union_scratch, t);
+    ensure_lists(st, L.n);
+    Scratch &sc = st.union_scratch;
+    uint32_t *list[2] = {st.lists, st.lists + st.list_cap};
+    const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
+    const size_t lds = lds_tables ? s.dev.lds_bytes : 0;
+    KETO_HIP(hipMemsetAsync(sc.ctrl, 0, 64, st.stream));
+    for (int tier = 0; tier < 3; tier++) {
+        UParams P{};
+        P.s = s.dev;
+        P.queries = L.queries;
+        P.qlist = tier == 0 ? nullptr : list[tier - 1];
+        P.qlist_count = tier == 0 ? nullptr : &sc.ctrl[3 + tier - 1];
+        P.n = (uint32_t)L.n;
+        P.out_allowed = L.out_allowed;
+        P.out_err = L.out_err;
+        P.next = &sc.ctrl[tier];
+        P.ovf_list = tier < 2 ? list[tier] : nullptr;
+        P.ovf_count = tier < 2 ? &sc.ctrl[3 + tier] : nullptr;
+        P.vis = sc.vis[tier];
+        P.stack = sc.stack[tier];
+        P.epochs = sc.epochs[tier];
+        P.vcap = t[tier].vcap;
+        P.scap = t[tier].scap / 2;  // frames are 2 x uint4
+        P.max_depth = L.max_depth;
+        P.max_width = L.max_width;
+        P.counters = st.counters + 8 * tier;
+        P.last_tier = tier == 2;
+        uint32_t lanes = t[tier].lanes;
+        if (tier == 0) {  // persistent grid: exactly the resident blocks (occupancy API), capped by the batch
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&check_union_kernel<false, true>),
+                                                             BLOCK, lds) != hipSuccess || per_cu <= 0)
+                per_cu = 4;
+            lanes = std::min<uint32_t>(lanes, (uint32_t)per_cu * cus * BLOCK);
+            lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + BLOCK - 1) / BLOCK) * BLOCK);
+        }
+        const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);
+        dim3 grid(lanes / bs), block(bs);
+        if (tier == 0) KETO_HIP(hipEventRecord(st.ev0, st.stream));
+        if (lds_tables) {
+            if (L.count) hipLaunchKernelGGL((check_union_kernel<true, true>), grid, block, lds, st.stream, P);
+            else hipLaunchKernelGGL((check_union_kernel<false, true>), grid, block, lds, st.stream, P);
+        } else {
+            if (L.count) hipLaunchKernelGGL((check_union_kernel<true, false>), grid, block, 0, st.stream, P);
+            else hipLaunchKernelGGL((check_union_kernel<false, false>), grid, block, 0, st.stream, P);
+        }
+        KETO_HIP(hipGetLastError());
+        if (tier == 0) KETO_HIP(hipEventRecord(st.ev1, st.stream));
+    }
+}
+
+}  // namespace keto

@@ -1,0 +1,116 @@
+// Device helpers shared by the check and expand kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "engine.hpp"
+
+namespace keto {
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+// 16-byte aligned window holding element i of a u32 array
+__device__ __forceinline__ const uint4 *win(const uint32_t *a, uint32_t i) {
+    return reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(a + i) & ~uintptr_t(15));
+}
+__device__ __forceinline__ uint32_t wword(const uint4 &v, uint32_t k) {
+    return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+// element i of array a, given the window loaded for it
+__device__ __forceinline__ uint32_t pick(const uint32_t *a, uint32_t i, const uint4 &v) {
+    return wword(v, (uint32_t)((reinterpret_cast<uintptr_t>(a + i) >> 2) & 3));
+}
+
+// Small per-snapshot tables (namespace table, relation info, rewrite program) staged in LDS.
+struct Tables {
+    const NsDev *ns;
+    const uint32_t *relinfo;
+    const uint32_t *nsrel;
+    const Op *ops;
+    const uint32_t *op_children;
+    uint32_t n_ns, n_rel;
+};
+
+__device__ __forceinline__ uint32_t t_ns_of(const Tables &T, uint32_t node) {
+    uint32_t lo = 0, hi = T.n_ns;  // last namespace whose node_base <= node
+    while (hi - lo > 1) {
+        uint32_t m = (lo + hi) >> 1;
+        if (T.ns[m].node_base <= node) lo = m;
+        else hi = m;
+    }
+    return lo;
+}
+
+struct NodeInfo {
+    uint32_t ns, slot, ri;
+};
+
+__device__ __forceinline__ NodeInfo t_node_info(const Tables &T, uint32_t node) {
+    NodeInfo r;
+    if (node & VIRT_BIT) {
+        r.ns = (node >> 16) & 0x7FFFu;
+        r.slot = NO_SLOT;
+        uint32_t st = r.ns < T.n_ns ? nr_status(T.nsrel[(size_t)r.ns * T.n_rel + (node & 0xFFFFu)]) : REL_NIL;
+        r.ri = make_ri(NO_OP, false, true, st, false);  // no rewrite: direct + expand of an empty row
+        return r;
+    }
+    r.ns = t_ns_of(T, node);
+    const NsDev nd = T.ns[r.ns];
+    r.slot = (node - nd.node_base) % nd.n_slots;
+    r.ri = T.relinfo[nd.slot_base + r.slot];
+    return r;
+}
+
+// node of (same entity as `node`, relation `rel`): computed usersets / tuple-to-userset hops
+__device__ __forceinline__ uint32_t t_sibling(const Tables &T, uint32_t node, const NodeInfo &ni, uint32_t rel) {
+    uint32_t w = rel < T.n_rel ? T.nsrel[(size_t)ni.ns * T.n_rel + rel] : (REL_NIL << 16) | NO_SLOT;
+    uint32_t slot = nr_slot(w);
+    if (slot == NO_SLOT || (node & VIRT_BIT)) return VIRT_BIT | (ni.ns << 16) | (rel & 0xFFFFu);
+    return node - ni.slot + slot;
+}
+
+// node of (ns, entity e, rel) given e; virtual if ns has no slot for rel
+__device__ __forceinline__ uint32_t t_node(const Tables &T, uint32_t ns, uint32_t e, uint32_t rel) {
+    uint32_t w = rel < T.n_rel ? T.nsrel[(size_t)ns * T.n_rel + rel] : (REL_NIL << 16) | NO_SLOT;
+    if (nr_slot(w) == NO_SLOT) return VIRT_BIT | (ns << 16) | (rel & 0xFFFFu);
+    const NsDev nd = T.ns[ns];
+    return nd.node_base + (e - nd.ent_base) * nd.n_slots + nr_slot(w);
+}
+
+// Copy the small tables into dynamic LDS (whole block cooperates); returns LDS views.
+__device__ __forceinline__ Tables stage_tables(const DevSnapshot &s, char *lds) {
+    Tables T;
+    T.n_ns = s.n_ns;
+    T.n_rel = s.n_rel;
+    const uint4 *src[5] = {reinterpret_cast<const uint4 *>(s.ns), reinterpret_cast<const uint4 *>(s.relinfo),
+                           reinterpret_cast<const uint4 *>(s.nsrel), reinterpret_cast<const uint4 *>(s.ops),
+                           reinterpret_cast<const uint4 *>(s.op_children)};
+    uint32_t off = 0;
+    char *dst[5];
+    for (int i = 0; i < 5; i++) {
+        dst[i] = lds + off;
+        const uint32_t n16 = s.tab_bytes[i] / 16;
+        for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) reinterpret_cast<uint4 *>(dst[i])[k] = src[i][k];
+        off += s.tab_bytes[i];
+    }
+    __syncthreads();
+    T.ns = reinterpret_cast<const NsDev *>(dst[0]);
+    T.relinfo = reinterpret_cast<const uint32_t *>(dst[1]);
+    T.nsrel = reinterpret_cast<const uint32_t *>(dst[2]);
+    T.ops = reinterpret_cast<const Op *>(dst[3]);
+    T.op_children = reinterpret_cast<const uint32_t *>(dst[4]);
+    return T;
+}
+
+__device__ __forceinline__ Tables global_tables(const DevSnapshot &s) {
+    return Tables{s.ns, s.relinfo, s.nsrel, s.ops, s.op_children, s.n_ns, s.n_rel};
+}
+
+}  // namespace keto

@@ -70,7 +70,7 @@ struct Stream {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // device workspace (allocated on first use, never inside a launch sequence)
-    Scratch check_scratch, expand_scratch;
+    Scratch check_scratch, union_scratch, expand_scratch;
     uint32_t *lists = nullptr;  // two overflow hand-off lists of list_cap entries
     uint64_t list_cap = 0;
     void *qbuf = nullptr, *obuf = nullptr;  // staging for host-pointer batches
@@ -81,7 +81,12 @@ struct Stream {
     ~Stream();
 };
 
-// kernels.hip
+// scratch.cpp
+int num_cus(int device);
+void ensure_scratch(Scratch &sc, const Tier t[3]);
+void ensure_lists(Stream &st, uint64_t n);
+
+// check.hip / expand.hip
 struct CheckLaunch {
     const keto_query *queries;
     uint64_t n;
@@ -90,7 +95,8 @@ struct CheckLaunch {
     int32_t max_depth, max_width;
     bool count;
 };
-void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);
+void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
+void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // rewrite-free snapshots
 
 struct ExpandLaunch {
     const keto_subject_set *roots;  // device

@@ -71,11 +71,23 @@ struct DevSnapshot {
     const uint32_t *nsrel;     // [n_ns * n_rel]
     const Op *ops;
     const uint32_t *op_children;
-    const unsigned long long *ent_keys; // open addressing: ((ns<<32)|obj)+1, 0 = empty
-    const uint32_t *ent_vals;
+    // (ns, obj) -> entity, open addressing over 16-byte slots {key lo, key hi, entity, 0};
+    // key = ((ns<<32)|obj)+1, 0 = empty
+    const uint4 *ent_table;
     uint32_t ent_mask;
+    // membership probe hash for "heavy" subjects (reverse row longer than probe_k):
+    // 16-byte buckets of two keys ((subject_idx<<32)|node)+1, linear probing over buckets
+    const uint4 *probe;
+    uint32_t probe_mask;  // bucket count - 1
+    uint32_t probe_k;     // reverse rows up to this length are kept in VGPRs instead
     uint32_t n_ns, n_rel, n_nodes, n_uuids;
     int32_t strict;
+    // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children: staged in LDS
+    uint32_t tab_bytes[5];
+    uint32_t lds_bytes;
 };
+
+constexpr uint32_t PROBE_K = 4;           // VGPR-resident reverse row capacity (<= 4: two windows)
+constexpr uint32_t LDS_TABLE_LIMIT = 48 * 1024;
 
 }  // namespace keto

@@ -131,13 +131,20 @@ struct Compiler {
 
 template <class T>
 T *upload(Snapshot &s, const std::vector<T> &v, size_t min_elems = 1) {
-    size_t bytes = std::max(v.size(), min_elems) * sizeof(T);
+    // padded to 16 bytes (+16) so 16-byte window loads past the end stay in bounds
+    size_t bytes = (std::max(v.size(), min_elems) * sizeof(T) + 31) / 16 * 16;
     void *p = nullptr;
     KETO_HIP(hipMalloc(&p, bytes));
     s.allocs.push_back(p);
+    KETO_HIP(hipMemset(p, 0, bytes));
     if (!v.empty()) KETO_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     s.info.device_bytes += bytes;
     return static_cast<T *>(p);
+}
+
+template <class T>
+uint32_t bytes16(const std::vector<T> &v) {
+    return (uint32_t)((v.size() * sizeof(T) + 15) / 16 * 16);
 }
 
 }  // namespace
@@ -320,7 +327,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     uint64_t cap = 16;
     while (cap < 2 * ek.size() + 2) cap <<= 1;
     std::vector<unsigned long long> ent_keys(cap, 0);
-    std::vector<uint32_t> ent_vals(cap, 0);
+    std::vector<uint32_t> ent_vals(cap, 0);  // host lookup copies; device gets 16-byte slots
     {
         std::vector<uint32_t> fill(s.n_ns, 0);
         for (uint64_t k : ek) {
@@ -480,9 +487,53 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.nsrel = upload(s, s.nsrel);
     D.ops = upload(s, s.ops);
     D.op_children = upload(s, s.op_children);
-    D.ent_keys = upload(s, ent_keys);
-    D.ent_vals = upload(s, ent_vals);
-    D.ent_mask = (uint32_t)(cap - 1);
+    D.tab_bytes[0] = bytes16(s.ns);
+    D.tab_bytes[1] = bytes16(s.relinfo);
+    D.tab_bytes[2] = bytes16(s.nsrel);
+    D.tab_bytes[3] = bytes16(s.ops);
+    D.tab_bytes[4] = bytes16(s.op_children);
+    D.lds_bytes = 0;
+    for (uint32_t b : D.tab_bytes) D.lds_bytes += b;
+    {
+        std::vector<uint32_t> et(4 * cap, 0);
+        for (uint64_t i = 0; i < cap; i++) {
+            et[4 * i + 0] = (uint32_t)ent_keys[i];
+            et[4 * i + 1] = (uint32_t)(ent_keys[i] >> 32);
+            et[4 * i + 2] = ent_vals[i];
+        }
+        D.ent_table = reinterpret_cast<const uint4 *>(upload(s, et));
+        D.ent_mask = (uint32_t)(cap - 1);
+    }
+    // membership probe hash for subjects whose reverse row exceeds PROBE_K
+    {
+        uint64_t heavy = 0;
+        for (uint64_t v = 0; v < n_subj_idx; v++)
+            if (rev_off[v + 1] - rev_off[v] > PROBE_K) heavy += rev_off[v + 1] - rev_off[v];
+        uint64_t buckets = 1;
+        while (buckets * 2 < heavy * 2 + 2) buckets <<= 1;  // load factor <= 1/2
+        std::vector<uint64_t> pt(2 * buckets, 0);
+        for (uint64_t v = 0; v < n_subj_idx; v++) {
+            if (rev_off[v + 1] - rev_off[v] <= PROBE_K) continue;
+            for (uint32_t i = rev_off[v]; i < rev_off[v + 1]; i++) {
+                uint64_t key = ((v << 32) | rev_nodes[i]) + 1;
+                uint64_t b = mix64(key) & (buckets - 1);
+                while (true) {
+                    if (!pt[2 * b]) {
+                        pt[2 * b] = key;
+                        break;
+                    }
+                    if (!pt[2 * b + 1]) {
+                        pt[2 * b + 1] = key;
+                        break;
+                    }
+                    b = (b + 1) & (buckets - 1);
+                }
+            }
+        }
+        D.probe = reinterpret_cast<const uint4 *>(upload(s, pt));
+        D.probe_mask = (uint32_t)(buckets - 1);
+        D.probe_k = PROBE_K;
+    }
     D.n_ns = s.n_ns;
     D.n_rel = s.n_rel;
     D.n_nodes = N;

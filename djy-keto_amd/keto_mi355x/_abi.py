@@ -8,6 +8,11 @@ import numpy as np
 
 LIB_NAME = "libketo_mi355x.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# A/B experiments and the CPU kernel-debug harness only (tools/): load another build of
+# the same ABI when explicitly unlocked.  Nothing in the product, tests' GPU runs or the
+# bench sets these variables.
+if os.environ.get("KETO_MI355X_ALLOW_OVERRIDE") == "tools" and os.environ.get("KETO_MI355X_LIB_OVERRIDE"):
+    LIB_PATH = os.environ["KETO_MI355X_LIB_OVERRIDE"]
 
 KETO_OK = 0
 KETO_E_INVALID, KETO_E_DEVICE, KETO_E_CAPACITY, KETO_E_LIMIT = -1, -2, -3, -4

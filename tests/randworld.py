@@ -20,7 +20,7 @@ def _rewrite(rng, rels, depth):
     return {"operator": op, "children": [_rewrite(rng, rels, depth - 1) for _ in range(n)]}
 
 
-def random_world(seed: int, n_obj=10, n_users=6, n_tuples=70):
+def random_world(seed: int, n_obj=10, n_users=6, n_tuples=70, rewrites: bool = True):
     rng = np.random.Generator(np.random.PCG64(seed))
     base_rels = ["a", "b", "c", "d"]
     namespaces = {}
@@ -31,7 +31,7 @@ def random_world(seed: int, n_obj=10, n_users=6, n_tuples=70):
             if rng.random() < 0.5:
                 rel["types"] = [{"namespace": "x", "relation": str(rng.choice(base_rels))}] if rng.random() < 0.5 \
                     else [{"namespace": "u"}]
-            if rng.random() < 0.45:
+            if rewrites and rng.random() < 0.45:
                 # mostly declared relations; occasionally an undeclared one ("zz") -> error path
                 pool = base_rels + (["zz"] if rng.random() < 0.15 else [])
                 rel["rewrite"] = _rewrite(rng, pool, 3)

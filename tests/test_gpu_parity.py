@@ -58,9 +58,10 @@ def test_golden_expands(stream, name):
         assert refsem.trees_equal_unordered(got, e["tree"]), (name, e["src"], got)
 
 
+@pytest.mark.parametrize("rewrites", [True, False])
 @pytest.mark.parametrize("seed", list(range(60)))
-def test_random_worlds_vs_oracle(stream, seed):
-    w, t, q, expands = random_world(seed)
+def test_random_worlds_vs_oracle(stream, seed, rewrites):
+    w, t, q, expands = random_world(seed, rewrites=rewrites)
     orc = refsem.Oracle(w, t)
     snap = product_snapshot(w, t)
     dec, err, st = _oracle_decisions(orc, q, w.max_depth, w.max_width)

@@ -1,0 +1,34 @@
+"""Profiling driver: C2 snapshot + a few 2^20-query check batches (no counting pass),
+short enough for one rocprofv3 --pmc pass.  KETO_MI355X_LIB_OVERRIDE selects an A/B build."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "djy-keto_amd"))
+import numpy as np  # noqa: E402
+
+import keto_mi355x as km  # noqa: E402
+from keto_mi355x import synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batches", type=int, default=3)
+ap.add_argument("--tuples", type=int, default=10_000_000)
+ap.add_argument("--workload", default="c2")
+a = ap.parse_args()
+if a.workload == "c2":
+    wl = synth.nested_groups(a.tuples, seed=1)
+    q = synth.nested_groups_queries(wl, 1 << 20, seed=7)
+else:
+    wl = synth.drive(depth=8, n_groups=200_000, n_users=2_000_000, seed=3)
+    q = synth.drive_queries(wl, 1 << 20, seed=11)
+snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+st = km.Stream(0)
+eng = km.CheckEngine(snap, st, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+dq, da, de = km.DeviceBuffer(0, q.nbytes), km.DeviceBuffer(0, len(q)), km.DeviceBuffer(0, 4 * len(q))
+dq.upload(st, q)
+for i in range(a.batches):
+    t0 = time.perf_counter()
+    eng.check_batch_device(dq, len(q), da, de, sync=True)
+    print(f"batch {i}: {(time.perf_counter() - t0) * 1e3:.2f} ms, tier-0 kernel {st.last_kernel_ms():.2f} ms",
+          flush=True)
