@@ -152,6 +152,8 @@ int keto_stream_counters(keto_stream *hs, keto_work_counters *out, int32_t reset
                 out->probes[t] = c[8 * t + 2];
                 out->out_nodes[t] = c[8 * t + 3];
                 out->queries[t] = c[8 * t + 4];
+                out->wave_steps[t] = c[8 * t + 5];
+                out->lane_steps[t] = c[8 * t + 6];
             }
         if (reset) KETO_HIP(hipMemset(s->counters, 0, sizeof c));
     });

@@ -43,17 +43,12 @@ __device__ __forceinline__ uint32_t set_phase(uint32_t w, uint32_t p) { return (
 // lane states; "pseudo" states need no load and are run by the same step loop
 enum State : uint32_t {
     S_IDLE = 0,
-    S_QREC,     // query record (2 x 16 B)
-    S_ENT,      // entity hash slot (root or subject set)
-    S_SUBJ,     // pseudo: resolve the subject
-    S_REVOFF0,  // pseudo: request reverse-row offsets
-    S_REVOFF,   // reverse-row offsets
-    S_REVREG,   // reverse-row entries -> VGPRs, then start
+    S_START,    // start record of the resolve pre-pass (2 x 16 B)
     S_RUN,      // pseudo: execute / resume the top frame
     S_RET,      // pseudo: return `res` to the parent frame
     S_POP,      // parent frame
     S_DPROBE,   // probe-hash answer for checkDirect
-    S_ROWOFF,   // set-row offsets (ES or TTU)
+    S_ROWOFF,   // {begin, end} of a subject-set row (ES or TTU)
     S_FSCAN,    // edge window of the ES found-lookahead
     S_FPROBE,   // probe-hash answers of the lookahead (<= 2)
     S_ESDONE,   // pseudo: lookahead exhausted -> truncate, open scope, child loop
@@ -68,8 +63,8 @@ enum State : uint32_t {
 
 struct CheckParams {
     DevSnapshot s;
-    const keto_query *queries;
-    const uint32_t *qlist;  // tiers >= 1: indices of queries to (re)run
+    const uint4 *start;     // resolve pre-pass records, in work order
+    const uint32_t *qlist;  // tiers >= 1: start-record positions to (re)run
     const uint32_t *qlist_count;
     uint32_t n;
     uint8_t *out_allowed;
@@ -111,12 +106,10 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
     const uint32_t W = (uint32_t)P.max_width;
     const uint32_t lane = __lane_id();
 
-    uint32_t q = 0, st = S_IDLE;
+    uint32_t q = 0, pos = 0, st = S_IDLE;
     bool exhausted = false;
-    // query and subject
-    uint32_t qns = 0, qobj = 0, qrel = 0, qkind = 0, qsobj = 0, qsns = 0, qsrel = 0, root = 0;
-    uint32_t sidx = NONE32, rb = 0, re = 0;
-    bool heavy = false, resolving_subject = false;
+    uint32_t sidx = NONE32;  // subject
+    bool heavy = false;
     uint32_t R0 = NONE32, R1 = NONE32, R2 = NONE32, R3 = NONE32;
     // interpreter
     uint4 top = make_uint4(0, 0, 0, 0);
@@ -124,13 +117,13 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
     bool have_res = false, scope = false;
     uint4 ew = make_uint4(0, 0, 0, 0);
     uint32_t ew_lo = 1, ew_hi = 0;      // edge indices present in ew
-    uint32_t aux = 0, aux2 = 0;         // entity slot / probe buckets / visited pair
+    uint32_t aux = 0, aux2 = 0;         // probe buckets / visited pair
     uint32_t pc0 = 0, pc1 = 0, pn = 0;  // probed nodes, count
     uint32_t cc = 0, vk = 0;            // child node / its visited key
     const uint4 *la0 = nullptr, *la1 = nullptr;
     uint32_t ln = 0;
     uint32_t q_rows = 0, q_edges = 0, q_probes = 0;
-    unsigned long long c_rows = 0, c_edges = 0, c_probes = 0, c_q = 0;
+    unsigned long long c_rows = 0, c_edges = 0, c_probes = 0, c_q = 0, c_wsteps = 0, c_lsteps = 0;
 
     while (true) {
         // ---- refill idle lanes: one atomic per wavefront (ballot + mbcnt) --------------------
@@ -145,9 +138,9 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                 const uint32_t my = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
                 if (my >= nq) exhausted = true;
                 else {
-                    q = P.qlist ? P.qlist[my] : my;
-                    st = S_QREC;
-                    la0 = reinterpret_cast<const uint4 *>(P.queries + q);
+                    pos = P.qlist ? P.qlist[my] : my;
+                    st = S_START;
+                    la0 = P.start + 2 * (size_t)pos;
                     la1 = la0 + 1;
                     ln = 2;
                     q_rows = q_edges = q_probes = 0;
@@ -160,6 +153,10 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
         if (ln > 0) v0 = *la0;
         if (ln > 1) v1 = *la1;
         ln = 0;
+        if (COUNT) {
+            c_wsteps += lane == 0 ? 1 : 0;
+            c_lsteps += st != S_IDLE ? 1 : 0;
+        }
         if (st == S_IDLE) continue;
 
         // fin: 0 running, 1 finished (res), 2 scratch outgrown
@@ -169,106 +166,20 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
             const uint32_t d = f_d(w);
             switch (st) {
             // ---------------------------------------------------------------- query entry
-            case S_QREC: {
-                qns = v0.x;
-                qobj = v0.y;
-                qrel = v0.z;
-                qkind = v0.w;
-                qsobj = v1.x;
-                qsns = v1.y;
-                qsrel = v1.z;
-                int32_t d0 = (int32_t)v1.w;
-                if (d0 <= 0 || P.max_depth < d0) d0 = P.max_depth;  // engine.go:82-84
-                top = make_uint4(0, 0, 0, fw(F_IA, (uint32_t)d0));
-                sidx = NONE32;
-                if (qns < s.n_ns) {
-                    resolving_subject = false;
-                    aux = (uint32_t)mix64((((uint64_t)qns << 32) | qobj) + 1) & s.ent_mask;
-                    la0 = s.ent_table + aux;
-                    ln = 1;
-                    st = S_ENT;
-                    break;
-                }
-                root = VIRT_BIT | (0x7FFFu << 16) | 0xFFFFu;  // unknown namespace
-                st = S_SUBJ;
-                break;
-            }
-            case S_ENT: {
-                const uint32_t ns = resolving_subject ? qsns : qns, obj = resolving_subject ? qsobj : qobj;
-                const uint64_t key = (((uint64_t)ns << 32) | obj) + 1;
-                const uint64_t k = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
-                if (k != key && k != 0) {
-                    aux = (aux + 1) & s.ent_mask;
-                    la0 = s.ent_table + aux;
-                    ln = 1;
-                    break;
-                }
-                uint32_t e = k == key ? v0.z : NONE32;
-                if (!resolving_subject) {
-                    if (e == NONE32) e = T.ns[qns + 1].ent_base - 1;  // phantom entity: no tuples
-                    root = t_node(T, qns, e, qrel);
-                    st = S_SUBJ;
-                } else {
-                    if (e != NONE32) {
-                        const uint32_t sn = t_node(T, qsns, e, qsrel);
-                        if (!(sn & VIRT_BIT)) sidx = s.n_uuids + sn;
-                    }
-                    st = S_REVOFF0;
-                }
-                break;
-            }
-            case S_SUBJ:
-                if (qkind == 1) {
-                    if (qsns < s.n_ns) {
-                        resolving_subject = true;
-                        aux = (uint32_t)mix64((((uint64_t)qsns << 32) | qsobj) + 1) & s.ent_mask;
-                        la0 = s.ent_table + aux;
-                        ln = 1;
-                        st = S_ENT;
-                        break;
-                    }
-                } else if (qsobj < s.n_uuids) {
-                    sidx = qsobj;
-                }
-                st = S_REVOFF0;
-                break;
-            case S_REVOFF0:
-                heavy = false;
-                rb = re = 0;
-                if (sidx == NONE32) {
-                    st = S_REVREG;
-                    break;
-                }
-                la0 = win(s.rev_off, sidx);
-                la1 = win(s.rev_off, sidx + 1);
-                ln = 2;
-                st = S_REVOFF;
-                break;
-            case S_REVOFF:
-                rb = pick(s.rev_off, sidx, v0);
-                re = pick(s.rev_off, sidx + 1, v1);
-                heavy = (re - rb) > PROBE_K;
-                st = S_REVREG;
-                if (!heavy && re > rb) {
-                    la0 = win(s.rev_nodes, rb);
-                    la1 = la0 + 1;  // PROBE_K = 4 entries span at most two windows
-                    ln = 2;
-                }
-                break;
-            case S_REVREG: {
-                const uint32_t o = (uint32_t)((reinterpret_cast<uintptr_t>(s.rev_nodes + rb) >> 2) & 3);
-                const uint32_t cnt = heavy ? 0 : re - rb;
-                R0 = cnt > 0 ? w8(v0, v1, o) : NONE32;
-                R1 = cnt > 1 ? w8(v0, v1, o + 1) : NONE32;
-                R2 = cnt > 2 ? w8(v0, v1, o + 2) : NONE32;
-                R3 = cnt > 3 ? w8(v0, v1, o + 3) : NONE32;
-                top.x = root;  // checkIsAllowed(root, d, false)
+            case S_START:
+                q = v0.w;
+                sidx = v0.y;
+                heavy = (v0.z & START_HEAVY) != 0;
+                R0 = v1.x;
+                R1 = v1.y;
+                R2 = v1.z;
+                R3 = v1.w;
+                top = make_uint4(v0.x, 0, 0, fw(F_IA, v0.z & 0xFFFFu));  // checkIsAllowed(root, d, false)
                 sp = 0;
                 have_res = false;
                 scope = false;
                 st = S_RUN;
                 break;
-            }
             // ---------------------------------------------------------------- returns
             case S_RET:
                 if (sp == 0) {
@@ -306,7 +217,7 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
             case S_ROWOFF: {
                 const bool is_es = f_type(w) == F_ES;
                 const uint32_t node = is_es ? top.x : top.y;  // TTU keeps the tupleset node in y
-                const uint32_t b = pick(s.set_off, node, v0), e = pick(s.set_off, node + 1, v1);
+                const uint32_t b = pick(s.set_row, 2 * node, v0), e = pick(s.set_row, 2 * node + 1, v0);
                 if (b == e) {
                     res = M_NOT;
                     st = S_RET;
@@ -662,9 +573,8 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                             action = 2;
                             break;
                         }
-                        la0 = win(s.set_off, top.x);
-                        la1 = win(s.set_off, top.x + 1);
-                        ln = 2;
+                        la0 = win(s.set_row, 2 * top.x);
+                        ln = 1;
                         top.w = set_phase(w, 1);
                         st = S_ROWOFF;
                         break;
@@ -839,9 +749,8 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                             break;
                         }
                         top = make_uint4(op.rel_computed >> 16, ts, 0, set_phase(w, 1));
-                        la0 = win(s.set_off, ts);
-                        la1 = win(s.set_off, ts + 1);
-                        ln = 2;
+                        la0 = win(s.set_row, 2 * ts);
+                        ln = 1;
                         st = S_ROWOFF;
                         break;
                     }
@@ -910,7 +819,7 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                     P.out_allowed[q] = 0;
                     P.out_err[q] = KETO_QERR_INTERNAL;
                 } else {
-                    P.ovf_list[atomicAdd(P.ovf_count, 1u)] = q;
+                    P.ovf_list[atomicAdd(P.ovf_count, 1u)] = pos;
                 }
             } else {
                 const uint32_t err = res >> 8;
@@ -934,12 +843,15 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
             c_edges += __shfl_down(c_edges, off);
             c_probes += __shfl_down(c_probes, off);
             c_q += __shfl_down(c_q, off);
+            c_lsteps += __shfl_down(c_lsteps, off);
         }
         if (lane == 0) {
             atomicAdd(&P.counters[0], c_rows);
             atomicAdd(&P.counters[1], c_edges);
             atomicAdd(&P.counters[2], c_probes);
             atomicAdd(&P.counters[4], c_q);
+            atomicAdd(&P.counters[5], c_wsteps);
+            atomicAdd(&P.counters[6], c_lsteps);
         }
     }
 }
@@ -955,11 +867,12 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     constexpr uint32_t BLOCK = 256;
     const uint32_t cus = (uint32_t)num_cus(s.device);
     // (lanes, visited slots per lane, frames per lane)
-    const Tier t[3] = {Tier{cus * 32 * 64, 256, 64},    // the common case (grid clipped to occupancy)
-                       Tier{cus * 64, 1u << 13, 1024},  // wide visited scopes
+    // HBM is plentiful (288 GB): tier 0 holds ~500 visited nodes per lane so restarts are rare
+    const Tier t[3] = {Tier{cus * 32 * 64, 1024, 64},    // the common case (grid clipped to occupancy)
+                       Tier{cus * 256, 1u << 13, 1024},  // wide visited scopes
                        Tier{64, 1u << 20, 1u << 14}};   // huge scopes / deep recursion
     ensure_scratch(st.check_scratch, t);
-    ensure_lists(st, L.n);
+    run_resolve(s, st, L.queries, L.n, L.max_depth);
     Scratch &sc = st.check_scratch;
     uint32_t *list[2] = {st.lists, st.lists + st.list_cap};
     const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
@@ -968,7 +881,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     for (int tier = 0; tier < 3; tier++) {
         CheckParams P{};
         P.s = s.dev;
-        P.queries = L.queries;
+        P.start = st.resolved;
         P.qlist = tier == 0 ? nullptr : list[tier - 1];
         P.qlist_count = tier == 0 ? nullptr : &sc.ctrl[3 + tier - 1];
         P.n = (uint32_t)L.n;

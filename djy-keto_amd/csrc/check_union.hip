@@ -21,12 +21,9 @@ namespace {
 
 enum UState : uint32_t {
     U_IDLE = 0,
-    U_QREC,    // query record
-    U_ENT,     // entity hash slot (root / subject set)
-    U_REVOFF,  // subject reverse-row offsets
-    U_REVREG,  // reverse-row entries -> VGPRs
+    U_START,   // start record of the resolve pre-pass (2 x 16 B)
     U_DPROBE,  // checkDirect of the root via the probe hash
-    U_ROWOFF,  // set-row offsets of the current node
+    U_ROWOFF,  // {begin, end} of the current node's subject-set row
     U_SCAN,    // edge window of the found-lookahead
     U_SPROBE,  // hash probes of the lookahead (2 per step)
     U_CEDGE,   // edge window of the child loop
@@ -37,7 +34,7 @@ enum UState : uint32_t {
 
 struct UParams {
     DevSnapshot s;
-    const keto_query *queries;
+    const uint4 *start;  // resolve pre-pass records, in work order
     const uint32_t *qlist;
     const uint32_t *qlist_count;
     uint32_t n;
@@ -81,24 +78,22 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
     const uint32_t W = (uint32_t)P.max_width;
     const uint32_t lane = __lane_id();
 
-    uint32_t q = 0, st = U_IDLE;
+    uint32_t q = 0, pos = 0, st = U_IDLE;
     bool exhausted = false;
-    // query + subject
-    uint32_t qns = 0, qobj = 0, qrel = 0, qkind = 0, qsobj = 0, qsns = 0, qsrel = 0;
-    uint32_t sidx = NONE32, rb = 0, re = 0;
+    uint32_t sidx = NONE32;  // subject
     bool heavy = false;
     uint32_t R0 = NONE32, R1 = NONE32, R2 = NONE32, R3 = NONE32;
     // current expand-subject frame: node, cursor, end, depth, row begin; edge window
     uint32_t node = 0, cur = 0, end = 0, d = 0, rbeg = 0;
     uint4 ew = make_uint4(0, 0, 0, 0);
     uint32_t ew_lo = 1, ew_hi = 0;
-    uint32_t sp = 0, vcount = 0, aux = 0, aux2 = 0;  // aux: entity slot / probe bucket / visited pair
+    uint32_t sp = 0, vcount = 0, aux = 0, aux2 = 0;  // aux: probe bucket / visited pair
     uint32_t vk = 0;                                  // visited key of the child being inserted
-    bool resolving_subject = false, root_ss = false;
+    bool root_ss = false;
     const uint4 *la0 = nullptr, *la1 = nullptr;
     uint32_t ln = 0;
     uint32_t q_rows = 0, q_edges = 0, q_probes = 0;
-    unsigned long long c_rows = 0, c_edges = 0, c_probes = 0, c_q = 0;
+    unsigned long long c_rows = 0, c_edges = 0, c_probes = 0, c_q = 0, c_wsteps = 0, c_lsteps = 0;
 
     while (true) {
         const bool need = (st == U_IDLE) && !exhausted;
@@ -112,9 +107,9 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 const uint32_t my = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
                 if (my >= nq) exhausted = true;
                 else {
-                    q = P.qlist ? P.qlist[my] : my;
-                    st = U_QREC;
-                    la0 = reinterpret_cast<const uint4 *>(P.queries + q);
+                    pos = P.qlist ? P.qlist[my] : my;
+                    st = U_START;
+                    la0 = P.start + 2 * (size_t)pos;
                     la1 = la0 + 1;
                     ln = 2;
                     q_rows = q_edges = q_probes = 0;
@@ -126,110 +121,26 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
         if (ln > 0) v0 = *la0;
         if (ln > 1) v1 = *la1;
         ln = 0;
+        if (COUNT) {
+            c_wsteps += lane == 0 ? 1 : 0;
+            c_lsteps += st != U_IDLE ? 1 : 0;
+        }
         if (st == U_IDLE) continue;
 
         // result: 0 = keep going, 1 = allowed, 2 = denied, 3 = relation error, 4 = overflow
         uint32_t fin = 0;
         for (int guard = 0; guard < 8 && ln == 0 && fin == 0; guard++) {
             switch (st) {
-            case U_QREC: {
-                qns = v0.x;
-                qobj = v0.y;
-                qrel = v0.z;
-                qkind = v0.w;
-                qsobj = v1.x;
-                qsns = v1.y;
-                qsrel = v1.z;
-                int32_t d0 = (int32_t)v1.w;
-                if (d0 <= 0 || P.max_depth < d0) d0 = P.max_depth;  // engine.go:82-84
-                d = (uint32_t)d0;
-                sidx = NONE32;
-                if (qns < s.n_ns) {  // resolve the root entity
-                    resolving_subject = false;
-                    aux = (uint32_t)mix64((((uint64_t)qns << 32) | qobj) + 1) & s.ent_mask;
-                    la0 = s.ent_table + aux;
-                    ln = 1;
-                    st = U_ENT;
-                    break;
-                }
-                node = VIRT_BIT | (0x7FFFu << 16) | 0xFFFFu;  // unknown namespace
-                st = U_ENT + 100;
-                break;
-            }
-            case U_ENT: {
-                const uint32_t ns = resolving_subject ? qsns : qns, obj = resolving_subject ? qsobj : qobj;
-                const uint64_t key = (((uint64_t)ns << 32) | obj) + 1;
-                const uint64_t k = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
-                if (k != key && k != 0) {  // keep probing
-                    aux = (aux + 1) & s.ent_mask;
-                    la0 = s.ent_table + aux;
-                    ln = 1;
-                    break;
-                }
-                uint32_t e = k == key ? v0.z : NONE32;
-                if (!resolving_subject) {
-                    if (e == NONE32) e = T.ns[qns + 1].ent_base - 1;  // phantom entity: no tuples
-                    node = t_node(T, qns, e, qrel);
-                    st = U_ENT + 100;
-                } else {
-                    if (e != NONE32) {
-                        const uint32_t sn = t_node(T, qsns, e, qsrel);
-                        if (!(sn & VIRT_BIT)) sidx = s.n_uuids + sn;
-                    }
-                    st = U_REVOFF + 100;
-                }
-                break;
-            }
-            case U_ENT + 100:  // subject: id, or subject set to resolve
-                if (qkind == 1) {
-                    if (qsns < s.n_ns) {
-                        resolving_subject = true;
-                        aux = (uint32_t)mix64((((uint64_t)qsns << 32) | qsobj) + 1) & s.ent_mask;
-                        la0 = s.ent_table + aux;
-                        ln = 1;
-                        st = U_ENT;
-                        break;
-                    }
-                } else if (qsobj < s.n_uuids) {
-                    sidx = qsobj;
-                }
-                st = U_REVOFF + 100;
-                break;
-            case U_REVOFF + 100:
-                heavy = false;
-                if (sidx == NONE32) {  // subject held by no tuple
-                    rb = re = 0;
-                    st = U_REVREG;
-                    break;
-                }
-                la0 = win(s.rev_off, sidx);
-                la1 = win(s.rev_off, sidx + 1);
-                ln = 2;
-                st = U_REVOFF;
-                break;
-            case U_REVOFF:
-                rb = pick(s.rev_off, sidx, v0);
-                re = pick(s.rev_off, sidx + 1, v1);
-                heavy = (re - rb) > PROBE_K;
-                if (heavy || re == rb) {
-                    v0 = v1 = make_uint4(NONE32, NONE32, NONE32, NONE32);
-                    rb = re;  // no register entries
-                    st = U_REVREG;
-                    break;
-                }
-                la0 = win(s.rev_nodes, rb);
-                la1 = la0 + 1;
-                ln = 2;
-                st = U_REVREG;
-                break;
-            case U_REVREG: {
-                // up to PROBE_K (=4) entries starting at rb, spread over the two windows
-                const uint32_t o = (uint32_t)((reinterpret_cast<uintptr_t>(s.rev_nodes + rb) >> 2) & 3);
-                const uint32_t cnt = re - rb;
-                R0 = cnt > 0 ? w8(v0, v1, o) : NONE32;
-                R1 = cnt > 1 ? w8(v0, v1, o + 1) : NONE32;
-                R2 = cnt > 2 ? w8(v0, v1, o + 2) : NONE32;
-                R3 = cnt > 3 ? w8(v0, v1, o + 3) : NONE32;
+            case U_START: {
+                node = v0.x;
+                sidx = v0.y;
+                d = v0.z & 0xFFFFu;
+                heavy = (v0.z & START_HEAVY) != 0;
+                q = v0.w;
+                R0 = v1.x;
+                R1 = v1.y;
+                R2 = v1.z;
+                R3 = v1.w;
                 // root checkIsAllowed(node, d, false) (engine.go:214-249)
                 const NodeInfo ni = t_node_info(T, node);
                 if (ri_status(ni.ri) == REL_ERROR) {
@@ -294,14 +205,13 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                     st = U_POP + 100;  // empty row: not a member, return
                     break;
                 }
-                la0 = win(s.set_off, node);
-                la1 = win(s.set_off, node + 1);
-                ln = 2;
+                la0 = win(s.set_row, 2 * node);
+                ln = 1;
                 st = U_ROWOFF;
                 break;
             case U_ROWOFF:
-                rbeg = pick(s.set_off, node, v0);
-                end = pick(s.set_off, node + 1, v1);
+                rbeg = pick(s.set_row, 2 * node, v0);
+                end = pick(s.set_row, 2 * node + 1, v0);
                 cur = rbeg;
                 if (rbeg == end) {
                     st = U_POP + 100;
@@ -533,7 +443,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                     P.out_allowed[q] = 0;
                     P.out_err[q] = KETO_QERR_INTERNAL;
                 } else {
-                    P.ovf_list[atomicAdd(P.ovf_count, 1u)] = q;
+                    P.ovf_list[atomicAdd(P.ovf_count, 1u)] = pos;
                 }
             } else {
                 P.out_allowed[q] = fin == 1 ? 1 : 0;
@@ -556,12 +466,15 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
             c_edges += __shfl_down(c_edges, off);
             c_probes += __shfl_down(c_probes, off);
             c_q += __shfl_down(c_q, off);
+            c_lsteps += __shfl_down(c_lsteps, off);
         }
         if (lane == 0) {
             atomicAdd(&P.counters[0], c_rows);
             atomicAdd(&P.counters[1], c_edges);
             atomicAdd(&P.counters[2], c_probes);
             atomicAdd(&P.counters[4], c_q);
+            atomicAdd(&P.counters[5], c_wsteps);
+            atomicAdd(&P.counters[6], c_lsteps);
         }
     }
 }
@@ -569,13 +482,16 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
 }  // namespace
 
 void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
+    if (L.n == 0) return;
+    if (L.n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
     constexpr uint32_t BLOCK = 256;
     const uint32_t cus = (uint32_t)num_cus(s.device);
-    const Tier t[3] = {Tier{cus * 32 * 64, 256, 32},   // 32 waves / CU
-                       Tier{cus * 64, 1u << 13, 512},
+    // HBM is plentiful (288 GB): tier 0 holds ~500 visited nodes per lane so restarts are rare
+    const Tier t[3] = {Tier{cus * 32 * 64, 1024, 32},   // 32 waves / CU (grid clipped to occupancy)
+                       Tier{cus * 256, 1u << 13, 512},
                        Tier{64, 1u << 20, 1u << 14}};
     ensure_scratch(st.union_scratch, t);
-    ensure_lists(st, L.n);
+    run_resolve(s, st, L.queries, L.n, L.max_depth);
     Scratch &sc = st.union_scratch;
     uint32_t *list[2] = {st.lists, st.lists + st.list_cap};
     const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
@@ -584,7 +500,7 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     for (int tier = 0; tier < 3; tier++) {
         UParams P{};
         P.s = s.dev;
-        P.queries = L.queries;
+        P.start = st.resolved;
         P.qlist = tier == 0 ? nullptr : list[tier - 1];
         P.qlist_count = tier == 0 ? nullptr : &sc.ctrl[3 + tier - 1];
         P.n = (uint32_t)L.n;

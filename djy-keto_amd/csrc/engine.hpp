@@ -71,7 +71,10 @@ struct Stream {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // device workspace (allocated on first use, never inside a launch sequence)
     Scratch check_scratch, union_scratch, expand_scratch;
-    uint32_t *lists = nullptr;  // two overflow hand-off lists of list_cap entries
+    // per-batch workspace of list_cap queries, one allocation:
+    uint32_t *lists = nullptr;       // two overflow hand-off lists (of start-record positions)
+    uint4 *resolved = nullptr;       // 2 x 16 B start record per query, longest-first (resolve.hip)
+    uint32_t *order_ctrl = nullptr;  // [0] heavy, [1] light counts
     uint64_t list_cap = 0;
     void *qbuf = nullptr, *obuf = nullptr;  // staging for host-pointer batches
     size_t qbuf_bytes = 0, obuf_bytes = 0;
@@ -95,6 +98,8 @@ struct CheckLaunch {
     int32_t max_depth, max_width;
     bool count;
 };
+// resolve.hip: per-query start records, longest-first, into st.resolved
+void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth);
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
 void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // rewrite-free snapshots
 

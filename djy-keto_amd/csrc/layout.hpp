@@ -59,8 +59,9 @@ struct alignas(16) NsDev {
 
 // Device view (all pointers device memory).  Passed by value to kernels.
 struct DevSnapshot {
-    const uint32_t *set_off;   // [n_nodes+1]  subject-set rows, shard order (ES + TTU)
-    const uint32_t *set_dst;   // node | EDGE_ALIAS
+    const uint32_t *set_row;   // [2*n_nodes] {begin, end} of each subject-set row (ES + TTU): one 8 B load
+    const uint32_t *set_dst;   // node | EDGE_ALIAS, shard order within a row
+    const uint32_t *weight;    // [n_nodes] capped path count below a node (longest-first scheduling)
     const uint32_t *vkey;      // [n_nodes] visited representative (only read for aliased nodes)
     const uint32_t *all_off;   // [n_nodes+1]  every tuple of a node, shard order (Expand)
     const uint32_t *all_subj;  // subject id, or SKEY_SET|node
@@ -87,6 +88,10 @@ struct DevSnapshot {
     uint32_t lds_bytes;
 };
 
+constexpr uint32_t WEIGHT_ROUNDS = 12;     // path-count relaxation rounds (> typical max depth)
+constexpr uint32_t WEIGHT_CAP = 1u << 20;
+constexpr uint32_t HEAVY_WEIGHT = 32;      // roots at or above this weight are scheduled first
+constexpr uint32_t START_HEAVY = 1u << 31;  // start record: subject row answered by the probe hash
 constexpr uint32_t PROBE_K = 4;           // VGPR-resident reverse row capacity (<= 4: two windows)
 constexpr uint32_t LDS_TABLE_LIMIT = 48 * 1024;
 

@@ -49,7 +49,11 @@ void ensure_lists(Stream &st, uint64_t n) {
     if (st.lists) KETO_HIP(hipFree(st.lists));
     st.lists = nullptr;
     st.list_cap = 0;
-    KETO_HIP(hipMalloc(&st.lists, 2 * n * sizeof(uint32_t)));
+    // [lists 2n u32][ctrl 64 B][resolved 2n uint4]
+    const size_t head = align256(2 * n * sizeof(uint32_t) + 64);
+    KETO_HIP(hipMalloc(&st.lists, head + 2 * n * sizeof(uint4)));
+    st.order_ctrl = st.lists + 2 * n;
+    st.resolved = reinterpret_cast<uint4 *>(reinterpret_cast<char *>(st.lists) + head);
     st.list_cap = n;
 }
 

@@ -475,7 +475,26 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
 
     // ---- upload ------------------------------------------------------------------------
     DevSnapshot &D = s.dev;
-    D.set_off = upload(s, set_off);
+    {
+        std::vector<uint32_t> set_row(2 * (size_t)N);
+        for (uint32_t v = 0; v < N; v++) {
+            set_row[2 * v] = set_off[v];
+            set_row[2 * v + 1] = set_off[v + 1];
+        }
+        D.set_row = upload(s, set_row);
+        // capped count of expansion paths below each node (relaxed to a fixed point over
+        // WEIGHT_ROUNDS rounds): a cost estimate that orders each batch longest-first
+        std::vector<uint32_t> wgt(N, 1), nxt(N);
+        for (int round = 0; round < WEIGHT_ROUNDS; round++) {
+            for (uint32_t v = 0; v < N; v++) {
+                uint64_t acc = 1;
+                for (uint32_t i = set_off[v]; i < set_off[v + 1] && acc < WEIGHT_CAP; i++) acc += wgt[set_dst[i] & ~EDGE_ALIAS];
+                nxt[v] = (uint32_t)std::min<uint64_t>(acc, WEIGHT_CAP);
+            }
+            wgt.swap(nxt);
+        }
+        D.weight = upload(s, wgt);
+    }
     D.set_dst = upload(s, set_dst);
     D.vkey = vkey.empty() ? nullptr : upload(s, vkey);
     D.all_off = upload(s, all_off);

@@ -48,7 +48,8 @@ class Limits(ctypes.Structure):
 
 class WorkCounters(ctypes.Structure):
     _fields_ = [("rows", ctypes.c_uint64 * 3), ("edges", ctypes.c_uint64 * 3), ("probes", ctypes.c_uint64 * 3),
-                ("out_nodes", ctypes.c_uint64 * 3), ("queries", ctypes.c_uint64 * 3)]
+                ("out_nodes", ctypes.c_uint64 * 3), ("queries", ctypes.c_uint64 * 3),
+                ("wave_steps", ctypes.c_uint64 * 3), ("lane_steps", ctypes.c_uint64 * 3)]
 
 
 # symbol -> (restype, argtypes); the header's complete export list

@@ -122,9 +122,12 @@ typedef struct keto_limits {
 
 /* Algorithmic work counters (BASELINE.md byte model), per scratch tier t = 0..2:
  * rows opened, subject-set edges read, membership probes, Expand nodes emitted and
- * queries completed by the kernels of tier t. */
+ * queries completed by the kernels of tier t; plus the Check interpreters' load-slot
+ * iterations summed over wavefronts (wave_steps) and over lanes holding a live query
+ * (lane_steps): lane_steps / (64 * wave_steps) is the SIMD-lane utilisation. */
 typedef struct keto_work_counters {
     uint64_t rows[3], edges[3], probes[3], out_nodes[3], queries[3];
+    uint64_t wave_steps[3], lane_steps[3];
 } keto_work_counters;
 
 typedef struct keto_snapshot keto_snapshot;

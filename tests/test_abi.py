@@ -38,7 +38,7 @@ def test_record_layouts_match_header():
     assert "uint8_t shard_id[16];" in src
     assert km.TUPLE_DT.itemsize == 48 and km.QUERY_DT.itemsize == 32
     assert km.SUBJSET_DT.itemsize == 16 and km.TREE_DT.itemsize == 24
-    assert ctypes.sizeof(_abi.Limits) == 8 and ctypes.sizeof(_abi.WorkCounters) == 120
+    assert ctypes.sizeof(_abi.Limits) == 8 and ctypes.sizeof(_abi.WorkCounters) == 168
 
 
 def test_invalid_arguments_are_rejected():

@@ -15,6 +15,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batches", type=int, default=3)
 ap.add_argument("--tuples", type=int, default=10_000_000)
 ap.add_argument("--workload", default="c2")
+ap.add_argument("--count", action="store_true", help="one counted batch first: per-tier work and step counters")
+ap.add_argument("--single", type=int, default=-1, help="time one query alone, x64 and x(full grid) copies")
 a = ap.parse_args()
 if a.workload == "c2":
     wl = synth.nested_groups(a.tuples, seed=1)
@@ -27,6 +29,30 @@ st = km.Stream(0)
 eng = km.CheckEngine(snap, st, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
 dq, da, de = km.DeviceBuffer(0, q.nbytes), km.DeviceBuffer(0, len(q)), km.DeviceBuffer(0, 4 * len(q))
 dq.upload(st, q)
+if a.single >= 0:
+    for copies in (1, 64, 6144 * 64):
+        qq = np.repeat(q[a.single:a.single + 1], copies)
+        d2 = km.DeviceBuffer(0, qq.nbytes)
+        d2.upload(st, qq)
+        st.counters(reset=True)
+        eng.check_batch_device(d2, copies, da, de, sync=True, count_work=True)
+        c = st.counters(reset=True)
+        ms = []
+        for _ in range(3):
+            eng.check_batch_device(d2, copies, da, de, sync=True)
+            ms.append(st.last_kernel_ms())
+        print(f"query {a.single} x{copies}: tier-0 kernel {min(ms):.3f} ms, lane_steps/query "
+              f"{c['lane_steps'] / copies:.0f}, wave_steps {c['wave_steps']}, "
+              f"us/step {min(ms) * 1e3 * ((copies + 63) // 64) / max(1, c['wave_steps']):.2f}",
+              flush=True)
+if a.count:
+    st.counters(reset=True)
+    eng.check_batch_device(dq, len(q), da, de, sync=True, count_work=True)
+    c = st.counters(reset=True)["per_tier"]
+    for t in range(3):
+        ws, ls = c["wave_steps"][t], c["lane_steps"][t]
+        print(f"tier {t}: queries {c['queries'][t]} rows {c['rows'][t]} edges {c['edges'][t]} probes {c['probes'][t]} "
+              f"wave_steps {ws} lane_steps {ls} util {ls / max(1, 64 * ws):.3f}", flush=True)
 for i in range(a.batches):
     t0 = time.perf_counter()
     eng.check_batch_device(dq, len(q), da, de, sync=True)
