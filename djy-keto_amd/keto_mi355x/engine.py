@@ -209,3 +209,11 @@ class ExpandEngine:
                 continue
             check(rc)
             return nodes[: int(offs[n])], offs, err[:n]
+
+    def build_tree(self, ns: int, obj: int, rel: int, rest_depth: int = 0):
+        """expand.Engine.BuildTree (expand/engine.go:43-52) for one subject-set root:
+        the pre-order TREE_DT nodes, or None for a nil tree."""
+        nodes, offs, err = self.build_trees(np.array([(ns, obj, rel, rest_depth)], dtype=_abi.SUBJSET_DT))
+        if err[0]:
+            raise KetoError(int(err[0]), "expand failed")
+        return nodes[int(offs[0]):int(offs[1])] if offs[1] > offs[0] else None

@@ -201,3 +201,17 @@ def test_scratch_tiers(stream):
     np.testing.assert_array_equal(e, err)
     np.testing.assert_array_equal(a, dec)
     assert list(dec) == [1, 0, 1, 0, 0]
+
+
+def test_build_tree_single_root_matches_batch(stream):
+    fx = load("expand_engine")
+    w, t, _ = world_for(fx)
+    snap = product_snapshot(w, t)
+    eng = km.ExpandEngine(snap, stream, max_read_depth=fx.get("global", 5))
+    for e in [e for e in fx["expands"] if "subject" in e]:
+        ns, obj, rel = refsem.parse_subject_set(e["subject"])
+        got = eng.build_tree(w.ns_names.ids[ns], w.uuids.ids[obj], w.rel_names.ids[rel], e["depth"])
+        if e["tree"] is None:
+            assert got is None
+        else:
+            assert refsem.trees_equal_unordered(product_tree_to_nested(w, got), e["tree"])

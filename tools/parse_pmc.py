@@ -1,0 +1,39 @@
+"""Per-launch FETCH_SIZE / WRITE_SIZE of bench.py's dominant kernel (tier-0 launches of the
+uncounted Check interpreter) from tools/pmc_traffic.sh output -> JSON for bench.py."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+out_dir, dst = sys.argv[1], sys.argv[2]
+
+
+def per_launch(counter, sub):
+    files = glob.glob(f"{out_dir}/{sub}/**/*counter_collection.csv", recursive=True)
+    vals = defaultdict(float)  # (dispatch, kernel, grid) -> summed value
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            vals[(r["Dispatch_Id"], r["Kernel_Name"], int(r["Grid_Size"]))] += float(r["Counter_Value"])
+    # dominant kernel: the uncounted interpreter (<false, ...>) at its largest grid (tier 0)
+    cands = [(k, v) for k, v in vals.items() if "check" in k[1] and "<false" in k[1]]
+    gmax = max(k[2] for k, _ in cands)
+    sel = [v for k, v in cands if k[2] == gmax]
+    name = next(k[1] for k, _ in cands if k[2] == gmax)
+    return name, gmax, sel
+
+
+name, grid, fetch = per_launch("FETCH_SIZE", "fetch")
+_, _, write = per_launch("WRITE_SIZE", "write")
+# rocprofv3 reports both in KB; gfx950 FETCH_SIZE tallies 128-B requests at 64 B -> x2
+fetch_b = 2 * 1024 * sum(fetch) / len(fetch)
+write_b = 1024 * sum(write) / len(write)
+res = {"kernel": name, "grid": grid, "launches": [len(fetch), len(write)],
+       "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+       "traffic_bytes_per_launch": fetch_b + write_b,
+       "correction": "FETCH_SIZE x2 (gfx950: 128-B requests tallied at 64 B, MI355X_MICROARCH.md HBM); "
+                     "KB -> bytes x1024; Infinity-Cache hits are counted by these counters"}
+json.dump(res, open(dst, "w"), indent=1)
+print(json.dumps(res))
