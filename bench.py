@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """Headline benchmark: batched permission Check (BASELINE.json metric: checks/sec + p99
-batch latency) on MI355X.
+batch latency, 1B-tuple depth-10 graph) on MI355X.
 
-Default workload = BASELINE configs[1] (C2: nested-group graph, 10M tuples, union-only,
-max_read_depth 8, 2^20 queries per batch, 50% random-walk positives, 1% truncation
-sub-batch); `--workload c3` = configs[2] (Drive-style folder tree, ~105M tuples, depth 10,
-OPL union + intersection + exclusion through the rewrite interpreter).  One "step" = one
-batch of 2^20 Checks through the whole device pipeline (resolve pre-pass -> interpreter
-tiers -> decisions) with the queries already resident in HBM.
+Workloads:
+  c4 (default) = configs[3]: Drive-style folder forest x10 -- ~1.05B tuples, fanout 5,
+      depth 10, OPL union + intersection + exclusion through the rewrite interpreter,
+      max_read_depth 16.  The configuration the metric is quoted on; it fits one GPU.
+  c3 = configs[2]: the same forest x1 (~105M tuples).
+  c2 = configs[1]: nested-group graph, 10M tuples, union-only, max_read_depth 8.
+One "step" = one batch of 2^20 Checks per GPU through the whole device pipeline (resolve
+pre-pass -> interpreter tiers -> decisions) with the queries already resident in HBM.
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`): every rank builds the same
-replica (queries shard naturally); each rank checks its own
-2^20-query batch per step, no collective on the data path; timing = max over ranks.
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): the graph is replicated on every GPU
+and the query stream shards by rank (no collective on the data path).  For c3/c4 rank 0
+generates the tuples and broadcasts them over RCCL/xGMI; every rank builds its replica on its
+own device (keto_snapshot_build_device).  Timing = max over ranks; value = all ranks' checks
+/ that time.
 """
 import argparse
 import glob
@@ -26,15 +30,25 @@ sys.path.insert(0, os.path.join(ROOT, "djy-keto_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "checks/sec (node) + p99 batch latency, 1B-tuple depth-10 graph, 1/2/4/8 GPU"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))  # the GPU box grants 16 host cores per GPU
+
+
 def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0):
-    """The oracle (C restatement of the reference, oracle/refsem.c) on the host cores,
-    on a bounded sample of the same batch -- reported beside the GPU, never the target."""
+    """The oracle (C restatement of the reference, oracle/refsem.c) on the host cores, on a
+    bounded sample of the same batch over the same graph -- reported beside the GPU, never
+    the target.  The oracle indexes the engine's tuple records in place (no copy)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refsem
 
@@ -45,24 +59,11 @@ def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0):
     for r in wl.rel_names:
         w.rel_names(r)
     w._walk_names()
-    t = np.zeros(len(wl.tuples), dtype=refsem.TUPLE_DT)
-    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
-                 ("sns", "s_ns"), ("srel", "s_rel")):
-        t[a] = wl.tuples[b]
-    sb = wl.tuples["shard_id"]
-    t["shard_hi"] = sb[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
-    t["shard_lo"] = sb[:, 8:].copy().view(">u8").reshape(-1).astype(np.uint64)
-    orc = refsem.Oracle(w, t)
-    del t
-    q = np.zeros(len(queries), dtype=refsem.QUERY_DT)
-    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
-                 ("sns", "s_ns"), ("srel", "s_rel"), ("depth", "max_depth")):
-        q[a] = queries[b]
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))  # the GPU box grants 16 host cores per GPU
+    cores = cpu_threads()
+    t0 = time.perf_counter()
+    orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+    build_s = time.perf_counter() - t0
+    q = np.ascontiguousarray(queries).view(refsem.QUERY_DT)
     n = 1 << 12
     while True:
         t0 = time.perf_counter()
@@ -73,8 +74,9 @@ def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0):
         n = min(len(q), int(n * max(2.0, min(8.0, budget_s / 2.5 / max(dt, 1e-3)))))
     orc.close()
     return {"value": n / dt, "unit": "checks/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} of the {len(q)}-query batch, oracle/refsem.c (C restatement of "
-                      f"internal/check + persistence/sql read path), {cores} threads, {dt:.2f} s"}, dec
+            "sample": f"first {n} of the {len(q)}-query batch over the full {len(wl.tuples)}-tuple graph, "
+                      f"oracle/refsem.c (C restatement of internal/check + persistence/sql read path), "
+                      f"{cores} threads, {dt:.2f} s (index build {build_s:.1f} s, untimed)"}, dec
 
 
 def job_rate(elapsed_local: float, units_local: int, device: str = "cpu"):
@@ -98,12 +100,55 @@ def shard_seed(base: int, rank: int) -> int:
     return base + rank
 
 
+def broadcast_tuples(host_tuples, n_bytes: int, device: int, rank: int):
+    """rank 0's tuple records -> a uint8 tensor on every rank's GPU (RCCL broadcast over xGMI,
+    in 1 GiB pieces)."""
+    import torch
+    import torch.distributed as dist
+
+    buf = torch.empty(n_bytes, dtype=torch.uint8, device=f"cuda:{device}")
+    if rank == 0:
+        buf.copy_(torch.from_numpy(host_tuples.view(np.uint8).reshape(-1)))
+    piece = 1 << 30
+    for off in range(0, n_bytes, piece):
+        dist.broadcast(buf[off:off + piece], src=0)
+    torch.cuda.synchronize(device)
+    return buf
+
+
+def build_workload(name, rank, world, device, args):
+    import keto_mi355x as km
+    from keto_mi355x import synth
+
+    t0 = time.perf_counter()
+    if name == "c2":
+        wl = synth.nested_groups(args.tuples, seed=1)  # cheap: every rank generates its replica
+        snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict,
+                           device=device)
+        return wl, snap, time.perf_counter() - t0
+    scale = 10 if name == "c4" else 1
+    wl = synth.drive_scaled(scale, materialize=(rank == 0))
+    if world == 1:
+        snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict,
+                           device=device)
+    else:
+        import torch
+
+        nt = wl.meta["n_tuples"]
+        buf = broadcast_tuples(wl.tuples, nt * km.TUPLE_DT.itemsize, device, rank)
+        snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict,
+                           device=device, device_tuples=(buf.data_ptr(), nt))
+        del buf
+        torch.cuda.empty_cache()
+    return wl, snap, time.perf_counter() - t0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["c2", "c3"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c4")
     ap.add_argument("--tuples", type=int, default=10_000_000, help="C2 graph size")
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--latency-batch", type=int, default=1 << 16)
@@ -119,24 +164,23 @@ def main():
     import torch.distributed as dist
 
     dist_on = world > 1
+    # one process per GPU; KETO_BENCH_BACKEND=gloo rehearses the multi-rank path with several
+    # ranks sharing one GPU (RCCL needs distinct devices)
+    device = local % max(1, torch.cuda.device_count())
     if dist_on:
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")
+        import datetime
+
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend=os.environ.get("KETO_BENCH_BACKEND", "nccl"),
+                                timeout=datetime.timedelta(minutes=30))
     import keto_mi355x as km
     from keto_mi355x import synth
 
-    device = local
-    t0 = time.perf_counter()
-    if args.workload == "c2":
-        wl = synth.nested_groups(args.tuples, seed=1)  # identical replica on every rank
-    else:
-        wl = synth.drive(seed=3)
-    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict,
-                       device=device)
+    wl, snap, setup_s = build_workload(args.workload, rank, world, device, args)
     info = snap.info()
     log(f"[rank {rank}] snapshot: {info['n_tuples']} tuples, {info['n_nodes']} nodes, "
-        f"{info['device_bytes'] / 2**20:.0f} MiB on device, build {info['build_seconds']:.2f}s "
-        f"(total setup {time.perf_counter() - t0:.1f}s)")
+        f"{info['device_bytes'] / 2**30:.1f} GiB on device, device build {info['build_seconds']:.2f}s "
+        f"(setup incl. generation {setup_s:.1f}s)")
     stream = km.Stream(device)
     eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
     # this rank's shard of the query stream: its own seeded 2^20 batch
@@ -177,23 +221,21 @@ def main():
         dist.barrier()
     elapsed_local = time.perf_counter() - t_start
     value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps,
-                                     f"cuda:{local}" if dist_on else "cpu")
+                                     f"cuda:{device}" if dist_on else "cpu")
     kernel_ms = float(np.mean(kms))
 
-    # p99 batch latency over >= 100 batches of 64Ki queries (one rank's stream)
     # PCIe-inclusive rate (host buffers: H2D queries, kernels, D2H decisions) -- never `value`
     t1 = time.perf_counter()
     for _ in range(3):
         eng.check_batch(q)
     pcie_rate = 3 * len(q) / (time.perf_counter() - t1)
-
+    # p99 batch latency over >= 100 batches of 64Ki queries (one rank's stream)
     lat = []
     nl = min(args.latency_batch, len(q))
+    dql = km.DeviceBuffer(device, q[:nl].nbytes)
     for i in range(args.latency_iters):
         off = (i * nl) % max(1, len(q) - nl + 1)
-        ql = q[off:off + nl]
-        dql = km.DeviceBuffer(device, ql.nbytes) if i == 0 else dql
-        dql.upload(stream, ql)
+        dql.upload(stream, q[off:off + nl])
         stream.sync()
         t1 = time.perf_counter()
         eng.check_batch_device(dql, nl, da, de, sync=True)
@@ -208,8 +250,17 @@ def main():
         t = json.load(open(tf[-1]))
         if kname in t.get("kernel", "") and int(t.get("grid", 0)) > 0:
             traffic = t["traffic_bytes_per_launch"]
+    if args.workload == "c2":
+        data, cfgno = "nested-group graph", 2
+        desc = (f"C2 nested groups: {info['n_tuples']} tuples, 5 levels, union-only, max_read_depth 8, "
+                f"{args.batch} checks/batch/GPU, 50% random-walk positives, 1% depth 1-4")
+    else:
+        data, cfgno = "Drive-style folder forest", 4 if args.workload == "c4" else 3
+        desc = (f"{args.workload.upper()} Drive-style: {info['n_tuples']} tuples, {wl.meta['roots']} forest(s) of fanout 5, "
+                f"depth 10, view = (viewers | editors | owners | parents.traverse(view)) & !banned, "
+                f"max_read_depth 16, {args.batch} checks/batch/GPU")
     out = {
-        "metric": "checks/sec (node) + p99 batch latency, 1B-tuple depth-10 graph, 1/2/4/8 GPU",
+        "metric": METRIC,
         "value": value,
         "unit": "checks/s",
         "n_gpus": world,
@@ -220,19 +271,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (seeded PCG64 %s, BASELINE config %d)" % (
-            ("nested-group graph", 2) if args.workload == "c2" else ("Drive-style folder tree", 3)),
-        "config": {"workload": (f"C2 nested groups: {info['n_tuples']} tuples, 5 levels, union-only, max_read_depth 8, "
-                                f"{args.batch} checks/batch/GPU, 50% random-walk positives, 1% depth 1-4")
-                   if args.workload == "c2" else
-                   (f"C3 Drive-style: {info['n_tuples']} tuples, fanout 5, depth 10, view = (viewers | editors | "
-                    f"owners | parents.traverse(view)) & !banned, max_read_depth 16, {args.batch} checks/batch/GPU"),
-                   "tuples": int(info["n_tuples"]), "batch_per_gpu": args.batch,
+        "data": f"synthetic (seeded {data}, BASELINE config {cfgno}; generated on the host, no dataset)",
+        "config": {"workload": desc, "tuples": int(info["n_tuples"]), "batch_per_gpu": args.batch,
                    "parallelism": f"replica x{world} (query batch sharded, no data-path collective)"},
         "p99_batch_latency_ms": p99_ms,
         "latency_batch": nl,
         "allowed_fraction": float(allowed.mean()),
         "pcie_inclusive_checks_per_s": pcie_rate,
+        "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kname + " (tier 0)", "kernel_ms": kernel_ms,

@@ -90,7 +90,16 @@ int keto_snapshot_build(const keto_snapshot_config *cfg, const keto_tuple *tuple
     if (!out) return fail(KETO_E_INVALID, "null output pointer");
     *out = nullptr;
     return guarded([&] {
-        *out = reinterpret_cast<keto_snapshot *>(keto::build_snapshot(cfg, tuples, n));
+        *out = reinterpret_cast<keto_snapshot *>(keto::build_snapshot(cfg, tuples, n, false));
+    });
+}
+
+int keto_snapshot_build_device(const keto_snapshot_config *cfg, const keto_tuple *device_tuples, uint64_t n,
+                               keto_snapshot **out) {
+    if (!out) return fail(KETO_E_INVALID, "null output pointer");
+    *out = nullptr;
+    return guarded([&] {
+        *out = reinterpret_cast<keto_snapshot *>(keto::build_snapshot(cfg, device_tuples, n, true));
     });
 }
 
@@ -116,7 +125,8 @@ int keto_stream_create(int32_t device, keto_stream **out) {
         KETO_HIP(hipEventCreate(&s->ev0));
         KETO_HIP(hipEventCreate(&s->ev1));
         KETO_HIP(hipMalloc(&s->counters, 24 * sizeof(unsigned long long)));
-        KETO_HIP(hipMemset(s->counters, 0, 24 * sizeof(unsigned long long)));
+        KETO_HIP(hipMemsetAsync(s->counters, 0, 24 * sizeof(unsigned long long), s->stream));
+        KETO_HIP(hipStreamSynchronize(s->stream));
         *out = reinterpret_cast<keto_stream *>(s.release());
     });
 }
@@ -143,8 +153,8 @@ int keto_stream_counters(keto_stream *hs, keto_work_counters *out, int32_t reset
     return guarded([&] {
         KETO_HIP(hipSetDevice(s->device));
         unsigned long long c[24];
+        KETO_HIP(hipMemcpyAsync(c, s->counters, sizeof c, hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipStreamSynchronize(s->stream));
-        KETO_HIP(hipMemcpy(c, s->counters, sizeof c, hipMemcpyDeviceToHost));
         if (out)
             for (int t = 0; t < 3; t++) {
                 out->rows[t] = c[8 * t + 0];
@@ -155,7 +165,10 @@ int keto_stream_counters(keto_stream *hs, keto_work_counters *out, int32_t reset
                 out->wave_steps[t] = c[8 * t + 5];
                 out->lane_steps[t] = c[8 * t + 6];
             }
-        if (reset) KETO_HIP(hipMemset(s->counters, 0, sizeof c));
+        if (reset) {  // stream-ordered: later kernels on this (non-blocking) stream see the zeros
+            KETO_HIP(hipMemsetAsync(s->counters, 0, sizeof c, s->stream));
+            KETO_HIP(hipStreamSynchronize(s->stream));
+        }
     });
 }
 

@@ -28,6 +28,18 @@ __device__ __forceinline__ uint32_t pick(const uint32_t *a, uint32_t i, const ui
     return wword(v, (uint32_t)((reinterpret_cast<uintptr_t>(a + i) >> 2) & 3));
 }
 
+// (ns, obj) -> entity id through the rank table (one 16-byte load); NONE32 if the object holds
+// no tuple in ns (the caller then uses the namespace's phantom entity)
+__device__ __forceinline__ uint32_t ent_lookup(const DevSnapshot &s, uint32_t ns, uint32_t obj) {
+    if (ns >= s.n_ns || obj >= s.n_uuids) return NONE32;
+    const uint64_t ck = (uint64_t)ns * s.ent_stride + obj;
+    const uint4 b = s.ent_rank[ck >> 6];
+    const uint64_t m = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    const uint32_t j = (uint32_t)(ck & 63);
+    if (!((m >> j) & 1ull)) return NONE32;
+    return b.z + (uint32_t)__popcll(m & ((1ull << j) - 1ull));
+}
+
 // Small per-snapshot tables (namespace table, relation info, rewrite program) staged in LDS.
 struct Tables {
     const NsDev *ns;

@@ -46,7 +46,51 @@ struct Snapshot {
     uint32_t ns_of(uint32_t node) const;
 };
 
-Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n);
+Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples);
+
+// build.hip: device-side snapshot construction (one-thread-per-item kernels)
+namespace build {
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t b);  // hipMalloc(b + 16): 16-byte window loads past the end stay in bounds
+    ~DevBuf();
+    DevBuf(DevBuf &&o) noexcept;
+    DevBuf &operator=(DevBuf &&o) noexcept;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    void reset();
+    void *release();
+    uint32_t *u32() const { return static_cast<uint32_t *>(p); }
+};
+void scan_excl(uint32_t *v, uint64_t n);  // v[0..n) -> exclusive prefix sums, v[n] = total
+uint32_t read_u32(const uint32_t *d, uint64_t i);
+void validate(const keto_tuple *t, uint64_t n, uint32_t n_ns, uint32_t n_rel_caller, uint32_t n_uuids, uint32_t n_rel,
+              uint32_t *used, unsigned long long *bad);
+void entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride, unsigned long long *bits, uint64_t nblk,
+                 uint32_t *rank);
+void entity_ids(const unsigned long long *bits, uint32_t *rank, uint64_t nblk, uint64_t bpn, uint64_t stride,
+                const uint32_t *ent_base, const uint32_t *rank0, uint32_t *ent_obj, uint4 *table);
+struct RowsIn {
+    const keto_tuple *tuples;       // device copy
+    const keto_tuple *host_tuples;  // caller's host array, or null (very long rows are sorted on the host)
+    uint64_t n, n_nodes, n_subj;
+    const unsigned long long *bits;
+    const uint32_t *rank;
+    const NsDev *ns;
+    const uint32_t *slot_of;
+    uint64_t stride;
+    uint32_t n_rel, n_uuids;
+};
+struct RowsOut {
+    uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *set_row, *weight;  // caller-allocated
+    DevBuf set_dst, probe;
+    uint64_t n_set = 0, probe_buckets = 0;
+};
+void rows(const RowsIn &in, RowsOut &out);
+void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey);
+}  // namespace build
 
 // scratch tier: per-lane visited capacity (slots, pow2) and stack frames
 struct Tier {

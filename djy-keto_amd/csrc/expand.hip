@@ -16,19 +16,7 @@ __device__ __forceinline__ uint32_t node_ri(const DevSnapshot &s, uint32_t node)
 
 __device__ __forceinline__ uint32_t resolve_node(const DevSnapshot &s, uint32_t ns, uint32_t obj, uint32_t rel) {
     if (ns >= s.n_ns) return VIRT_BIT | (0x7FFFu << 16) | 0xFFFFu;
-    const uint64_t key = (((uint64_t)ns << 32) | obj) + 1;
-    uint32_t h = (uint32_t)mix64(key) & s.ent_mask;
-    uint32_t e = NONE32;
-    for (uint32_t probe = 0; probe <= s.ent_mask; probe++) {
-        const uint4 slot = s.ent_table[h];
-        const uint64_t k = (uint64_t)slot.x | ((uint64_t)slot.y << 32);
-        if (k == key) {
-            e = slot.z;
-            break;
-        }
-        if (k == 0) break;
-        h = (h + 1) & s.ent_mask;
-    }
+    uint32_t e = ent_lookup(s, ns, obj);
     if (e == NONE32) e = s.ns[ns + 1].ent_base - 1;  // phantom entity: no tuples
     return t_node(global_tables(s), ns, e, rel);
 }

@@ -72,10 +72,10 @@ struct DevSnapshot {
     const uint32_t *nsrel;     // [n_ns * n_rel]
     const Op *ops;
     const uint32_t *op_children;
-    // (ns, obj) -> entity, open addressing over 16-byte slots {key lo, key hi, entity, 0};
-    // key = ((ns<<32)|obj)+1, 0 = empty
-    const uint4 *ent_table;
-    uint32_t ent_mask;
+    // (ns, obj) -> entity rank table: block b covers ids [64b, 64b+64) of ck = ns*ent_stride+obj,
+    // {set bits lo, hi, entity of the block's first set bit, 0}; an unset bit = no entity
+    const uint4 *ent_rank;
+    uint64_t ent_stride;
     // membership probe hash for "heavy" subjects (reverse row longer than probe_k):
     // 16-byte buckets of two keys ((subject_idx<<32)|node)+1, linear probing over buckets
     const uint4 *probe;

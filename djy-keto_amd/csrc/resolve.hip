@@ -3,7 +3,7 @@
 //
 // Per query (one lane each, no persistent loop -- every step is a fixed handful of
 // independent loads, so plain oversubscription hides the latency):
-//   * root node of (namespace, object, relation): entity hash, phantom entity for objects
+//   * root node of (namespace, object, relation): entity rank table, phantom entity for objects
 //     that hold no tuple, virtual node for unconfigured namespaces / relations
 //     (engine.go:76-100 resolution of the request tuple);
 //   * subject index: subject id, or the node of a subject set (no phantom: a set that holds
@@ -53,29 +53,11 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
         int32_t d0 = (int32_t)b.w;
         if (d0 <= 0 || P.max_depth < d0) d0 = P.max_depth;
         const uint32_t d = (uint32_t)std::min<int32_t>(d0, 0xFFFF);  // deeper walks overflow every scratch tier
-        // root and subject-set entities: both hash walks advance in the same iterations
-        const bool want_r = qns < s.n_ns, want_s = qkind == 1 && qsns < s.n_ns;
-        const uint64_t kr = (((uint64_t)qns << 32) | qobj) + 1, ks = (((uint64_t)qsns << 32) | qsobj) + 1;
-        uint32_t hr = (uint32_t)mix64(kr) & s.ent_mask, hs = (uint32_t)mix64(ks) & s.ent_mask;
-        uint32_t er = NONE32, es = NONE32;
-        bool run_r = want_r, run_s = want_s;
-        while (run_r || run_s) {
-            uint4 vr = make_uint4(0, 0, 0, 0), vs = make_uint4(0, 0, 0, 0);
-            if (run_r) vr = s.ent_table[hr];
-            if (run_s) vs = s.ent_table[hs];
-            if (run_r) {
-                const uint64_t k = (uint64_t)vr.x | ((uint64_t)vr.y << 32);
-                if (k == kr) er = vr.z;
-                if (k == kr || k == 0) run_r = false;
-                else hr = (hr + 1) & s.ent_mask;
-            }
-            if (run_s) {
-                const uint64_t k = (uint64_t)vs.x | ((uint64_t)vs.y << 32);
-                if (k == ks) es = vs.z;
-                if (k == ks || k == 0) run_s = false;
-                else hs = (hs + 1) & s.ent_mask;
-            }
-        }
+        // root and subject-set entities: two independent rank-table loads
+        const bool want_r = qns < s.n_ns;
+        const uint32_t er0 = ent_lookup(s, qns, qobj);
+        const uint32_t es = qkind == 1 ? ent_lookup(s, qsns, qsobj) : NONE32;
+        uint32_t er = er0;
         uint32_t root = VIRT_BIT | (0x7FFFu << 16) | 0xFFFFu;  // unknown namespace
         if (want_r) {
             if (er == NONE32) er = T.ns[qns + 1].ent_base - 1;  // phantom entity: holds no tuple

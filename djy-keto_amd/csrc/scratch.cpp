@@ -27,6 +27,9 @@ void ensure_scratch(Scratch &sc, const Tier t[3]) {
     for (int i = 0; i < 3; i++) bytes += align256((size_t)t[i].lanes * t[i].vcap * 8ull) + align256((size_t)t[i].lanes * t[i].scap * 16ull);
     KETO_HIP(hipMalloc(&sc.mem, bytes));
     KETO_HIP(hipMemset(sc.mem, 0, bytes));
+    // the interpreters run on non-blocking streams, which do not wait for the null stream:
+    // the zero fill must be complete before any of them can read an epoch or visited slot
+    KETO_HIP(hipDeviceSynchronize());
     sc.bytes = bytes;
     char *p = static_cast<char *>(sc.mem);
     sc.ctrl = reinterpret_cast<uint32_t *>(p);

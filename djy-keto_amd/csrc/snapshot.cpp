@@ -10,10 +10,12 @@
 // and compiles the namespace AST (internal/namespace/ast) into a flat op table.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <numeric>
 #include <thread>
 #include <unordered_map>
+#include <cstdlib>
 
 #include "engine.hpp"
 #include "json.hpp"
@@ -21,41 +23,6 @@
 namespace keto {
 
 namespace {
-
-template <class T>
-void parallel_sort(std::vector<T> &v) {
-    const size_t n = v.size();
-    unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (n < (1u << 20) || hw == 1) {
-        std::sort(v.begin(), v.end());
-        return;
-    }
-    size_t parts = 1;
-    while (parts * 2 <= hw) parts *= 2;
-    std::vector<size_t> bounds(parts + 1);
-    for (size_t i = 0; i <= parts; i++) bounds[i] = n * i / parts;
-    std::vector<std::thread> th;
-    for (size_t i = 0; i < parts; i++)
-        th.emplace_back([&, i] { std::sort(v.begin() + bounds[i], v.begin() + bounds[i + 1]); });
-    for (auto &t : th) t.join();
-    for (size_t w = 1; w < parts; w *= 2) {
-        std::vector<std::thread> mt;
-        for (size_t i = 0; i + w < parts; i += 2 * w) {
-            size_t a = bounds[i], m = bounds[i + w], b = bounds[std::min(parts, i + 2 * w)];
-            mt.emplace_back([&v, a, m, b] { std::inplace_merge(v.begin() + a, v.begin() + m, v.begin() + b); });
-        }
-        for (auto &t : mt) t.join();
-    }
-}
-
-uint64_t mix64(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdULL;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ULL;
-    x ^= x >> 33;
-    return x;
-}
 
 struct Decl {
     uint32_t rel;
@@ -130,19 +97,6 @@ struct Compiler {
 };
 
 template <class T>
-T *upload(Snapshot &s, const std::vector<T> &v, size_t min_elems = 1) {
-    // padded to 16 bytes (+16) so 16-byte window loads past the end stay in bounds
-    size_t bytes = (std::max(v.size(), min_elems) * sizeof(T) + 31) / 16 * 16;
-    void *p = nullptr;
-    KETO_HIP(hipMalloc(&p, bytes));
-    s.allocs.push_back(p);
-    KETO_HIP(hipMemset(p, 0, bytes));
-    if (!v.empty()) KETO_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    s.info.device_bytes += bytes;
-    return static_cast<T *>(p);
-}
-
-template <class T>
 uint32_t bytes16(const std::vector<T> &v) {
     return (uint32_t)((v.size() * sizeof(T) + 15) / 16 * 16);
 }
@@ -165,7 +119,7 @@ uint32_t Snapshot::ns_of(uint32_t node) const {
     return lo;
 }
 
-Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n) {
+Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples) {
     auto t0 = std::chrono::steady_clock::now();
     if (!cfg) throw Error(KETO_E_INVALID, "null config");
     if (n && !tuples) throw Error(KETO_E_INVALID, "null tuples");
@@ -230,18 +184,63 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         if (it != C.rel_ids.end()) empty_rel = it->second;
     }
 
+    // Everything below scales to ~1B tuples (BASELINE config 4): the tuples are uploaded once
+    // and every pass over them runs on the device (build.hip); the host keeps the small tables.
+    const bool verbose = getenv("KETO_BUILD_VERBOSE") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto phase = [&](const char *what) {
+        if (!verbose) return;
+        KETO_HIP(hipDeviceSynchronize());
+        auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[keto build] %-14s %.3f s\n", what, std::chrono::duration<double>(now - tp).count());
+        tp = now;
+    };
+    using build::DevBuf;
+    // final device arrays: zero-filled, 16 bytes of slack for window loads past the end
+    auto dalloc = [&](size_t bytes) -> void * {
+        bytes = (bytes + 31) / 16 * 16;
+        void *p = nullptr;
+        KETO_HIP(hipMalloc(&p, bytes));
+        s.allocs.push_back(p);
+        KETO_HIP(hipMemset(p, 0, bytes));
+        s.info.device_bytes += bytes;
+        return p;
+    };
+    auto adopt = [&](DevBuf &b) -> void * {
+        s.info.device_bytes += b.bytes;
+        s.allocs.push_back(b.p);
+        return b.release();
+    };
+
     // ---- validate tuples, collect (ns, rel) pairs ------------------------------
     const size_t NR = (size_t)s.n_ns * s.n_rel;
     if (NR > (1ull << 28)) throw Error(KETO_E_LIMIT, "n_namespaces * n_relations too large");
-    std::vector<uint8_t> used(NR, 0);
-    for (uint64_t i = 0; i < n; i++) {
-        const keto_tuple &t = tuples[i];
-        if (t.ns >= s.n_ns || t.rel >= s.n_rel_caller || t.obj >= s.n_uuids || t.s_obj >= s.n_uuids || t.subj_kind > 1 ||
-            (t.subj_kind == 1 && (t.s_ns >= s.n_ns || t.s_rel >= s.n_rel_caller)))
-            throw Error(KETO_E_INVALID, "tuple " + std::to_string(i) + " has an out-of-range id");
-        used[(size_t)t.ns * s.n_rel + t.rel] = 1;
-        if (t.subj_kind == 1) used[(size_t)t.s_ns * s.n_rel + t.s_rel] = 1;
+    if (n >= (1ull << 32)) throw Error(KETO_E_LIMIT, "more than 2^32 tuples");
+    // tuples resident in HBM: uploaded once here, or already there (keto_snapshot_build_device:
+    // e.g. a replica received over RCCL from the rank that loaded the store)
+    DevBuf d_t;
+    const keto_tuple *dt = tuples;
+    if (!device_tuples) {
+        d_t = DevBuf(sizeof(keto_tuple) * n);
+        if (n) KETO_HIP(hipMemcpy(d_t.p, tuples, sizeof(keto_tuple) * n, hipMemcpyHostToDevice));
+        dt = static_cast<const keto_tuple *>(d_t.p);
     }
+    phase("upload");
+    std::vector<uint8_t> used(NR, 0);
+    {
+        DevBuf d_used(4 * NR), d_bad(8);
+        KETO_HIP(hipMemset(d_used.p, 0, 4 * NR));
+        KETO_HIP(hipMemset(d_bad.p, 0xFF, 8));
+        if (n) build::validate(dt, n, s.n_ns, s.n_rel_caller, s.n_uuids, s.n_rel, d_used.u32(),
+                               static_cast<unsigned long long *>(d_bad.p));
+        unsigned long long bad = 0;
+        KETO_HIP(hipMemcpy(&bad, d_bad.p, 8, hipMemcpyDeviceToHost));
+        if (bad != ~0ull) throw Error(KETO_E_INVALID, "tuple " + std::to_string(bad) + " has an out-of-range id");
+        std::vector<uint32_t> u(NR);
+        KETO_HIP(hipMemcpy(u.data(), d_used.p, 4 * NR, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < NR; i++) used[i] = u[i] != 0;
+    }
+    phase("validate");
 
     // ---- relation slots + status (namespace.ASTRelationFor, definitions.go:37-62) -------
     s.nsrel.assign(NR, 0);
@@ -299,20 +298,24 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
             s.relinfo[s.ns[ns].slot_base + k] = make_ri(rw ? decl->op : NO_OP, rw, ss, status, false);
         }
 
-    // ---- entities: (ns, obj) of tuple objects and subject-set objects -----------------
-    std::vector<uint64_t> ek;
-    ek.reserve(n + n / 2);
-    for (uint64_t i = 0; i < n; i++) {
-        ek.push_back(((uint64_t)tuples[i].ns << 32) | tuples[i].obj);
-        if (tuples[i].subj_kind == 1) ek.push_back(((uint64_t)tuples[i].s_ns << 32) | tuples[i].s_obj);
-    }
-    parallel_sort(ek);
-    ek.erase(std::unique(ek.begin(), ek.end()), ek.end());
-    std::vector<uint32_t> n_real(s.n_ns, 0);
-    for (uint64_t k : ek) n_real[k >> 32]++;
+    // ---- entities: rank table over (ns, obj) -------------------------------------------
+    // bit ns*stride + obj is set when (ns, obj) is a tuple object or a subject-set object.
+    // Entities of a namespace are its set bits in uuid order (+ one phantom at the end); a
+    // 16-byte block {bits lo, bits hi, entity of the block's first set bit, 0} answers
+    // (ns, obj) -> entity with one load (resolve / expand kernels, and the build itself).
+    const uint64_t stride = ((uint64_t)s.n_uuids + 63) / 64 * 64;
+    const uint64_t nblk = (uint64_t)s.n_ns * stride / 64, bpn = stride / 64;
+    if (nblk > (1ull << 31)) throw Error(KETO_E_LIMIT, "n_namespaces * n_uuids exceeds the entity rank table (2^37 ids)");
+    DevBuf d_bits(8 * nblk), d_rank(4 * (nblk + 1));
+    KETO_HIP(hipMemset(d_bits.p, 0, 8 * nblk));
+    build::entity_bits(dt, n, stride, static_cast<unsigned long long *>(d_bits.p), nblk, d_rank.u32());
+    std::vector<uint32_t> n_real(s.n_ns, 0), rank0(s.n_ns + 1);
+    for (uint32_t ns = 0; ns <= s.n_ns; ns++) rank0[ns] = build::read_u32(d_rank.u32(), ns * bpn);
     uint64_t ent_total = 0, node_total = 0;
+    std::vector<uint32_t> ent_base(s.n_ns);
     for (uint32_t ns = 0; ns < s.n_ns; ns++) {
-        s.ns[ns].ent_base = (uint32_t)ent_total;
+        n_real[ns] = rank0[ns + 1] - rank0[ns];
+        s.ns[ns].ent_base = ent_base[ns] = (uint32_t)ent_total;
         s.ns[ns].node_base = (uint32_t)node_total;
         uint64_t ne = (uint64_t)n_real[ns] + 1;  // + phantom
         ent_total += ne;
@@ -322,115 +325,59 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     s.ns[s.n_ns] = NsDev{(uint32_t)ent_total, (uint32_t)node_total, 0, total_slots};
     const uint32_t N = (uint32_t)node_total;
     if ((uint64_t)s.n_uuids + N + 1 >= (1ull << 32)) throw Error(KETO_E_LIMIT, "n_uuids + nodes exceeds 2^32");
-    s.ent_obj.assign(ent_total, NONE32);
-    // entity hash: ((ns<<32)|obj)+1 -> entity
-    uint64_t cap = 16;
-    while (cap < 2 * ek.size() + 2) cap <<= 1;
-    std::vector<unsigned long long> ent_keys(cap, 0);
-    std::vector<uint32_t> ent_vals(cap, 0);  // host lookup copies; device gets 16-byte slots
+    DevSnapshot &D = s.dev;
     {
-        std::vector<uint32_t> fill(s.n_ns, 0);
-        for (uint64_t k : ek) {
-            uint32_t ns = (uint32_t)(k >> 32);
-            uint32_t e = s.ns[ns].ent_base + fill[ns]++;
-            s.ent_obj[e] = (uint32_t)k;
-            uint64_t h = mix64(k + 1) & (cap - 1);
-            while (ent_keys[h]) h = (h + 1) & (cap - 1);
-            ent_keys[h] = k + 1;
-            ent_vals[h] = e;
-        }
+        DevBuf d_eb(4 * s.n_ns), d_r0(4 * s.n_ns), d_eo(4 * ent_total);
+        KETO_HIP(hipMemcpy(d_eb.p, ent_base.data(), 4 * s.n_ns, hipMemcpyHostToDevice));
+        KETO_HIP(hipMemcpy(d_r0.p, rank0.data(), 4 * s.n_ns, hipMemcpyHostToDevice));
+        KETO_HIP(hipMemset(d_eo.p, 0xFF, 4 * ent_total));  // phantoms: NONE32
+        uint4 *table = static_cast<uint4 *>(dalloc(16 * nblk));
+        build::entity_ids(static_cast<unsigned long long *>(d_bits.p), d_rank.u32(), nblk, bpn, stride, d_eb.u32(),
+                          d_r0.u32(), d_eo.u32(), table);
+        D.ent_rank = table;
+        D.ent_stride = stride;
+        s.ent_obj.resize(ent_total);
+        KETO_HIP(hipMemcpy(s.ent_obj.data(), d_eo.p, 4 * ent_total, hipMemcpyDeviceToHost));
     }
-    auto ent_lookup = [&](uint32_t ns, uint32_t obj) -> uint32_t {
-        uint64_t key = (((uint64_t)ns << 32) | obj) + 1;
-        uint64_t h = mix64(key) & (cap - 1);
-        while (ent_keys[h]) {
-            if (ent_keys[h] == key) return ent_vals[h];
-            h = (h + 1) & (cap - 1);
-        }
-        return NONE32;
-    };
-    auto node_of = [&](uint32_t ns, uint32_t e, uint32_t rel) -> uint32_t {
-        uint32_t slot = slot_of[(size_t)ns * s.n_rel + rel];
-        return s.ns[ns].node_base + (e - s.ns[ns].ent_base) * s.ns[ns].n_slots + slot;
-    };
+    phase("entities");
 
-    // ---- shard order rank (ORDER BY shard_id, UUID bytes big-endian) --------------------
-    std::vector<uint32_t> src(n), dst(n), rank(n);
-    {
-        struct SK {
-            uint64_t hi, lo;
-            uint32_t idx;
-            bool operator<(const SK &o) const { return hi != o.hi ? hi < o.hi : (lo != o.lo ? lo < o.lo : idx < o.idx); }
-        };
-        std::vector<SK> sk(n);
-        for (uint64_t i = 0; i < n; i++) {
-            uint64_t hi = 0, lo = 0;
-            for (int b = 0; b < 8; b++) hi = (hi << 8) | tuples[i].shard_id[b];
-            for (int b = 8; b < 16; b++) lo = (lo << 8) | tuples[i].shard_id[b];
-            sk[i] = SK{hi, lo, (uint32_t)i};
-        }
-        parallel_sort(sk);
-        for (uint64_t r = 0; r < n; r++) rank[sk[r].idx] = (uint32_t)r;
-    }
-    for (uint64_t i = 0; i < n; i++) {
-        const keto_tuple &t = tuples[i];
-        src[i] = node_of(t.ns, ent_lookup(t.ns, t.obj), t.rel);
-        dst[i] = t.subj_kind == 1 ? node_of(t.s_ns, ent_lookup(t.s_ns, t.s_obj), t.s_rel) : t.s_obj;
-    }
-
-    // ---- rows: (node, shard rank) sorted ----------------------------------------------
-    std::vector<uint32_t> by_rank(n);
-    for (uint64_t i = 0; i < n; i++) by_rank[rank[i]] = (uint32_t)i;
-    std::vector<uint32_t> set_off(N + 1, 0), all_off(N + 1, 0), set_dst, all_subj;
-    {
-        std::vector<uint64_t> keys;
-        keys.reserve(n);
-        for (uint64_t i = 0; i < n; i++) keys.push_back(((uint64_t)src[i] << 32) | rank[i]);
-        parallel_sort(keys);
-        all_subj.resize(n);
-        uint64_t n_set = 0;
-        for (uint64_t i = 0; i < n; i++) n_set += tuples[i].subj_kind == 1;
-        set_dst.resize(n_set);
-        uint64_t si = 0;
-        for (uint64_t i = 0; i < n; i++) {
-            uint32_t node = (uint32_t)(keys[i] >> 32);
-            uint32_t ti = by_rank[(uint32_t)keys[i]];
-            all_off[node + 1]++;
-            bool is_set = tuples[ti].subj_kind == 1;
-            all_subj[i] = is_set ? (SKEY_SET | dst[ti]) : dst[ti];
-            if (is_set) {
-                set_off[node + 1]++;
-                set_dst[si++] = dst[ti];
-            }
-        }
-        for (uint32_t v = 0; v < N; v++) {
-            all_off[v + 1] += all_off[v];
-            set_off[v + 1] += set_off[v];
-        }
-        if (n >= (1ull << 32)) throw Error(KETO_E_LIMIT, "more than 2^32 tuples");
-    }
-
-    // ---- reverse membership rows: subject -> sorted nodes ---------------------------------
+    // ---- rows, reverse rows, probe hash, weights (build::rows) ------------------------
     const uint64_t n_subj_idx = (uint64_t)s.n_uuids + N;
-    std::vector<uint32_t> rev_off(n_subj_idx + 1, 0), rev_nodes;
+    D.ns = static_cast<const NsDev *>(dalloc(sizeof(NsDev) * s.ns.size()));
+    KETO_HIP(hipMemcpy(const_cast<NsDev *>(D.ns), s.ns.data(), sizeof(NsDev) * s.ns.size(), hipMemcpyHostToDevice));
+    build::RowsOut ro;
+    ro.all_off = static_cast<uint32_t *>(dalloc(4 * ((uint64_t)N + 1)));
+    ro.rev_off = static_cast<uint32_t *>(dalloc(4 * (n_subj_idx + 1)));
+    ro.all_subj = static_cast<uint32_t *>(dalloc(4 * n));
+    ro.rev_nodes = static_cast<uint32_t *>(dalloc(4 * n));
+    ro.set_row = static_cast<uint32_t *>(dalloc(8 * (uint64_t)N));
+    ro.weight = static_cast<uint32_t *>(dalloc(4 * (uint64_t)N));
     {
-        std::vector<uint64_t> keys(n);
-        for (uint64_t i = 0; i < n; i++) {
-            uint64_t idx = tuples[i].subj_kind == 1 ? (uint64_t)s.n_uuids + dst[i] : dst[i];
-            keys[i] = (idx << 32) | src[i];
-        }
-        parallel_sort(keys);
-        keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-        rev_nodes.resize(keys.size());
-        for (size_t i = 0; i < keys.size(); i++) {
-            rev_off[(keys[i] >> 32) + 1]++;
-            rev_nodes[i] = (uint32_t)keys[i];
-        }
-        for (uint64_t v = 0; v < n_subj_idx; v++) rev_off[v + 1] += rev_off[v];
+        DevBuf d_slot(4 * NR);
+        KETO_HIP(hipMemcpy(d_slot.p, slot_of.data(), 4 * NR, hipMemcpyHostToDevice));
+        build::RowsIn ri{dt, device_tuples ? nullptr : tuples, n, N, n_subj_idx, static_cast<const unsigned long long *>(d_bits.p), d_rank.u32(),
+                         D.ns, d_slot.u32(), stride, s.n_rel, s.n_uuids};
+        build::rows(ri, ro);
     }
+    d_t.reset();
+    d_bits.reset();
+    d_rank.reset();
+    phase("rows");
+    D.all_off = ro.all_off;
+    D.all_subj = ro.all_subj;
+    D.rev_off = ro.rev_off;
+    D.rev_nodes = ro.rev_nodes;
+    D.set_row = ro.set_row;
+    D.weight = ro.weight;
+    D.set_dst = static_cast<const uint32_t *>(adopt(ro.set_dst));
+    D.probe = static_cast<const uint4 *>(adopt(ro.probe));
+    D.probe_mask = (uint32_t)(ro.probe_buckets - 1);
+    D.probe_k = PROBE_K;
+    s.info.n_set_edges = ro.n_set;
+    s.info.n_rev_entries = n;
 
     // ---- visited keys: UUIDv5(obj, ns+"-"+rel) (relationtuple/definitions.go:114-116) -------
-    std::vector<uint32_t> vkey;
+    D.vkey = nullptr;
     {
         std::unordered_map<std::string, std::vector<uint32_t>> cls;  // class string -> global slots
         for (uint32_t ns = 0; ns < s.n_ns; ns++)
@@ -440,7 +387,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         for (auto &kv : cls)
             if (kv.second.size() > 1) any_shared = true;
         if (any_shared) {
-            vkey.resize(N);
+            std::vector<uint32_t> vkey(N);
             std::iota(vkey.begin(), vkey.end(), 0u);
             std::vector<uint32_t> slot_ns(total_slots);
             for (uint32_t ns = 0; ns < s.n_ns; ns++)
@@ -468,44 +415,22 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
                     vkey[node] = rep[s.ent_obj[e]];
                 }
             }
-            for (auto &d : set_dst)
-                if (vkey[d] != d) d |= EDGE_ALIAS;
+            uint32_t *dv = static_cast<uint32_t *>(dalloc(4ull * N));
+            KETO_HIP(hipMemcpy(dv, vkey.data(), 4ull * N, hipMemcpyHostToDevice));
+            build::alias_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, dv);
+            D.vkey = dv;
         }
     }
-
-    // ---- upload ------------------------------------------------------------------------
-    DevSnapshot &D = s.dev;
-    {
-        std::vector<uint32_t> set_row(2 * (size_t)N);
-        for (uint32_t v = 0; v < N; v++) {
-            set_row[2 * v] = set_off[v];
-            set_row[2 * v + 1] = set_off[v + 1];
-        }
-        D.set_row = upload(s, set_row);
-        // capped count of expansion paths below each node (relaxed to a fixed point over
-        // WEIGHT_ROUNDS rounds): a cost estimate that orders each batch longest-first
-        std::vector<uint32_t> wgt(N, 1), nxt(N);
-        for (int round = 0; round < WEIGHT_ROUNDS; round++) {
-            for (uint32_t v = 0; v < N; v++) {
-                uint64_t acc = 1;
-                for (uint32_t i = set_off[v]; i < set_off[v + 1] && acc < WEIGHT_CAP; i++) acc += wgt[set_dst[i] & ~EDGE_ALIAS];
-                nxt[v] = (uint32_t)std::min<uint64_t>(acc, WEIGHT_CAP);
-            }
-            wgt.swap(nxt);
-        }
-        D.weight = upload(s, wgt);
-    }
-    D.set_dst = upload(s, set_dst);
-    D.vkey = vkey.empty() ? nullptr : upload(s, vkey);
-    D.all_off = upload(s, all_off);
-    D.all_subj = upload(s, all_subj);
-    D.rev_off = upload(s, rev_off);
-    D.rev_nodes = upload(s, rev_nodes);
-    D.ns = upload(s, s.ns);
-    D.relinfo = upload(s, s.relinfo);
-    D.nsrel = upload(s, s.nsrel);
-    D.ops = upload(s, s.ops);
-    D.op_children = upload(s, s.op_children);
+    auto upload_small = [&](const auto &v) {
+        using T = typename std::decay_t<decltype(v)>::value_type;
+        T *p = static_cast<T *>(dalloc(std::max<size_t>(1, v.size()) * sizeof(T)));
+        if (!v.empty()) KETO_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+        return static_cast<const T *>(p);
+    };
+    D.relinfo = upload_small(s.relinfo);
+    D.nsrel = upload_small(s.nsrel);
+    D.ops = upload_small(s.ops);
+    D.op_children = upload_small(s.op_children);
     D.tab_bytes[0] = bytes16(s.ns);
     D.tab_bytes[1] = bytes16(s.relinfo);
     D.tab_bytes[2] = bytes16(s.nsrel);
@@ -513,57 +438,16 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.tab_bytes[4] = bytes16(s.op_children);
     D.lds_bytes = 0;
     for (uint32_t b : D.tab_bytes) D.lds_bytes += b;
-    {
-        std::vector<uint32_t> et(4 * cap, 0);
-        for (uint64_t i = 0; i < cap; i++) {
-            et[4 * i + 0] = (uint32_t)ent_keys[i];
-            et[4 * i + 1] = (uint32_t)(ent_keys[i] >> 32);
-            et[4 * i + 2] = ent_vals[i];
-        }
-        D.ent_table = reinterpret_cast<const uint4 *>(upload(s, et));
-        D.ent_mask = (uint32_t)(cap - 1);
-    }
-    // membership probe hash for subjects whose reverse row exceeds PROBE_K
-    {
-        uint64_t heavy = 0;
-        for (uint64_t v = 0; v < n_subj_idx; v++)
-            if (rev_off[v + 1] - rev_off[v] > PROBE_K) heavy += rev_off[v + 1] - rev_off[v];
-        uint64_t buckets = 1;
-        while (buckets * 2 < heavy * 2 + 2) buckets <<= 1;  // load factor <= 1/2
-        std::vector<uint64_t> pt(2 * buckets, 0);
-        for (uint64_t v = 0; v < n_subj_idx; v++) {
-            if (rev_off[v + 1] - rev_off[v] <= PROBE_K) continue;
-            for (uint32_t i = rev_off[v]; i < rev_off[v + 1]; i++) {
-                uint64_t key = ((v << 32) | rev_nodes[i]) + 1;
-                uint64_t b = mix64(key) & (buckets - 1);
-                while (true) {
-                    if (!pt[2 * b]) {
-                        pt[2 * b] = key;
-                        break;
-                    }
-                    if (!pt[2 * b + 1]) {
-                        pt[2 * b + 1] = key;
-                        break;
-                    }
-                    b = (b + 1) & (buckets - 1);
-                }
-            }
-        }
-        D.probe = reinterpret_cast<const uint4 *>(upload(s, pt));
-        D.probe_mask = (uint32_t)(buckets - 1);
-        D.probe_k = PROBE_K;
-    }
     D.n_ns = s.n_ns;
     D.n_rel = s.n_rel;
     D.n_nodes = N;
     D.n_uuids = s.n_uuids;
     D.strict = s.strict;
-
+    KETO_HIP(hipDeviceSynchronize());
+    phase("finish");
+    s.info.n_entities = ent_total;
     s.info.n_tuples = n;
     s.info.n_nodes = N;
-    s.info.n_entities = ent_total;
-    s.info.n_set_edges = set_dst.size();
-    s.info.n_rev_entries = rev_nodes.size();
     s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return S.release();
 }

@@ -1,0 +1,201 @@
+// Seeded synthetic Drive-style workloads (BASELINE configs 3 and 4):
+// bench/test infrastructure, built into its own libketo_synth.so -- never part of the engine.
+//
+// File/Folder forest: `roots` trees of fanout F and depth D (levels 0..D-1 are folders, level D
+// files), one `parents` tuple per non-root node; A ACL tuples per node (50% viewers, 20% editors,
+// 20% owners, 10% banned; 30% of the non-banned ones name Group#members, the rest a user);
+// G groups x M members (mostly users, ~1 nested group each, acyclic: subgroup id > group id).
+// C3 = 1 root, 1M groups, 10M users (~105M tuples); C4 = C3 x 10 (10 roots, 10M groups,
+// 100M users: ~1.05B tuples).
+//
+// Every value is a pure function of (seed, stream, index) through splitmix64, so the arrays
+// fill in parallel and every rank of a multi-GPU run regenerates the identical replica.
+#include <algorithm>
+#include <cstdint>
+#include <thread>
+#include <vector>
+
+#include "../../include/keto_mi355x.h"
+
+namespace {
+
+constexpr uint32_t NS_USER = 0, NS_GROUP = 1, NS_FOLDER = 2, NS_FILE = 3;
+// relation ids: the order of synth.DRIVE_RELATIONS
+constexpr uint32_t R_PARENTS = 0, R_VIEWERS = 1, R_EDITORS = 2, R_OWNERS = 3, R_BANNED = 4, R_VIEW = 5,
+                   R_EDIT = 6, R_MEMBERS = 7, R_EMPTY = 8;
+
+inline uint64_t sm64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+inline uint64_t hsh(uint64_t seed, uint64_t stream, uint64_t i) { return sm64(sm64(seed ^ (stream << 48)) ^ i); }
+inline double u01(uint64_t x) { return (double)(x >> 11) * (1.0 / 9007199254740992.0); }
+
+template <class F>
+void parallel_chunks(uint64_t n, int threads, F fn) {
+    threads = std::max(1, std::min(threads, 64));
+    if (n < (1u << 16) || threads == 1) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++)
+        th.emplace_back([=] { fn(n * t / threads, n * (t + 1) / threads); });
+    for (auto &x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+typedef struct ks_drive_params {
+    uint32_t roots, depth, fanout, acl_per_node;
+    uint32_t n_groups, members_per_group, n_users, pad;
+    uint64_t seed;
+} ks_drive_params;
+
+typedef struct ks_drive_layout {
+    uint64_t nodes_per_root, folders_per_root, n_nodes;
+    uint64_t n_parent_tuples, n_acl_tuples, n_member_tuples, n_tuples;
+    uint64_t gbase, ubase, n_uuids;
+} ks_drive_layout;
+
+int ks_drive_layout_get(const ks_drive_params *p, ks_drive_layout *L) {
+    if (!p || !L || p->fanout < 2 || p->roots == 0 || p->n_groups == 0 || p->n_users == 0) return -1;
+    uint64_t per = 0, lvl = 1, folders = 0;
+    for (uint32_t k = 0; k <= p->depth; k++) {
+        per += lvl;
+        if (k < p->depth) folders += lvl;
+        lvl *= p->fanout;
+    }
+    L->nodes_per_root = per;
+    L->folders_per_root = folders;
+    L->n_nodes = per * p->roots;
+    L->n_parent_tuples = (per - 1) * p->roots;
+    L->n_acl_tuples = L->n_nodes * p->acl_per_node;
+    L->n_member_tuples = (uint64_t)p->n_groups * p->members_per_group;
+    L->n_tuples = L->n_parent_tuples + L->n_acl_tuples + L->n_member_tuples;
+    L->gbase = L->n_nodes;
+    L->ubase = L->n_nodes + p->n_groups;
+    L->n_uuids = L->ubase + p->n_users;
+    return L->n_uuids < 0x80000000ull ? 0 : -2;
+}
+
+static inline uint32_t node_ns(const ks_drive_layout &L, uint64_t node) {
+    return node % L.nodes_per_root < L.folders_per_root ? NS_FOLDER : NS_FILE;
+}
+
+// ACL tuple j: (relation, is-group, subject uuid)
+static inline void acl_of(const ks_drive_params &p, const ks_drive_layout &L, uint64_t j, uint32_t &rel, bool &grp,
+                          uint32_t &subj) {
+    const double r = u01(hsh(p.seed, 1, j));
+    rel = r < 0.5 ? R_VIEWERS : (r < 0.7 ? R_EDITORS : (r < 0.9 ? R_OWNERS : R_BANNED));
+    grp = rel != R_BANNED && u01(hsh(p.seed, 2, j)) < 0.3;
+    subj = grp ? (uint32_t)(L.gbase + hsh(p.seed, 3, j) % p.n_groups) : (uint32_t)(L.ubase + hsh(p.seed, 4, j) % p.n_users);
+}
+
+static inline void shard(const ks_drive_params &p, uint64_t i, uint8_t *b) {
+    uint64_t a = hsh(p.seed, 8, i), c = hsh(p.seed, 9, i);
+    for (int k = 0; k < 8; k++) {
+        b[k] = (uint8_t)(a >> (8 * k));
+        b[8 + k] = (uint8_t)(c >> (8 * k));
+    }
+    b[6] = (b[6] & 0x0F) | 0x40;  // UUIDv4 version
+    b[8] = (b[8] & 0x3F) | 0x80;  // RFC 4122 variant
+}
+
+int ks_drive_tuples(const ks_drive_params *pp, keto_tuple *out, uint64_t n, int threads) {
+    ks_drive_layout L;
+    if (ks_drive_layout_get(pp, &L) != 0 || n != L.n_tuples || !out) return -1;
+    const ks_drive_params p = *pp;
+    parallel_chunks(n, threads, [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) {
+            keto_tuple t{};
+            if (i < L.n_parent_tuples) {  // node#parents@Folder:parent#""
+                const uint64_t r = i / (L.nodes_per_root - 1), c = 1 + i % (L.nodes_per_root - 1);
+                const uint64_t node = r * L.nodes_per_root + c, par = r * L.nodes_per_root + (c - 1) / p.fanout;
+                t.ns = node_ns(L, node);
+                t.obj = (uint32_t)node;
+                t.rel = R_PARENTS;
+                t.subj_kind = 1;
+                t.s_obj = (uint32_t)par;
+                t.s_ns = NS_FOLDER;
+                t.s_rel = R_EMPTY;
+            } else if (i < L.n_parent_tuples + L.n_acl_tuples) {
+                const uint64_t j = i - L.n_parent_tuples, node = j / p.acl_per_node;
+                uint32_t rel, subj;
+                bool grp;
+                acl_of(p, L, j, rel, grp, subj);
+                t.ns = node_ns(L, node);
+                t.obj = (uint32_t)node;
+                t.rel = rel;
+                t.subj_kind = grp ? 1 : 0;
+                t.s_obj = subj;
+                t.s_ns = grp ? NS_GROUP : 0;
+                t.s_rel = grp ? R_MEMBERS : 0;
+            } else {  // Group:g#members@(user | Group:sub#members), sub > g
+                const uint64_t k = i - L.n_parent_tuples - L.n_acl_tuples, g = k / p.members_per_group;
+                const bool nested = g + 1 < p.n_groups && u01(hsh(p.seed, 5, k)) < 1.0 / p.members_per_group;
+                t.ns = NS_GROUP;
+                t.obj = (uint32_t)(L.gbase + g);
+                t.rel = R_MEMBERS;
+                if (nested) {
+                    const uint64_t span = p.n_groups - g - 1;
+                    const uint64_t sub = g + 1 + std::min<uint64_t>(span - 1, (uint64_t)(u01(hsh(p.seed, 6, k)) * span));
+                    t.subj_kind = 1;
+                    t.s_obj = (uint32_t)(L.gbase + sub);
+                    t.s_ns = NS_GROUP;
+                    t.s_rel = R_MEMBERS;
+                } else {
+                    t.s_obj = (uint32_t)(L.ubase + hsh(p.seed, 7, k) % p.n_users);
+                }
+            }
+            shard(p, i, t.shard_id);
+            out[i] = t;
+        }
+    });
+    return 0;
+}
+
+// view (80%) / edit checks: half name a user taken from a random user ACL tuple of the queried
+// node (likely positives, unless banned or truncated), half a uniform node and user.
+int ks_drive_queries(const ks_drive_params *pp, uint64_t qseed, keto_query *out, uint64_t n, int threads) {
+    ks_drive_layout L;
+    if (ks_drive_layout_get(pp, &L) != 0 || !out) return -1;
+    const ks_drive_params p = *pp;
+    parallel_chunks(n, threads, [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) {
+            keto_query q{};
+            uint64_t node;
+            uint32_t user;
+            if (u01(hsh(qseed, 1, i)) < 0.5) {
+                for (uint64_t t = 0;; t++) {
+                    const uint64_t j = hsh(qseed, 2, i * 64 + t) % L.n_acl_tuples;
+                    uint32_t rel, subj;
+                    bool grp;
+                    acl_of(p, L, j, rel, grp, subj);
+                    if ((rel == R_VIEWERS || rel == R_EDITORS || rel == R_OWNERS) && !grp) {
+                        node = j / p.acl_per_node;
+                        user = subj;
+                        break;
+                    }
+                }
+            } else {
+                node = hsh(qseed, 3, i) % L.n_nodes;
+                user = (uint32_t)(L.ubase + hsh(qseed, 4, i) % p.n_users);
+            }
+            q.ns = node_ns(L, node);
+            q.obj = (uint32_t)node;
+            q.rel = u01(hsh(qseed, 5, i)) < 0.8 ? R_VIEW : R_EDIT;
+            q.subj_kind = 0;
+            q.s_obj = user;
+            q.max_depth = 0;
+            out[i] = q;
+        }
+    });
+    return 0;
+}
+
+}  // extern "C"

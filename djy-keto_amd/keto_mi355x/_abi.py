@@ -58,6 +58,7 @@ SIGNATURES = {
     "keto_abi_version": (ctypes.c_int, []),
     "keto_last_error": (_SZ, [ctypes.c_char_p, _SZ]),
     "keto_snapshot_build": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, ctypes.POINTER(_VP)]),
+    "keto_snapshot_build_device": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, ctypes.POINTER(_VP)]),
     "keto_snapshot_free": (ctypes.c_int, [_VP]),
     "keto_snapshot_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(SnapshotInfo)]),
     "keto_stream_create": (ctypes.c_int, [_I32, ctypes.POINTER(_VP)]),

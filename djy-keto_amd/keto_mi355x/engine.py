@@ -59,17 +59,23 @@ class Snapshot:
     """Immutable device-resident snapshot (CSR rows + compiled rewrite program)."""
 
     def __init__(self, namespaces_json: str | dict, tuples: np.ndarray, ns_names: list, rel_names: list,
-                 n_uuids: int, strict: bool = False, device: int = 0):
+                 n_uuids: int, strict: bool = False, device: int = 0, device_tuples: tuple | None = None):
+        """tuples: host TUPLE_DT array; or tuples=None and device_tuples=(device pointer, count)
+        for records already resident on `device` (keto_snapshot_build_device)."""
         if isinstance(namespaces_json, dict):
             namespaces_json = json.dumps(namespaces_json)
-        tuples = np.ascontiguousarray(tuples, dtype=_abi.TUPLE_DT)
         self._ns = (ctypes.c_char_p * max(1, len(ns_names)))(*[n.encode() for n in ns_names])
         self._rel = (ctypes.c_char_p * max(1, len(rel_names)))(*[r.encode() for r in rel_names])
         self._json = namespaces_json.encode()
         cfg = _abi.SnapshotConfig(len(ns_names), self._ns, len(rel_names), self._rel, n_uuids, self._json,
                                   int(strict), device)
         h = ctypes.c_void_p()
-        check(lib().keto_snapshot_build(ctypes.byref(cfg), tuples.ctypes.data, len(tuples), ctypes.byref(h)))
+        if device_tuples is not None:
+            ptr, count = device_tuples
+            check(lib().keto_snapshot_build_device(ctypes.byref(cfg), ptr, count, ctypes.byref(h)))
+        else:
+            tuples = np.ascontiguousarray(tuples, dtype=_abi.TUPLE_DT)
+            check(lib().keto_snapshot_build(ctypes.byref(cfg), tuples.ctypes.data, len(tuples), ctypes.byref(h)))
         self.handle = h
         self.device = device
         self.ns_names, self.rel_names = list(ns_names), list(rel_names)

@@ -144,6 +144,11 @@ size_t keto_last_error(char *buf, size_t len);
 
 int keto_snapshot_build(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n_tuples,
                         keto_snapshot **out);
+/* Same, from tuples already resident in device memory of cfg->device (for example a
+ * replica broadcast over RCCL/xGMI from the rank that read the store); the caller
+ * keeps them alive for the duration of the call only. */
+int keto_snapshot_build_device(const keto_snapshot_config *cfg, const keto_tuple *device_tuples, uint64_t n_tuples,
+                               keto_snapshot **out);
 int keto_snapshot_free(keto_snapshot *snap);
 int keto_snapshot_info_get(const keto_snapshot *snap, keto_snapshot_info *out);
 

@@ -11,8 +11,10 @@
  * schedule-dependent (visited-set pruning interacting with truncation) this
  * is the canonical legal order both the oracle and the GPU engine follow.
  */
+#define _GNU_SOURCE
 #include "refsem.h"
 
+#include <sched.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
@@ -25,10 +27,13 @@ typedef struct {
 } key7;
 
 struct rs_db {
-    rs_tuple *t;       /* sorted by (ns, obj, rel, shard) */
+    const rs_tuple *t; /* the caller's tuples: read while the indexes are built */
     size_t n;
-    key7 *ex;          /* sorted exact keys for EXISTS */
-    size_t n_ex;
+    uint32_t *perm;    /* build only: tuple indices sorted by (ns, obj, rel, shard) */
+    uint32_t *exq;     /* build only: tuple indices sorted by (ns, obj, rel, subject) */
+    key7 *rt;          /* rows: (ns, obj, rel, subject) in (ns, obj, rel, shard) order */
+    key7 *ex;          /* EXISTS keys, sorted */
+    int shard_bytes;   /* shard_hi/lo hold the raw UUID bytes (product layout) */
     rs_ns *ns;
     rs_rel *rels;
     rs_ast *ast;
@@ -39,29 +44,138 @@ struct rs_db {
 };
 
 /* ------------------------------------------------------------------ */
-/* indexes                                                             */
+/* indexes: a parallel LSD radix sort of packed (ns, obj, rel) keys, then */
+/* each equal-key run ordered by shard (rows) or by subject (EXISTS).     */
 
 static int cmp_u32(uint32_t a, uint32_t b) { return a < b ? -1 : a > b; }
 static int cmp_u64(uint64_t a, uint64_t b) { return a < b ? -1 : a > b; }
 
-static int cmp_tuple(const void *pa, const void *pb) {
-    const rs_tuple *a = pa, *b = pb;
-    int c;
-    if ((c = cmp_u32(a->ns, b->ns))) return c;
-    if ((c = cmp_u32(a->obj, b->obj))) return c;
-    if ((c = cmp_u32(a->rel, b->rel))) return c;
-    /* ORDER BY nid, shard_id  (traverser.go:88, relationtuples.go:216) */
-    if ((c = cmp_u64(a->shard_hi, b->shard_hi))) return c;
-    return cmp_u64(a->shard_lo, b->shard_lo);
+static uint64_t sh_hi(const rs_db *db, const rs_tuple *t) {
+    return db->shard_bytes ? __builtin_bswap64(t->shard_hi) : t->shard_hi;
+}
+static uint64_t sh_lo(const rs_db *db, const rs_tuple *t) {
+    return db->shard_bytes ? __builtin_bswap64(t->shard_lo) : t->shard_lo;
 }
 
-static int cmp_key7(const void *pa, const void *pb) {
-    const uint32_t *a = pa, *b = pb;
-    for (int i = 0; i < 7; i++) {
-        int c = cmp_u32(a[i], b[i]);
-        if (c) return c;
+/* ORDER BY nid, shard_id  (traverser.go:88, relationtuples.go:216) within one row */
+static int cmp_shard(const rs_db *db, uint32_t ia, uint32_t ib) {
+    const rs_tuple *a = &db->t[ia], *b = &db->t[ib];
+    int c;
+    if ((c = cmp_u64(sh_hi(db, a), sh_hi(db, b)))) return c;
+    if ((c = cmp_u64(sh_lo(db, a), sh_lo(db, b)))) return c;
+    return cmp_u32(ia, ib);
+}
+static int cmp_subject(const rs_db *db, uint32_t ia, uint32_t ib) {
+    const rs_tuple *a = &db->t[ia], *b = &db->t[ib];
+    int c;
+    if ((c = cmp_u32(a->kind, b->kind))) return c;
+    if ((c = cmp_u32(a->sid, b->sid))) return c;
+    if (a->kind == 1) {
+        if ((c = cmp_u32(a->sns, b->sns))) return c;
+        if ((c = cmp_u32(a->srel, b->srel))) return c;
     }
-    return 0;
+    return cmp_u32(ia, ib);
+}
+
+typedef int (*idx_cmp)(const rs_db *, uint32_t, uint32_t);
+
+static void sift(const rs_db *db, idx_cmp cmp, uint32_t *a, size_t root, size_t len) {
+    for (;;) {
+        size_t c = 2 * root + 1;
+        if (c >= len) return;
+        if (c + 1 < len && cmp(db, a[c], a[c + 1]) < 0) c++;
+        if (cmp(db, a[root], a[c]) >= 0) return;
+        uint32_t x = a[root];
+        a[root] = a[c];
+        a[c] = x;
+        root = c;
+    }
+}
+static void sort_idx(const rs_db *db, idx_cmp cmp, uint32_t *a, size_t len) {
+    if (len <= 24) {
+        for (size_t i = 1; i < len; i++) {
+            uint32_t x = a[i];
+            size_t j = i;
+            while (j > 0 && cmp(db, x, a[j - 1]) < 0) {
+                a[j] = a[j - 1];
+                j--;
+            }
+            a[j] = x;
+        }
+        return;
+    }
+    for (size_t r = len / 2; r-- > 0;) sift(db, cmp, a, r, len);
+    for (size_t e = len - 1; e > 0; e--) {
+        uint32_t x = a[0];
+        a[0] = a[e];
+        a[e] = x;
+        sift(db, cmp, a, 0, e);
+    }
+}
+
+static int build_threads(void) {
+    const char *e = getenv("REFSEM_THREADS");
+    if (e && atoi(e) > 0) return atoi(e);
+    cpu_set_t cs;
+    int n = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : 1;
+    return n < 1 ? 1 : (n > 16 ? 16 : n);
+}
+
+typedef struct {
+    const rs_db *db;
+    uint64_t *key, *key2;
+    uint32_t *idx, *idx2;
+    size_t n, b, e;
+    int shift, nth, tid;
+    size_t *hist; /* [nth][2048] */
+    uint32_t bn, bo, br;
+    uint32_t *runs_perm, *runs_exq;
+} sort_job;
+
+#define RADIX 11
+#define NBUCKET (1u << RADIX)
+
+static void *job_keys(void *p) {
+    sort_job *j = p;
+    for (size_t i = j->b; i < j->e; i++) {
+        const rs_tuple *t = &j->db->t[i];
+        j->key[i] = (((uint64_t)t->ns << j->bo | t->obj) << j->br) | t->rel;
+        j->idx[i] = (uint32_t)i;
+    }
+    return NULL;
+}
+static void *job_hist(void *p) {
+    sort_job *j = p;
+    size_t *h = j->hist + (size_t)j->tid * NBUCKET;
+    memset(h, 0, NBUCKET * sizeof *h);
+    for (size_t i = j->b; i < j->e; i++) h[(j->key[i] >> j->shift) & (NBUCKET - 1)]++;
+    return NULL;
+}
+static void *job_scatter(void *p) {
+    sort_job *j = p;
+    size_t *h = j->hist + (size_t)j->tid * NBUCKET; /* per-thread write cursors */
+    for (size_t i = j->b; i < j->e; i++) {
+        size_t o = h[(j->key[i] >> j->shift) & (NBUCKET - 1)]++;
+        j->key2[o] = j->key[i];
+        j->idx2[o] = j->idx[i];
+    }
+    return NULL;
+}
+/* order each equal-key run: rows by shard, EXISTS by subject */
+static void *job_runs(void *p) {
+    sort_job *j = p;
+    size_t i = j->b;
+    while (i > 0 && i < j->n && j->key[i] == j->key[i - 1]) i++; /* runs start in their own chunk */
+    while (i < j->e) {
+        size_t k = i + 1;
+        while (k < j->n && j->key[k] == j->key[i]) k++;
+        if (k - i > 1) {
+            sort_idx(j->db, cmp_shard, j->runs_perm + i, k - i);
+            sort_idx(j->db, cmp_subject, j->runs_exq + i, k - i);
+        }
+        i = k;
+    }
+    return NULL;
 }
 
 static key7 mk_key(const rs_tuple *t) {
@@ -72,17 +186,105 @@ static key7 mk_key(const rs_tuple *t) {
     }
     return k;
 }
+static void *job_gather(void *p) {
+    sort_job *j = p;
+    for (size_t i = j->b; i < j->e; i++) {
+        j->db->rt[i] = mk_key(&j->db->t[j->db->perm[i]]);
+        j->db->ex[i] = mk_key(&j->db->t[j->db->exq[i]]);
+    }
+    return NULL;
+}
+
+static void run_jobs(sort_job *jobs, int nth, void *(*fn)(void *)) {
+    pthread_t th[64];
+    for (int t = 0; t < nth; t++) pthread_create(&th[t], NULL, fn, &jobs[t]);
+    for (int t = 0; t < nth; t++) pthread_join(th[t], NULL);
+}
+
+static int bits_for(uint64_t v) {
+    int b = 0;
+    while (b < 64 && (v >> b)) b++;
+    return b;
+}
+
+static void build_index(rs_db *db) {
+    const size_t n = db->n;
+    db->perm = malloc((n ? n : 1) * sizeof *db->perm);
+    db->exq = malloc((n ? n : 1) * sizeof *db->exq);
+    if (!n) {
+        db->rt = malloc(sizeof *db->rt);
+        db->ex = malloc(sizeof *db->ex);
+        return;
+    }
+    uint32_t mns = 0, mobj = 0, mrel = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (db->t[i].ns > mns) mns = db->t[i].ns;
+        if (db->t[i].obj > mobj) mobj = db->t[i].obj;
+        if (db->t[i].rel > mrel) mrel = db->t[i].rel;
+    }
+    const uint32_t bo = bits_for(mobj), br = bits_for(mrel), bn = bits_for(mns);
+    const int total = bn + bo + br;
+    int nth = build_threads();
+    if (n < (1u << 16)) nth = 1;
+    if (nth > 64) nth = 64;
+    uint64_t *key = malloc(n * sizeof *key), *key2 = malloc(n * sizeof *key2);
+    uint32_t *idx2 = malloc(n * sizeof *idx2);
+    uint32_t *idx = db->perm;
+    size_t *hist = malloc((size_t)nth * NBUCKET * sizeof *hist);
+    sort_job jobs[64];
+    for (int t = 0; t < nth; t++) {
+        jobs[t] = (sort_job){db, key, key2, idx, idx2, n, n * t / nth, n * (t + 1) / nth, 0, nth, t, hist, bn, bo, br,
+                             NULL, NULL};
+    }
+    run_jobs(jobs, nth, job_keys);
+    for (int shift = 0; shift < total; shift += RADIX) {
+        for (int t = 0; t < nth; t++) jobs[t].shift = shift;
+        run_jobs(jobs, nth, job_hist);
+        size_t acc = 0; /* bucket-major, thread-minor: a stable LSD pass */
+        for (uint32_t b = 0; b < NBUCKET; b++)
+            for (int t = 0; t < nth; t++) {
+                size_t c = hist[(size_t)t * NBUCKET + b];
+                hist[(size_t)t * NBUCKET + b] = acc;
+                acc += c;
+            }
+        run_jobs(jobs, nth, job_scatter);
+        for (int t = 0; t < nth; t++) {
+            uint64_t *k = jobs[t].key;
+            jobs[t].key = jobs[t].key2;
+            jobs[t].key2 = k;
+            uint32_t *x = jobs[t].idx;
+            jobs[t].idx = jobs[t].idx2;
+            jobs[t].idx2 = x;
+        }
+    }
+    uint64_t *fk = jobs[0].key; /* after the passes: sorted keys and indices */
+    if (jobs[0].idx != db->perm) memcpy(db->perm, jobs[0].idx, n * sizeof *idx);
+    memcpy(db->exq, db->perm, n * sizeof *db->perm);
+    for (int t = 0; t < nth; t++) {
+        jobs[t].key = fk;
+        jobs[t].runs_perm = db->perm;
+        jobs[t].runs_exq = db->exq;
+    }
+    run_jobs(jobs, nth, job_runs);
+    free(hist);
+    free(key);
+    free(key2);
+    free(idx2);
+    /* materialize both orders as compact records: sequential row scans, no indirection */
+    db->rt = malloc(n * sizeof *db->rt);
+    db->ex = malloc(n * sizeof *db->ex);
+    run_jobs(jobs, nth, job_gather);
+    free(db->perm);
+    free(db->exq);
+    db->perm = db->exq = NULL;
+}
 
 rs_db *rs_build(const rs_tuple *tuples, size_t n, const rs_config *cfg) {
     rs_db *db = calloc(1, sizeof *db);
     db->n = n;
-    db->t = malloc((n ? n : 1) * sizeof *db->t);
-    memcpy(db->t, tuples, n * sizeof *db->t);
-    qsort(db->t, n, sizeof *db->t, cmp_tuple);
-    db->ex = malloc((n ? n : 1) * sizeof *db->ex);
-    for (size_t i = 0; i < n; i++) db->ex[i] = mk_key(&tuples[i]);
-    qsort(db->ex, n, sizeof *db->ex, cmp_key7);
-    db->n_ex = n;
+    db->t = tuples;
+    db->shard_bytes = cfg->shard_bytes;
+    build_index(db);
 
     db->n_ns = cfg->n_ns;
     db->n_relnames = cfg->n_relnames;
@@ -110,7 +312,9 @@ rs_db *rs_build(const rs_tuple *tuples, size_t n, const rs_config *cfg) {
 
 void rs_free(rs_db *db) {
     if (!db) return;
-    free(db->t);
+    free(db->perm);
+    free(db->exq);
+    free(db->rt);
     free(db->ex);
     free(db->ns);
     free(db->rels);
@@ -125,35 +329,39 @@ void rs_set_limits(rs_db *db, int32_t max_depth, int32_t max_width) {
     db->max_width = max_width;
 }
 
-/* rows of (ns,obj,rel): [lo, hi) in shard order */
-static void node_rows(const rs_db *db, uint32_t ns, uint32_t obj, uint32_t rel, size_t *lo,
-                      size_t *hi) {
-    rs_tuple probe = {ns, obj, rel, 0, 0, 0, 0, 0, 0, 0};
+static int cmp_row(const key7 *t, uint32_t ns, uint32_t obj, uint32_t rel) {
+    int c = cmp_u32(t->ns, ns);
+    if (!c) c = cmp_u32(t->obj, obj);
+    if (!c) c = cmp_u32(t->rel, rel);
+    return c;
+}
+
+/* rows of (ns,obj,rel): rt[lo, hi) in shard order */
+static void node_rows(const rs_db *db, uint32_t ns, uint32_t obj, uint32_t rel, size_t *lo, size_t *hi) {
     size_t a = 0, b = db->n;
     while (a < b) {
         size_t m = (a + b) / 2;
-        const rs_tuple *t = &db->t[m];
-        int c = cmp_u32(t->ns, probe.ns);
-        if (!c) c = cmp_u32(t->obj, probe.obj);
-        if (!c) c = cmp_u32(t->rel, probe.rel);
-        if (c < 0) a = m + 1;
+        if (cmp_row(&db->rt[m], ns, obj, rel) < 0) a = m + 1;
         else b = m;
     }
     *lo = a;
     b = db->n;
-    size_t e = a;
     while (a < b) {
         size_t m = (a + b) / 2;
-        const rs_tuple *t = &db->t[m];
-        int c = cmp_u32(t->ns, probe.ns);
-        if (!c) c = cmp_u32(t->obj, probe.obj);
-        if (!c) c = cmp_u32(t->rel, probe.rel);
-        if (c <= 0) a = m + 1;
+        if (cmp_row(&db->rt[m], ns, obj, rel) <= 0) a = m + 1;
         else b = m;
     }
     *hi = a;
-    (void)e;
 }
+static int cmp_key7(const void *pa, const void *pb) {
+    const uint32_t *a = pa, *b = pb;
+    for (int i = 0; i < 7; i++) {
+        int c = cmp_u32(a[i], b[i]);
+        if (c) return c;
+    }
+    return 0;
+}
+#define ROW(db, i) (&(db)->rt[i])
 
 /* ------------------------------------------------------------------ */
 /* per-query evaluation context                                         */
@@ -242,7 +450,7 @@ static int exists(const qctx *c, uint32_t ns, uint32_t obj, uint32_t rel) {
         k.srel = c->srel;
     }
     c->st->probes++;
-    return bsearch(&k, c->db->ex, c->db->n_ex, sizeof k, cmp_key7) != NULL;
+    return bsearch(&k, c->db->ex, c->db->n, sizeof k, cmp_key7) != NULL;
 }
 
 /* namespace.ASTRelationFor (internal/namespace/definitions.go:37-62).
@@ -283,7 +491,7 @@ static res check_expand_subject(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel
     /* subject-set rows in shard order, each with EXISTS(found) lookahead; stop at first found */
     size_t nres = 0;
     for (size_t i = lo; i < hi; i++) {
-        const rs_tuple *t = &db->t[i];
+        const key7 *t = ROW(db, i);
         if (t->kind != 1) continue; /* current.subject_id IS NULL (traverser.go:87) */
         c->st->edges++;
         nres++;
@@ -297,7 +505,7 @@ static res check_expand_subject(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel
     if ((long)nres > (long)db->max_width) keep = db->max_width > 0 ? (size_t)(db->max_width - 1) : 0;
     size_t seen = 0;
     for (size_t i = lo; i < hi && seen < keep; i++) {
-        const rs_tuple *t = &db->t[i];
+        const key7 *t = ROW(db, i);
         if (t->kind != 1) continue;
         seen++;
         /* CheckAndAddVisited (engine.go:157-160) */
@@ -326,7 +534,7 @@ static res check_ttu(qctx *c, uint32_t ns, uint32_t obj, const rs_ast *a, int d,
     node_rows(db, ns, obj, a->rel, &lo, &hi);
     c->st->rows++;
     for (size_t i = lo; i < hi; i++) {
-        const rs_tuple *t = &db->t[i];
+        const key7 *t = ROW(db, i);
         if (t->kind != 1) continue; /* subject IDs are skipped (:280) */
         c->st->edges++;
         res r = check_is_allowed(c, t->sns, t->sid, a->computed, d - 1, 0, vs); /* :281-286 */
@@ -619,7 +827,7 @@ static int build_tree(xctx *x, uint32_t kind, uint32_t sid, uint32_t sns, uint32
     emit(x, 1, 1, sid, sns, srel);
     x->st->out_nodes++;
     for (size_t i = lo; i < hi; i++) { /* :106-119 */
-        const rs_tuple *t = &db->t[i];
+        const key7 *t = ROW(db, i);
         x->st->edges++;
         if (!build_tree(x, t->kind, t->sid, t->sns, t->srel, d - 1)) {
             emit(x, 4, t->kind, t->sid, t->sns, t->srel); /* nil child -> leaf (:112-117) */

@@ -25,7 +25,8 @@ extern "C" {
 
 /* One relation tuple, ids interned by the caller.  kind 0 = SubjectID
  * (sid = subject id), kind 1 = SubjectSet (sns:sid#srel).  shard_hi/lo is
- * the tuple's shard_id UUID as two big-endian halves; it fixes every
+ * the tuple's shard_id UUID as two big-endian halves (or its raw bytes, see
+ * rs_config.shard_bytes); it fixes every
  * iteration order (reference: persistence/sql/relationtuples.go:113). */
 typedef struct {
     uint32_t ns, obj, rel;
@@ -82,6 +83,9 @@ typedef struct {
      * (visited key, relationtuple/definitions.go:114-116) */
     const uint32_t *vclass;
     int32_t strict, max_depth, max_width;
+    /* 1: shard_hi/lo hold the shard_id's raw UUID bytes (the engine's keto_tuple layout),
+     * 0: the two big-endian halves as numbers */
+    int32_t shard_bytes;
 } rs_config;
 
 /* Work counters for the algorithmic-byte model:

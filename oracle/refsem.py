@@ -41,7 +41,7 @@ class _Cfg(ctypes.Structure):
                 ("ns", ctypes.c_void_p), ("rels", ctypes.c_void_p), ("n_rels", ctypes.c_uint32),
                 ("ast", ctypes.c_void_p), ("n_ast", ctypes.c_uint32), ("children", ctypes.c_void_p),
                 ("n_children", ctypes.c_uint32), ("vclass", ctypes.c_void_p), ("strict", ctypes.c_int32),
-                ("max_depth", ctypes.c_int32), ("max_width", ctypes.c_int32)]
+                ("max_depth", ctypes.c_int32), ("max_width", ctypes.c_int32), ("shard_bytes", ctypes.c_int32)]
 
 
 class Stats(ctypes.Structure):
@@ -266,7 +266,9 @@ class World:
 class Oracle:
     """The oracle DB over a World + tuple array."""
 
-    def __init__(self, world: World, tuples: np.ndarray):
+    def __init__(self, world: World, tuples: np.ndarray, shard_bytes: bool = False):
+        """tuples: TUPLE_DT, or the engine's keto_tuple layout (same 48-byte record with the
+        shard_id as raw UUID bytes) with shard_bytes=True.  Not copied: kept referenced."""
         self.world = world
         self._keep = []
         nsarr, rels, ast, children = world.flatten()
@@ -293,7 +295,11 @@ class Oracle:
         cfg.max_depth = world.max_depth
         cfg.max_width = world.max_width
         self.n_ns, self.n_rel = vcls.shape
+        cfg.shard_bytes = int(shard_bytes)
         tuples = np.ascontiguousarray(tuples)
+        if tuples.dtype.itemsize != TUPLE_DT.itemsize:
+            raise ValueError("tuple records must be 48 bytes")
+        self._tuples = tuples  # rs_build indexes the caller's array in place
         self.db = lib().rs_build(tuples.ctypes.data, len(tuples), ctypes.byref(cfg))
 
     def close(self):

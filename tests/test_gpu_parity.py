@@ -215,3 +215,49 @@ def test_build_tree_single_root_matches_batch(stream):
             assert got is None
         else:
             assert refsem.trees_equal_unordered(product_tree_to_nested(w, got), e["tree"])
+
+
+def test_fresh_stream_device_path_first_call():
+    """Regression: a new stream's first batch on the device-pointer path, right after a
+    snapshot build freed large temporaries (scratch zero-fill must finish before the
+    interpreter reads its epochs / visited slots)."""
+    from keto_mi355x import synth
+    wl = synth.drive(depth=7, n_groups=20_000, n_users=200_000, seed=6)
+    q = synth.drive_queries(wl, 1 << 16, seed=5)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    s = km.Stream(0)
+    eng = km.CheckEngine(snap, s, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    dq, da, de = km.DeviceBuffer(0, q.nbytes), km.DeviceBuffer(0, len(q)), km.DeviceBuffer(0, 4 * len(q))
+    dq.upload(s, q)
+    eng.check_batch_device(dq, len(q), da, de, sync=True, count_work=True)
+    allowed = da.download(s, np.zeros(len(q), np.uint8))
+    w, _ = _world_from_workload(wl)
+    orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)  # engine layout, in place
+    dec, err, _ = orc.check_batch(q.view(refsem.QUERY_DT), threads=8)
+    np.testing.assert_array_equal(allowed, dec)
+    s.close()
+
+
+def test_device_tuple_build_matches_host_build(stream):
+    """keto_snapshot_build_device (tuples already in HBM, e.g. received over RCCL) builds the
+    same snapshot as the host-pointer build: identical decisions and work counters."""
+    import torch
+    from keto_mi355x import synth
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=8)
+    q = synth.drive_queries(wl, 8192, seed=2)
+    host = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    buf = torch.from_numpy(wl.tuples.view(np.uint8).reshape(-1)).to("cuda:0")
+    dev = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids,
+                      device_tuples=(buf.data_ptr(), len(wl.tuples)))
+    del buf
+    res = []
+    for snap in (host, dev):
+        eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+        stream.counters(reset=True)
+        a, e = eng.check_batch(q, count_work=True)
+        c = stream.counters(reset=True)
+        res.append((a, e, (c["rows"], c["edges"], c["probes"])))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    assert res[0][2] == res[1][2]
+    assert host.info()["n_set_edges"] == dev.info()["n_set_edges"]

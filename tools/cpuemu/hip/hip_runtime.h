@@ -44,6 +44,7 @@ enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount };
 inline const char *hipGetErrorString(hipError_t) { return "emu error"; }
 inline hipError_t hipGetLastError() { return hipSuccess; }
 inline hipError_t hipSetDevice(int) { return hipSuccess; }
+inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
 inline hipError_t hipGetDeviceCount(int *n) { *n = 1; return hipSuccess; }
 inline hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t, int) { *v = 2; return hipSuccess; }
 inline hipError_t hipMalloc(void **p, size_t n) { *p = std::calloc(1, n + 64); return *p ? hipSuccess : 1; }
@@ -77,6 +78,13 @@ inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 inline void __syncthreads() {}
 inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
 inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) { auto o = *p; *p += v; return o; }
+inline unsigned long long atomicOr(unsigned long long *p, unsigned long long v) { auto o = *p; *p |= v; return o; }
+inline unsigned long long atomicMin(unsigned long long *p, unsigned long long v) { auto o = *p; *p = std::min(o, v); return o; }
+inline unsigned long long atomicCAS(unsigned long long *p, unsigned long long c, unsigned long long v) {
+    auto o = *p;
+    if (o == c) *p = v;
+    return o;
+}
 
 // every lane runs to completion in turn: a persistent lane drains the work queue alone
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...)                          \
