@@ -241,15 +241,15 @@ def test_fresh_stream_device_path_first_call():
 def test_device_tuple_build_matches_host_build(stream):
     """keto_snapshot_build_device (tuples already in HBM, e.g. received over RCCL) builds the
     same snapshot as the host-pointer build: identical decisions and work counters."""
-    import torch
     from keto_mi355x import synth
     wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=8)
     q = synth.drive_queries(wl, 8192, seed=2)
     host = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
-    buf = torch.from_numpy(wl.tuples.view(np.uint8).reshape(-1)).to("cuda:0")
+    buf = km.DeviceBuffer(0, wl.tuples.nbytes)
+    buf.upload(stream, wl.tuples)
     dev = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids,
-                      device_tuples=(buf.data_ptr(), len(wl.tuples)))
-    del buf
+                      device_tuples=(buf.ptr, len(wl.tuples)))
+    buf.free()
     res = []
     for snap in (host, dev):
         eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
