@@ -249,11 +249,22 @@ __global__ __launch_bounds__(BLK) void k_set_fill(const uint32_t *all_off, const
     for (uint32_t p = all_off[v]; p < all_off[v + 1]; p++)
         if (all_subj[p] & SKEY_SET) set_dst[o++] = all_subj[p] & ~SKEY_SET;
 }
-__global__ __launch_bounds__(BLK) void k_set_row(const uint32_t *set_off, uint64_t n_rows, uint32_t *set_row) {
+// row descriptor {begin, end, first edge, second edge} (edges NONE32 past the end): rows of
+// <= 2 subject sets -- TTU parents, most ACL and group rows -- need no edge load at all
+__global__ __launch_bounds__(BLK) void k_set_row(const uint32_t *set_off, uint64_t n_rows, const uint32_t *set_dst,
+                                                 uint4 *set_row) {
     const uint64_t v = gid();
     if (v >= n_rows) return;
-    set_row[2 * v] = set_off[v];
-    set_row[2 * v + 1] = set_off[v + 1];
+    const uint32_t b = set_off[v], e = set_off[v + 1];
+    set_row[v] = make_uint4(b, e, e > b ? set_dst[b] : NONE32, e > b + 1 ? set_dst[b + 1] : NONE32);
+}
+__global__ __launch_bounds__(BLK) void k_row_inline(uint4 *set_row, uint64_t n_rows, const uint32_t *set_dst) {
+    const uint64_t v = gid();
+    if (v >= n_rows) return;
+    uint4 r = set_row[v];
+    r.z = r.y > r.x ? set_dst[r.x] : NONE32;
+    r.w = r.y > r.x + 1 ? set_dst[r.x + 1] : NONE32;
+    set_row[v] = r;
 }
 
 // ---------------------------------------------------------------- reverse rows + probe hash
@@ -444,7 +455,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         out.set_dst = DevBuf(4ull * out.n_set + 16);
         hipLaunchKernelGGL(k_set_fill, grid_for(N), dim3(BLK), 0, 0, out.all_off, set_cnt.u32(), N, out.all_subj,
                            out.set_dst.u32());
-        hipLaunchKernelGGL(k_set_row, grid_for(N), dim3(BLK), 0, 0, set_cnt.u32(), N, out.set_row);
+        hipLaunchKernelGGL(k_set_row, grid_for(N), dim3(BLK), 0, 0, set_cnt.u32(), N, out.set_dst.u32(), out.set_row);
         KETO_HIP(hipGetLastError());
         // scheduling weights: capped path counts relaxed to a fixed point (<= WEIGHT_ROUNDS)
         DevBuf w2(4 * (N + 1)), changed(4);
@@ -484,8 +495,9 @@ void rows(const RowsIn &in, RowsOut &out) {
     KETO_HIP(hipDeviceSynchronize());
 }
 
-void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey) {
+void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows) {
     hipLaunchKernelGGL(k_alias_mark, grid_for(n), dim3(BLK), 0, 0, set_dst, n, vkey);
+    hipLaunchKernelGGL(k_row_inline, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, set_dst);  // inline copies too
     KETO_HIP(hipGetLastError());
 }
 

@@ -31,7 +31,8 @@ __device__ __forceinline__ bool decisive(uint32_t r) { return (r >> 8) != 0 || (
 
 // frame word w: bits 0-15 depth, 16-19 type, 20-23 phase, 24 skip_direct, 25 visited-scope owner
 enum FrameType : uint32_t { F_IA = 0, F_ES = 1, F_RW = 2, F_SC = 3, F_TTU = 4, F_INV = 5 };
-constexpr uint32_t FL_SKIP = 1u << 24, FL_OWNER = 1u << 25;
+// FL_INLINE: S_FSCAN's window is the row descriptor's two inline edges (set by S_ROWOFF)
+constexpr uint32_t FL_SKIP = 1u << 24, FL_OWNER = 1u << 25, FL_INLINE = 1u << 26;
 __device__ __forceinline__ uint32_t fw(uint32_t type, uint32_t d, uint32_t phase = 0, uint32_t flags = 0) {
     return (d & 0xFFFFu) | (type << 16) | (phase << 20) | flags;
 }
@@ -216,21 +217,22 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
             }
             case S_ROWOFF: {
                 const bool is_es = f_type(w) == F_ES;
-                const uint32_t node = is_es ? top.x : top.y;  // TTU keeps the tupleset node in y
-                const uint32_t b = pick(s.set_row, 2 * node, v0), e = pick(s.set_row, 2 * node + 1, v0);
+                const uint32_t b = v0.x, e = v0.y;
                 if (b == e) {
                     res = M_NOT;
                     st = S_RET;
                     break;
                 }
-                la0 = win(s.set_dst, b);
-                ln = 1;
+                ew = make_uint4(v0.z, v0.w, NONE32, NONE32);  // the row's first two edges, inline
+                ew_lo = b;
+                ew_hi = b + 2;
                 if (is_es) {
-                    top = make_uint4(b, b, e, set_phase(w, 2));  // x = row begin, y = cursor, z = end
+                    top = make_uint4(b, b, e, set_phase(w, 2) | FL_INLINE);  // x = row begin, y = cursor, z = end
+                    v0 = ew;
                     st = S_FSCAN;
                 } else {
                     top = make_uint4(top.x, b, e, set_phase(w, 2));  // x = computed relation
-                    st = S_TEDGE;
+                    st = S_TNEXT;
                 }
                 break;
             }
@@ -238,8 +240,14 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                 ew = v0;
                 uint32_t cur = top.y;
                 const uint32_t e = top.z;
-                ew_lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + cur) >> 2) & 3);
-                ew_hi = ew_lo + 4;
+                if (w & FL_INLINE) {  // the row descriptor's edges (entered from S_ROWOFF)
+                    top.w &= ~FL_INLINE;
+                    ew_lo = cur;
+                    ew_hi = cur + 2;
+                } else {
+                    ew_lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + cur) >> 2) & 3);
+                    ew_hi = ew_lo + 4;
+                }
                 if (!heavy) {
                     bool found = false;
                     while (cur < e && cur < ew_hi) {
@@ -428,6 +436,8 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                     fin = 2;
                     break;
                 }
+                // the caller's next edge rides in the frame's free z word: no window reload on return
+                top.z = (top.x < top.y && top.x >= ew_lo && top.x < ew_hi) ? wword(ew, top.x - ew_lo) : NONE32;
                 stk[sp++] = top;
                 // without a rewrite the child's group is just expandSubject(c, d-1)
                 top = rw ? make_uint4(cc, 0, 0, fw(F_IA, d, 0, FL_SKIP)) : make_uint4(cc, 0, 0, fw(F_ES, d - 1));
@@ -573,7 +583,7 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                             action = 2;
                             break;
                         }
-                        la0 = win(s.set_row, 2 * top.x);
+                        la0 = s.set_row + top.x;
                         ln = 1;
                         top.w = set_phase(w, 1);
                         st = S_ROWOFF;
@@ -585,8 +595,14 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                         action = 2;
                         break;
                     }
-                    ew_lo = 1;  // window unknown after the child: reload
-                    ew_hi = 0;
+                    if (top.z != NONE32) {  // the next edge saved at the call
+                        ew = make_uint4(top.z, NONE32, NONE32, NONE32);
+                        ew_lo = top.x;
+                        ew_hi = top.x + 1;
+                    } else {
+                        ew_lo = 1;
+                        ew_hi = 0;
+                    }
                     st = S_CNEXT;
                     break;
                 case F_RW: {  // checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73)
@@ -749,7 +765,7 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                             break;
                         }
                         top = make_uint4(op.rel_computed >> 16, ts, 0, set_phase(w, 1));
-                        la0 = win(s.set_row, 2 * ts);
+                        la0 = s.set_row + ts;
                         ln = 1;
                         st = S_ROWOFF;
                         break;

@@ -32,6 +32,10 @@ enum UState : uint32_t {
     U_POP,     // parent frame (2 x 16 B)
 };
 
+// bit of the depth word: the current window is a row descriptor's two inline edges
+// (set by U_ROWOFF for U_SCAN; kept in pushed frames so U_POP restores the window origin)
+constexpr uint32_t FR_INLINE = 1u << 16;
+
 struct UParams {
     DevSnapshot s;
     const uint4 *start;  // resolve pre-pass records, in work order
@@ -205,26 +209,32 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                     st = U_POP + 100;  // empty row: not a member, return
                     break;
                 }
-                la0 = win(s.set_row, 2 * node);
+                la0 = s.set_row + node;
                 ln = 1;
                 st = U_ROWOFF;
                 break;
-            case U_ROWOFF:
-                rbeg = pick(s.set_row, 2 * node, v0);
-                end = pick(s.set_row, 2 * node + 1, v0);
+            case U_ROWOFF:  // {begin, end, edge 0, edge 1}: the first two edges come inline
+                rbeg = v0.x;
+                end = v0.y;
                 cur = rbeg;
                 if (rbeg == end) {
                     st = U_POP + 100;
                     break;
                 }
-                la0 = win(s.set_dst, cur);
-                ln = 1;
+                v0 = make_uint4(v0.z, v0.w, NONE32, NONE32);
+                d |= FR_INLINE;
                 st = U_SCAN;
                 break;
             case U_SCAN: {  // found-lookahead over one window (traverser.go:73-80, 109-111)
                 ew = v0;
-                ew_lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + cur) >> 2) & 3);
-                ew_hi = ew_lo + 4;
+                if (d & FR_INLINE) {
+                    d &= ~FR_INLINE;
+                    ew_lo = cur;
+                    ew_hi = cur + 2;
+                } else {
+                    ew_lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + cur) >> 2) & 3);
+                    ew_hi = ew_lo + 4;
+                }
                 if (!heavy) {
                     bool found = false;
                     while (cur < end && cur < ew_hi) {
@@ -401,7 +411,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                     break;
                 }
                 // push the parent (cursor, end, depth, row begin | window)
-                stk[2 * sp] = make_uint4(cur, end, d, rbeg);
+                stk[2 * sp] = make_uint4(cur, end, d | (ew_lo == rbeg ? FR_INLINE : 0u), rbeg);
                 stk[2 * sp + 1] = ew;
                 sp++;
                 node = aux2;
@@ -423,10 +433,13 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
             case U_POP:
                 cur = v0.x;
                 end = v0.y;
-                d = v0.z;
+                d = v0.z & 0xFFFFu;
                 rbeg = v0.w;
                 ew = v1;
-                {
+                if (v0.z & FR_INLINE) {  // the row descriptor's inline edges
+                    ew_lo = rbeg;
+                    ew_hi = rbeg + 2;
+                } else {
                     const uint32_t pc = cur > rbeg ? cur - 1 : cur;  // the window held edge cur-1
                     ew_lo = pc - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + pc) >> 2) & 3);
                     ew_hi = ew_lo + 4;

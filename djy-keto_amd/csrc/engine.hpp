@@ -84,12 +84,13 @@ struct RowsIn {
     uint32_t n_rel, n_uuids;
 };
 struct RowsOut {
-    uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *set_row, *weight;  // caller-allocated
+    uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *weight;  // caller-allocated
+    uint4 *set_row;
     DevBuf set_dst, probe;
     uint64_t n_set = 0, probe_buckets = 0;
 };
 void rows(const RowsIn &in, RowsOut &out);
-void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey);
+void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows);
 }  // namespace build
 
 // scratch tier: per-lane visited capacity (slots, pow2) and stack frames

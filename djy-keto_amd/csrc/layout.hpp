@@ -59,7 +59,8 @@ struct alignas(16) NsDev {
 
 // Device view (all pointers device memory).  Passed by value to kernels.
 struct DevSnapshot {
-    const uint32_t *set_row;   // [2*n_nodes] {begin, end} of each subject-set row (ES + TTU): one 8 B load
+    const uint4 *set_row;      // [n_nodes] {begin, end, edge 0, edge 1} of each subject-set row (ES + TTU):
+                               // one 16 B load; rows of <= 2 edges need no set_dst load
     const uint32_t *set_dst;   // node | EDGE_ALIAS, shard order within a row
     const uint32_t *weight;    // [n_nodes] capped path count below a node (longest-first scheduling)
     const uint32_t *vkey;      // [n_nodes] visited representative (only read for aliased nodes)

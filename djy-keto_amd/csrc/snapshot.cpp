@@ -350,7 +350,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     ro.rev_off = static_cast<uint32_t *>(dalloc(4 * (n_subj_idx + 1)));
     ro.all_subj = static_cast<uint32_t *>(dalloc(4 * n));
     ro.rev_nodes = static_cast<uint32_t *>(dalloc(4 * n));
-    ro.set_row = static_cast<uint32_t *>(dalloc(8 * (uint64_t)N));
+    ro.set_row = static_cast<uint4 *>(dalloc(16 * (uint64_t)N));
     ro.weight = static_cast<uint32_t *>(dalloc(4 * (uint64_t)N));
     {
         DevBuf d_slot(4 * NR);
@@ -417,7 +417,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
             }
             uint32_t *dv = static_cast<uint32_t *>(dalloc(4ull * N));
             KETO_HIP(hipMemcpy(dv, vkey.data(), 4ull * N, hipMemcpyHostToDevice));
-            build::alias_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, dv);
+            build::alias_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, dv, ro.set_row, N);
             D.vkey = dv;
         }
     }
