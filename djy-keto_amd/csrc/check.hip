@@ -882,8 +882,9 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     if (L.n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
     constexpr uint32_t BLOCK = 256;
     const uint32_t cus = (uint32_t)num_cus(s.device);
-    // (lanes, visited slots per lane, frames per lane)
-    // HBM is plentiful (288 GB): tier 0 holds ~500 visited nodes per lane so restarts are rare
+    // Queries that outgrow a tier's scratch go to the next (lanes, visited slots per lane,
+    // frames per lane); HBM is plentiful (288 GB): tier 0 holds ~500 visited nodes per lane,
+    // tier 1 ~4k, tier 2 ~500k.
     const Tier t[3] = {Tier{cus * 32 * 64, 1024, 64},    // the common case (grid clipped to occupancy)
                        Tier{cus * 256, 1u << 13, 1024},  // wide visited scopes
                        Tier{64, 1u << 20, 1u << 14}};   // huge scopes / deep recursion
