@@ -8,6 +8,8 @@ Workloads:
       max_read_depth 16.  The configuration the metric is quoted on; it fits one GPU.
   c3 = configs[2]: the same forest x1 (~105M tuples).
   c2 = configs[1]: nested-group graph, 10M tuples, union-only, max_read_depth 8.
+  c5 = configs[4]: the forest x40 (~4.2B tuples) partitioned by object over the ranks;
+      per batch a closure exchange over RCCL, a device build of the closure, then Check.
 One "step" = one batch of 2^20 Checks per GPU through the whole device pipeline (resolve
 pre-pass -> interpreter tiers -> decisions) with the queries already resident in HBM.
 
@@ -143,12 +145,75 @@ def build_workload(name, rank, world, device, args):
     return wl, snap, time.perf_counter() - t0
 
 
+def run_c5(args, rank, world, device, dist_on):
+    """configs[4]: a graph partitioned by object over the ranks (keto_mi355x/partition.py).
+    One step = one batch of this rank's Checks: closure exchange (RCCL all-to-all per BFS
+    level) -> device snapshot build of the closure -> the Check kernels.  Every phase is
+    inside the timed region."""
+    import torch
+
+    import keto_mi355x as km
+    from keto_mi355x import partition, synth
+
+    t0 = time.perf_counter()
+    wl = synth.drive_scaled(args.scale, materialize=False)
+    part = synth.drive_partition(wl, world, rank)
+    n_part = len(part)
+    eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
+                                      device=device, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    del part
+    setup_s = time.perf_counter() - t0
+    log(f"[rank {rank}] partition {rank}/{world}: {n_part} of {wl.meta['n_tuples']} tuples, setup {setup_s:.1f}s")
+    q = synth.drive_queries(wl, args.batch, seed=shard_seed(11, rank))
+    allowed, err = eng.check_batch(q)  # first batch: warm-up and the decision summary
+    assert (err == 0).all(), "unexpected query errors"
+    for _ in range(max(0, args.warmup - 1)):
+        eng.check_batch(q)
+    if dist_on:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    phases = {"closure_s": 0.0, "build_s": 0.0, "check_s": 0.0}
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        eng.check_batch(q)
+        for k in phases:
+            phases[k] += eng.last[k]
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    elapsed_local = time.perf_counter() - t_start
+    value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps, f"cuda:{device}" if dist_on else "cpu")
+    out = {
+        "metric": METRIC, "value": value, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (seeded Drive-style folder forest, BASELINE config 5; generated per partition)",
+        "config": {"workload": f"C5 Drive-style x{args.scale}: {wl.meta['n_tuples']} tuples partitioned by "
+                               f"object over {world} rank(s), {args.batch} checks/batch/GPU, closure of "
+                               f"max_read_depth+1 = {eng.levels()} levels per batch",
+                   "tuples": int(wl.meta["n_tuples"]), "batch_per_gpu": args.batch,
+                   "parallelism": f"object partition x{world} (RCCL all-to-all closure exchange per level)"},
+        "allowed_fraction": float(allowed.mean()),
+        "phases_ms_per_step": {k: v / args.steps * 1e3 for k, v in phases.items()},
+        "closure": {"tuples": eng.last["tuples"], "objects": eng.last["objects"], "levels": eng.last["levels"],
+                    "partition_tuples": n_part},
+        "roofline": None, "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist_on:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c4")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c4")
+    ap.add_argument("--scale", type=int, default=40, help="C5 graph = C3 x scale (40: ~4.2B tuples)")
     ap.add_argument("--tuples", type=int, default=10_000_000, help="C2 graph size")
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--latency-batch", type=int, default=1 << 16)
@@ -173,6 +238,8 @@ def main():
         torch.cuda.set_device(device)
         dist.init_process_group(backend=os.environ.get("KETO_BENCH_BACKEND", "nccl"),
                                 timeout=datetime.timedelta(minutes=30))
+    if args.workload == "c5":
+        return run_c5(args, rank, world, device, dist_on)
     import keto_mi355x as km
     from keto_mi355x import synth
 

@@ -106,56 +106,95 @@ static inline void shard(const ks_drive_params &p, uint64_t i, uint8_t *b) {
     b[8] = (b[8] & 0x3F) | 0x80;  // RFC 4122 variant
 }
 
+static inline keto_tuple drive_tuple(const ks_drive_params &p, const ks_drive_layout &L, uint64_t i) {
+    keto_tuple t{};
+    if (i < L.n_parent_tuples) {  // node#parents@Folder:parent#""
+        const uint64_t r = i / (L.nodes_per_root - 1), c = 1 + i % (L.nodes_per_root - 1);
+        const uint64_t node = r * L.nodes_per_root + c, par = r * L.nodes_per_root + (c - 1) / p.fanout;
+        t.ns = node_ns(L, node);
+        t.obj = (uint32_t)node;
+        t.rel = R_PARENTS;
+        t.subj_kind = 1;
+        t.s_obj = (uint32_t)par;
+        t.s_ns = NS_FOLDER;
+        t.s_rel = R_EMPTY;
+    } else if (i < L.n_parent_tuples + L.n_acl_tuples) {
+        const uint64_t j = i - L.n_parent_tuples, node = j / p.acl_per_node;
+        uint32_t rel, subj;
+        bool grp;
+        acl_of(p, L, j, rel, grp, subj);
+        t.ns = node_ns(L, node);
+        t.obj = (uint32_t)node;
+        t.rel = rel;
+        t.subj_kind = grp ? 1 : 0;
+        t.s_obj = subj;
+        t.s_ns = grp ? NS_GROUP : 0;
+        t.s_rel = grp ? R_MEMBERS : 0;
+    } else {  // Group:g#members@(user | Group:sub#members), sub > g
+        const uint64_t k = i - L.n_parent_tuples - L.n_acl_tuples, g = k / p.members_per_group;
+        const bool nested = g + 1 < p.n_groups && u01(hsh(p.seed, 5, k)) < 1.0 / p.members_per_group;
+        t.ns = NS_GROUP;
+        t.obj = (uint32_t)(L.gbase + g);
+        t.rel = R_MEMBERS;
+        if (nested) {
+            const uint64_t span = p.n_groups - g - 1;
+            const uint64_t sub = g + 1 + std::min<uint64_t>(span - 1, (uint64_t)(u01(hsh(p.seed, 6, k)) * span));
+            t.subj_kind = 1;
+            t.s_obj = (uint32_t)(L.gbase + sub);
+            t.s_ns = NS_GROUP;
+            t.s_rel = R_MEMBERS;
+        } else {
+            t.s_obj = (uint32_t)(L.ubase + hsh(p.seed, 7, k) % p.n_users);
+        }
+    }
+    shard(p, i, t.shard_id);
+    return t;
+}
+
 int ks_drive_tuples(const ks_drive_params *pp, keto_tuple *out, uint64_t n, int threads) {
     ks_drive_layout L;
     if (ks_drive_layout_get(pp, &L) != 0 || n != L.n_tuples || !out) return -1;
     const ks_drive_params p = *pp;
     parallel_chunks(n, threads, [&](uint64_t b, uint64_t e) {
-        for (uint64_t i = b; i < e; i++) {
-            keto_tuple t{};
-            if (i < L.n_parent_tuples) {  // node#parents@Folder:parent#""
-                const uint64_t r = i / (L.nodes_per_root - 1), c = 1 + i % (L.nodes_per_root - 1);
-                const uint64_t node = r * L.nodes_per_root + c, par = r * L.nodes_per_root + (c - 1) / p.fanout;
-                t.ns = node_ns(L, node);
-                t.obj = (uint32_t)node;
-                t.rel = R_PARENTS;
-                t.subj_kind = 1;
-                t.s_obj = (uint32_t)par;
-                t.s_ns = NS_FOLDER;
-                t.s_rel = R_EMPTY;
-            } else if (i < L.n_parent_tuples + L.n_acl_tuples) {
-                const uint64_t j = i - L.n_parent_tuples, node = j / p.acl_per_node;
-                uint32_t rel, subj;
-                bool grp;
-                acl_of(p, L, j, rel, grp, subj);
-                t.ns = node_ns(L, node);
-                t.obj = (uint32_t)node;
-                t.rel = rel;
-                t.subj_kind = grp ? 1 : 0;
-                t.s_obj = subj;
-                t.s_ns = grp ? NS_GROUP : 0;
-                t.s_rel = grp ? R_MEMBERS : 0;
-            } else {  // Group:g#members@(user | Group:sub#members), sub > g
-                const uint64_t k = i - L.n_parent_tuples - L.n_acl_tuples, g = k / p.members_per_group;
-                const bool nested = g + 1 < p.n_groups && u01(hsh(p.seed, 5, k)) < 1.0 / p.members_per_group;
-                t.ns = NS_GROUP;
-                t.obj = (uint32_t)(L.gbase + g);
-                t.rel = R_MEMBERS;
-                if (nested) {
-                    const uint64_t span = p.n_groups - g - 1;
-                    const uint64_t sub = g + 1 + std::min<uint64_t>(span - 1, (uint64_t)(u01(hsh(p.seed, 6, k)) * span));
-                    t.subj_kind = 1;
-                    t.s_obj = (uint32_t)(L.gbase + sub);
-                    t.s_ns = NS_GROUP;
-                    t.s_rel = R_MEMBERS;
-                } else {
-                    t.s_obj = (uint32_t)(L.ubase + hsh(p.seed, 7, k) % p.n_users);
-                }
-            }
-            shard(p, i, t.shard_id);
-            out[i] = t;
-        }
+        for (uint64_t i = b; i < e; i++) out[i] = drive_tuple(p, L, i);
     });
+    return 0;
+}
+
+// The tuples whose object belongs to partition `part` of `nparts` (keto_object_owner), in
+// generation order: what one rank of a partitioned (config 5) job loads.  out == NULL only
+// counts.  Two passes over the index space (count per chunk, then fill at exact offsets), so
+// no partition ever needs the whole graph in host memory.
+int ks_drive_tuples_part(const ks_drive_params *pp, uint32_t nparts, uint32_t part, keto_tuple *out, uint64_t cap,
+                         int threads, uint64_t *count) {
+    ks_drive_layout L;
+    if (ks_drive_layout_get(pp, &L) != 0 || nparts == 0 || part >= nparts || !count) return -1;
+    const ks_drive_params p = *pp;
+    const int T = std::max(1, std::min(threads, 64));
+    const uint64_t n = L.n_tuples;
+    std::vector<uint64_t> cnt(T + 1, 0);
+    auto run = [&](bool fill) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                const uint64_t b = n * t / T, e = n * (t + 1) / T;
+                uint64_t c = 0, o = fill ? cnt[t] : 0;
+                for (uint64_t i = b; i < e; i++) {
+                    const keto_tuple x = drive_tuple(p, L, i);
+                    if (keto_object_owner(x.ns, x.obj, nparts) != part) continue;
+                    if (fill) out[o++] = x;
+                    c++;
+                }
+                if (!fill) cnt[t + 1] = c;
+            });
+        for (auto &x : th) x.join();
+    };
+    run(false);
+    for (int t = 0; t < T; t++) cnt[t + 1] += cnt[t];
+    *count = cnt[T];
+    if (!out) return 0;
+    if (cap < cnt[T]) return -2;
+    run(true);
     return 0;
 }
 

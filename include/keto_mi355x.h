@@ -173,6 +173,16 @@ int keto_expand_batch(keto_snapshot *snap, keto_stream *s, const keto_subject_se
                       const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap,
                       uint64_t *out_offsets, int32_t *out_err);
 
+/* Owner of an object in a graph partitioned over nparts GPUs (BASELINE config 5,
+ * SURVEY.md 8.1 (e)): every tuple of (ns, obj) lives on one rank, so all relation slots of
+ * an object -- its direct rows, computed usersets and tuple-to-userset rows -- are local to
+ * one partition.  The loader selects a rank's tuples with it; keto_mi355x/partition.py
+ * routes object requests with the same function. */
+static inline uint32_t keto_object_owner(uint32_t ns, uint32_t obj, uint32_t nparts) {
+    const uint64_t h = ((((uint64_t)ns) << 32) | obj) * 0x9E3779B97F4A7C15ull;
+    return (uint32_t)((h >> 32) % nparts);
+}
+
 /* device memory helpers (for callers without their own allocator) */
 int keto_device_alloc(int32_t device, uint64_t bytes, void **out);
 int keto_device_free(void *p);

@@ -39,3 +39,32 @@ def product_tree_to_nested(world: refsem.World, nodes: np.ndarray):
     conv["srel"] = nodes["s_rel"]
     conv["n_children"] = nodes["n_children"]
     return refsem.tree_to_nested(world, conv)
+
+
+def world_from_workload(wl):
+    """oracle World over a synth Workload (same ids as the product snapshot)"""
+    w = refsem.World(namespaces=wl.namespaces, strict=wl.strict, max_depth=wl.max_depth, max_width=wl.max_width)
+    w.ns_names = refsem.Interner()
+    w.rel_names = refsem.Interner()
+    w.uuids = refsem.Interner()
+    for n in wl.ns_names:
+        w.ns_names(n)
+    for r in wl.rel_names:
+        w.rel_names(r)
+    w._walk_names()
+    t = np.zeros(len(wl.tuples), dtype=refsem.TUPLE_DT)
+    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
+                 ("sns", "s_ns"), ("srel", "s_rel")):
+        t[a] = wl.tuples[b]
+    sb = wl.tuples["shard_id"]
+    t["shard_hi"] = sb[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+    t["shard_lo"] = sb[:, 8:].copy().view(">u8").reshape(-1).astype(np.uint64)
+    return w, t
+
+
+def queries_to_oracle(q):
+    o = np.zeros(len(q), dtype=refsem.QUERY_DT)
+    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
+                 ("sns", "s_ns"), ("srel", "s_rel"), ("depth", "max_depth")):
+        o[a] = q[b]
+    return o

@@ -6,7 +6,8 @@ import pytest
 import keto_mi355x as km
 import refsem
 from fixtures import fixture_names, load, world_for
-from product_helpers import product_snapshot, product_tree_to_nested, queries_to_product
+from product_helpers import (product_snapshot, product_tree_to_nested, queries_to_oracle, queries_to_product,
+                             world_from_workload)
 from randworld import random_world
 
 pytestmark = pytest.mark.gpu
@@ -85,35 +86,6 @@ def test_random_worlds_vs_oracle(stream, seed, rewrites):
         assert product_tree_to_nested(w, nodes[int(offs[i]):int(offs[i + 1])]) == refsem.tree_to_nested(w, on)
 
 
-def _world_from_workload(wl):
-    """oracle World over a synth Workload (same ids as the product snapshot)"""
-    w = refsem.World(namespaces=wl.namespaces, strict=wl.strict, max_depth=wl.max_depth, max_width=wl.max_width)
-    w.ns_names = refsem.Interner()
-    w.rel_names = refsem.Interner()
-    w.uuids = refsem.Interner()
-    for n in wl.ns_names:
-        w.ns_names(n)
-    for r in wl.rel_names:
-        w.rel_names(r)
-    w._walk_names()
-    t = np.zeros(len(wl.tuples), dtype=refsem.TUPLE_DT)
-    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
-                 ("sns", "s_ns"), ("srel", "s_rel")):
-        t[a] = wl.tuples[b]
-    sb = wl.tuples["shard_id"]
-    t["shard_hi"] = sb[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
-    t["shard_lo"] = sb[:, 8:].copy().view(">u8").reshape(-1).astype(np.uint64)
-    return w, t
-
-
-def _q_to_oracle(q):
-    o = np.zeros(len(q), dtype=refsem.QUERY_DT)
-    for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
-                 ("sns", "s_ns"), ("srel", "s_rel"), ("depth", "max_depth")):
-        o[a] = q[b]
-    return o
-
-
 @pytest.mark.parametrize("wl_name", ["nested_groups", "drive"])
 def test_synthetic_small_vs_oracle(stream, wl_name):
     from keto_mi355x import synth
@@ -124,9 +96,9 @@ def test_synthetic_small_vs_oracle(stream, wl_name):
         wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=4)
         q = synth.drive_queries(wl, 20_000, seed=3)
     snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
-    w, t = _world_from_workload(wl)
+    w, t = world_from_workload(wl)
     orc = refsem.Oracle(w, t)
-    dec, err, st = orc.check_batch(_q_to_oracle(q), threads=8)
+    dec, err, st = orc.check_batch(queries_to_oracle(q), threads=8)
     eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
     stream.counters(reset=True)
     allowed, gerr = eng.check_batch(q, count_work=True)
@@ -158,10 +130,10 @@ def test_nested_groups_full_size_properties(stream):
     full = q["max_depth"] == 0
     assert a1[full].mean() > 0.45
     # a sample of 4096 checked exactly against the oracle
-    w, t = _world_from_workload(wl)
+    w, t = world_from_workload(wl)
     orc = refsem.Oracle(w, t)
     idx = rng.choice(len(q), size=4096, replace=False)
-    dec, err, _ = orc.check_batch(_q_to_oracle(q[idx]), threads=8)
+    dec, err, _ = orc.check_batch(queries_to_oracle(q[idx]), threads=8)
     np.testing.assert_array_equal(a1[idx], dec)
 
 
@@ -231,7 +203,7 @@ def test_fresh_stream_device_path_first_call():
     dq.upload(s, q)
     eng.check_batch_device(dq, len(q), da, de, sync=True, count_work=True)
     allowed = da.download(s, np.zeros(len(q), np.uint8))
-    w, _ = _world_from_workload(wl)
+    w, _ = world_from_workload(wl)
     orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)  # engine layout, in place
     dec, err, _ = orc.check_batch(q.view(refsem.QUERY_DT), threads=8)
     np.testing.assert_array_equal(allowed, dec)

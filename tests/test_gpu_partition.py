@@ -1,0 +1,104 @@
+"""Config-5 partitioned path on the GPU: closure exchange -> device snapshot build -> the
+unmodified Check / Expand kernels, against the oracle over the whole graph (bit-exact), on
+one rank and on two gloo ranks sharing the box's GPU."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import keto_mi355x as km
+import refsem
+from keto_mi355x import partition, synth
+from product_helpers import queries_to_oracle, world_from_workload
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _wl():
+    return synth.drive(depth=6, fanout=4, acl_per_node=6, n_groups=3000, members_per_group=10, n_users=20_000,
+                       seed=12)
+
+
+def _roots(wl, rng, n):
+    r = np.zeros(n, dtype=km.SUBJSET_DT)
+    h = n // 2
+    r["ns"][:h], r["rel"][:h] = 1, wl.rel_names.index("members")
+    r["obj"][:h] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], h)
+    r["ns"][h:], r["rel"][h:] = 2, wl.rel_names.index("viewers")
+    r["obj"][h:] = rng.integers(0, wl.meta["folders_per_root"], n - h)
+    return r
+
+
+def test_single_rank_partitioned_matches_oracle():
+    wl = _wl()
+    q = synth.drive_queries(wl, 20_000, seed=31)
+    q["max_depth"][:2000] = np.random.default_rng(0).integers(1, 8, 2000)
+    eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, wl.tuples,
+                                      max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    allowed, err = eng.check_batch(q)
+    assert 0 < eng.last["tuples"] < len(wl.tuples)
+    w, t = world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+    np.testing.assert_array_equal(err, oerr)
+    np.testing.assert_array_equal(allowed, dec)
+    roots = _roots(wl, np.random.default_rng(1), 256)
+    nodes, offs, xerr = eng.expand_batch(roots)
+    assert (xerr == 0).all()
+    for i, r in enumerate(roots):
+        on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), wl.max_depth)
+        mine = nodes[int(offs[i]):int(offs[i + 1])]
+        assert len(mine) == len(on)
+        for f_p, f_o in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"),
+                         ("s_rel", "srel"), ("n_children", "n_children")):
+            np.testing.assert_array_equal(mine[f_p], on[f_o])
+    eng.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    for p in (ROOT, os.path.join(ROOT, "djy-keto_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        wl = _wl()
+        eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids,
+                                          synth.drive_partition(wl, world, rank), max_read_depth=wl.max_depth,
+                                          max_read_width=wl.max_width)
+        q = synth.drive_queries(wl, 8192, seed=40 + rank)
+        allowed, err = eng.check_batch(q)
+        w, t = world_from_workload(wl)
+        orc = refsem.Oracle(w, t)
+        orc.set_limits(wl.max_depth, wl.max_width)
+        dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=4)
+        out[rank] = (int((allowed != dec).sum()), int((err != oerr).sum()), int(dec.sum()), eng.comm.bytes_sent)
+        eng.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_partitioned_matches_oracle():
+    world = 2
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    for r in range(world):
+        dmis, emis, n_allowed, sent = res[r]
+        assert dmis == 0 and emis == 0
+        assert n_allowed > 0 and sent > 0
