@@ -343,3 +343,13 @@ int keto_memcpy_d2h(keto_stream *hs, void *dst, const void *src, uint64_t bytes)
 }
 
 }  // extern "C"
+
+int keto_trees_to_json(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,
+                       const keto_name_tables *names, char *out, uint64_t cap, uint64_t *out_offsets) {
+    return guarded([&] { keto::trees_to_json(nodes, offsets, n_trees, names, out, cap, out_offsets); });
+}
+
+int keto_trees_to_proto(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,
+                        const keto_name_tables *names, uint8_t *out, uint64_t cap, uint64_t *out_offsets) {
+    return guarded([&] { keto::trees_to_proto(nodes, offsets, n_trees, names, out, cap, out_offsets); });
+}

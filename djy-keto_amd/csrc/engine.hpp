@@ -160,4 +160,10 @@ struct ExpandLaunch {
 };
 void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L);
 
+// treefmt.cpp: Expand trees -> API form (Mapper.ToTree + JSON / Tree.ToProto), host only
+void trees_to_json(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,
+                   const keto_name_tables *names, char *out, uint64_t cap, uint64_t *out_offsets);
+void trees_to_proto(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,
+                    const keto_name_tables *names, uint8_t *out, uint64_t cap, uint64_t *out_offsets);
+
 }  // namespace keto

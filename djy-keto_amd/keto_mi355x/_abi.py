@@ -52,6 +52,12 @@ class WorkCounters(ctypes.Structure):
                 ("wave_steps", ctypes.c_uint64 * 3), ("lane_steps", ctypes.c_uint64 * 3)]
 
 
+class NameTables(ctypes.Structure):
+    _fields_ = [("n_namespaces", ctypes.c_uint32), ("namespace_names", ctypes.POINTER(ctypes.c_char_p)),
+                ("n_relations", ctypes.c_uint32), ("relation_names", ctypes.POINTER(ctypes.c_char_p)),
+                ("n_uuids", ctypes.c_uint64), ("uuid_strings", ctypes.POINTER(ctypes.c_char_p))]
+
+
 # symbol -> (restype, argtypes); the header's complete export list
 _VP, _U32, _I32, _U64, _SZ = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
 SIGNATURES = {
@@ -73,6 +79,8 @@ SIGNATURES = {
     "keto_memcpy_h2d": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
     "keto_memcpy_d2h": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
     "keto_device_count": (ctypes.c_int, [ctypes.POINTER(_I32)]),
+    "keto_trees_to_json": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
+    "keto_trees_to_proto": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
 }
 
 

@@ -173,6 +173,31 @@ int keto_expand_batch(keto_snapshot *snap, keto_stream *s, const keto_subject_se
                       const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap,
                       uint64_t *out_offsets, int32_t *out_err);
 
+/* Name tables for the API form of a result (Mapper, uuid_mapping.go:199-399): id -> string
+ * for namespaces, relations and interned UUIDs (the shim's MapUUIDsToStrings view of
+ * keto_uuid_mappings, persistence/sql/uuid_mapping.go:19-33). */
+typedef struct keto_name_tables {
+    uint32_t n_namespaces;
+    const char *const *namespace_names;
+    uint32_t n_relations;
+    const char *const *relation_names;
+    uint64_t n_uuids;
+    const char *const *uuid_strings;
+} keto_name_tables;
+
+/* Expand trees (keto_expand_batch output: nodes + offsets[n_trees+1]) -> API form, host
+ * only.  Tree i becomes out[out_offsets[i] .. out_offsets[i+1]); a nil tree (empty range)
+ * becomes zero bytes.  If cap is too small returns KETO_E_CAPACITY with
+ * out_offsets[n_trees] = bytes required.
+ *   json:  Mapper.ToTree (uuid_mapping.go:347-399) + encoding/json of ketoapi.Tree
+ *          (ketoapi/public_api_definitions.go:217-229): the REST expand response body.
+ *   proto: Mapper.ToTree + Tree.ToProto (ketoapi/enc_proto.go:119-133): serialized
+ *          SubjectTree (expand_service.proto:77-92), the gRPC ExpandResponse.tree. */
+int keto_trees_to_json(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,
+                       const keto_name_tables *names, char *out, uint64_t cap, uint64_t *out_offsets);
+int keto_trees_to_proto(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,
+                        const keto_name_tables *names, uint8_t *out, uint64_t cap, uint64_t *out_offsets);
+
 /* Owner of an object in a graph partitioned over nparts GPUs (BASELINE config 5,
  * SURVEY.md 8.1 (e)): every tuple of (ns, obj) lives on one rank, so all relation slots of
  * an object -- its direct rows, computed usersets and tuple-to-userset rows -- are local to

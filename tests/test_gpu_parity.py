@@ -233,3 +233,26 @@ def test_device_tuple_build_matches_host_build(stream):
     np.testing.assert_array_equal(res[0][1], res[1][1])
     assert res[0][2] == res[1][2]
     assert host.info()["n_set_edges"] == dev.info()["n_set_edges"]
+
+
+def test_expand_api_form_matches_docs_output(stream):
+    """GPU Expand -> keto_trees_to_json: the docs sample's printed tree
+    (01-expand-beach/expected_output.json), children compared without order."""
+    import json
+    import os
+
+    from fixtures import GOLDEN
+    from keto_mi355x import api
+    from test_tree_api import _canon
+
+    fx = load("docs_expand_beach")
+    w, t, _ = world_for(fx)
+    snap = product_snapshot(w, t)
+    e = fx["expands"][0]
+    ns, obj, rel = refsem.parse_subject_set(e["subject"])
+    roots = np.array([(w.ns_names.ids[ns], w.uuids.ids[obj], w.rel_names.ids[rel], e["depth"])], dtype=km.SUBJSET_DT)
+    nodes, offs, err = km.ExpandEngine(snap, stream, max_read_depth=w.max_depth).build_trees(roots)
+    assert err[0] == 0
+    out = api.trees_to_json(nodes, offs, api.NameTables(w.ns_names.names, w.rel_names.names, w.uuids.names))
+    with open(os.path.join(GOLDEN, "api", "docs_expand_beach_expected_output.json")) as f:
+        assert _canon(json.loads(out[0])) == _canon(json.load(f))
