@@ -256,3 +256,52 @@ def test_expand_api_form_matches_docs_output(stream):
     out = api.trees_to_json(nodes, offs, api.NameTables(w.ns_names.names, w.rel_names.names, w.uuids.names))
     with open(os.path.join(GOLDEN, "api", "docs_expand_beach_expected_output.json")) as f:
         assert _canon(json.loads(out[0])) == _canon(json.load(f))
+
+
+@pytest.mark.parametrize("name", [n for n in fixture_names() if load(n).get("checks")])
+def test_sqlite_loaded_snapshot_on_gpu(stream, tmp_path, name):
+    """Keto SQLite store -> loader -> device snapshot -> Check kernels: the reference's own
+    expected answers (tests/golden)."""
+    import os
+
+    from keto_mi355x.loader import KetoStore
+    from keto_sqlite import subject_of, write_store
+
+    fx = load(name)
+    path = os.path.join(tmp_path, "keto.sqlite")
+    write_store(path, fx["tuples"], seed=len(name))
+    store = KetoStore(path, fx["namespaces"], strict=fx.get("strict", False))
+    snap = store.snapshot()
+    for c in fx["checks"]:
+        t = refsem.parse_tuple(c["query"])
+        q = store.query(t["ns"], t["obj"], t["rel"], subject_of(t), c.get("depth", 0))
+        eng = km.CheckEngine(snap, stream, max_read_depth=c.get("global", fx.get("global", 5)),
+                             max_read_width=fx.get("max_width", 100))
+        allowed, err = eng.check_batch(q)
+        assert err[0] == c.get("err", 0), (name, c)
+        assert bool(allowed[0]) == c["allowed"], (name, c)
+
+
+def test_sqlite_to_api_tree_on_gpu(stream, tmp_path):
+    """the whole (f) path: Keto SQLite store -> device snapshot -> Expand kernel -> API JSON,
+    against the docs sample's printed tree"""
+    import json
+    import os
+
+    from fixtures import GOLDEN
+    from keto_mi355x import api
+    from keto_mi355x.loader import KetoStore
+    from keto_sqlite import write_store
+    from test_tree_api import _canon
+
+    fx = load("docs_expand_beach")
+    path = os.path.join(tmp_path, "keto.sqlite")
+    write_store(path, fx["tuples"], seed=3)
+    store = KetoStore(path, fx["namespaces"])
+    q = store.query("files", "/photos/beach.jpg", "access", "x")[0]
+    roots = np.array([(q["ns"], q["obj"], q["rel"], 3)], dtype=km.SUBJSET_DT)
+    nodes, offs, err = km.ExpandEngine(store.snapshot(), stream, max_read_depth=5).build_trees(roots)
+    assert err[0] == 0
+    out = api.trees_to_json(nodes, offs, store.name_tables())
+    with open(os.path.join(GOLDEN, "api", "docs_expand_beach_expected_output.json")) as f:
+        assert _canon(json.loads(out[0])) == _canon(json.load(f))
