@@ -145,6 +145,41 @@ def build_workload(name, rank, world, device, args):
     return wl, snap, time.perf_counter() - t0
 
 
+def serving_probe(km, snap, q, wl, clients: int, req: int, seconds: float):
+    """Closed-loop serving load through the coalescing dispatcher (keto_dispatcher_*): `clients`
+    threads each send `req`-query requests back to back.  Reported beside the batch numbers;
+    the per-request latency includes the queueing a request sees behind the batch in flight."""
+    import threading
+
+    d = km.Dispatcher(snap, wl.max_depth, wl.max_width, max_batch=1 << 16)
+    lat = [[] for _ in range(clients)]
+    stop = time.perf_counter() + seconds
+
+    def client(t):
+        i = (t * 7919 * req) % max(1, len(q) - req)
+        while time.perf_counter() < stop:
+            t0 = time.perf_counter()
+            d.check(q[i:i + req])
+            lat[t].append(time.perf_counter() - t0)
+            i = (i + clients * req) % max(1, len(q) - req)
+
+    th = [threading.Thread(target=client, args=(t,)) for t in range(clients)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    dt = time.perf_counter() - t0
+    st = d.stats()
+    d.close()
+    allv = np.concatenate([np.array(x) for x in lat if x]) * 1e3
+    return {"clients": clients, "request_checks": req, "seconds": dt,
+            "checks_per_s": st["queries"] / dt, "requests_per_s": st["requests"] / dt,
+            "mean_batch": st["queries"] / max(1, st["batches"]),
+            "p50_request_ms": float(np.percentile(allv, 50)), "p99_request_ms": float(np.percentile(allv, 99)),
+            "host_client": "Python threads over ctypes (GIL released in the call)"}
+
+
 def run_c5(args, rank, world, device, dist_on):
     """configs[4]: a graph partitioned by object over the ranks (keto_mi355x/partition.py).
     One step = one batch of this rank's Checks: closure exchange (RCCL all-to-all per BFS
@@ -160,7 +195,8 @@ def run_c5(args, rank, world, device, dist_on):
     part = synth.drive_partition(wl, world, rank)
     n_part = len(part)
     eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
-                                      device=device, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+                                      device=device, max_read_depth=wl.max_depth, max_read_width=wl.max_width,
+                                      store_device=f"cuda:{device}")
     del part
     setup_s = time.perf_counter() - t0
     log(f"[rank {rank}] partition {rank}/{world}: {n_part} of {wl.meta['n_tuples']} tuples, setup {setup_s:.1f}s")
@@ -220,6 +256,9 @@ def main():
     ap.add_argument("--latency-iters", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--serve-clients", type=int, default=128, help="0 skips the dispatcher probe")
+    ap.add_argument("--serve-request", type=int, default=64)
+    ap.add_argument("--serve-seconds", type=float, default=3.0)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -309,6 +348,9 @@ def main():
         lat.append(time.perf_counter() - t1)
     p99_ms = float(np.percentile(np.array(lat) * 1e3, 99)) if lat else None
 
+    serving = serving_probe(km, snap, q, wl, args.serve_clients, args.serve_request, args.serve_seconds) \
+        if args.serve_clients > 0 else None
+
     achieved = bytes_t0 / (kernel_ms * 1e-3) / 1e9
     kname = "check_union_kernel" if union_only else "check_kernel"
     traffic = None  # HBM bytes per tier-0 launch from the committed PMC passes (tools/pmc_traffic.sh)
@@ -345,6 +387,7 @@ def main():
         "latency_batch": nl,
         "allowed_fraction": float(allowed.mean()),
         "pcie_inclusive_checks_per_s": pcie_rate,
+        "serving": serving,
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

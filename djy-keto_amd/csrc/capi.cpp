@@ -353,3 +353,31 @@ int keto_trees_to_proto(const keto_tree_node *nodes, const uint64_t *offsets, ui
                         const keto_name_tables *names, uint8_t *out, uint64_t cap, uint64_t *out_offsets) {
     return guarded([&] { keto::trees_to_proto(nodes, offsets, n_trees, names, out, cap, out_offsets); });
 }
+
+int keto_dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, keto_dispatcher **out) {
+    if (out) *out = nullptr;
+    return guarded([&] { keto::dispatcher_create(snap, cfg, out); });
+}
+
+int keto_dispatcher_destroy(keto_dispatcher *d) {
+    return guarded([&] { keto::dispatcher_destroy(d); });
+}
+
+int keto_dispatcher_check(keto_dispatcher *d, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
+                          int32_t *out_err) {
+    int rc = KETO_OK;
+    const int g = guarded([&] {
+        std::string msg;
+        rc = keto::dispatcher_check(d, queries, n, out_allowed, out_err, msg);
+        if (rc != KETO_OK) g_err = msg;
+    });
+    return g != KETO_OK ? g : rc;
+}
+
+int keto_dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap) {
+    return guarded([&] { keto::dispatcher_set_snapshot(d, snap); });
+}
+
+int keto_dispatcher_stats_get(keto_dispatcher *d, keto_dispatcher_stats *out) {
+    return guarded([&] { keto::dispatcher_stats(d, out); });
+}

@@ -1,0 +1,276 @@
+// Request coalescing for serving: the batching dispatcher a Go
+// cgo shim puts behind check.Engine.CheckIsMember / the gRPC CheckService handler
+// (check/handler.go:304-331).
+//
+// The reference evaluates every request on its own goroutine.  Here concurrent callers
+// block in keto_dispatcher_check while `inflight` slots (a worker thread + a HIP stream
+// with its own scratch each) do the batching:
+//   - a free slot takes every request queued since the last launch (up to max_batch
+//     queries; a request is never split);
+//   - it packs them into pinned host memory and runs them as one batch (H2D -> resolve +
+//     interpreter kernels -> D2H, one stream, one synchronisation);
+//   - it scatters the decisions back to the callers.
+// While batches are on the GPU, new requests queue up, so the batch size follows the load
+// with no timer (max_wait_us > 0 adds an explicit coalescing window).  A batch lasts as
+// long as its longest query; several batches in flight on their own streams keep the CUs
+// busy that a small batch's finished lanes leave idle.  The snapshot can be
+// swapped between batches (keto_dispatcher_set_snapshot), which is how a new snaptoken's
+// snapshot goes live without stopping the service.
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace keto {
+namespace {
+
+struct Request {
+    const keto_query *q;
+    uint64_t n;
+    uint8_t *allowed;
+    int32_t *err;
+    int rc = KETO_OK;
+    std::string msg;
+    bool done = false;
+    std::condition_variable cv;
+};
+
+struct Dispatcher;
+
+// one in-flight batch: its own stream (and so its own scratch), staging and worker thread
+struct Slot {
+    Dispatcher *d = nullptr;
+    keto_stream *stream = nullptr;
+    keto_query *hq = nullptr;  // pinned staging for max_batch records
+    uint8_t *ha = nullptr;
+    int32_t *he = nullptr;
+    void *dq = nullptr, *da = nullptr, *de = nullptr;
+    std::thread th;
+
+    void run();
+    int launch(keto_snapshot *snap, uint64_t n, std::string &msg);
+};
+
+struct Dispatcher {
+    keto_snapshot *snap = nullptr;
+    keto_limits limits{5, 100};
+    uint32_t max_batch = 1u << 16, max_wait_us = 0;
+    int device = 0;
+    std::mutex m;                // queue, stats
+    std::shared_mutex snap_mu;   // shared while a batch runs; a snapshot swap takes it exclusively
+    std::condition_variable cv_in;
+    std::deque<Request *> queue;
+    uint64_t queued = 0;
+    bool stop = false;
+    std::vector<std::unique_ptr<Slot>> slots;
+    keto_dispatcher_stats stats{};
+};
+
+// one packed batch through the device: async copies around the kernels, one sync
+int Slot::launch(keto_snapshot *snap, uint64_t n, std::string &msg) {
+    hipStream_t hs = reinterpret_cast<Stream *>(stream)->stream;
+    int rc = KETO_OK;
+    try {
+        KETO_HIP(hipMemcpyAsync(dq, hq, n * sizeof(keto_query), hipMemcpyHostToDevice, hs));
+        rc = keto_check_batch(snap, stream, static_cast<const keto_query *>(dq), n, &d->limits,
+                              static_cast<uint8_t *>(da), static_cast<int32_t *>(de), KETO_F_DEVICE_PTRS | KETO_F_ASYNC);
+        if (rc == KETO_OK) {
+            KETO_HIP(hipMemcpyAsync(ha, da, n, hipMemcpyDeviceToHost, hs));
+            KETO_HIP(hipMemcpyAsync(he, de, n * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+            KETO_HIP(hipStreamSynchronize(hs));
+        } else {
+            char buf[512];
+            keto_last_error(buf, sizeof(buf));
+            msg = buf;
+        }
+    } catch (const Error &e) {
+        rc = e.code;
+        msg = e.what();
+    }
+    return rc;
+}
+
+void Slot::run() {
+    std::vector<Request *> take;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(d->m);
+            d->cv_in.wait(lk, [&] { return d->stop || !d->queue.empty(); });
+            if (d->stop && d->queue.empty()) return;
+            if (d->max_wait_us) {
+                const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(d->max_wait_us);
+                d->cv_in.wait_until(lk, until, [&] { return d->stop || d->queued >= d->max_batch; });
+                if (d->queue.empty()) continue;  // another slot took them
+            }
+            take.clear();
+            uint64_t n = 0;
+            while (!d->queue.empty() && (take.empty() || n + d->queue.front()->n <= d->max_batch)) {
+                n += d->queue.front()->n;
+                d->queued -= d->queue.front()->n;
+                take.push_back(d->queue.front());
+                d->queue.pop_front();
+            }
+        }
+        std::shared_lock<std::shared_mutex> sl(d->snap_mu);
+        uint64_t n = 0;
+        for (auto *r : take) n += r->n;
+        int rc = KETO_OK;
+        std::string msg;
+        const bool staged = n <= d->max_batch;
+        if (staged) {
+            uint64_t o = 0;
+            for (auto *r : take) {
+                std::memcpy(hq + o, r->q, r->n * sizeof(keto_query));
+                o += r->n;
+            }
+            rc = launch(d->snap, n, msg);
+        } else {  // a single request larger than the staging: the host-pointer path
+            Request *r = take[0];
+            rc = keto_check_batch(d->snap, stream, r->q, r->n, &d->limits, r->allowed, r->err, 0);
+            if (rc != KETO_OK) {
+                char buf[512];
+                keto_last_error(buf, sizeof(buf));
+                msg = buf;
+            }
+        }
+        sl.unlock();
+        uint64_t o = 0;
+        std::lock_guard<std::mutex> lk(d->m);
+        for (auto *r : take) {
+            if (rc == KETO_OK && staged) {
+                std::memcpy(r->allowed, ha + o, r->n);
+                std::memcpy(r->err, he + o, r->n * sizeof(int32_t));
+            }
+            o += r->n;
+            r->rc = rc;
+            r->msg = msg;
+            r->done = true;
+            r->cv.notify_one();
+        }
+        d->stats.batches++;
+        d->stats.queries += n;
+        d->stats.requests += take.size();
+        if (n > d->stats.max_batch_seen) d->stats.max_batch_seen = n;
+    }
+}
+
+Dispatcher *DP(keto_dispatcher *d) { return reinterpret_cast<Dispatcher *>(d); }
+
+void release_slot(Slot *x) {
+    if (x->stream) keto_stream_destroy(x->stream);
+    if (x->hq) (void)hipHostFree(x->hq);
+    if (x->ha) (void)hipHostFree(x->ha);
+    if (x->he) (void)hipHostFree(x->he);
+    if (x->dq) (void)hipFree(x->dq);
+    if (x->da) (void)hipFree(x->da);
+    if (x->de) (void)hipFree(x->de);
+}
+
+void shutdown(Dispatcher *d) {
+    {
+        std::lock_guard<std::mutex> lk(d->m);
+        d->stop = true;
+    }
+    d->cv_in.notify_all();
+    for (auto &x : d->slots)
+        if (x->th.joinable()) x->th.join();
+    for (auto &x : d->slots) release_slot(x.get());
+    delete d;
+}
+
+}  // namespace
+
+void dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, keto_dispatcher **out) {
+    if (!snap || !cfg || !out) throw Error(KETO_E_INVALID, "null argument");
+    if (cfg->max_batch == 0 || cfg->max_batch > (1u << 24)) throw Error(KETO_E_INVALID, "max_batch out of range");
+    if (cfg->inflight > 16) throw Error(KETO_E_INVALID, "inflight out of range (0..16)");
+    const keto_limits &l = cfg->limits;
+    if (l.max_read_depth < 1 || l.max_read_depth > 65535 || l.max_read_width < 1 || l.max_read_width > 65535)
+        throw Error(KETO_E_INVALID, "limits out of range");
+    auto *d = new Dispatcher();
+    d->snap = snap;
+    d->limits = l;
+    d->max_batch = cfg->max_batch;
+    d->max_wait_us = cfg->max_wait_us;
+    d->device = reinterpret_cast<Snapshot *>(snap)->device;
+    try {
+        KETO_HIP(hipSetDevice(d->device));
+        const size_t nb = cfg->max_batch;
+        const uint32_t k = cfg->inflight ? cfg->inflight : 4;
+        for (uint32_t i = 0; i < k; i++) {
+            d->slots.push_back(std::make_unique<Slot>());
+            Slot *x = d->slots.back().get();
+            x->d = d;
+            if (keto_stream_create(d->device, &x->stream) != KETO_OK)
+                throw Error(KETO_E_DEVICE, "stream creation failed");
+            KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&x->hq), nb * sizeof(keto_query), 0));
+            KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&x->ha), nb, 0));
+            KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&x->he), nb * sizeof(int32_t), 0));
+            KETO_HIP(hipMalloc(&x->dq, nb * sizeof(keto_query)));
+            KETO_HIP(hipMalloc(&x->da, nb));
+            KETO_HIP(hipMalloc(&x->de, nb * sizeof(int32_t)));
+        }
+        for (auto &x : d->slots) {
+            Slot *p = x.get();
+            p->th = std::thread([p] {
+                (void)hipSetDevice(p->d->device);
+                p->run();
+            });
+        }
+    } catch (...) {
+        shutdown(d);
+        throw;
+    }
+    *out = reinterpret_cast<keto_dispatcher *>(d);
+}
+
+void dispatcher_destroy(keto_dispatcher *hd) {
+    if (Dispatcher *d = DP(hd)) shutdown(d);
+}
+
+int dispatcher_check(keto_dispatcher *hd, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err,
+                     std::string &msg) {
+    Dispatcher *d = DP(hd);
+    if (!d) throw Error(KETO_E_INVALID, "null dispatcher");
+    if (n == 0) return KETO_OK;
+    if (!q || !allowed || !err) throw Error(KETO_E_INVALID, "null buffer");
+    Request r;
+    r.q = q;
+    r.n = n;
+    r.allowed = allowed;
+    r.err = err;
+    std::unique_lock<std::mutex> lk(d->m);
+    if (d->stop) throw Error(KETO_E_INVALID, "dispatcher is shutting down");
+    d->queue.push_back(&r);
+    d->queued += n;
+    d->cv_in.notify_one();
+    r.cv.wait(lk, [&] { return r.done; });
+    msg = r.msg;
+    return r.rc;
+}
+
+void dispatcher_set_snapshot(keto_dispatcher *hd, keto_snapshot *snap) {
+    Dispatcher *d = DP(hd);
+    if (!d || !snap) throw Error(KETO_E_INVALID, "null argument");
+    if (reinterpret_cast<Snapshot *>(snap)->device != d->device)
+        throw Error(KETO_E_INVALID, "snapshot is on another device");
+    std::unique_lock<std::shared_mutex> bl(d->snap_mu);  // when this returns the old snapshot is idle
+    d->snap = snap;
+}
+
+void dispatcher_stats(keto_dispatcher *hd, keto_dispatcher_stats *out) {
+    Dispatcher *d = DP(hd);
+    if (!d || !out) throw Error(KETO_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(d->m);
+    *out = d->stats;
+}
+
+}  // namespace keto

@@ -166,4 +166,12 @@ void trees_to_json(const keto_tree_node *nodes, const uint64_t *offsets, uint64_
 void trees_to_proto(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,
                     const keto_name_tables *names, uint8_t *out, uint64_t cap, uint64_t *out_offsets);
 
+// dispatcher.cpp: request coalescing (keto_dispatcher_*)
+void dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, keto_dispatcher **out);
+void dispatcher_destroy(keto_dispatcher *d);
+int dispatcher_check(keto_dispatcher *d, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err,
+                     std::string &msg);
+void dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap);
+void dispatcher_stats(keto_dispatcher *d, keto_dispatcher_stats *out);
+
 }  // namespace keto

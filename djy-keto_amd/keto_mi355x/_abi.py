@@ -52,6 +52,16 @@ class WorkCounters(ctypes.Structure):
                 ("wave_steps", ctypes.c_uint64 * 3), ("lane_steps", ctypes.c_uint64 * 3)]
 
 
+class DispatcherConfig(ctypes.Structure):
+    _fields_ = [("limits", Limits), ("max_batch", ctypes.c_uint32), ("max_wait_us", ctypes.c_uint32),
+                ("inflight", ctypes.c_uint32)]
+
+
+class DispatcherStats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("queries", ctypes.c_uint64),
+                ("max_batch_seen", ctypes.c_uint64)]
+
+
 class NameTables(ctypes.Structure):
     _fields_ = [("n_namespaces", ctypes.c_uint32), ("namespace_names", ctypes.POINTER(ctypes.c_char_p)),
                 ("n_relations", ctypes.c_uint32), ("relation_names", ctypes.POINTER(ctypes.c_char_p)),
@@ -79,6 +89,11 @@ SIGNATURES = {
     "keto_memcpy_h2d": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
     "keto_memcpy_d2h": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
     "keto_device_count": (ctypes.c_int, [ctypes.POINTER(_I32)]),
+    "keto_dispatcher_create": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherConfig), ctypes.POINTER(_VP)]),
+    "keto_dispatcher_destroy": (ctypes.c_int, [_VP]),
+    "keto_dispatcher_check": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP]),
+    "keto_dispatcher_set_snapshot": (ctypes.c_int, [_VP, _VP]),
+    "keto_dispatcher_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherStats)]),
     "keto_trees_to_json": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
     "keto_trees_to_proto": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
 }

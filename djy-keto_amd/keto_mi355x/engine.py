@@ -223,3 +223,41 @@ class ExpandEngine:
         if err[0]:
             raise KetoError(int(err[0]), "expand failed")
         return nodes[int(offs[0]):int(offs[1])] if offs[1] > offs[0] else None
+
+
+class Dispatcher:
+    """Request coalescing (keto_dispatcher_*): many threads call check(); one dispatcher
+    thread in the library batches whatever is queued into each launch.  ctypes releases the
+    GIL for the blocking call, so Python threads coalesce like goroutines in the Go shim."""
+
+    def __init__(self, snapshot: Snapshot, max_read_depth: int = 5, max_read_width: int = 100,
+                 max_batch: int = 1 << 16, max_wait_us: int = 0, inflight: int = 4):
+        cfg = _abi.DispatcherConfig(_abi.Limits(max_read_depth, max_read_width), max_batch, max_wait_us, inflight)
+        h = ctypes.c_void_p()
+        check(lib().keto_dispatcher_create(snapshot.handle, ctypes.byref(cfg), ctypes.byref(h)))
+        self.handle = h
+        self.snapshot = snapshot
+
+    def check(self, queries: np.ndarray):
+        q = np.ascontiguousarray(queries, dtype=_abi.QUERY_DT)
+        allowed = np.zeros(len(q), dtype=np.uint8)
+        err = np.zeros(max(1, len(q)), dtype=np.int32)
+        check(lib().keto_dispatcher_check(self.handle, q.ctypes.data, len(q), allowed.ctypes.data, err.ctypes.data))
+        return allowed, err[: len(q)]
+
+    def set_snapshot(self, snapshot: Snapshot):
+        check(lib().keto_dispatcher_set_snapshot(self.handle, snapshot.handle))
+        self.snapshot = snapshot
+
+    def stats(self) -> dict:
+        st = _abi.DispatcherStats()
+        check(lib().keto_dispatcher_stats_get(self.handle, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in st._fields_}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().keto_dispatcher_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()

@@ -40,7 +40,7 @@ import torch
 import torch.distributed as dist
 
 from . import _abi
-from .engine import CheckEngine, ExpandEngine, Snapshot, Stream
+from .engine import CheckEngine, DeviceBuffer, ExpandEngine, Snapshot, Stream
 
 _MULT = 0x9E3779B97F4A7C15
 _MULT_I64 = _MULT - (1 << 64)   # the same bits as a signed 64-bit multiplier
@@ -178,7 +178,12 @@ class PartitionedEngine:
         self.n_uuids, self.strict, self.device = n_uuids, strict, device
         self.max_read_depth, self.max_read_width = max_read_depth, max_read_width
         self.comm = _Comm(group)
-        self.store = ObjectStore(part_tuples, store_device or f"cuda:{device}")
+        # the exchange runs where the process group's tensors live: on the GPU under RCCL, on
+        # the host under gloo (and for a single rank), where the closure is uploaded through
+        # the library's own allocator
+        if store_device is None:
+            store_device = f"cuda:{device}" if self.comm.dev == "cuda" else "cpu"
+        self.store = ObjectStore(part_tuples, store_device)
         self.stream = None
         self.last = {}
 
@@ -193,12 +198,21 @@ class PartitionedEngine:
         return closure(self.store, self.comm, keys, self.levels())
 
     def _snapshot(self, rows: torch.Tensor) -> Snapshot:
-        rows = rows.to(f"cuda:{self.device}").contiguous()
-        torch.cuda.synchronize(self.device)  # the builder reads them from its own stream
-        snap = Snapshot(self.namespaces, None, self.ns_names, self.rel_names, self.n_uuids, strict=self.strict,
-                        device=self.device, device_tuples=(rows.data_ptr(), int(rows.shape[0])))
-        snap._rows = rows  # keep alive with the snapshot (the build has finished reading it)
-        return snap
+        n = int(rows.shape[0])
+        if rows.is_cuda:
+            rows = rows.contiguous()
+            torch.cuda.synchronize(rows.device)  # the builder reads them from its own stream
+            return Snapshot(self.namespaces, None, self.ns_names, self.rel_names, self.n_uuids, strict=self.strict,
+                            device=self.device, device_tuples=(rows.data_ptr(), n))
+        host = np.ascontiguousarray(rows.numpy()).view(_abi.TUPLE_DT).reshape(-1)
+        buf = DeviceBuffer(self.device, max(1, host.nbytes))
+        try:
+            if n:
+                buf.upload(self._stream(), host)
+            return Snapshot(self.namespaces, None, self.ns_names, self.rel_names, self.n_uuids, strict=self.strict,
+                            device=self.device, device_tuples=(buf.ptr, n))
+        finally:
+            buf.free()  # the build has finished reading the records
 
     def _stream(self) -> Stream:
         if self.stream is None:

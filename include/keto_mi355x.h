@@ -173,6 +173,30 @@ int keto_expand_batch(keto_snapshot *snap, keto_stream *s, const keto_subject_se
                       const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap,
                       uint64_t *out_offsets, int32_t *out_err);
 
+/* Request coalescing for serving: concurrent callers, one batch per launch (the
+ * dispatcher a Go shim puts behind CheckService, check/handler.go:304-331). */
+typedef struct keto_dispatcher keto_dispatcher;
+typedef struct keto_dispatcher_config {
+    keto_limits limits;
+    uint32_t max_batch;   /* queries per launch (staging size); a larger request runs alone */
+    uint32_t max_wait_us; /* 0: launch as soon as a slot is free with whatever is queued */
+    uint32_t inflight;    /* batches in flight on their own streams (0 -> 4, at most 16) */
+} keto_dispatcher_config;
+typedef struct keto_dispatcher_stats {
+    uint64_t batches, requests, queries, max_batch_seen;
+} keto_dispatcher_stats;
+
+/* The snapshot must outlive the dispatcher (or be replaced with set_snapshot first). */
+int keto_dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, keto_dispatcher **out);
+int keto_dispatcher_destroy(keto_dispatcher *d);
+/* Thread-safe; blocks until the n queries are decided.  Same outputs as keto_check_batch. */
+int keto_dispatcher_check(keto_dispatcher *d, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
+                          int32_t *out_err);
+/* Switch to another snapshot (same device) between batches; when this returns the previous
+ * snapshot is no longer in use and may be freed. */
+int keto_dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap);
+int keto_dispatcher_stats_get(keto_dispatcher *d, keto_dispatcher_stats *out);
+
 /* Name tables for the API form of a result (Mapper, uuid_mapping.go:199-399): id -> string
  * for namespaces, relations and interned UUIDs (the shim's MapUUIDsToStrings view of
  * keto_uuid_mappings, persistence/sql/uuid_mapping.go:19-33). */
