@@ -381,3 +381,41 @@ int keto_dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap) {
 int keto_dispatcher_stats_get(keto_dispatcher *d, keto_dispatcher_stats *out) {
     return guarded([&] { keto::dispatcher_stats(d, out); });
 }
+
+int keto_store_create(int32_t device, const keto_tuple *tuples, uint64_t n, uint32_t flags, keto_store **out) {
+    if (!out) return fail(KETO_E_INVALID, "null output pointer");
+    *out = nullptr;
+    if (n && !tuples) return fail(KETO_E_INVALID, "null tuples");
+    return guarded([&] {
+        *out = reinterpret_cast<keto_store *>(keto::store_create(device, tuples, n, (flags & KETO_F_DEVICE_PTRS) != 0));
+    });
+}
+
+int keto_store_transact(keto_store *st, const keto_tuple *ins, uint64_t n_ins, const keto_tuple *del, uint64_t n_del,
+                        uint32_t flags) {
+    if (!st) return fail(KETO_E_INVALID, "null store");
+    if ((n_ins && !ins) || (n_del && !del)) return fail(KETO_E_INVALID, "null delta");
+    return guarded([&] {
+        keto::store_transact(*reinterpret_cast<keto::TupleStore *>(st), ins, n_ins, del, n_del,
+                             (flags & KETO_F_DEVICE_PTRS) != 0);
+    });
+}
+
+int keto_store_snapshot(keto_store *st, const keto_snapshot_config *cfg, keto_snapshot **out) {
+    if (!st || !out) return fail(KETO_E_INVALID, "null argument");
+    *out = nullptr;
+    return guarded([&] {
+        *out = reinterpret_cast<keto_snapshot *>(keto::store_snapshot(*reinterpret_cast<keto::TupleStore *>(st), cfg));
+    });
+}
+
+int keto_store_info(keto_store *st, uint64_t *n_tuples, uint64_t *version) {
+    if (!st) return fail(KETO_E_INVALID, "null store");
+    keto::store_info(*reinterpret_cast<keto::TupleStore *>(st), n_tuples, version);
+    return KETO_OK;
+}
+
+int keto_store_free(keto_store *st) {
+    keto::store_free(reinterpret_cast<keto::TupleStore *>(st));
+    return KETO_OK;
+}

@@ -174,4 +174,13 @@ int dispatcher_check(keto_dispatcher *d, const keto_query *q, uint64_t n, uint8_
 void dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap);
 void dispatcher_stats(keto_dispatcher *d, keto_dispatcher_stats *out);
 
+// store.hip: device tuple store with TransactRelationTuples deltas (keto_store_*)
+struct TupleStore;
+TupleStore *store_create(int device, const keto_tuple *tuples, uint64_t n, bool device_ptrs);
+void store_transact(TupleStore &st, const keto_tuple *ins, uint64_t n_ins, const keto_tuple *del, uint64_t n_del,
+                    bool device_ptrs);
+Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg);
+void store_free(TupleStore *st);
+void store_info(const TupleStore &st, uint64_t *n, uint64_t *version);
+
 }  // namespace keto

@@ -39,7 +39,7 @@ class SnapshotConfig(ctypes.Structure):
 class SnapshotInfo(ctypes.Structure):
     _fields_ = [("n_tuples", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64), ("n_entities", ctypes.c_uint64),
                 ("n_set_edges", ctypes.c_uint64), ("n_rev_entries", ctypes.c_uint64),
-                ("device_bytes", ctypes.c_uint64), ("build_seconds", ctypes.c_double)]
+                ("device_bytes", ctypes.c_uint64), ("build_seconds", ctypes.c_double), ("version", ctypes.c_uint64)]
 
 
 class Limits(ctypes.Structure):
@@ -89,6 +89,11 @@ SIGNATURES = {
     "keto_memcpy_h2d": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
     "keto_memcpy_d2h": (ctypes.c_int, [_VP, _VP, _VP, _U64]),
     "keto_device_count": (ctypes.c_int, [ctypes.POINTER(_I32)]),
+    "keto_store_create": (ctypes.c_int, [_I32, _VP, _U64, _U32, ctypes.POINTER(_VP)]),
+    "keto_store_transact": (ctypes.c_int, [_VP, _VP, _U64, _VP, _U64, _U32]),
+    "keto_store_snapshot": (ctypes.c_int, [_VP, ctypes.POINTER(SnapshotConfig), ctypes.POINTER(_VP)]),
+    "keto_store_info": (ctypes.c_int, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    "keto_store_free": (ctypes.c_int, [_VP]),
     "keto_dispatcher_create": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherConfig), ctypes.POINTER(_VP)]),
     "keto_dispatcher_destroy": (ctypes.c_int, [_VP]),
     "keto_dispatcher_check": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP]),

@@ -59,9 +59,11 @@ class Snapshot:
     """Immutable device-resident snapshot (CSR rows + compiled rewrite program)."""
 
     def __init__(self, namespaces_json: str | dict, tuples: np.ndarray, ns_names: list, rel_names: list,
-                 n_uuids: int, strict: bool = False, device: int = 0, device_tuples: tuple | None = None):
+                 n_uuids: int, strict: bool = False, device: int = 0, device_tuples: tuple | None = None,
+                 store: "TupleStore | None" = None):
         """tuples: host TUPLE_DT array; or tuples=None and device_tuples=(device pointer, count)
-        for records already resident on `device` (keto_snapshot_build_device)."""
+        for records already resident on `device` (keto_snapshot_build_device); or tuples=None
+        and store=TupleStore for its current content (keto_store_snapshot)."""
         if isinstance(namespaces_json, dict):
             namespaces_json = json.dumps(namespaces_json)
         self._ns = (ctypes.c_char_p * max(1, len(ns_names)))(*[n.encode() for n in ns_names])
@@ -70,7 +72,9 @@ class Snapshot:
         cfg = _abi.SnapshotConfig(len(ns_names), self._ns, len(rel_names), self._rel, n_uuids, self._json,
                                   int(strict), device)
         h = ctypes.c_void_p()
-        if device_tuples is not None:
+        if store is not None:
+            check(lib().keto_store_snapshot(store.handle, ctypes.byref(cfg), ctypes.byref(h)))
+        elif device_tuples is not None:
             ptr, count = device_tuples
             check(lib().keto_snapshot_build_device(ctypes.byref(cfg), ptr, count, ctypes.byref(h)))
         else:
@@ -88,6 +92,36 @@ class Snapshot:
     def close(self):
         if getattr(self, "handle", None):
             lib().keto_snapshot_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+class TupleStore:
+    """Device-resident tuple store of one network (keto_store_*): TransactRelationTuples
+    deltas, versioned snapshots (the version is the snaptoken)."""
+
+    def __init__(self, tuples: np.ndarray, device: int = 0):
+        t = np.ascontiguousarray(tuples, dtype=_abi.TUPLE_DT)
+        h = ctypes.c_void_p()
+        check(lib().keto_store_create(device, t.ctypes.data if len(t) else None, len(t), 0, ctypes.byref(h)))
+        self.handle, self.device = h, device
+
+    def transact(self, insert: np.ndarray | None = None, delete: np.ndarray | None = None):
+        ins = np.ascontiguousarray(insert if insert is not None else np.zeros(0, _abi.TUPLE_DT), dtype=_abi.TUPLE_DT)
+        dele = np.ascontiguousarray(delete if delete is not None else np.zeros(0, _abi.TUPLE_DT), dtype=_abi.TUPLE_DT)
+        check(lib().keto_store_transact(self.handle, ins.ctypes.data if len(ins) else None, len(ins),
+                                        dele.ctypes.data if len(dele) else None, len(dele), 0))
+
+    def info(self) -> tuple:
+        n, v = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().keto_store_info(self.handle, ctypes.byref(n), ctypes.byref(v)))
+        return n.value, v.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().keto_store_free(self.handle)
             self.handle = None
 
     def __del__(self):

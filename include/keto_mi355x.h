@@ -112,6 +112,7 @@ typedef struct keto_snapshot_info {
     uint64_t n_tuples, n_nodes, n_entities, n_set_edges, n_rev_entries;
     uint64_t device_bytes;
     double build_seconds;
+    uint64_t version; /* keto_store version it was cut from (the snaptoken); 0 if built directly */
 } keto_snapshot_info;
 
 /* limit.max_read_depth / limit.max_read_width (internal/driver/config/provider.go:180-185) */
@@ -172,6 +173,20 @@ int keto_check_batch(keto_snapshot *snap, keto_stream *s, const keto_query *quer
 int keto_expand_batch(keto_snapshot *snap, keto_stream *s, const keto_subject_set *roots, uint64_t n,
                       const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap,
                       uint64_t *out_offsets, int32_t *out_err);
+
+/* Incremental snapshots: a device-resident tuple store of one network that applies
+ * TransactRelationTuples deltas (persistence/sql/relationtuples.go:277-287: insert every row
+ * of ins -- the caller supplies their fresh shard_ids --, then delete every row matching a
+ * row of del on (namespace, object, relation, subject), :168-189) and cuts snapshots of its
+ * current content, stamped with its version.  flags: KETO_F_DEVICE_PTRS for device inputs. */
+typedef struct keto_store keto_store;
+int keto_store_create(int32_t device, const keto_tuple *tuples, uint64_t n, uint32_t flags, keto_store **out);
+int keto_store_transact(keto_store *st, const keto_tuple *ins, uint64_t n_ins, const keto_tuple *del, uint64_t n_del,
+                        uint32_t flags);
+/* cfg->device must be the store's device; cfg->n_uuids must cover every id written so far */
+int keto_store_snapshot(keto_store *st, const keto_snapshot_config *cfg, keto_snapshot **out);
+int keto_store_info(keto_store *st, uint64_t *n_tuples, uint64_t *version);
+int keto_store_free(keto_store *st);
 
 /* Request coalescing for serving: concurrent callers, one batch per launch (the
  * dispatcher a Go shim puts behind CheckService, check/handler.go:304-331). */
