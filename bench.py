@@ -145,6 +145,30 @@ def build_workload(name, rank, world, device, args):
     return wl, snap, time.perf_counter() - t0
 
 
+def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
+    """Batched Expand (configs[4]'s "4096 Expand queries per batch"): n subject-set roots (half
+    Group#members, half Folder#viewers) per batch, host buffers in and out, both kernel passes
+    (count, emit) included.  Bytes model 8*rows + 4*edges + 12*out_nodes."""
+    rng = np.random.default_rng(5)
+    r = np.zeros(n, dtype=km.SUBJSET_DT)
+    h = n // 2
+    r["ns"][:h], r["rel"][:h] = 1, wl.rel_names.index("members")
+    r["obj"][:h] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], h)
+    r["ns"][h:], r["rel"][h:] = 2, wl.rel_names.index("viewers")
+    r["obj"][h:] = rng.integers(0, wl.meta["folders_per_root"], n - h)
+    xe = km.ExpandEngine(snap, stream, max_read_depth=wl.max_depth)
+    nodes, offs, err = xe.build_trees(r)  # warm-up (sizes the output buffer)
+    stream.counters(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        nodes, offs, err = xe.build_trees(r)
+    dt = (time.perf_counter() - t0) / reps
+    c = stream.counters(reset=True)
+    return {"roots_per_batch": n, "ms_per_batch": dt * 1e3, "trees_per_s": n / dt, "nodes_per_batch": int(offs[n]),
+            "errors": int((err != 0).sum()), "max_read_depth": wl.max_depth,
+            "note": "host buffers in/out, count + emit passes; roots: Group#members and Folder#viewers"}
+
+
 def serving_probe(km, snap, q, wl, clients: int, req: int, seconds: float):
     """Closed-loop serving load through the coalescing dispatcher (keto_dispatcher_*): `clients`
     threads each send `req`-query requests back to back.  Reported beside the batch numbers;
@@ -316,11 +340,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     stream.sync()
-    kms = []
+    stream.kernel_time(reset=True)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         eng.check_batch_device(dq, len(q), da, de, sync=True)
-        kms.append(stream.last_kernel_ms())
     stream.sync()
     torch.cuda.synchronize()
     if dist_on:
@@ -328,7 +351,11 @@ def main():
     elapsed_local = time.perf_counter() - t_start
     value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps,
                                      f"cuda:{device}" if dist_on else "cpu")
-    kernel_ms = float(np.mean(kms))
+    # average tier-0 kernel duration over the timed region: HIP event pairs recorded on the
+    # kernel's own stream around every launch, summed natively
+    k_sum, k_n = stream.kernel_time(reset=True)
+    assert k_n == args.steps, f"timed {k_n} kernel launches, expected {args.steps}"
+    kernel_ms = k_sum / k_n
 
     # PCIe-inclusive rate (host buffers: H2D queries, kernels, D2H decisions) -- never `value`
     t1 = time.perf_counter()
@@ -348,6 +375,7 @@ def main():
         lat.append(time.perf_counter() - t1)
     p99_ms = float(np.percentile(np.array(lat) * 1e3, 99)) if lat else None
 
+    expand = expand_probe(km, snap, wl, stream) if args.workload in ("c3", "c4") else None
     serving = serving_probe(km, snap, q, wl, args.serve_clients, args.serve_request, args.serve_seconds) \
         if args.serve_clients > 0 else None
 
@@ -388,6 +416,7 @@ def main():
         "allowed_fraction": float(allowed.mean()),
         "pcie_inclusive_checks_per_s": pcie_rate,
         "serving": serving,
+        "expand": expand,
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -54,9 +54,42 @@ Stream::~Stream() {
     if (qbuf) (void)hipFree(qbuf);
     if (obuf) (void)hipFree(obuf);
     if (counters) (void)hipFree(counters);
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
+    for (int i = 0; i < TIMER_SLOTS; i++) {
+        if (ev_a[i]) (void)hipEventDestroy(ev_a[i]);
+        if (ev_b[i]) (void)hipEventDestroy(ev_b[i]);
+    }
     if (stream) (void)hipStreamDestroy(stream);
+}
+
+void Stream::mark_begin() {
+    if (timer_issued - timer_harvested == (uint64_t)TIMER_SLOTS) {  // ring full: wait for the oldest
+        const int o = (int)(timer_harvested % TIMER_SLOTS);
+        KETO_HIP(hipEventSynchronize(ev_b[o]));
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, ev_a[o], ev_b[o]) == hipSuccess) {
+            timer_ms_sum += ms;
+            timer_count++;
+            last_kernel_ms = ms;
+        }
+        timer_harvested++;
+    }
+    KETO_HIP(hipEventRecord(ev_a[timer_issued % TIMER_SLOTS], stream));
+}
+
+void Stream::mark_end() {
+    KETO_HIP(hipEventRecord(ev_b[timer_issued % TIMER_SLOTS], stream));
+    timer_issued++;
+}
+
+void Stream::harvest() {
+    for (; timer_harvested < timer_issued; timer_harvested++) {
+        const int o = (int)(timer_harvested % TIMER_SLOTS);
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, ev_a[o], ev_b[o]) != hipSuccess) break;  // not complete yet
+        timer_ms_sum += ms;
+        timer_count++;
+        last_kernel_ms = ms;
+    }
 }
 }  // namespace keto
 
@@ -122,8 +155,10 @@ int keto_stream_create(int32_t device, keto_stream **out) {
         auto s = std::make_unique<keto::Stream>();
         s->device = device;
         KETO_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-        KETO_HIP(hipEventCreate(&s->ev0));
-        KETO_HIP(hipEventCreate(&s->ev1));
+        for (int i = 0; i < keto::Stream::TIMER_SLOTS; i++) {
+            KETO_HIP(hipEventCreate(&s->ev_a[i]));
+            KETO_HIP(hipEventCreate(&s->ev_b[i]));
+        }
         KETO_HIP(hipMalloc(&s->counters, 24 * sizeof(unsigned long long)));
         KETO_HIP(hipMemsetAsync(s->counters, 0, 24 * sizeof(unsigned long long), s->stream));
         KETO_HIP(hipStreamSynchronize(s->stream));
@@ -142,8 +177,23 @@ int keto_stream_sync(keto_stream *hs) {
     return guarded([&] {
         KETO_HIP(hipSetDevice(s->device));
         KETO_HIP(hipStreamSynchronize(s->stream));
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, s->ev0, s->ev1) == hipSuccess) s->last_kernel_ms = ms;
+        s->harvest();
+    });
+}
+
+int keto_stream_kernel_time(keto_stream *hs, double *ms_sum, uint64_t *launches, int32_t reset) {
+    keto::Stream *s = ST(hs);
+    if (!s) return fail(KETO_E_INVALID, "null stream");
+    return guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        KETO_HIP(hipStreamSynchronize(s->stream));
+        s->harvest();
+        if (ms_sum) *ms_sum = s->timer_ms_sum;
+        if (launches) *launches = s->timer_count;
+        if (reset) {
+            s->timer_ms_sum = 0;
+            s->timer_count = 0;
+        }
     });
 }
 
@@ -203,8 +253,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
             (snap->ops.empty() ? keto::run_check_union : keto::run_check)(*snap, *s, L);
             if (!(flags & KETO_F_ASYNC)) {
                 KETO_HIP(hipStreamSynchronize(s->stream));
-                float ms = 0;
-                if (n && hipEventElapsedTime(&ms, s->ev0, s->ev1) == hipSuccess) s->last_kernel_ms = ms;
+                s->harvest();
             }
             return;
         }
@@ -222,8 +271,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipStreamSynchronize(s->stream));
-        float ms = 0;
-        if (n && hipEventElapsedTime(&ms, s->ev0, s->ev1) == hipSuccess) s->last_kernel_ms = ms;
+        s->harvest();
     });
 }
 

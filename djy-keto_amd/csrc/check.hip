@@ -927,7 +927,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         }
         const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);  // every launched lane owns scratch
         dim3 grid(lanes / bs), block(bs);
-        if (tier == 0) KETO_HIP(hipEventRecord(st.ev0, st.stream));
+        if (tier == 0) st.mark_begin();
         if (lds_tables) {
             if (L.count) hipLaunchKernelGGL((check_kernel<true, true>), grid, block, lds, st.stream, P);
             else hipLaunchKernelGGL((check_kernel<false, true>), grid, block, lds, st.stream, P);
@@ -936,7 +936,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             else hipLaunchKernelGGL((check_kernel<false, false>), grid, block, 0, st.stream, P);
         }
         KETO_HIP(hipGetLastError());
-        if (tier == 0) KETO_HIP(hipEventRecord(st.ev1, st.stream));
+        if (tier == 0) st.mark_end();
     }
 }
 

@@ -113,7 +113,15 @@ struct Scratch {
 struct Stream {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // main-kernel timing: HIP event pairs recorded around every batch's tier-0 launch on this
+    // stream, harvested after synchronisation (a ring, so async batches can queue up)
+    static constexpr int TIMER_SLOTS = 64;
+    hipEvent_t ev_a[TIMER_SLOTS] = {}, ev_b[TIMER_SLOTS] = {};
+    uint64_t timer_issued = 0, timer_harvested = 0, timer_count = 0;
+    double timer_ms_sum = 0;
+    void mark_begin();  // before the main kernel (stream-ordered)
+    void mark_end();    // after it
+    void harvest();     // accumulate every completed pair (call after a stream sync)
     // device workspace (allocated on first use, never inside a launch sequence)
     Scratch check_scratch, union_scratch, expand_scratch;
     // per-batch workspace of list_cap queries, one allocation:

@@ -82,6 +82,7 @@ SIGNATURES = {
     "keto_stream_sync": (ctypes.c_int, [_VP]),
     "keto_stream_counters": (ctypes.c_int, [_VP, ctypes.POINTER(WorkCounters), _I32]),
     "keto_stream_last_kernel_ms": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double)]),
+    "keto_stream_kernel_time": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64), _I32]),
     "keto_check_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),
     "keto_expand_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _U64, _VP, _VP]),
     "keto_device_alloc": (ctypes.c_int, [_I32, _U64, ctypes.POINTER(_VP)]),

@@ -147,6 +147,12 @@ class Stream:
         out["per_tier"] = per
         return out
 
+    def kernel_time(self, reset: bool = False) -> tuple:
+        """(summed main-kernel ms, launches) timed with HIP events on this stream"""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        check(lib().keto_stream_kernel_time(self.handle, ctypes.byref(ms), ctypes.byref(n), int(reset)))
+        return ms.value, n.value
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_double()
         check(lib().keto_stream_last_kernel_ms(self.handle, ctypes.byref(ms)))

@@ -160,6 +160,10 @@ int keto_stream_counters(keto_stream *s, keto_work_counters *out, int32_t reset)
 /* average device time (ms) of the last batch's main check kernel, measured with
  * HIP events on the stream the kernel ran on */
 int keto_stream_last_kernel_ms(keto_stream *s, double *ms);
+/* Synchronises the stream, then reports the summed device time (ms) and count of the main
+ * check kernel launches timed on it (HIP events around every batch's launch, async batches
+ * included); reset != 0 zeroes the sums afterwards. */
+int keto_stream_kernel_time(keto_stream *s, double *ms_sum, uint64_t *launches, int32_t reset);
 
 /* Check n queries: out_allowed[i] = CheckIsMember's bool, out_err[i] = error code.
  * Replaces check.Engine.CheckIsMember (engine.go:65-71) for a whole batch. */
