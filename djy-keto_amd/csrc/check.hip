@@ -165,6 +165,19 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
         for (int guard = 0; guard < 24 && ln == 0 && fin == 0; guard++) {
             const uint32_t w = top.w;
             const uint32_t d = f_d(w);
+#ifdef KETO_PROF_STATES  // profiling builds only (tools/ab_build.sh, tools/prof_states.py)
+            if (COUNT) {     // tiers 1-2 counter slots <- per dispatch key: rounds a wave runs it (1) or lanes in it (2)
+                const int lead = __ffsll((long long)__ballot(true)) - 1;
+                const uint32_t key = st == S_RUN ? 17 + f_type(w) : st;  // slots 7 and 15 are not exported
+                const uint32_t keys[16] = {S_RET, S_POP, S_ROWOFF, S_FSCAN, S_ESDONE, S_CNEXT, S_VIS, S_CEDGE,
+                                           S_TNEXT, 17, 18, 19, 20, 21, 22, S_TEDGE};
+                for (uint32_t k = 0; k < 16; k++) {
+                    const unsigned long long b = __ballot(key == keys[k]);
+                    const unsigned long long v = KETO_PROF_STATES == 1 ? (b != 0) : (unsigned long long)__popcll(b);
+                    if ((int)lane == lead && v) atomicAdd(&P.counters[8 + k], v);
+                }
+            }
+#endif
             switch (st) {
             // ---------------------------------------------------------------- query entry
             case S_START:

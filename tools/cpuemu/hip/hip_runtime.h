@@ -66,6 +66,7 @@ inline hipError_t hipEventRecord(hipEvent_t e, hipStream_t) {
     *(double *)e = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
     return hipSuccess;
 }
+inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipEventElapsedTime(float *ms, hipEvent_t a, hipEvent_t b) { *ms = float(*(double *)b - *(double *)a); return hipSuccess; }
 template <class K>
 inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int *n, K, int, size_t) { *n = 2; return hipSuccess; }
@@ -76,6 +77,7 @@ inline unsigned long long __ballot(int p) { return p ? 1ull : 0ull; }
 template <class T> inline T __shfl(T v, int) { return v; }
 template <class T> inline T __shfl_down(T, int) { return T(0); }
 inline int __ffsll(long long v) { return __builtin_ffsll(v); }
+inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 inline void __syncthreads() {}
 inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
@@ -89,6 +91,7 @@ inline uint32_t atomicCAS(uint32_t *p, uint32_t c, uint32_t v) {
 }
 constexpr int warpSize = 1;
 #define __builtin_amdgcn_readfirstlane(x) (x)
+#define __builtin_amdgcn_readlane(x, l) (x)
 #define __builtin_amdgcn_fence(...) ((void)0)
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 inline unsigned long long atomicCAS(unsigned long long *p, unsigned long long c, unsigned long long v) {
