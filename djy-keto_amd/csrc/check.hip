@@ -82,6 +82,10 @@ struct CheckParams {
     uint32_t last_tier;
 };
 
+#ifndef KETO_GUARD
+#define KETO_GUARD 24
+#endif
+
 __device__ __forceinline__ uint32_t w8(const uint4 &v0, const uint4 &v1, uint32_t j) {
     return j < 4 ? wword(v0, j) : wword(v1, j - 4);
 }
@@ -162,7 +166,10 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
 
         // fin: 0 running, 1 finished (res), 2 scratch outgrown
         uint32_t fin = 0;
-        for (int guard = 0; guard < 24 && ln == 0 && fin == 0; guard++) {
+        // At most KETO_GUARD transitions per step; the rest carry over to the next step.  S_FSCAN
+        // entered by a transition reads its window from v0 (set to the cached `ew`), which does
+        // not survive the step boundary: such a lane always runs it before leaving.
+        for (int guard = 0; (guard < KETO_GUARD || st == S_FSCAN) && ln == 0 && fin == 0; guard++) {
             const uint32_t w = top.w;
             const uint32_t d = f_d(w);
 #ifdef KETO_PROF_STATES  // profiling builds only (tools/ab_build.sh, tools/prof_states.py)

@@ -1,0 +1,30 @@
+"""CPU emulation of the Check interpreter's step boundary (no GPU).
+
+tools/cpuemu builds the kernel SOURCES for the host, one lane per wavefront.  Built with
+KETO_GUARD=1, every lane runs exactly one transition per load slot, so every pseudo
+transition crosses a step boundary -- the path a lane takes on the GPU when its 24-transition
+budget runs out.  The GPU parity suite (golden fixtures + random worlds) must still agree with
+the oracle.  Without the S_FSCAN rule in check.hip's transition loop 41 of those cases failed.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.slow
+def test_one_transition_per_step_matches_oracle(tmp_path):
+    lib = tmp_path / "libketo_emu_g1.so"
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(ROOT, "tools", "cpuemu"),
+                    f"OBJDIR={tmp_path / 'obj'}", f"LIB={lib}", "OPT=-O1 -DKETO_GUARD=1"],
+                   check=True, timeout=600)
+    env = dict(os.environ, KETO_MI355X_ALLOW_OVERRIDE="tools", KETO_MI355X_LIB_OVERRIDE=str(lib))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_gpu_parity.py"), "-k", "golden or random_worlds"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert " passed" in r.stdout
