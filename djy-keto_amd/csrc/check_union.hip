@@ -19,6 +19,10 @@
 namespace keto {
 namespace {
 
+#ifndef KETO_GUARD
+#define KETO_GUARD 8
+#endif
+
 enum UState : uint32_t {
     U_IDLE = 0,
     U_START,   // start record of the resolve pre-pass (2 x 16 B)
@@ -133,7 +137,10 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
 
         // result: 0 = keep going, 1 = allowed, 2 = denied, 3 = relation error, 4 = overflow
         uint32_t fin = 0;
-        for (int guard = 0; guard < 8 && ln == 0 && fin == 0; guard++) {
+        // At most KETO_GUARD transitions per step; the rest carry over to the next step.  U_SCAN
+        // entered by a transition reads its window from v0, which does not survive the step
+        // boundary: such a lane always runs it before leaving.
+        for (int guard = 0; (guard < KETO_GUARD || st == U_SCAN) && ln == 0 && fin == 0; guard++) {
             switch (st) {
             case U_START: {
                 node = v0.x;

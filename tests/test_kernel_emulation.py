@@ -24,7 +24,7 @@ def test_one_transition_per_step_matches_oracle(tmp_path):
                    check=True, timeout=600)
     env = dict(os.environ, KETO_MI355X_ALLOW_OVERRIDE="tools", KETO_MI355X_LIB_OVERRIDE=str(lib))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
-                        os.path.join(ROOT, "tests", "test_gpu_parity.py"), "-k", "golden or random_worlds"],
+                        os.path.join(ROOT, "tests", "test_gpu_parity.py"), "-k", "golden or random_worlds or synthetic_small"],
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert " passed" in r.stdout
