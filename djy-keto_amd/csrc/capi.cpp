@@ -321,39 +321,13 @@ int keto_expand_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_
             return;
         }
         if (total == 0) return;
-        void *d_out = nullptr;
-        grow(s->obuf, s->obuf_bytes, total * 12);
-        d_out = s->obuf;
+        grow(s->obuf, s->obuf_bytes, total * sizeof(keto_tree_node));
         KETO_HIP(hipMemcpyAsync(d_offs, out_offsets, n * 8, hipMemcpyHostToDevice, s->stream));
         L.emit = true;
-        L.out = static_cast<uint32_t *>(d_out);
-        keto::run_expand(*snap, *s, L);  // pass 2: emit pre-order nodes
-        std::vector<uint32_t> raw(total * 3);
-        KETO_HIP(hipMemcpyAsync(raw.data(), d_out, total * 12, hipMemcpyDeviceToHost, s->stream));
+        L.out = static_cast<keto_tree_node *>(s->obuf);
+        keto::run_expand(*snap, *s, L);  // pass 2: emit pre-order nodes, already in API form
+        KETO_HIP(hipMemcpyAsync(out_nodes, s->obuf, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipStreamSynchronize(s->stream));
-        const keto::Snapshot &S = *snap;
-        for (uint64_t i = 0; i < total; i++) {
-            keto_tree_node &o = out_nodes[i];
-            o.type = raw[3 * i];
-            o.n_children = raw[3 * i + 2];
-            uint32_t sk = raw[3 * i + 1];
-            if (sk & keto::SKEY_SET) {
-                uint32_t node = sk & ~keto::SKEY_SET;
-                uint32_t ns = S.ns_of(node);
-                const keto::NsDev &nd = S.ns[ns];
-                uint32_t e = nd.ent_base + (node - nd.node_base) / nd.n_slots;
-                uint32_t slot = (node - nd.node_base) % nd.n_slots;
-                o.subj_kind = 1;
-                o.s_obj = S.ent_obj[e];
-                o.s_ns = ns;
-                o.s_rel = S.slot_rel[nd.slot_base + slot];
-            } else {
-                o.subj_kind = 0;
-                o.s_obj = sk;
-                o.s_ns = 0;
-                o.s_rel = 0;
-            }
-        }
     });
     return g != KETO_OK ? g : rc;
 }

@@ -162,7 +162,7 @@ struct ExpandLaunch {
     int32_t max_depth;
     uint64_t *sizes;    // device [n] (count pass output)
     const uint64_t *offsets; // device [n] (emit pass input)
-    uint32_t *out;      // device nodes: 3 x u32 each {type, skey, n_children}
+    keto_tree_node *out;  // device nodes in API form (emit pass)
     int32_t *err;       // device [n]
     bool emit;
 };

@@ -21,6 +21,29 @@ __device__ __forceinline__ uint32_t resolve_node(const DevSnapshot &s, uint32_t 
     return t_node(global_tables(s), ns, e, rel);
 }
 
+// one output node in API form (Mapper.ToTree, uuid_mapping.go:356-385): a subject id, or a
+// subject set mapped back to (namespace, object uuid id, relation name id)
+__device__ __forceinline__ keto_tree_node api_node(const DevSnapshot &s, uint32_t type, uint32_t skey, uint32_t nch) {
+    keto_tree_node o;
+    o.type = type;
+    o.n_children = nch;
+    if (skey & SKEY_SET) {
+        const uint32_t node = skey & ~SKEY_SET;
+        const NodeInfo ni = t_node_info(global_tables(s), node);
+        const NsDev nd = s.ns[ni.ns];
+        o.subj_kind = 1;
+        o.s_obj = s.ent_obj[nd.ent_base + (node - nd.node_base) / nd.n_slots];
+        o.s_ns = ni.ns;
+        o.s_rel = s.slot_rel[nd.slot_base + ni.slot];
+    } else {
+        o.subj_kind = 0;
+        o.s_obj = skey;
+        o.s_ns = 0;
+        o.s_rel = 0;
+    }
+    return o;
+}
+
 struct ExpandParams {
     DevSnapshot s;
     const keto_subject_set *roots;
@@ -30,7 +53,7 @@ struct ExpandParams {
     int32_t max_depth;
     unsigned long long *sizes;
     const unsigned long long *offsets;
-    uint32_t *out;
+    keto_tree_node *out;  // emit pass: API records (keto_mi355x.h), pre-order per root
     int32_t *err;
     uint32_t *next;
     uint32_t *ovf_list, *ovf_count;
@@ -82,13 +105,9 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams P) {
         uint32_t vcount = 0;
         bool ovf = false;
         uint64_t cnt = 0;
-        uint32_t *out = P.emit ? P.out + 3ull * P.offsets[q] : nullptr;
+        keto_tree_node *out = P.emit ? P.out + P.offsets[q] : nullptr;
         auto emit = [&](uint32_t type, uint32_t skey, uint32_t nch) {
-            if (out) {
-                out[3 * cnt + 0] = type;
-                out[3 * cnt + 1] = skey;
-                out[3 * cnt + 2] = nch;
-            }
+            if (out) out[cnt] = api_node(s, type, skey, nch);
             cnt++;
         };
         uint64_t rows = 0, edges = 0;
@@ -205,8 +224,10 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
         P.last_tier = tier == 2;
         P.counters = L.emit ? nullptr : st.counters + 8 * tier;
         uint32_t lanes = t[tier].lanes;
-        if (tier == 0) lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + BLOCK - 1) / BLOCK) * BLOCK);
-        const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);  // every launched lane owns scratch
+        // tier 0: one-wave blocks, so a batch of a few thousand roots spreads over many CUs
+        // instead of filling a handful of them (each lane walks a whole tree)
+        if (tier == 0) lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + 63) / 64) * 64);
+        const uint32_t bs = std::min<uint32_t>(tier == 0 ? 64 : BLOCK, lanes);  // every launched lane owns scratch
         hipLaunchKernelGGL(expand_kernel, dim3(lanes / bs), dim3(bs), 0, st.stream, P);
         KETO_HIP(hipGetLastError());
     }

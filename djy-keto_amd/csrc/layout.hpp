@@ -63,6 +63,8 @@ struct DevSnapshot {
                                // one 16 B load; rows of <= 2 edges need no set_dst load
     const uint32_t *set_dst;   // node | EDGE_ALIAS, shard order within a row
     const uint32_t *weight;    // [n_nodes] capped path count below a node (longest-first scheduling)
+    const uint32_t *ent_obj;   // [n_entities] entity -> uuid id (NONE32 for phantoms): Expand output
+    const uint32_t *slot_rel;  // [total slots] global slot -> relation name id: Expand output
     const uint32_t *vkey;      // [n_nodes] visited representative (only read for aliased nodes)
     const uint32_t *all_off;   // [n_nodes+1]  every tuple of a node, shard order (Expand)
     const uint32_t *all_subj;  // subject id, or SKEY_SET|node

@@ -327,17 +327,23 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     if ((uint64_t)s.n_uuids + N + 1 >= (1ull << 32)) throw Error(KETO_E_LIMIT, "n_uuids + nodes exceeds 2^32");
     DevSnapshot &D = s.dev;
     {
-        DevBuf d_eb(4 * s.n_ns), d_r0(4 * s.n_ns), d_eo(4 * ent_total);
+        DevBuf d_eb(4 * s.n_ns), d_r0(4 * s.n_ns);
+        uint32_t *d_eo = static_cast<uint32_t *>(dalloc(4 * ent_total));  // kept: Expand output mapping
         KETO_HIP(hipMemcpy(d_eb.p, ent_base.data(), 4 * s.n_ns, hipMemcpyHostToDevice));
         KETO_HIP(hipMemcpy(d_r0.p, rank0.data(), 4 * s.n_ns, hipMemcpyHostToDevice));
-        KETO_HIP(hipMemset(d_eo.p, 0xFF, 4 * ent_total));  // phantoms: NONE32
+        KETO_HIP(hipMemset(d_eo, 0xFF, 4 * ent_total));  // phantoms: NONE32
         uint4 *table = static_cast<uint4 *>(dalloc(16 * nblk));
         build::entity_ids(static_cast<unsigned long long *>(d_bits.p), d_rank.u32(), nblk, bpn, stride, d_eb.u32(),
-                          d_r0.u32(), d_eo.u32(), table);
+                          d_r0.u32(), d_eo, table);
         D.ent_rank = table;
         D.ent_stride = stride;
+        D.ent_obj = d_eo;
         s.ent_obj.resize(ent_total);
-        KETO_HIP(hipMemcpy(s.ent_obj.data(), d_eo.p, 4 * ent_total, hipMemcpyDeviceToHost));
+        KETO_HIP(hipMemcpy(s.ent_obj.data(), d_eo, 4 * ent_total, hipMemcpyDeviceToHost));
+        uint32_t *d_sr = static_cast<uint32_t *>(dalloc(4 * std::max<size_t>(1, s.slot_rel.size())));
+        if (!s.slot_rel.empty())
+            KETO_HIP(hipMemcpy(d_sr, s.slot_rel.data(), 4 * s.slot_rel.size(), hipMemcpyHostToDevice));
+        D.slot_rel = d_sr;
     }
     phase("entities");
 

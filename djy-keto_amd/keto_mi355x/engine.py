@@ -237,6 +237,7 @@ class ExpandEngine:
         self.snapshot = snapshot
         self.stream = stream or Stream(snapshot.device)
         self.limits = _abi.Limits(max_read_depth, 100)
+        self._cap = 0  # output nodes the last batch needed: sizes the next one (no count-pass retry)
 
     def build_trees(self, roots: np.ndarray):
         """roots: SUBJSET_DT array -> (nodes TREE_DT, offsets uint64[n+1], err int32[n])."""
@@ -244,14 +245,14 @@ class ExpandEngine:
         n = len(r)
         offs = np.zeros(n + 1, dtype=np.uint64)
         err = np.zeros(max(1, n), dtype=np.int32)
-        cap = max(64, 16 * n)
+        cap = max(64, 16 * n, self._cap)
         while True:
-            nodes = np.zeros(cap, dtype=_abi.TREE_DT)
+            nodes = np.empty(cap, dtype=_abi.TREE_DT)  # filled by the library up to offs[n]
             rc = lib().keto_expand_batch(self.snapshot.handle, self.stream.handle, r.ctypes.data, n,
                                          ctypes.byref(self.limits), nodes.ctypes.data, cap, offs.ctypes.data,
                                          err.ctypes.data)
             if rc == _abi.KETO_E_CAPACITY:
-                cap = int(offs[n]) + 1
+                cap = self._cap = int(offs[n]) + 1
                 continue
             check(rc)
             return nodes[: int(offs[n])], offs, err[:n]
