@@ -171,37 +171,20 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
 
 def serving_probe(km, snap, q, wl, clients: int, req: int, seconds: float):
     """Closed-loop serving load through the coalescing dispatcher (keto_dispatcher_*): `clients`
-    threads each send `req`-query requests back to back.  Reported beside the batch numbers;
-    the per-request latency includes the queueing a request sees behind the batch in flight."""
-    import threading
+    native threads (synth.closed_loop, C++) each send `req`-query requests back to back, the way
+    the Go shim's goroutines call it through cgo.  Reported beside the batch numbers; the
+    per-request latency includes the queueing a request sees behind the batch in flight."""
+    from keto_mi355x import synth
 
     d = km.Dispatcher(snap, wl.max_depth, wl.max_width, max_batch=1 << 16)
-    lat = [[] for _ in range(clients)]
-    stop = time.perf_counter() + seconds
-
-    def client(t):
-        i = (t * 7919 * req) % max(1, len(q) - req)
-        while time.perf_counter() < stop:
-            t0 = time.perf_counter()
-            d.check(q[i:i + req])
-            lat[t].append(time.perf_counter() - t0)
-            i = (i + clients * req) % max(1, len(q) - req)
-
-    th = [threading.Thread(target=client, args=(t,)) for t in range(clients)]
-    t0 = time.perf_counter()
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
-    dt = time.perf_counter() - t0
+    r = synth.closed_loop(d, q, clients, req, seconds)
     st = d.stats()
     d.close()
-    allv = np.concatenate([np.array(x) for x in lat if x]) * 1e3
-    return {"clients": clients, "request_checks": req, "seconds": dt,
-            "checks_per_s": st["queries"] / dt, "requests_per_s": st["requests"] / dt,
+    return {"clients": clients, "request_checks": req, "seconds": r["seconds"],
+            "checks_per_s": r["checks"] / r["seconds"], "requests_per_s": r["requests"] / r["seconds"],
             "mean_batch": st["queries"] / max(1, st["batches"]),
-            "p50_request_ms": float(np.percentile(allv, 50)), "p99_request_ms": float(np.percentile(allv, 99)),
-            "host_client": "Python threads over ctypes (GIL released in the call)"}
+            "p50_request_ms": r["p50_ms"], "p99_request_ms": r["p99_ms"], "max_request_ms": r["max_ms"],
+            "host_client": "native closed loop: C++ threads calling keto_dispatcher_check"}
 
 
 def run_c5(args, rank, world, device, dist_on):

@@ -11,6 +11,7 @@
 // Every value is a pure function of (seed, stream, index) through splitmix64, so the arrays
 // fill in parallel and every rank of a multi-GPU run regenerates the identical replica.
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <thread>
 #include <vector>
@@ -234,6 +235,66 @@ int ks_drive_queries(const ks_drive_params *pp, uint64_t qseed, keto_query *out,
             out[i] = q;
         }
     });
+    return 0;
+}
+
+// Closed-loop serving load (bench infrastructure): `clients` native threads each send `req`-query
+// requests back to back through `check` (keto_dispatcher_check, passed in by the caller) for
+// `seconds`, the way goroutines of the Go shim would call it through cgo.  Per-request latency
+// percentiles over all threads.
+typedef int (*ks_check_fn)(void *dispatcher, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
+                           int32_t *out_err);
+typedef struct ks_load_result {
+    uint64_t requests, checks;
+    double seconds, p50_ms, p99_ms, max_ms;
+    int32_t rc;  // first non-zero return code of any request, else 0
+} ks_load_result;
+
+int ks_closed_loop(ks_check_fn check, void *dispatcher, const keto_query *queries, uint64_t nq, uint32_t clients,
+                   uint32_t req, double seconds, ks_load_result *out) {
+    if (!check || !dispatcher || !queries || !out || clients == 0 || req == 0 || nq < req) return -1;
+    using clk = std::chrono::steady_clock;
+    const auto stop = clk::now() + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(seconds));
+    std::vector<std::vector<float>> lat(clients);
+    std::vector<int32_t> rcs(clients, 0);
+    const uint64_t span = nq - req + 1;
+    const auto t0 = clk::now();
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < clients; t++)
+        th.emplace_back([&, t] {
+            std::vector<uint8_t> allowed(req);
+            std::vector<int32_t> err(req);
+            uint64_t i = ((uint64_t)t * 7919u * req) % span;
+            while (clk::now() < stop) {
+                const auto a = clk::now();
+                const int rc = check(dispatcher, queries + i, req, allowed.data(), err.data());
+                const auto b = clk::now();
+                if (rc != 0) {
+                    rcs[t] = rc;
+                    return;
+                }
+                lat[t].push_back(std::chrono::duration<float, std::milli>(b - a).count());
+                i = (i + (uint64_t)clients * req) % span;
+            }
+        });
+    for (auto &x : th) x.join();
+    const double dt = std::chrono::duration<double>(clk::now() - t0).count();
+    std::vector<float> all;
+    for (auto &v : lat) all.insert(all.end(), v.begin(), v.end());
+    out->rc = 0;
+    for (int32_t r : rcs)
+        if (r != 0 && out->rc == 0) out->rc = r;
+    out->requests = all.size();
+    out->checks = all.size() * (uint64_t)req;
+    out->seconds = dt;
+    out->p50_ms = out->p99_ms = out->max_ms = 0;
+    if (!all.empty()) {
+        std::sort(all.begin(), all.end());
+        auto pct = [&](double p) { return (double)all[std::min<size_t>(all.size() - 1, (size_t)(p * all.size()))]; };
+        out->p50_ms = pct(0.50);
+        out->p99_ms = pct(0.99);
+        out->max_ms = all.back();
+    }
     return 0;
 }
 

@@ -69,3 +69,17 @@ def test_snapshot_swap_between_batches():
     a2, _ = d.check(q)
     assert a2.sum() == 0
     d.close()
+
+
+def test_native_closed_loop_load():
+    """bench.py's serving probe: native client threads through keto_dispatcher_check."""
+    wl = synth.drive(depth=4, n_groups=500, n_users=2000, seed=6)
+    q = synth.drive_queries(wl, 4096, seed=2)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    d = km.Dispatcher(snap, wl.max_depth, wl.max_width, max_batch=1024)
+    r = synth.closed_loop(d, q, clients=16, req=32, seconds=0.5)
+    st = d.stats()
+    d.close()
+    assert r["requests"] > 0 and r["checks"] == 32 * r["requests"]
+    assert st["queries"] >= r["checks"]  # every request went through the dispatcher's batches
+    assert 0 < r["p50_ms"] <= r["p99_ms"] <= r["max_ms"]
