@@ -85,6 +85,12 @@ struct CheckParams {
 #ifndef KETO_GUARD
 #define KETO_GUARD 24
 #endif
+// Tier-0 resident blocks per CU (5 x 256 lanes = 5 waves per SIMD), below the 6 the register
+// budget allows: fewer lanes, each running more queries, waste fewer lane-steps in the batch's
+// tail.  C4 tier-0 kernel at 3 / 4 / 5 / 6 blocks per CU: 25.1 / 22.6 / 21.6 / 22.0 ms.
+#ifndef KETO_T0_BLOCKS_PER_CU
+#define KETO_T0_BLOCKS_PER_CU 5
+#endif
 
 __device__ __forceinline__ uint32_t w8(const uint4 &v0, const uint4 &v1, uint32_t j) {
     return j < 4 ? wword(v0, j) : wword(v1, j - 4);
@@ -942,6 +948,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&check_kernel<false, true>),
                                                              BLOCK, lds) != hipSuccess || per_cu <= 0)
                 per_cu = 4;
+            per_cu = std::min(per_cu, KETO_T0_BLOCKS_PER_CU);
             lanes = std::min<uint32_t>(lanes, (uint32_t)per_cu * cus * BLOCK);
             lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + BLOCK - 1) / BLOCK) * BLOCK);
         }
