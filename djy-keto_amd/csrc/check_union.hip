@@ -22,6 +22,12 @@ namespace {
 #ifndef KETO_GUARD
 #define KETO_GUARD 8
 #endif
+// Tier-0 resident blocks per CU (4 x 256 lanes = 4 waves per SIMD), below the 6 the register
+// budget allows, as in check.hip.  C2 tier-0 kernel at 4 / 5 / 6 blocks per CU: 7.72 / 7.78 /
+// 7.94 ms.
+#ifndef KETO_T0_BLOCKS_PER_CU
+#define KETO_T0_BLOCKS_PER_CU 4
+#endif
 
 enum UState : uint32_t {
     U_IDLE = 0,
@@ -544,6 +550,7 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&check_union_kernel<false, true>),
                                                              BLOCK, lds) != hipSuccess || per_cu <= 0)
                 per_cu = 4;
+            per_cu = std::min(per_cu, KETO_T0_BLOCKS_PER_CU);
             lanes = std::min<uint32_t>(lanes, (uint32_t)per_cu * cus * BLOCK);
             lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + BLOCK - 1) / BLOCK) * BLOCK);
         }
