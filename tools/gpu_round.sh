@@ -1,6 +1,8 @@
 #!/bin/bash
 # One GPU-box pass: parity tests, the default bench line, its kernel-trace summary and the
 # HBM traffic passes.  Every GPU step has its own time limit; the first failure ends the run.
+# The kernel trace runs the bench without the latency and serving probes, so that every check
+# launch it averages is a 2^20-query batch, the launch the bench line times.
 #   usage: tools/gpu_round.sh r01 c4 [skip-tests]
 set -eu
 cd "$(dirname "$0")/.."
@@ -16,6 +18,6 @@ fi
 timeout -k 10 400 python3 -u bench.py --workload $WL > gpurun_out/bench_$WL.log 2>&1
 tail -1 gpurun_out/bench_$WL.log
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_$WL -o kt --output-format csv \
-  -- python3 bench.py --workload $WL --no-cpu-baseline > gpurun_out/kt_$WL.log 2>&1
+  -- python3 bench.py --workload $WL --no-cpu-baseline --serve-clients 0 --latency-iters 0 > gpurun_out/kt_$WL.log 2>&1
 tail -1 gpurun_out/kt_$WL.log
 tools/pmc_traffic.sh $ROUND $WL
