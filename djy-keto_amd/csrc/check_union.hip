@@ -25,6 +25,9 @@ namespace {
 // Tier-0 resident blocks per CU (4 x 256 lanes = 4 waves per SIMD), below the 6 the register
 // budget allows, as in check.hip.  C2 tier-0 kernel at 4 / 5 / 6 blocks per CU: 7.72 / 7.78 /
 // 7.94 ms.
+#ifndef KETO_SPREAD_MAX
+#define KETO_SPREAD_MAX 64
+#endif
 #ifndef KETO_T0_BLOCKS_PER_CU
 #define KETO_T0_BLOCKS_PER_CU 4
 #endif
@@ -64,6 +67,7 @@ struct UParams {
     int32_t max_depth, max_width;
     unsigned long long *counters;
     uint32_t last_tier;
+    uint32_t live_lanes;  // lanes [live_lanes, 64) of every wave take no queries
 };
 
 // word j (0..7) of the two consecutive windows v0, v1 -- selects, no scratch
@@ -93,7 +97,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
     const uint32_t lane = __lane_id();
 
     uint32_t q = 0, pos = 0, st = U_IDLE;
-    bool exhausted = false;
+    bool exhausted = lane >= P.live_lanes;
     uint32_t sidx = NONE32;  // subject
     bool heavy = false;
     uint32_t R0 = NONE32, R1 = NONE32, R2 = NONE32, R3 = NONE32;
@@ -552,7 +556,14 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
                 per_cu = 4;
             per_cu = std::min(per_cu, KETO_T0_BLOCKS_PER_CU);
             lanes = std::min<uint32_t>(lanes, (uint32_t)per_cu * cus * BLOCK);
-            lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + BLOCK - 1) / BLOCK) * BLOCK);
+            // a batch smaller than the resident grid is spread over more waves with fewer live
+            // lanes each (check.hip: fewer distinct interpreter states per wave-step)
+            uint32_t spread = 1;
+            while (spread < KETO_SPREAD_MAX && L.n * spread * 2 <= lanes) spread *= 2;
+            P.live_lanes = 64 / spread;
+            lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n * spread + BLOCK - 1) / BLOCK) * BLOCK);
+        } else {
+            P.live_lanes = 64;
         }
         const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);
         dim3 grid(lanes / bs), block(bs);

@@ -2,6 +2,7 @@
 # A/B (tool): tier-0 kernel time and per-tier work of the current build and every tools/ab lib
 # on the prof_check Drive workload.   usage: tools/ab_run.sh [drive|c2]
 cd "$(dirname "$0")/.."
+shopt -s nullglob
 mkdir -p gpurun_out
 for lib in cur tools/ab/libketo_*.so; do
   if [ $lib = cur ]; then unset KETO_MI355X_LIB_OVERRIDE; else export KETO_MI355X_ALLOW_OVERRIDE=tools KETO_MI355X_LIB_OVERRIDE=$PWD/$lib; fi
