@@ -61,6 +61,7 @@ struct ExpandParams {
     uint4 *stack;
     uint32_t *epochs;
     uint32_t vcap, scap, emit, last_tier;
+    uint32_t live_lanes;  // lanes [live_lanes, 64) of every wave exit at once
     unsigned long long *counters;
 };
 
@@ -83,6 +84,15 @@ __device__ __forceinline__ bool vis_insert(unsigned long long *vis, uint32_t vma
     return false;
 }
 
+// Largest spread of a small batch over more waves (live lanes per wave = 64 / spread)
+#ifndef KETO_XSPREAD_MAX
+#define KETO_XSPREAD_MAX 64
+#endif
+// tier-0 lanes with scratch per CU (36 KB each)
+#ifndef KETO_XLANES_PER_CU
+#define KETO_XLANES_PER_CU 128
+#endif
+
 __global__ __launch_bounds__(256) void expand_kernel(ExpandParams P) {
     const DevSnapshot &s = P.s;
     const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
@@ -91,6 +101,7 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams P) {
     uint32_t epoch = P.epochs[gl];
     const uint32_t nq = P.qlist ? *P.qlist_count : P.n;
     const uint32_t vmask = P.vcap - 1;
+    if (__lane_id() >= P.live_lanes) return;  // no wave-level operations below
     unsigned long long c_rows = 0, c_edges = 0, c_out = 0;
     while (true) {
         uint32_t my = atomicAdd(P.next, 1u);
@@ -194,7 +205,7 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
     if (L.n == 0) return;
     if (L.n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
     const uint32_t cus = (uint32_t)num_cus(s.device);
-    const Tier t[3] = {Tier{cus * 64, 1u << 12, 256}, Tier{256, 1u << 18, 1u << 13}, Tier{8, 1u << 24, 1u << 18}};
+    const Tier t[3] = {Tier{cus * KETO_XLANES_PER_CU, 1u << 12, 256}, Tier{256, 1u << 18, 1u << 13}, Tier{8, 1u << 24, 1u << 18}};
     ensure_scratch(st.expand_scratch, t);
     ensure_lists(st, L.n);
     Scratch &sc = st.expand_scratch;
@@ -226,7 +237,15 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
         uint32_t lanes = t[tier].lanes;
         // tier 0: one-wave blocks, so a batch of a few thousand roots spreads over many CUs
         // instead of filling a handful of them (each lane walks a whole tree)
-        if (tier == 0) lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n + 63) / 64) * 64);
+        // and a batch smaller than the scratch's lanes runs with fewer live lanes per wave: each
+        // lane's DFS then shares its wave's issue with fewer divergent walks
+        P.live_lanes = 64;
+        if (tier == 0) {
+            uint32_t spread = 1;
+            while (spread < KETO_XSPREAD_MAX && L.n * spread * 2 <= lanes) spread *= 2;
+            P.live_lanes = 64 / spread;
+            lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n * spread + 63) / 64) * 64);
+        }
         const uint32_t bs = std::min<uint32_t>(tier == 0 ? 64 : BLOCK, lanes);  // every launched lane owns scratch
         hipLaunchKernelGGL(expand_kernel, dim3(lanes / bs), dim3(bs), 0, st.stream, P);
         KETO_HIP(hipGetLastError());
