@@ -89,12 +89,6 @@ struct CheckParams {
 // Tier-0 resident blocks per CU (5 x 256 lanes = 5 waves per SIMD), below the 6 the register
 // budget allows: fewer lanes, each running more queries, waste fewer lane-steps in the batch's
 // tail.  C4 tier-0 kernel at 3 / 4 / 5 / 6 blocks per CU: 25.1 / 22.6 / 21.6 / 22.0 ms.
-// Largest spread of a small batch (live lanes per wave = 64 / spread).  C4, 64Ki batches: p99
-// 9.0 -> 6.7 ms; native serving probe (dispatcher batches of ~1.5k): 0.39 -> 1.69 M checks/s,
-// request p99 42 -> 9 ms at spread 64.
-#ifndef KETO_SPREAD_MAX
-#define KETO_SPREAD_MAX 64
-#endif
 #ifndef KETO_T0_BLOCKS_PER_CU
 #define KETO_T0_BLOCKS_PER_CU 5
 #endif
@@ -960,10 +954,10 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             // A batch smaller than the resident grid is spread over more waves with fewer live
             // lanes each: a wave-step then runs fewer distinct interpreter states, which is what
             // sets the step time (and so a small batch's latency).
-            uint32_t spread = 1;
-            while (spread < KETO_SPREAD_MAX && L.n * spread * 2 <= lanes) spread *= 2;
-            P.live_lanes = 64 / spread;
-            lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n * spread + BLOCK - 1) / BLOCK) * BLOCK);
+            const uint64_t waves = lanes / 64;
+            P.live_lanes = (uint32_t)std::min<uint64_t>(64, (L.n + waves - 1) / waves);
+            const uint64_t need = (L.n + P.live_lanes - 1) / P.live_lanes * 64;
+            lanes = (uint32_t)std::min<uint64_t>(lanes, (need + BLOCK - 1) / BLOCK * BLOCK);
         } else {
             P.live_lanes = 64;
         }

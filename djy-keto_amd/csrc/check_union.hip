@@ -25,9 +25,6 @@ namespace {
 // Tier-0 resident blocks per CU (4 x 256 lanes = 4 waves per SIMD), below the 6 the register
 // budget allows, as in check.hip.  C2 tier-0 kernel at 4 / 5 / 6 blocks per CU: 7.72 / 7.78 /
 // 7.94 ms.
-#ifndef KETO_SPREAD_MAX
-#define KETO_SPREAD_MAX 64
-#endif
 #ifndef KETO_T0_BLOCKS_PER_CU
 #define KETO_T0_BLOCKS_PER_CU 4
 #endif
@@ -558,10 +555,10 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             lanes = std::min<uint32_t>(lanes, (uint32_t)per_cu * cus * BLOCK);
             // a batch smaller than the resident grid is spread over more waves with fewer live
             // lanes each (check.hip: fewer distinct interpreter states per wave-step)
-            uint32_t spread = 1;
-            while (spread < KETO_SPREAD_MAX && L.n * spread * 2 <= lanes) spread *= 2;
-            P.live_lanes = 64 / spread;
-            lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n * spread + BLOCK - 1) / BLOCK) * BLOCK);
+            const uint64_t waves = lanes / 64;
+            P.live_lanes = (uint32_t)std::min<uint64_t>(64, (L.n + waves - 1) / waves);
+            const uint64_t need = (L.n + P.live_lanes - 1) / P.live_lanes * 64;
+            lanes = (uint32_t)std::min<uint64_t>(lanes, (need + BLOCK - 1) / BLOCK * BLOCK);
         } else {
             P.live_lanes = 64;
         }

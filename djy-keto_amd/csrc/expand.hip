@@ -84,10 +84,6 @@ __device__ __forceinline__ bool vis_insert(unsigned long long *vis, uint32_t vma
     return false;
 }
 
-// Largest spread of a small batch over more waves (live lanes per wave = 64 / spread)
-#ifndef KETO_XSPREAD_MAX
-#define KETO_XSPREAD_MAX 64
-#endif
 // tier-0 lanes with scratch per CU (36 KB each)
 #ifndef KETO_XLANES_PER_CU
 #define KETO_XLANES_PER_CU 128
@@ -241,10 +237,9 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
         // lane's DFS then shares its wave's issue with fewer divergent walks
         P.live_lanes = 64;
         if (tier == 0) {
-            uint32_t spread = 1;
-            while (spread < KETO_XSPREAD_MAX && L.n * spread * 2 <= lanes) spread *= 2;
-            P.live_lanes = 64 / spread;
-            lanes = (uint32_t)std::min<uint64_t>(lanes, ((L.n * spread + 63) / 64) * 64);
+            const uint64_t waves = lanes / 64;
+            P.live_lanes = (uint32_t)std::min<uint64_t>(64, (L.n + waves - 1) / waves);
+            lanes = (uint32_t)std::min<uint64_t>(lanes, (L.n + P.live_lanes - 1) / P.live_lanes * 64);
         }
         const uint32_t bs = std::min<uint32_t>(tier == 0 ? 64 : BLOCK, lanes);  // every launched lane owns scratch
         hipLaunchKernelGGL(expand_kernel, dim3(lanes / bs), dim3(bs), 0, st.stream, P);
