@@ -210,6 +210,29 @@ def test_fresh_stream_device_path_first_call():
     s.close()
 
 
+def test_small_batch_spreading_is_exact(stream):
+    """Batches smaller than the resident grid run with fewer live lanes per wave (down to one):
+    every batch size gives the same decisions, equal to the oracle's."""
+    from keto_mi355x import synth
+    wl = synth.drive(depth=6, n_groups=5000, n_users=20000, seed=11)
+    q = synth.drive_queries(wl, 1 << 16, seed=4)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    whole, werr = eng.check_batch(q)
+    cuts = [0, 1, 18, 1018, 21018, len(q)]
+    parts = [eng.check_batch(q[i:j]) for i, j in zip(cuts[:-1], cuts[1:])]
+    np.testing.assert_array_equal(np.concatenate([a for a, _ in parts]), whole)
+    np.testing.assert_array_equal(np.concatenate([e for _, e in parts]), werr)
+    big, _ = eng.check_batch(np.concatenate([q] * 8))  # full grid, 64 live lanes
+    np.testing.assert_array_equal(big, np.tile(whole, 8))
+    w, _ = world_from_workload(wl)
+    orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+    dec, err, _ = orc.check_batch(q.view(refsem.QUERY_DT), threads=8)
+    np.testing.assert_array_equal(whole, dec)
+    np.testing.assert_array_equal(werr, err)
+    assert 0.05 < whole.mean() < 0.95
+
+
 def test_device_tuple_build_matches_host_build(stream):
     """keto_snapshot_build_device (tuples already in HBM, e.g. received over RCCL) builds the
     same snapshot as the host-pointer build: identical decisions and work counters."""
