@@ -396,6 +396,17 @@ int keto_dispatcher_check(keto_dispatcher *d, const keto_query *queries, uint64_
     return g != KETO_OK ? g : rc;
 }
 
+int keto_dispatcher_expand(keto_dispatcher *d, const keto_subject_set *roots, uint64_t n, keto_tree_node *out_nodes,
+                           uint64_t out_cap, uint64_t *out_offsets, int32_t *out_err) {
+    int rc = KETO_OK;
+    const int g = guarded([&] {
+        std::string msg;
+        rc = keto::dispatcher_expand(d, roots, n, out_nodes, out_cap, out_offsets, out_err, msg);
+        if (rc != KETO_OK) g_err = msg;
+    });
+    return g != KETO_OK ? g : rc;
+}
+
 int keto_dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap) {
     return guarded([&] { keto::dispatcher_set_snapshot(d, snap); });
 }

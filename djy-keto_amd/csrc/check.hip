@@ -41,6 +41,11 @@ __device__ __forceinline__ uint32_t f_type(uint32_t w) { return (w >> 16) & 0xFu
 __device__ __forceinline__ uint32_t f_phase(uint32_t w) { return (w >> 20) & 0xFu; }
 __device__ __forceinline__ uint32_t set_phase(uint32_t w, uint32_t p) { return (w & ~(0xFu << 20)) | (p << 20); }
 
+// ES child loop (oracle/refsem.c SCHED_EAGER): checkgroup's Add returns as soon as child k is
+// handed to the group's consumer (concurrent_checkgroup.go:150-159), so engine.go:151-162 marks
+// the following siblings -- up to the next one that was not visited -- before child k runs, and
+// after a decisive child marks all the rest before its result is sent.  Phase-3 ES frames keep
+// {x cursor, y end, z pending sibling (marked, not run yet; NONE32 = none)}; phase 4 = draining.
 // lane states; "pseudo" states need no load and are run by the same step loop
 enum State : uint32_t {
     S_IDLE = 0,
@@ -60,6 +65,7 @@ enum State : uint32_t {
     S_TNEXT,    // pseudo: TTU loop, next parent
     S_TEDGE,    // edge window of the TTU loop
     S_SPROBE,   // probe-hash answers of the OR shortcut IN query (<= 2)
+    S_CDISP,    // pseudo: the advance found the next unvisited sibling `cc` (NONE32: none left)
 };
 
 struct CheckParams {
@@ -380,16 +386,15 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                     vcount = 0;
                     flags = FL_OWNER;
                 }
-                top = make_uint4(b, e, 0, fw(F_ES, d, 3, flags));  // x = cursor, y = end
+                top = make_uint4(b, e, NONE32, fw(F_ES, d, 3, flags));  // x = cursor, y = end, z = pending
                 st = S_CNEXT;
                 break;
             }
-            case S_CNEXT: {
+            case S_CNEXT: {  // advance: mark the next children until one was not visited (engine.go:151-160)
                 const uint32_t cur = top.x;
                 if (cur >= top.y) {
-                    if (w & FL_OWNER) scope = false;
-                    res = M_NOT;
-                    st = S_RET;
+                    cc = NONE32;
+                    st = S_CDISP;
                     break;
                 }
                 if (cur < ew_lo || cur >= ew_hi) {
@@ -448,26 +453,58 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                 }
                 vis[2 * aux + (e0 ? 0 : 1)] = tag;
                 vcount++;
-                // child checkIsAllowed(c, d, skipDirect=true) (engine.go:161)
-                const NodeInfo ni = t_node_info(T, cc);
-                st = S_CNEXT;
-                if (ri_status(ni.ri) == REL_ERROR) {  // engine.go:228-232
-                    if (w & FL_OWNER) scope = false;
+                st = S_CDISP;
+                break;
+            }
+            case S_CDISP: {
+                if (f_phase(w) == 4) {  // draining after a decisive child: mark, never run
+                    if (cc == NONE32) st = S_RET;  // `res` still holds the decisive result
+                    else st = S_CNEXT;
+                    break;
+                }
+                const uint32_t c = top.z;
+                top.z = cc;
+                if (c == NONE32) {  // nothing was pending: the loop's first child, or none left
+                    if (cc == NONE32) {
+                        if (w & FL_OWNER) scope = false;
+                        res = M_NOT;
+                        st = S_RET;
+                    } else {
+                        st = S_CNEXT;  // find its successor before it runs
+                    }
+                    break;
+                }
+                // run the pending child checkIsAllowed(c, d, skipDirect=true) (engine.go:161)
+                const NodeInfo ni = t_node_info(T, c);
+                if (ri_status(ni.ri) == REL_ERROR) {  // engine.go:228-232: decisive
                     res = mk_err(KETO_QERR_NO_RELATION);
-                    st = S_RET;
+                    if (w & FL_OWNER) {
+                        scope = false;
+                        st = S_RET;
+                    } else {
+                        top.w = set_phase(w, 4);
+                        st = cc == NONE32 ? S_RET : S_CNEXT;
+                    }
                     break;
                 }
                 const bool rw = ri_rw(ni.ri);
-                if (!rw && (!ri_ss(ni.ri) || d <= 1)) break;  // empty group / Unknown -> not a member
+                if (!rw && (!ri_ss(ni.ri) || d <= 1)) {  // empty group / Unknown -> not a member
+                    if (cc == NONE32) {
+                        if (w & FL_OWNER) scope = false;
+                        res = M_NOT;
+                        st = S_RET;
+                    } else {
+                        st = S_CNEXT;
+                    }
+                    break;
+                }
                 if (sp + 1 >= P.scap) {
                     fin = 2;
                     break;
                 }
-                // the caller's next edge rides in the frame's free z word: no window reload on return
-                top.z = (top.x < top.y && top.x >= ew_lo && top.x < ew_hi) ? wword(ew, top.x - ew_lo) : NONE32;
                 stk[sp++] = top;
                 // without a rewrite the child's group is just expandSubject(c, d-1)
-                top = rw ? make_uint4(cc, 0, 0, fw(F_IA, d, 0, FL_SKIP)) : make_uint4(cc, 0, 0, fw(F_ES, d - 1));
+                top = rw ? make_uint4(c, 0, 0, fw(F_IA, d, 0, FL_SKIP)) : make_uint4(c, 0, 0, fw(F_ES, d - 1));
                 have_res = false;
                 st = S_RUN;
                 break;
@@ -617,20 +654,29 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                         break;
                     }
                     have_res = false;  // phase 3: a child returned
+                    ew_lo = 1;         // the edge window did not survive the child
+                    ew_hi = 0;
                     if (decisive(res)) {
+                        if (w & FL_OWNER) {  // the scope dies with this frame: no marks needed
+                            scope = false;
+                            action = 2;
+                            break;
+                        }
+                        top.w = set_phase(w, 4);  // mark the remaining siblings, then return res
+                        if (top.z == NONE32) {
+                            action = 2;
+                            break;
+                        }
+                        st = S_CNEXT;
+                        break;
+                    }
+                    if (top.z == NONE32) {  // no sibling pending: the loop is done
                         if (w & FL_OWNER) scope = false;
+                        res = M_NOT;
                         action = 2;
                         break;
                     }
-                    if (top.z != NONE32) {  // the next edge saved at the call
-                        ew = make_uint4(top.z, NONE32, NONE32, NONE32);
-                        ew_lo = top.x;
-                        ew_hi = top.x + 1;
-                    } else {
-                        ew_lo = 1;
-                        ew_hi = 0;
-                    }
-                    st = S_CNEXT;
+                    st = S_CNEXT;  // find the pending sibling's successor, then run it
                     break;
                 case F_RW: {  // checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73)
                     const uint32_t node = top.x;
@@ -912,8 +958,10 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     // Queries that outgrow a tier's scratch go to the next (lanes, visited slots per lane,
     // frames per lane); HBM is plentiful (288 GB): tier 0 holds ~500 visited nodes per lane,
     // tier 1 ~4k, tier 2 ~500k.
-    const Tier t[3] = {Tier{cus * 32 * 64, 1024, 64},    // the common case (grid clipped to occupancy)
-                       Tier{cus * 256, 1u << 13, 1024},  // wide visited scopes
+    // Tier 0 is sized to the persistent grid it can ever launch (KETO_T0_BLOCKS_PER_CU resident
+    // blocks per CU): 1.3k lanes x 9 KiB per CU, ~3 GiB per stream on 256 CUs.
+    const Tier t[3] = {Tier{cus * KETO_T0_BLOCKS_PER_CU * 256, 1024, 64},  // the common case
+                       Tier{cus * 64, 1u << 13, 1024},                      // wide visited scopes
                        Tier{64, 1u << 20, 1u << 14}};   // huge scopes / deep recursion
     ensure_scratch(st.check_scratch, t);
     run_resolve(s, st, L.queries, L.n, L.max_depth);

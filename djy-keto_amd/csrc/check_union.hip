@@ -8,8 +8,14 @@
 // visited scope per query (opened by the root's expandSubject), and the only frames are
 // expand-subject frames.  That makes a compact lane-per-query state machine: few states,
 // small live state (<= 64 VGPRs target: 8 waves/SIMD), two independent 16-byte loads per
-// step issued by every lane in the same instructions, frames of 32 B that carry the parent's
-// edge window so returning from a child needs no edge reload.
+// step issued by every lane in the same instructions, frames of 32 B that carry the rest of
+// the parent's edge window so returning from a child needs no edge reload.
+//
+// Child order is the reference's (oracle/refsem.c SCHED_EAGER): checkgroup's Add returns as
+// soon as child k is handed to the group's consumer (concurrent_checkgroup.go:150-159), so the
+// loop of engine.go:151-162 marks the following siblings visited -- up to the next one that
+// was not -- before child k runs.  The lane keeps that next sibling `pend`ing (already marked)
+// while child k runs.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,6 +46,7 @@ enum UState : uint32_t {
     U_VKEY,    // visited alias key
     U_VIS,     // visited slot pair
     U_POP,     // parent frame (2 x 16 B)
+    U_DISP = 200,  // pseudo: the advance found the next unvisited sibling `nx` (or none)
 };
 
 // bit of the depth word: the current window is a row descriptor's two inline edges
@@ -104,6 +111,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
     uint32_t ew_lo = 1, ew_hi = 0;
     uint32_t sp = 0, vcount = 0, aux = 0, aux2 = 0;  // aux: probe bucket / visited pair
     uint32_t vk = 0;                                  // visited key of the child being inserted
+    uint32_t pend = NONE32, nx = NONE32;              // marked sibling waiting to run / just found
     bool root_ss = false;
     const uint4 *la0 = nullptr, *la1 = nullptr;
     uint32_t ln = 0;
@@ -289,6 +297,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 // lookahead done: width truncation, then the child loop (engine.go:141-162)
                 if (end - rbeg > W) end = rbeg + (W > 0 ? W - 1 : 0);
                 cur = rbeg;
+                pend = NONE32;
                 st = U_CEDGE + 100;
                 break;
             }
@@ -346,12 +355,14 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 }
                 if (end - rbeg > W) end = rbeg + (W > 0 ? W - 1 : 0);
                 cur = rbeg;
+                pend = NONE32;
                 st = U_CEDGE + 100;
                 break;
             }
-            case U_CEDGE + 100: {  // next child (engine.go:151-162)
+            case U_CEDGE + 100: {  // advance: mark the next children until one was not visited (engine.go:151-160)
                 if (cur >= end) {
-                    st = U_POP + 100;
+                    nx = NONE32;
+                    st = U_DISP;
                     break;
                 }
                 if (cur < ew_lo || cur >= ew_hi) {
@@ -410,25 +421,46 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 }
                 vis[2 * aux + (e0 ? 0 : 1)] = tag;
                 vcount++;
-                // child checkIsAllowed(c, d, skipDirect=true) -> expandSubject(c, d-1)
-                const NodeInfo ni = t_node_info(T, aux2);
+                nx = aux2;
+                st = U_DISP;
+                break;
+            }
+            case U_DISP: {  // run the pending child; the one just found becomes pending
+                if (pend == NONE32) {
+                    if (nx == NONE32) {
+                        st = U_POP + 100;  // no child left: NotMember
+                        break;
+                    }
+                    pend = nx;  // the loop's first child: find its successor before it runs
+                    st = U_CEDGE + 100;
+                    break;
+                }
+                const uint32_t c = pend;
+                pend = nx;
+                // child checkIsAllowed(c, d, skipDirect=true) -> expandSubject(c, d-1) (engine.go:161)
+                const NodeInfo ni = t_node_info(T, c);
                 if (ri_status(ni.ri) == REL_ERROR) {
                     fin = 3;
                     break;
                 }
-                if (!ri_ss(ni.ri) || d <= 1) {
-                    st = U_CEDGE + 100;
+                if (!ri_ss(ni.ri) || d <= 1) {  // empty group / Unknown: not a member
+                    st = pend == NONE32 ? U_POP + 100 : U_CEDGE + 100;
                     break;
                 }
                 if (sp + 1 >= P.scap) {
                     fin = 4;
                     break;
                 }
-                // push the parent (cursor, end, depth, row begin | window)
-                stk[2 * sp] = make_uint4(cur, end, d | (ew_lo == rbeg ? FR_INLINE : 0u), rbeg);
-                stk[2 * sp + 1] = ew;
+                // push the parent: cursor, end, depth, window end | the pending sibling and the
+                // window's edges from the cursor on (at most 3: the window held edge cur-1)
+                const bool inwin = cur >= ew_lo && cur < ew_hi;
+                const uint32_t k0 = inwin ? cur - ew_lo : 0;
+                stk[2 * sp] = make_uint4(cur, end, d, inwin ? ew_hi : cur);
+                stk[2 * sp + 1] = make_uint4(pend, inwin ? wword(ew, k0) : NONE32,
+                                             inwin && k0 + 1 < 4 ? wword(ew, k0 + 1) : NONE32,
+                                             inwin && k0 + 2 < 4 ? wword(ew, k0 + 2) : NONE32);
                 sp++;
-                node = aux2;
+                node = c;
                 d -= 1;
                 st = U_ROWOFF + 100;
                 break;
@@ -444,21 +476,15 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 ln = 2;
                 st = U_POP;
                 break;
-            case U_POP:
+            case U_POP:  // a child returned NotMember: run the pending sibling next
                 cur = v0.x;
                 end = v0.y;
                 d = v0.z & 0xFFFFu;
-                rbeg = v0.w;
-                ew = v1;
-                if (v0.z & FR_INLINE) {  // the row descriptor's inline edges
-                    ew_lo = rbeg;
-                    ew_hi = rbeg + 2;
-                } else {
-                    const uint32_t pc = cur > rbeg ? cur - 1 : cur;  // the window held edge cur-1
-                    ew_lo = pc - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + pc) >> 2) & 3);
-                    ew_hi = ew_lo + 4;
-                }
-                st = U_CEDGE + 100;
+                ew_lo = cur;
+                ew_hi = v0.w;
+                pend = v1.x;
+                ew = make_uint4(v1.y, v1.z, v1.w, NONE32);
+                st = pend == NONE32 ? U_POP + 100 : U_CEDGE + 100;
                 break;
             default:
                 fin = 4;
@@ -514,8 +540,8 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     constexpr uint32_t BLOCK = 256;
     const uint32_t cus = (uint32_t)num_cus(s.device);
     // HBM is plentiful (288 GB): tier 0 holds ~500 visited nodes per lane so restarts are rare
-    const Tier t[3] = {Tier{cus * 32 * 64, 1024, 32},   // 32 waves / CU (grid clipped to occupancy)
-                       Tier{cus * 256, 1u << 13, 512},
+    const Tier t[3] = {Tier{cus * KETO_T0_BLOCKS_PER_CU * 256, 1024, 32},  // the persistent grid's lanes
+                       Tier{cus * 64, 1u << 13, 512},
                        Tier{64, 1u << 20, 1u << 14}};
     ensure_scratch(st.union_scratch, t);
     run_resolve(s, st, L.queries, L.n, L.max_depth);

@@ -69,7 +69,8 @@ __device__ __forceinline__ NodeInfo t_node_info(const Tables &T, uint32_t node) 
     if (node & VIRT_BIT) {
         r.ns = (node >> 16) & 0x7FFFu;
         r.slot = NO_SLOT;
-        uint32_t st = r.ns < T.n_ns ? nr_status(T.nsrel[(size_t)r.ns * T.n_rel + (node & 0xFFFFu)]) : REL_NIL;
+        const uint32_t rel = node & 0xFFFFu;
+        uint32_t st = (r.ns < T.n_ns && rel < T.n_rel) ? nr_status(T.nsrel[(size_t)r.ns * T.n_rel + rel]) : REL_NIL;
         r.ri = make_ri(NO_OP, false, true, st, false);  // no rewrite: direct + expand of an empty row
         return r;
     }
@@ -81,8 +82,14 @@ __device__ __forceinline__ NodeInfo t_node_info(const Tables &T, uint32_t node) 
 }
 
 // node of (same entity as `node`, relation `rel`): computed usersets / tuple-to-userset hops
+// Relation ids past the snapshot's name table (a caller-side id the snapshot never saw) are
+// clamped to the reserved last name, which no namespace declares: ASTRelationFor's
+// "relation does not exist" for a configured namespace, nil otherwise (definitions.go:37-62).
+__device__ __forceinline__ uint32_t t_rel(const Tables &T, uint32_t rel) { return rel < T.n_rel ? rel : T.n_rel - 1; }
+
 __device__ __forceinline__ uint32_t t_sibling(const Tables &T, uint32_t node, const NodeInfo &ni, uint32_t rel) {
-    uint32_t w = rel < T.n_rel ? T.nsrel[(size_t)ni.ns * T.n_rel + rel] : (REL_NIL << 16) | NO_SLOT;
+    rel = t_rel(T, rel);
+    const uint32_t w = T.nsrel[(size_t)ni.ns * T.n_rel + rel];
     uint32_t slot = nr_slot(w);
     if (slot == NO_SLOT || (node & VIRT_BIT)) return VIRT_BIT | (ni.ns << 16) | (rel & 0xFFFFu);
     return node - ni.slot + slot;
@@ -90,7 +97,8 @@ __device__ __forceinline__ uint32_t t_sibling(const Tables &T, uint32_t node, co
 
 // node of (ns, entity e, rel) given e; virtual if ns has no slot for rel
 __device__ __forceinline__ uint32_t t_node(const Tables &T, uint32_t ns, uint32_t e, uint32_t rel) {
-    uint32_t w = rel < T.n_rel ? T.nsrel[(size_t)ns * T.n_rel + rel] : (REL_NIL << 16) | NO_SLOT;
+    rel = t_rel(T, rel);
+    const uint32_t w = T.nsrel[(size_t)ns * T.n_rel + rel];
     if (nr_slot(w) == NO_SLOT) return VIRT_BIT | (ns << 16) | (rel & 0xFFFFu);
     const NsDev nd = T.ns[ns];
     return nd.node_base + (e - nd.ent_base) * nd.n_slots + nr_slot(w);

@@ -15,14 +15,22 @@
 // long as its longest query; several batches in flight on their own streams keep the CUs
 // busy that a small batch's finished lanes leave idle.  The snapshot can be
 // swapped between batches (keto_dispatcher_set_snapshot), which is how a new snaptoken's
-// snapshot goes live without stopping the service.
+// snapshot goes live without stopping the service: a slot captures the current snapshot
+// (and counts itself as a user of it) when it takes a batch, a swap replaces the pointer at
+// once and then waits only for the old snapshot's users to drain -- it cannot be starved by
+// a stream of overlapping batches.
+//
+// Expand requests (expand.Engine.BuildTree behind ExpandService.Expand, expand/handler.go:
+// 115-152) coalesce the same way on their own queue: a slot takes either Check or Expand
+// requests, runs one keto_expand_batch over all their roots and hands every caller its own
+// trees (node ranges rebased to the caller's buffer).
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
 #include <memory>
 #include <mutex>
-#include <shared_mutex>
+#include <unordered_map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -33,10 +41,15 @@ namespace keto {
 namespace {
 
 struct Request {
-    const keto_query *q;
-    uint64_t n;
-    uint8_t *allowed;
-    int32_t *err;
+    const keto_query *q = nullptr;
+    uint64_t n = 0;
+    uint8_t *allowed = nullptr;
+    int32_t *err = nullptr;
+    // Expand requests: roots in, nodes + offsets[n+1] out
+    const keto_subject_set *roots = nullptr;
+    keto_tree_node *nodes = nullptr;
+    uint64_t cap = 0;
+    uint64_t *offsets = nullptr;
     int rc = KETO_OK;
     std::string msg;
     bool done = false;
@@ -55,8 +68,14 @@ struct Slot {
     void *dq = nullptr, *da = nullptr, *de = nullptr;
     std::thread th;
 
+    // Expand: host node buffer grown on demand
+    std::vector<keto_tree_node> xnodes;
+    std::vector<uint64_t> xoffs;
+    std::vector<int32_t> xerr;
+
     void run();
     int launch(keto_snapshot *snap, uint64_t n, std::string &msg);
+    void run_expand(keto_snapshot *snap, std::vector<Request *> &take);
 };
 
 struct Dispatcher {
@@ -64,11 +83,12 @@ struct Dispatcher {
     keto_limits limits{5, 100};
     uint32_t max_batch = 1u << 16, max_wait_us = 0;
     int device = 0;
-    std::mutex m;                // queue, stats
-    std::shared_mutex snap_mu;   // shared while a batch runs; a snapshot swap takes it exclusively
+    std::mutex m;                // queues, stats, snapshot pointer and its users
     std::condition_variable cv_in;
-    std::deque<Request *> queue;
+    std::condition_variable cv_idle;  // a snapshot's last in-flight batch finished
+    std::deque<Request *> queue, xqueue;
     uint64_t queued = 0;
+    std::unordered_map<keto_snapshot *, uint32_t> users;  // batches in flight per snapshot
     bool stop = false;
     std::vector<std::unique_ptr<Slot>> slots;
     keto_dispatcher_stats stats{};
@@ -98,28 +118,98 @@ int Slot::launch(keto_snapshot *snap, uint64_t n, std::string &msg) {
     return rc;
 }
 
+// Expand batch for every taken request: one keto_expand_batch over all roots, then each
+// caller's trees are copied to its buffer with offsets rebased to it
+void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
+    uint64_t n = 0;
+    for (auto *r : take) n += r->n;
+    int rc = KETO_OK;
+    std::string msg;
+    std::vector<keto_subject_set> roots;
+    roots.reserve(n);
+    for (auto *r : take) roots.insert(roots.end(), r->roots, r->roots + r->n);
+    xoffs.assign(n + 1, 0);
+    xerr.assign(n, 0);
+    if (xnodes.empty()) xnodes.resize(1u << 16);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        rc = keto_expand_batch(snap, stream, roots.data(), n, &d->limits, xnodes.data(), xnodes.size(), xoffs.data(),
+                               xerr.data());
+        if (rc != KETO_E_CAPACITY) break;
+        xnodes.resize(xoffs[n]);  // the count pass reported the exact size
+    }
+    if (rc != KETO_OK) {
+        char buf[512];
+        keto_last_error(buf, sizeof(buf));
+        msg = buf;
+    }
+    uint64_t o = 0;
+    std::lock_guard<std::mutex> lk(d->m);
+    for (auto *r : take) {
+        int rrc = rc;
+        std::string rmsg = msg;
+        if (rc == KETO_OK) {
+            const uint64_t base = xoffs[o], need = xoffs[o + r->n] - base;
+            for (uint64_t i = 0; i <= r->n; i++) r->offsets[i] = xoffs[o + i] - base;
+            std::memcpy(r->err, xerr.data() + o, r->n * sizeof(int32_t));
+            if (need > r->cap || (need && !r->nodes)) {
+                rrc = KETO_E_CAPACITY;
+                rmsg = "expand output needs " + std::to_string(need) + " nodes";
+            } else if (need) {
+                std::memcpy(r->nodes, xnodes.data() + base, need * sizeof(keto_tree_node));
+            }
+        }
+        o += r->n;
+        r->rc = rrc;
+        r->msg = rmsg;
+        r->done = true;
+        r->cv.notify_one();
+    }
+    d->stats.batches++;
+    d->stats.queries += n;
+    d->stats.requests += take.size();
+    if (n > d->stats.max_batch_seen) d->stats.max_batch_seen = n;
+}
+
 void Slot::run() {
     std::vector<Request *> take;
     for (;;) {
+        keto_snapshot *snap = nullptr;
+        bool expand = false;
         {
             std::unique_lock<std::mutex> lk(d->m);
-            d->cv_in.wait(lk, [&] { return d->stop || !d->queue.empty(); });
-            if (d->stop && d->queue.empty()) return;
-            if (d->max_wait_us) {
+            d->cv_in.wait(lk, [&] { return d->stop || !d->queue.empty() || !d->xqueue.empty(); });
+            if (d->stop && d->queue.empty() && d->xqueue.empty()) return;
+            if (d->max_wait_us && !d->queue.empty()) {
                 const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(d->max_wait_us);
                 d->cv_in.wait_until(lk, until, [&] { return d->stop || d->queued >= d->max_batch; });
-                if (d->queue.empty()) continue;  // another slot took them
             }
+            // Check first; Expand requests (rare, latency-tolerant) when no Check is waiting
+            std::deque<Request *> &qq = !d->queue.empty() ? d->queue : d->xqueue;
+            if (qq.empty()) continue;  // another slot took them
+            expand = &qq == &d->xqueue;
             take.clear();
             uint64_t n = 0;
-            while (!d->queue.empty() && (take.empty() || n + d->queue.front()->n <= d->max_batch)) {
-                n += d->queue.front()->n;
-                d->queued -= d->queue.front()->n;
-                take.push_back(d->queue.front());
-                d->queue.pop_front();
+            while (!qq.empty() && (take.empty() || n + qq.front()->n <= d->max_batch)) {
+                n += qq.front()->n;
+                if (!expand) d->queued -= qq.front()->n;
+                take.push_back(qq.front());
+                qq.pop_front();
             }
+            snap = d->snap;  // captured with the batch: a swap never waits on later batches
+            d->users[snap]++;
         }
-        std::shared_lock<std::shared_mutex> sl(d->snap_mu);
+        auto release = [&] {  // called with d->m held
+            if (--d->users[snap] == 0) {
+                d->users.erase(snap);
+                d->cv_idle.notify_all();
+            }
+        };
+        if (expand) {
+            run_expand(snap, take);
+            std::lock_guard<std::mutex> lk(d->m);
+            release();
+            continue;
+        }
         uint64_t n = 0;
         for (auto *r : take) n += r->n;
         int rc = KETO_OK;
@@ -131,19 +221,19 @@ void Slot::run() {
                 std::memcpy(hq + o, r->q, r->n * sizeof(keto_query));
                 o += r->n;
             }
-            rc = launch(d->snap, n, msg);
+            rc = launch(snap, n, msg);
         } else {  // a single request larger than the staging: the host-pointer path
             Request *r = take[0];
-            rc = keto_check_batch(d->snap, stream, r->q, r->n, &d->limits, r->allowed, r->err, 0);
+            rc = keto_check_batch(snap, stream, r->q, r->n, &d->limits, r->allowed, r->err, 0);
             if (rc != KETO_OK) {
                 char buf[512];
                 keto_last_error(buf, sizeof(buf));
                 msg = buf;
             }
         }
-        sl.unlock();
         uint64_t o = 0;
         std::lock_guard<std::mutex> lk(d->m);
+        release();
         for (auto *r : take) {
             if (rc == KETO_OK && staged) {
                 std::memcpy(r->allowed, ha + o, r->n);
@@ -218,6 +308,16 @@ void dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, k
             KETO_HIP(hipMalloc(&x->da, nb));
             KETO_HIP(hipMalloc(&x->de, nb * sizeof(int32_t)));
         }
+        // every slot's scratch is allocated now (one 1-query batch on its stream), not by its
+        // first live batch: the allocation synchronises the device, which would stall the
+        // other slots' batches in flight
+        for (auto &x : d->slots) {
+            keto_query q0{};
+            uint8_t a0 = 0;
+            int32_t e0 = 0;
+            if (keto_check_batch(snap, x->stream, &q0, 1, &d->limits, &a0, &e0, 0) != KETO_OK)
+                throw Error(KETO_E_DEVICE, "dispatcher slot warm-up failed");
+        }
         for (auto &x : d->slots) {
             Slot *p = x.get();
             p->th = std::thread([p] {
@@ -262,8 +362,36 @@ void dispatcher_set_snapshot(keto_dispatcher *hd, keto_snapshot *snap) {
     if (!d || !snap) throw Error(KETO_E_INVALID, "null argument");
     if (reinterpret_cast<Snapshot *>(snap)->device != d->device)
         throw Error(KETO_E_INVALID, "snapshot is on another device");
-    std::unique_lock<std::shared_mutex> bl(d->snap_mu);  // when this returns the old snapshot is idle
-    d->snap = snap;
+    std::unique_lock<std::mutex> lk(d->m);
+    keto_snapshot *old = d->snap;
+    d->snap = snap;  // batches taken from now on run on the new snapshot
+    if (old == snap) return;
+    // when this returns the old snapshot is idle: only batches taken before the swap use it
+    d->cv_idle.wait(lk, [&] { return d->users.find(old) == d->users.end(); });
+}
+
+int dispatcher_expand(keto_dispatcher *hd, const keto_subject_set *roots, uint64_t n, keto_tree_node *nodes,
+                      uint64_t cap, uint64_t *offsets, int32_t *err, std::string &msg) {
+    Dispatcher *d = DP(hd);
+    if (!d) throw Error(KETO_E_INVALID, "null dispatcher");
+    if (!offsets) throw Error(KETO_E_INVALID, "null buffer");
+    offsets[0] = 0;
+    if (n == 0) return KETO_OK;
+    if (!roots || !err) throw Error(KETO_E_INVALID, "null buffer");
+    Request r;
+    r.roots = roots;
+    r.n = n;
+    r.nodes = nodes;
+    r.cap = cap;
+    r.offsets = offsets;
+    r.err = err;
+    std::unique_lock<std::mutex> lk(d->m);
+    if (d->stop) throw Error(KETO_E_INVALID, "dispatcher is shutting down");
+    d->xqueue.push_back(&r);
+    d->cv_in.notify_one();
+    r.cv.wait(lk, [&] { return r.done; });
+    msg = r.msg;
+    return r.rc;
 }
 
 void dispatcher_stats(keto_dispatcher *hd, keto_dispatcher_stats *out) {

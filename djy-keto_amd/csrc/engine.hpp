@@ -180,6 +180,8 @@ void dispatcher_destroy(keto_dispatcher *d);
 int dispatcher_check(keto_dispatcher *d, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err,
                      std::string &msg);
 void dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap);
+int dispatcher_expand(keto_dispatcher *d, const keto_subject_set *roots, uint64_t n, keto_tree_node *nodes, uint64_t cap,
+                      uint64_t *offsets, int32_t *err, std::string &msg);
 void dispatcher_stats(keto_dispatcher *d, keto_dispatcher_stats *out);
 
 // store.hip: device tuple store with TransactRelationTuples deltas (keto_store_*)

@@ -176,6 +176,9 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
             decls[it->second] = std::move(ds);
         }
     }
+    // reserved last name: query relation ids outside the name table are clamped to it on the
+    // device (device_common.hpp t_rel), so they resolve like any undeclared relation
+    s.rel_names.push_back(std::string("\x01keto-unnamed-relation"));
     s.n_rel = (uint32_t)s.rel_names.size();
     if (s.n_rel >= 0xFFFF) throw Error(KETO_E_LIMIT, "more than 65534 relation names");
     int64_t empty_rel = -1;

@@ -98,6 +98,7 @@ SIGNATURES = {
     "keto_dispatcher_create": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherConfig), ctypes.POINTER(_VP)]),
     "keto_dispatcher_destroy": (ctypes.c_int, [_VP]),
     "keto_dispatcher_check": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP]),
+    "keto_dispatcher_expand": (ctypes.c_int, [_VP, _VP, _U64, _VP, _U64, _VP, _VP]),
     "keto_dispatcher_set_snapshot": (ctypes.c_int, [_VP, _VP]),
     "keto_dispatcher_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherStats)]),
     "keto_trees_to_json": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),

@@ -286,6 +286,24 @@ class Dispatcher:
         check(lib().keto_dispatcher_check(self.handle, q.ctypes.data, len(q), allowed.ctypes.data, err.ctypes.data))
         return allowed, err[: len(q)]
 
+    def expand(self, roots: np.ndarray, cap: int = 0):
+        """ExpandService.Expand coalescing (expand/handler.go:115-152): SUBJSET_DT roots ->
+        (nodes TREE_DT, offsets uint64[n+1], err int32[n]), like ExpandEngine.build_trees."""
+        r = np.ascontiguousarray(roots, dtype=_abi.SUBJSET_DT)
+        n = len(r)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        err = np.zeros(max(1, n), dtype=np.int32)
+        cap = cap or max(64, 16 * n)
+        while True:
+            nodes = np.empty(max(1, cap), dtype=_abi.TREE_DT)
+            rc = lib().keto_dispatcher_expand(self.handle, r.ctypes.data, n, nodes.ctypes.data, cap, offs.ctypes.data,
+                                              err.ctypes.data)
+            if rc == _abi.KETO_E_CAPACITY:
+                cap = int(offs[n]) + 1
+                continue
+            check(rc)
+            return nodes[: int(offs[n])], offs, err[:n]
+
     def set_snapshot(self, snapshot: Snapshot):
         check(lib().keto_dispatcher_set_snapshot(self.handle, snapshot.handle))
         self.snapshot = snapshot

@@ -113,8 +113,11 @@ class KetoStore:
     # ---- the shim's Mapper for requests (uuid_mapping.go:269-317, read-only) --------------
 
     def uuid_id(self, s: str) -> int:
-        """API string -> dense id of UUIDv5(nid, s); ids >= n_uuids are unknown to the snapshot"""
-        return self.uuids(str(_uuid.uuid5(self.nid, s)))
+        """API string -> dense id of UUIDv5(nid, s).  A UUID the snapshot does not hold is
+        looked up, never interned (a long-running service sees unboundedly many): it maps to
+        the one sentinel id n_uuids, which every kernel treats as absent."""
+        i = self.uuids.ids.get(str(_uuid.uuid5(self.nid, s)))
+        return self.n_uuids if i is None else i
 
     def rel_id(self, r: str) -> int:
         i = self.rel.ids.get(r)

@@ -211,8 +211,16 @@ int keto_dispatcher_destroy(keto_dispatcher *d);
 /* Thread-safe; blocks until the n queries are decided.  Same outputs as keto_check_batch. */
 int keto_dispatcher_check(keto_dispatcher *d, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
                           int32_t *out_err);
-/* Switch to another snapshot (same device) between batches; when this returns the previous
- * snapshot is no longer in use and may be freed. */
+/* Thread-safe Expand coalescing (expand.Engine.BuildTree behind ExpandService.Expand,
+ * expand/handler.go:115-152): blocks until the n roots are expanded.  Same outputs as
+ * keto_expand_batch for these roots (offsets relative to out_nodes; KETO_E_CAPACITY with
+ * out_offsets[n] = required nodes if out_cap is too small). */
+int keto_dispatcher_expand(keto_dispatcher *d, const keto_subject_set *roots, uint64_t n, keto_tree_node *out_nodes,
+                           uint64_t out_cap, uint64_t *out_offsets, int32_t *out_err);
+/* Switch to another snapshot (same device) between batches: batches taken after the call
+ * use the new one; when this returns the previous snapshot is no longer in use and may be
+ * freed (only batches taken before the swap are waited for, so sustained load cannot
+ * starve it). */
 int keto_dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap);
 int keto_dispatcher_stats_get(keto_dispatcher *d, keto_dispatcher_stats *out);
 

@@ -5,11 +5,20 @@
  *
  * Schedule: the reference evaluates sub-checks through checkgroup with one
  * reservation per group (internal/check/checkgroup/concurrent_checkgroup.go:
- * 66-138), i.e. sequentially in add order.  This restatement fixes the
- * "one-worker sequential order" (SURVEY.md section 8.0 H3): every sub-check
- * completes before the next one is constructed.  Where the reference is
- * schedule-dependent (visited-set pruning interacting with truncation) this
- * is the canonical legal order both the oracle and the GPU engine follow.
+ * 66-138): results are consumed in add order, but Add returns as soon as the
+ * sub-check's goroutine is handed to the consumer (:150-159).  So in
+ * checkExpandSubject's child loop (engine.go:151-162) the parent marks the NEXT
+ * sibling visited right after starting child k -- in practice long before child
+ * k's subtree does its first read -- and keeps marking siblings that were
+ * already visited until it reaches one that was not; it then blocks in Add until
+ * child k is done.  After a decisive (IsMember / error) child, Add no longer
+ * blocks and the loop marks every remaining sibling before the result is sent.
+ * The canonical order (SCHED_EAGER) is exactly that: mark siblings up to the
+ * next unvisited one before running child k; drain the rest after a decisive
+ * child.  Every other sub-check runs to completion in add order.
+ * SCHED_SEQUENTIAL (each child completes before the next is even marked, the
+ * round-1 order) is kept as the alternative legal schedule the schedule-
+ * sensitivity report (rs_check_ex) compares against.
  */
 #define _GNU_SOURCE
 #include "refsem.h"
@@ -368,15 +377,35 @@ static int cmp_key7(const void *pa, const void *pb) {
 
 typedef struct {
     uint64_t *slot;
+    int32_t *dep; /* rest depth at which each key was marked */
     size_t cap, cnt;
+    /* schedule-sensitivity evidence of this visited scope: siblings pruned as already
+     * visited (dskips: marked at another rest depth than the pruned occurrence), depth
+     * truncation inside the scope, and the order-sensitive events (width truncation, errors,
+     * AND / NOT evaluated) */
+    uint32_t skips, dskips, trunc, events;
 } vset;
+
+enum { SCHED_EAGER = 0, SCHED_SEQUENTIAL = 1 };
 
 typedef struct {
     const rs_db *db;
     uint32_t kind, sid, sns, srel; /* the query subject: never changes (traverser.go:102) */
     rs_stats *st;
     int depth_guard;
+    int sched;
+    uint32_t flags; /* RS_F_SENSITIVE */
 } qctx;
+
+/* an order-sensitive event inside the current visited scope (if any) */
+static void scope_event(vset *vs) {
+    if (vs) vs->events++;
+}
+/* depth truncation inside the current scope: order-sensitive only where pruned nodes can be
+ * reached at different rest depths */
+static void scope_trunc(vset *vs) {
+    if (vs) vs->trunc++;
+}
 
 typedef struct {
     int m;
@@ -393,13 +422,23 @@ static vset *vset_new(void) {
     vset *v = calloc(1, sizeof *v);
     v->cap = 64;
     v->slot = calloc(v->cap, sizeof *v->slot);
+    v->dep = calloc(v->cap, sizeof *v->dep);
     return v;
 }
 static void vset_free(vset *v) {
     if (v) {
         free(v->slot);
+        free(v->dep);
         free(v);
     }
+}
+/* end of a scope owned by the ES that opened it.  Another legal schedule only changes WHICH
+ * occurrence of a node reached twice is explored; that can change the scope's result only if
+ * pruning meets an order-sensitive event -- width truncation, an error, AND / NOT -- or if the
+ * occurrences carry different rest depths and some depth truncation happened in the scope. */
+static void scope_close(uint32_t *flags, vset *own) {
+    if (own && ((own->skips && own->events) || (own->dskips && own->trunc))) *flags |= RS_F_SENSITIVE;
+    vset_free(own);
 }
 static uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
@@ -409,35 +448,47 @@ static uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
     return x;
 }
-/* stringSet.addNoDuplicate (x/graph/graph_utils.go:27-36): returns 1 if present */
-static int vset_add(vset *v, uint64_t key) {
+/* stringSet.addNoDuplicate (x/graph/graph_utils.go:27-36): returns 1 if present (*prev = the
+ * rest depth it was marked at), else inserts the key with rest depth d */
+static int vset_add_d(vset *v, uint64_t key, int32_t d, int32_t *prev) {
     key += 1; /* 0 = empty slot */
     if (2 * (v->cnt + 1) > v->cap) {
         size_t nc = v->cap * 2;
         uint64_t *ns = calloc(nc, sizeof *ns);
+        int32_t *nd = calloc(nc, sizeof *nd);
         for (size_t i = 0; i < v->cap; i++) {
             uint64_t k = v->slot[i];
             if (!k) continue;
             size_t h = mix64(k) & (nc - 1);
             while (ns[h]) h = (h + 1) & (nc - 1);
             ns[h] = k;
+            nd[h] = v->dep[i];
         }
         free(v->slot);
+        free(v->dep);
         v->slot = ns;
+        v->dep = nd;
         v->cap = nc;
     }
     size_t h = mix64(key) & (v->cap - 1);
     while (v->slot[h]) {
-        if (v->slot[h] == key) return 1;
+        if (v->slot[h] == key) {
+            if (prev) *prev = v->dep[h];
+            return 1;
+        }
         h = (h + 1) & (v->cap - 1);
     }
     v->slot[h] = key;
+    v->dep[h] = d;
     v->cnt++;
     return 0;
 }
+static int vset_add(vset *v, uint64_t key) { return vset_add_d(v, key, 0, NULL); }
 
 /* SubjectSet.UniqueID = UUIDv5(obj, ns+"-"+rel) (relationtuple/definitions.go:114-116) */
 static uint64_t vkey(const rs_db *db, uint32_t ns, uint32_t obj, uint32_t rel) {
+    /* ids outside the tables name a (namespace, relation) no tuple holds: a class of its own */
+    if (ns >= db->n_ns || rel >= db->n_relnames) return ((uint64_t)obj << 32) | (0x80000000u | (ns << 16) | (rel & 0xFFFFu));
     uint32_t cls = db->vclass[(size_t)ns * db->n_relnames + rel];
     return ((uint64_t)obj << 32) | cls;
 }
@@ -474,14 +525,46 @@ static res check_rewrite(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset
 static res check_inverted(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs);
 
 /* checkDirect (internal/check/engine.go:167-208) */
-static res check_direct(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d) {
-    if (d <= 0) return R_UNK; /* :168-173 */
+static res check_direct(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, vset *vs) {
+    if (d <= 0) { /* :168-173 */
+        scope_trunc(vs);
+        return R_UNK;
+    }
     return exists(c, ns, obj, rel) ? R_IS : R_NOT;
+}
+
+/* checkExpandSubject's child list: the kept subject-set rows of [lo, hi) in shard order */
+typedef struct {
+    size_t i, hi, left; /* next row, row end, children not yet reached */
+} kids;
+
+/* CheckAndAddVisited over the next children until one was not visited (engine.go:157-160);
+ * 1 + its row index in *at, or 0 when the list is exhausted */
+static int advance(qctx *c, kids *k, vset *vs, int d, size_t *at) {
+    const rs_db *db = c->db;
+    while (k->left && k->i < k->hi) {
+        const key7 *t = ROW(db, k->i);
+        const size_t i = k->i++;
+        if (t->kind != 1) continue;
+        k->left--;
+        int32_t prev = d;
+        if (vset_add_d(vs, vkey(db, t->sns, t->sid, t->srel), d, &prev)) {
+            vs->skips++;
+            if (prev != d) vs->dskips++;
+            continue;
+        }
+        *at = i;
+        return 1;
+    }
+    return 0;
 }
 
 /* checkExpandSubject (engine.go:102-164) + TraverseSubjectSetExpansion (traverser.go:53-121) */
 static res check_expand_subject(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, vset *vs) {
-    if (d <= 0) return R_UNK; /* :103-108 */
+    if (d <= 0) { /* :103-108 */
+        scope_trunc(vs);
+        return R_UNK;
+    }
     const rs_db *db = c->db;
     vset *own = NULL;
     if (!vs) vs = own = vset_new(); /* graph.InitVisited (graph_utils.go:38-43) */
@@ -496,39 +579,71 @@ static res check_expand_subject(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel
         c->st->edges++;
         nres++;
         if (exists(c, t->sns, t->sid, t->srel)) { /* :109-111, engine.go:133-138 */
-            vset_free(own);
+            scope_close(&c->flags, own);
             return R_IS;
         }
     }
     /* width truncation: results[:maxWidth-1] (engine.go:141-150) */
     size_t keep = nres;
-    if ((long)nres > (long)db->max_width) keep = db->max_width > 0 ? (size_t)(db->max_width - 1) : 0;
-    size_t seen = 0;
-    for (size_t i = lo; i < hi && seen < keep; i++) {
-        const key7 *t = ROW(db, i);
-        if (t->kind != 1) continue;
-        seen++;
-        /* CheckAndAddVisited (engine.go:157-160) */
-        if (vset_add(vs, vkey(db, t->sns, t->sid, t->srel))) continue;
+    if ((long)nres > (long)db->max_width) {
+        keep = db->max_width > 0 ? (size_t)(db->max_width - 1) : 0;
+        scope_event(vs);
+    }
+    kids k = {lo, hi, keep};
+    res out = R_NOT;
+    size_t at;
+    if (c->sched == SCHED_SEQUENTIAL) {
+        while (advance(c, &k, vs, d, &at)) {
+            const key7 *t = ROW(db, at);
+            res r = check_is_allowed(c, t->sns, t->sid, t->srel, d, 1, vs); /* :161 */
+            if (decisive(r)) {
+                out = r;
+                break;
+            }
+        }
+        scope_close(&c->flags, own);
+        return out;
+    }
+    /* SCHED_EAGER: g.Add(check_k) returns once check_k is handed to the group's consumer
+     * (concurrent_checkgroup.go:150-159), so the loop marks the following siblings -- up to
+     * and including the next one that was not visited yet -- before check_k runs, then
+     * waits in the next Add for check_k's result. */
+    size_t next;
+    int have = advance(c, &k, vs, d, &next);
+    while (have) {
+        const key7 *t = ROW(db, next);
+        have = advance(c, &k, vs, d, &next);
         res r = check_is_allowed(c, t->sns, t->sid, t->srel, d, 1, vs); /* :161 */
         if (decisive(r)) {
-            vset_free(own);
-            return r;
+            /* the group is done, so every later Add returns at once: the loop still marks
+             * every remaining sibling before its deferred result is sent (:119, :151-162).
+             * Marks in a scope this ES owns die with it. */
+            if (!own)
+                while (advance(c, &k, vs, d, &at)) {
+                }
+            out = r;
+            break;
         }
     }
-    vset_free(own);
-    return R_NOT;
+    scope_close(&c->flags, own);
+    return out;
 }
 
 /* checkComputedSubjectSet (rewrites.go:208-230) */
 static res check_css(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, vset *vs) {
-    if (d < 0) return R_UNK; /* :214-217 */
+    if (d < 0) { /* :214-217 */
+        scope_trunc(vs);
+        return R_UNK;
+    }
     return check_is_allowed(c, ns, obj, rel, d, 0, vs);
 }
 
 /* checkTupleToSubjectSet (rewrites.go:242-293) + GetRelationTuples (relationtuples.go:207-247) */
 static res check_ttu(qctx *c, uint32_t ns, uint32_t obj, const rs_ast *a, int d, vset *vs) {
-    if (d < 0) return R_UNK; /* :247-250 */
+    if (d < 0) { /* :247-250 */
+        scope_trunc(vs);
+        return R_UNK;
+    }
     const rs_db *db = c->db;
     size_t lo, hi;
     node_rows(db, ns, obj, a->rel, &lo, &hi);
@@ -588,10 +703,15 @@ static res check_child(qctx *c, uint32_t ns, uint32_t obj, int ci, int d, int ne
 
 /* checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73) */
 static res check_rewrite(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs) {
-    if (d <= 0) return R_UNK; /* :39-42 */
+    if (d <= 0) { /* :39-42 */
+        scope_trunc(vs);
+        return R_UNK;
+    }
     const rs_db *db = c->db;
     const rs_ast *a = &db->ast[ai];
+    if (a->op == RS_OP_AND) scope_event(vs);
     if (a->op != RS_OP_OR && a->op != RS_OP_AND) {
+        scope_event(vs);
         res r = {RS_UNKNOWN, RS_ERR_NOT_IMPLEMENTED}; /* :58-59 */
         return r;
     }
@@ -640,6 +760,7 @@ done:
 
 /* checkInverted (rewrites.go:136-200) */
 static res check_inverted(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs) {
+    scope_event(vs);
     if (d < 0) return R_UNK; /* :142-145 */
     const rs_ast *a = &c->db->ast[ai];
     if (a->child_count != 1) {
@@ -662,7 +783,10 @@ static res check_inverted(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vse
 /* checkIsAllowed (engine.go:214-249) */
 static res check_is_allowed(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip_direct,
                             vset *vs) {
-    if (d <= 0) return R_UNK; /* :215-220 */
+    if (d <= 0) { /* :215-220 */
+        scope_trunc(vs);
+        return R_UNK;
+    }
     const rs_db *db = c->db;
     if (++c->depth_guard > MAX_RECURSION) {
         c->depth_guard--;
@@ -673,6 +797,7 @@ static res check_is_allowed(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, in
     int ri = ast_relation_for(db, ns, rel, &err); /* :228-232 */
     res out = R_NOT;
     if (err) {
+        scope_event(vs);
         out.m = RS_UNKNOWN;
         out.err = err;
         goto done;
@@ -687,7 +812,7 @@ static res check_is_allowed(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, in
         }
     }
     if ((!db->strict || !has_rewrite) && !skip_direct) { /* :239-243 */
-        res r = check_direct(c, ns, obj, rel, d - 1);
+        res r = check_direct(c, ns, obj, rel, d - 1, vs);
         if (decisive(r)) {
             out = r;
             goto done;
@@ -705,16 +830,34 @@ done:
     return out;
 }
 
-/* Engine.CheckRelationTuple (engine.go:76-95) */
-int rs_check(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st) {
+/* Engine.CheckRelationTuple (engine.go:76-95) under schedule `sched` */
+static int check_sched(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, int sched, uint32_t *flags) {
     rs_stats dummy = {0, 0, 0, 0};
     qctx c = {db, q->kind, q->sid, q->kind == 1 ? q->sns : 0, q->kind == 1 ? q->srel : 0,
-              st ? st : &dummy, 0};
+              st ? st : &dummy, 0, sched, 0};
     int d = q->depth;
     if (d <= 0 || db->max_depth < d) d = db->max_depth; /* :82-84 */
     res r = check_is_allowed(&c, q->ns, q->obj, q->rel, d, 0, NULL);
     if (err) *err = r.err;
+    if (flags) *flags = c.flags;
     return r.m;
+}
+
+int rs_check(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st) {
+    return check_sched(db, q, err, st, SCHED_EAGER, NULL);
+}
+
+int rs_check_ex(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, uint32_t *flags) {
+    uint32_t f0 = 0, f1 = 0;
+    int32_t e0 = 0, e1 = 0;
+    const int m0 = check_sched(db, q, &e0, st, SCHED_EAGER, &f0);
+    const int m1 = check_sched(db, q, &e1, NULL, SCHED_SEQUENTIAL, &f1);
+    const int a0 = e0 == 0 && m0 == RS_IS_MEMBER, a1 = e1 == 0 && m1 == RS_IS_MEMBER;
+    uint32_t f = (f0 | f1) & RS_F_SENSITIVE;
+    if (a0 != a1 || e0 != e1) f |= RS_F_SEQ_DIFFERS;
+    if (err) *err = e0;
+    if (flags) *flags = f;
+    return m0;
 }
 
 /* ------------------------------------------------------------------ */
@@ -726,6 +869,7 @@ typedef struct {
     size_t n;
     uint8_t *decision;
     int32_t *err;
+    uint32_t *flags; /* NULL: canonical schedule only */
     atomic_size_t next;
     pthread_mutex_t mu;
     rs_stats total;
@@ -740,7 +884,7 @@ static void *batch_worker(void *arg) {
         size_t e = i + 64 < j->n ? i + 64 : j->n;
         for (; i < e; i++) {
             int32_t er = 0;
-            int m = rs_check(j->db, &j->q[i], &er, &st);
+            int m = j->flags ? rs_check_ex(j->db, &j->q[i], &er, &st, &j->flags[i]) : rs_check(j->db, &j->q[i], &er, &st);
             j->decision[i] = (er == 0 && m == RS_IS_MEMBER); /* engine.go:65-71 */
             j->err[i] = er;
         }
@@ -755,6 +899,11 @@ static void *batch_worker(void *arg) {
 
 void rs_check_batch(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t *decision,
                     int32_t *err, rs_stats *st) {
+    rs_check_batch_ex(db, q, n, threads, decision, err, NULL, st);
+}
+
+void rs_check_batch_ex(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t *decision,
+                       int32_t *err, uint32_t *flags, rs_stats *st) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     batch_job j;
@@ -763,6 +912,7 @@ void rs_check_batch(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t
     j.n = n;
     j.decision = decision;
     j.err = err;
+    j.flags = flags;
     atomic_init(&j.next, 0);
     pthread_mutex_init(&j.mu, NULL);
     memset(&j.total, 0, sizeof j.total);

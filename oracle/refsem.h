@@ -116,6 +116,18 @@ int rs_check(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st);
 void rs_check_batch(rs_db *db, const rs_query *q, size_t n, int threads,
                     uint8_t *decision, int32_t *err, rs_stats *st);
 
+/* Schedule-sensitivity report.  The canonical (eager-marking) result,
+ * plus flags: RS_F_SENSITIVE when some visited scope both pruned a sibling as already
+ * visited and saw an order-sensitive event (depth or width truncation, an error, AND / NOT)
+ * under either simulated schedule (the conservative criterion); RS_F_SEQ_DIFFERS when the
+ * sequential schedule (every child done before the next sibling is marked) decides
+ * differently.  Runs each query twice. */
+#define RS_F_SENSITIVE 1u
+#define RS_F_SEQ_DIFFERS 2u
+int rs_check_ex(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, uint32_t *flags);
+void rs_check_batch_ex(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t *decision,
+                       int32_t *err, uint32_t *flags, rs_stats *st);
+
 /* Expand: returns number of nodes written (0 = nil tree), -1 if cap too small. */
 long rs_expand(rs_db *db, uint32_t kind, uint32_t sid, uint32_t sns, uint32_t srel,
                int32_t depth, rs_tree_node *out, size_t cap, rs_stats *st);

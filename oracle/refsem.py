@@ -33,6 +33,7 @@ TREE_DT = np.dtype([("type", "<u4"), ("kind", "<u4"), ("sid", "<u4"), ("sns", "<
                     ("n_children", "<u4")])
 
 REWRITE, CSS, TTU, INVERT = 0, 1, 2, 3
+F_SENSITIVE, F_SEQ_DIFFERS = 1, 2  # rs_check_ex flags
 IS_MEMBER, NOT_MEMBER, UNKNOWN = 1, 2, 0
 
 
@@ -67,6 +68,8 @@ def lib():
                                ctypes.POINTER(Stats)]
         L.rs_check_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Stats)]
+        L.rs_check_batch_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.rs_expand.restype = ctypes.c_long
         L.rs_expand.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
@@ -341,6 +344,19 @@ class Oracle:
         lib().rs_check_batch(self.db, q.ctypes.data, len(q), threads, dec.ctypes.data, err.ctypes.data,
                              ctypes.byref(st))
         return dec, err, st
+
+    def check_batch_ex(self, queries: np.ndarray, threads: int):
+        """canonical decisions plus the schedule-sensitivity flags (F_SENSITIVE, F_SEQ_DIFFERS):
+        each query also runs under the sequential schedule (refsem.h rs_check_ex)"""
+        q = np.ascontiguousarray(queries)
+        self._check_ids(q)
+        dec = np.zeros(len(q), dtype=np.uint8)
+        err = np.zeros(len(q), dtype=np.int32)
+        flags = np.zeros(len(q), dtype=np.uint32)
+        st = Stats()
+        lib().rs_check_batch_ex(self.db, q.ctypes.data, len(q), threads, dec.ctypes.data, err.ctypes.data,
+                                flags.ctypes.data, ctypes.byref(st))
+        return dec, err, flags, st
 
     def expand(self, kind, sid, sns, srel, depth, cap=1 << 16):
         out = np.zeros(cap, dtype=TREE_DT)

@@ -384,6 +384,57 @@ FIXTURES["cat_videos"] = {
     ],
 }
 
+# ---------------------------------------------------------------------------
+# Hand-derived cases for two reference behaviours no reference test pins (answers derived
+# from the reference source, cited per case; "derived": True marks them as such).
+
+# H3: the visited key is UUIDv5(obj, ns+"-"+rel) (relationtuple/definitions.go:114-116,
+# x/graph/graph_utils.go:45-53), so a-b:o#c and a:o#b-c are ONE visited node.  Fixture order
+# is shard order.  root#m's row is [a-b:o#c, a:o#b-c]; the found-lookahead (traverser.go:73-80)
+# finds alice directly in neither; the child loop (engine.go:151-162) visits a-b:o#c (nothing
+# below it) and then skips a:o#b-c as already visited, so alice -- reachable only through
+# a:o#b-c -> g:x#m -- is NOT found.  bob, in a-b:o#c's own subtree, is.  Expand (global visited
+# set incl. the root, expand/engine.go:69-72) shows the second set as a leaf.
+FIXTURES["visited_alias_h3"] = {
+    "src": "relationtuple/definitions.go:114-116 + x/graph/graph_utils.go:45-53 (hand-derived)",
+    "derived": True,
+    "namespaces": {"g": [], "a-b": [], "a": []},
+    "tuples": ["g:root#m@(a-b:o#c)", "g:root#m@(a:o#b-c)", "a-b:o#c@(g:y#m)", "g:y#m@bob",
+               "a:o#b-c@(g:x#m)", "g:x#m@alice", "g:other#m@(a:o#b-c)"],
+    "checks": [
+        {"query": "g:root#m@alice", "depth": 0, "allowed": False, "src": "alias prunes a:o#b-c"},
+        {"query": "g:root#m@bob", "depth": 0, "allowed": True, "src": "a-b:o#c -> g:y#m"},
+        {"query": "g:other#m@alice", "depth": 0, "allowed": True, "src": "no collision in this scope"},
+        {"query": "a:o#b-c@alice", "depth": 0, "allowed": True, "src": "root not inserted (engine.go:119)"},
+    ],
+    "expands": [
+        {"subject": "g:root#m", "depth": 5, "src": "expand/engine.go:69-72, 106-119", "exact": True,
+         "tree": union("g", "root", "m", union("a-b", "o", "c", union("g", "y", "m", leaf_id("bob"))),
+                       leaf_set("a", "o", "b-c"))},
+    ],
+}
+
+# Sibling marking order (engine.go:151-162 + concurrent_checkgroup.go:150-159): g.Add(check_A)
+# returns as soon as check_A is handed to the consumer, so the loop marks B before A's subtree
+# makes its first read.  root#view = [A#member, B#member], A#member includes B#member, alice is
+# in C#member below B.  Global depth 3: ES(root#view, 2) -> A at 2: A's ES (1) sees B already
+# visited and skips it; B at 2: ES(B, 1) finds alice in C#member by lookahead -> allowed.  (If
+# A's subtree ran before B was marked, A would reach B at depth 1, miss, and B would then be
+# skipped: denied.)  Depth 2: B's ES would run at 0 -> Unknown -> denied.  Depth 4: allowed.
+FIXTURES["sibling_marking_order"] = {
+    "src": "internal/check/engine.go:151-162, checkgroup/concurrent_checkgroup.go:150-159 (hand-derived)",
+    "derived": True,
+    "namespaces": {"g": []},
+    "tuples": ["g:root#view@(g:A#member)", "g:root#view@(g:B#member)", "g:A#member@(g:B#member)",
+               "g:B#member@(g:C#member)", "g:C#member@alice"],
+    "checks": [
+        {"query": "g:root#view@alice", "depth": 3, "allowed": True, "src": "B marked before A runs"},
+        {"query": "g:root#view@alice", "depth": 2, "allowed": False, "src": "depth ledger"},
+        {"query": "g:root#view@alice", "depth": 4, "allowed": True, "src": "both orders"},
+        {"query": "g:A#member@alice", "depth": 3, "allowed": True, "src": "A -> B -> C by lookahead"},
+    ],
+}
+
 
 def main():
     for name, fx in FIXTURES.items():

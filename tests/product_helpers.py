@@ -41,8 +41,10 @@ def product_tree_to_nested(world: refsem.World, nodes: np.ndarray):
     return refsem.tree_to_nested(world, conv)
 
 
-def world_from_workload(wl):
-    """oracle World over a synth Workload (same ids as the product snapshot)"""
+def world_from_workload(wl, with_tuples: bool = True):
+    """oracle World over a synth Workload (same ids as the product snapshot); with the
+    tuples converted to the oracle's record layout unless with_tuples=False (then t is None:
+    give the oracle wl.tuples.view(refsem.TUPLE_DT) with shard_bytes=True instead)"""
     w = refsem.World(namespaces=wl.namespaces, strict=wl.strict, max_depth=wl.max_depth, max_width=wl.max_width)
     w.ns_names = refsem.Interner()
     w.rel_names = refsem.Interner()
@@ -52,6 +54,8 @@ def world_from_workload(wl):
     for r in wl.rel_names:
         w.rel_names(r)
     w._walk_names()
+    if not with_tuples:
+        return w, None
     t = np.zeros(len(wl.tuples), dtype=refsem.TUPLE_DT)
     for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("kind", "subj_kind"), ("sid", "s_obj"),
                  ("sns", "s_ns"), ("srel", "s_rel")):

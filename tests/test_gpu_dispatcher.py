@@ -1,24 +1,42 @@
-"""Request coalescing (keto_dispatcher_*): many concurrent callers, batched launches, the
-same decisions as one keto_check_batch over the same queries, and a live snapshot swap."""
+"""Request coalescing (keto_dispatcher_*): many concurrent callers, batched launches, answers
+equal to the oracle's (oracle/refsem.c), a snapshot swap under sustained load, and Expand
+coalescing (expand/handler.go:115-152) against the oracle's trees."""
 import threading
+import time
 
 import numpy as np
 import pytest
 
 import keto_mi355x as km
+import refsem
 from keto_mi355x import synth
+from product_helpers import world_from_workload
 
 pytestmark = pytest.mark.gpu
 
 
-def test_concurrent_callers_get_batch_identical_answers():
+def _oracle(wl, tuples=None):
+    w, _ = world_from_workload(wl, with_tuples=False)
+    t = wl.tuples if tuples is None else tuples
+    orc = refsem.Oracle(w, np.ascontiguousarray(t).view(refsem.TUPLE_DT), shard_bytes=True)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    return orc
+
+
+def _oracle_answers(orc, q):
+    dec, err, _ = orc.check_batch(q.view(refsem.QUERY_DT), threads=8)
+    return dec, err
+
+
+def test_concurrent_callers_match_oracle():
     wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=4)
     q = synth.drive_queries(wl, 24_000, seed=3)
+    q["max_depth"][:500] = np.random.default_rng(1).integers(1, 5, 500)
     snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
-    want, werr = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    want, werr = _oracle_answers(_oracle(wl), q)
     d = km.Dispatcher(snap, wl.max_depth, wl.max_width, max_batch=4096)
-    got = np.zeros(len(q), np.uint8)
-    gerr = np.zeros(len(q), np.int32)
+    got = np.full(len(q), 7, np.uint8)
+    gerr = np.full(len(q), -1, np.int32)
     errors = []
 
     def client(t, T):
@@ -43,32 +61,114 @@ def test_concurrent_callers_get_batch_identical_answers():
     st = d.stats()
     assert st["batches"] < st["requests"]  # requests really were coalesced
     assert st["max_batch_seen"] <= 4096
+    covered = got != 7
+    assert covered.sum() > len(q) // 2
+    np.testing.assert_array_equal(got[covered], want[covered])
+    np.testing.assert_array_equal(gerr[covered], werr[covered])
     # a request larger than the staging runs alone through the host path
     a, e = d.check(q[:10_000])
     np.testing.assert_array_equal(a, want[:10_000])
-    # every caller's slice came back intact: compare the ranges the clients covered
-    covered = np.zeros(len(q), bool)
-    for t in range(T):
-        for i in range(t * 64, len(q), T * 64):
-            covered[i:i + 1] = True
-    np.testing.assert_array_equal(got[covered], want[covered])
-    np.testing.assert_array_equal(gerr[covered], werr[covered])
+    np.testing.assert_array_equal(e, werr[:10_000])
     d.close()
 
 
-def test_snapshot_swap_between_batches():
-    wl = synth.drive(depth=4, n_groups=500, n_users=2000, seed=9)
-    q = synth.drive_queries(wl, 4096, seed=1)
-    full = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
-    empty = km.Snapshot(wl.namespaces, wl.tuples[:0], wl.ns_names, wl.rel_names, wl.n_uuids)
-    d = km.Dispatcher(full, wl.max_depth, wl.max_width)
-    a1, _ = d.check(q)
-    assert a1.sum() > 0
-    d.set_snapshot(empty)
-    full.close()  # no longer in use once set_snapshot returned
-    a2, _ = d.check(q)
-    assert a2.sum() == 0
+def test_snapshot_swap_under_load():
+    """set_snapshot while 16 clients keep the dispatcher busy: the swap returns (no
+    starvation), every answer is the oracle's on the old or the new tuples, and every
+    request issued after the swap returned gets the new snapshot's (oracle) answer."""
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=9)
+    q = synth.drive_queries(wl, 8192, seed=1)
+    keep = np.random.default_rng(2).random(len(wl.tuples)) < 0.6  # the new snapshot: 60% of the tuples
+    t_new = wl.tuples[keep]
+    old = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    new = km.Snapshot(wl.namespaces, t_new, wl.ns_names, wl.rel_names, wl.n_uuids)
+    a_old, _ = _oracle_answers(_oracle(wl), q)
+    a_new, _ = _oracle_answers(_oracle(wl, t_new), q)
+    assert (a_old != a_new).sum() > 100
+    d = km.Dispatcher(old, wl.max_depth, wl.max_width, max_batch=2048, inflight=4)
+    stop = threading.Event()
+    swapped_at = [None]
+    log, errors = [], []
+
+    def client(t):
+        rng = np.random.default_rng(100 + t)
+        try:
+            while not stop.is_set():
+                i = int(rng.integers(0, len(q) - 64))
+                t0 = time.monotonic()
+                a, _ = d.check(q[i:i + 64])
+                log.append((t0, i, a.copy()))
+        except Exception as ex:
+            errors.append(ex)
+
+    th = [threading.Thread(target=client, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    time.sleep(0.5)
+    t0 = time.monotonic()
+    d.set_snapshot(new)
+    swapped_at[0] = time.monotonic()
+    swap_s = swapped_at[0] - t0
+    old.close()  # no longer in use once set_snapshot returned
+    time.sleep(0.5)
+    stop.set()
+    for x in th:
+        x.join()
     d.close()
+    assert not errors
+    assert swap_s < 5.0
+    after = 0
+    for ts, i, a in log:
+        want_new, want_old = a_new[i:i + 64], a_old[i:i + 64]
+        if ts > swapped_at[0]:
+            np.testing.assert_array_equal(a, want_new)
+            after += 1
+        else:
+            assert (a == want_new).all() or (a == want_old).all()
+    assert after > 10
+
+
+def test_expand_coalescing_matches_oracle():
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=7)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    orc = _oracle(wl)
+    rng = np.random.default_rng(3)
+    roots = np.zeros(600, dtype=km.SUBJSET_DT)
+    roots["ns"][:300], roots["rel"][:300] = wl.ns_names.index("Group"), wl.rel_names.index("members")
+    roots["obj"][:300] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], 300)
+    roots["ns"][300:], roots["rel"][300:] = wl.ns_names.index("Folder"), wl.rel_names.index("viewers")
+    roots["obj"][300:] = rng.integers(0, wl.meta["folders_per_root"], 300)
+    roots["max_depth"] = rng.integers(0, 6, 600)
+    d = km.Dispatcher(snap, wl.max_depth, wl.max_width, max_batch=256)
+    results, errors = {}, []
+
+    def client(t):
+        try:
+            for k in range(t, 600 // 10, 12):
+                results[k] = d.expand(roots[10 * k:10 * k + 10], cap=4 if k % 3 == 0 else 0)
+        except Exception as ex:
+            errors.append(ex)
+
+    th = [threading.Thread(target=client, args=(t,)) for t in range(12)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    st = d.stats()
+    d.close()
+    assert not errors
+    assert st["batches"] < st["requests"]
+    orc.set_limits(wl.max_depth, wl.max_width)
+    for k, (nodes, offs, err) in results.items():
+        assert (err == 0).all()
+        for j in range(10):
+            r = roots[10 * k + j]
+            on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), int(r["max_depth"]))
+            mine = nodes[int(offs[j]):int(offs[j + 1])]
+            assert len(mine) == len(on)
+            for f_p, f_o in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"),
+                             ("s_rel", "srel"), ("n_children", "n_children")):
+                np.testing.assert_array_equal(mine[f_p], on[f_o])
 
 
 def test_native_closed_loop_load():
