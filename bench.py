@@ -21,6 +21,7 @@ own device (keto_snapshot_build_device).  Timing = max over ranks; value = all r
 """
 import argparse
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -47,7 +48,45 @@ def cpu_threads():
     return max(1, min(n, 16))  # the GPU box grants 16 host cores per GPU
 
 
-def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0):
+def lib_sha256():
+    import keto_mi355x._abi as abi
+    with open(abi.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def committed_traffic(workload: str, kname: str):
+    """HBM bytes per tier-0 launch from the newest committed PMC passes (tools/pmc_traffic.sh ->
+    profiles/r*_traffic_<workload>.json) -- only if they profiled THIS library build (sha256 of
+    libketo_mi355x.so); a kernel change makes the figure stale and it is dropped (null)."""
+    tf = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{workload}.json")))
+    if not tf:
+        return None, "no PMC profile committed"
+    t = json.load(open(tf[-1]))
+    if kname not in t.get("kernel", "") or int(t.get("grid", 0)) <= 0:
+        return None, f"{os.path.basename(tf[-1])} profiled another kernel"
+    if t.get("lib_sha256") != lib_sha256():
+        return None, f"{os.path.basename(tf[-1])} profiled another build of libketo_mi355x.so"
+    return t["traffic_bytes_per_launch"], os.path.basename(tf[-1])
+
+
+def schedule_report(orc, q, gpu_allowed, n: int, cores: int):
+    """the oracle's schedule-sensitivity flags (refsem.h rs_check_ex) on the
+    first n queries of the batch, and the GPU's agreement with the canonical answer on them"""
+    import refsem
+
+    n = min(n, len(q))
+    dec, err, flags, _ = orc.check_batch_ex(q[:n], threads=cores)
+    sens = (flags & refsem.F_SENSITIVE) != 0
+    diff = (flags & refsem.F_SEQ_DIFFERS) != 0
+    return {"n": int(n), "flagged": int(sens.sum()), "flagged_frac": float(sens.mean()),
+            "sequential_schedule_differs": int(diff.sum()),
+            "gpu_mismatches_on_flagged": int((dec[sens] != gpu_allowed[:n][sens]).sum()),
+            "gpu_mismatches": int((dec != gpu_allowed[:n]).sum()),
+            "criterion": "a visited scope pruned a sibling and saw width truncation / an error / AND-NOT, or "
+                         "pruned occurrences at different rest depths plus depth truncation (oracle/refsem.c)"}
+
+
+def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0, gpu_allowed=None):
     """The oracle (C restatement of the reference, oracle/refsem.c) on the host cores, on a
     bounded sample of the same batch over the same graph -- reported beside the GPU, never
     the target.  The oracle indexes the engine's tuple records in place (no copy)."""
@@ -74,8 +113,14 @@ def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0):
         if dt * 2.5 > budget_s or n >= len(q):
             break
         n = min(len(q), int(n * max(2.0, min(8.0, budget_s / 2.5 / max(dt, 1e-3)))))
+    log(f"cpu baseline: {n} checks in {dt:.2f}s on {cores} threads (index {build_s:.1f}s)")
+    sched = None
+    if gpu_allowed is not None:
+        t0 = time.perf_counter()
+        sched = schedule_report(orc, q, gpu_allowed, max(1 << 12, min(n, 1 << 16)), cores)
+        log(f"schedule report ({sched['n']} queries): {time.perf_counter() - t0:.1f}s")
     orc.close()
-    return {"value": n / dt, "unit": "checks/s", "cores": cores, "kind": "port",
+    return sched, {"value": n / dt, "unit": "checks/s", "cores": cores, "kind": "port",
             "sample": f"first {n} of the {len(q)}-query batch over the full {len(wl.tuples)}-tuple graph, "
                       f"oracle/refsem.c (C restatement of internal/check + persistence/sql read path), "
                       f"{cores} threads, {dt:.2f} s (index build {build_s:.1f} s, untimed)"}, dec
@@ -289,6 +334,7 @@ def main():
     import keto_mi355x as km
     from keto_mi355x import synth
 
+    t_setup = time.perf_counter()
     wl, snap, setup_s = build_workload(args.workload, rank, world, device, args)
     info = snap.info()
     log(f"[rank {rank}] snapshot: {info['n_tuples']} tuples, {info['n_nodes']} nodes, "
@@ -309,6 +355,7 @@ def main():
 
     # algorithmic bytes per launch: one counted batch outside the timed region
     stream.counters(reset=True)
+    log(f"[rank {rank}] counted batch ({time.perf_counter() - t_setup:.1f}s since start)")
     eng.check_batch_device(dq, len(q), da, de, sync=True, count_work=True)
     c = stream.counters(reset=True)
     pt = c["per_tier"]
@@ -340,6 +387,8 @@ def main():
     assert k_n == args.steps, f"timed {k_n} kernel launches, expected {args.steps}"
     kernel_ms = k_sum / k_n
 
+    log(f"[rank {rank}] timed: {elapsed_local / args.steps * 1e3:.2f} ms/step, kernel {kernel_ms:.2f} ms "
+        f"({time.perf_counter() - t_setup:.1f}s since start)")
     # PCIe-inclusive rate (host buffers: H2D queries, kernels, D2H decisions) -- never `value`
     t1 = time.perf_counter()
     for _ in range(3):
@@ -358,18 +407,15 @@ def main():
         lat.append(time.perf_counter() - t1)
     p99_ms = float(np.percentile(np.array(lat) * 1e3, 99)) if lat else None
 
+    log(f"[rank {rank}] latency probe done ({time.perf_counter() - t_setup:.1f}s since start)")
     expand = expand_probe(km, snap, wl, stream) if args.workload in ("c3", "c4") else None
     serving = serving_probe(km, snap, q, wl, args.serve_clients, args.serve_request, args.serve_seconds) \
         if args.serve_clients > 0 else None
+    log(f"[rank {rank}] expand + serving probes done ({time.perf_counter() - t_setup:.1f}s since start)")
 
     achieved = bytes_t0 / (kernel_ms * 1e-3) / 1e9
     kname = "check_union_kernel" if union_only else "check_kernel"
-    traffic = None  # HBM bytes per tier-0 launch from the committed PMC passes (tools/pmc_traffic.sh)
-    tf = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{args.workload}.json")))
-    if tf:
-        t = json.load(open(tf[-1]))
-        if kname in t.get("kernel", "") and int(t.get("grid", 0)) > 0:
-            traffic = t["traffic_bytes_per_launch"]
+    traffic, traffic_src = committed_traffic(args.workload, kname)
     if args.workload == "c2":
         data, cfgno = "nested-group graph", 2
         desc = (f"C2 nested groups: {info['n_tuples']} tuples, 5 levels, union-only, max_read_depth 8, "
@@ -402,7 +448,7 @@ def main():
         "expand": expand,
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kname + " (tier 0)", "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": int(bytes_t0),
                      "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (BASELINE.md)",
@@ -412,10 +458,11 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, dec = cpu_baseline(wl, q, wl.max_depth, wl.max_width, args.cpu_budget)
+        sched, cb, dec = cpu_baseline(wl, q, wl.max_depth, wl.max_width, args.cpu_budget, gpu_allowed=allowed)
         out["cpu_baseline"] = cb
         ns = len(dec)
         out["cpu_parity_sample"] = {"n": ns, "mismatches": int((dec != allowed[:ns]).sum())}
+        out["schedule_sensitivity"] = sched
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist_on:

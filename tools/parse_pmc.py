@@ -2,7 +2,9 @@
 uncounted Check interpreter) from tools/pmc_traffic.sh output -> JSON for bench.py."""
 import csv
 import glob
+import hashlib
 import json
+import os
 import sys
 from collections import defaultdict
 
@@ -30,7 +32,11 @@ _, _, write = per_launch("WRITE_SIZE", "write")
 # rocprofv3 reports both in KB; gfx950 FETCH_SIZE tallies 128-B requests at 64 B -> x2
 fetch_b = 2 * 1024 * sum(fetch) / len(fetch)
 write_b = 1024 * sum(write) / len(write)
-res = {"kernel": name, "grid": grid, "launches": [len(fetch), len(write)],
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "djy-keto_amd", "keto_mi355x",
+                   "libketo_mi355x.so")
+res = {"kernel": name, "grid": grid,
+       # the library the passes profiled: bench.py reports this traffic only for the same build
+       "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(), "launches": [len(fetch), len(write)],
        "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
        "traffic_bytes_per_launch": fetch_b + write_b,
        "correction": "FETCH_SIZE x2 (gfx950: 128-B requests tallied at 64 B, MI355X_MICROARCH.md HBM); "
