@@ -246,6 +246,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         L.max_depth = lim.max_read_depth;
         L.max_width = lim.max_read_width;
         L.count = (flags & KETO_F_COUNT_WORK) != 0;
+        L.err_detail = (flags & KETO_F_ERR_DETAIL) != 0;
         if (flags & KETO_F_DEVICE_PTRS) {
             L.queries = queries;
             L.out_allowed = out_allowed;

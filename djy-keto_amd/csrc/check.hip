@@ -87,6 +87,7 @@ struct CheckParams {
     unsigned long long *counters;
     uint32_t last_tier;
     uint32_t live_lanes;  // lanes [live_lanes, 64) of every wave take no queries
+    uint32_t err_detail;
 };
 
 #ifndef KETO_GUARD
@@ -477,7 +478,7 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                 // run the pending child checkIsAllowed(c, d, skipDirect=true) (engine.go:161)
                 const NodeInfo ni = t_node_info(T, c);
                 if (ri_status(ni.ri) == REL_ERROR) {  // engine.go:228-232: decisive
-                    res = mk_err(KETO_QERR_NO_RELATION);
+                    res = mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16);
                     if (w & FL_OWNER) {
                         scope = false;
                         st = S_RET;
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                         const NodeInfo ni = t_node_info(T, node);
                         top.y = ni.ri;
                         if (ri_status(ni.ri) == REL_ERROR) {  // :228-232
-                            res = mk_err(KETO_QERR_NO_RELATION);
+                            res = mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, node, ni) << 16);
                             action = 2;
                             break;
                         }
@@ -911,9 +912,9 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
                     P.ovf_list[atomicAdd(P.ovf_count, 1u)] = pos;
                 }
             } else {
-                const uint32_t err = res >> 8;
+                const uint32_t err = res >> 8;  // code | relation name id << 8 (KETO_F_ERR_DETAIL)
                 P.out_allowed[q] = (err == 0 && (res & 3u) == M_IS) ? 1 : 0;
-                P.out_err[q] = (int32_t)err;
+                P.out_err[q] = (int32_t)(P.err_detail ? err : err & 0xFFu);
                 if (COUNT) {
                     c_rows += q_rows;
                     c_edges += q_edges;
@@ -991,6 +992,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         P.max_width = L.max_width;
         P.counters = st.counters + 8 * tier;
         P.last_tier = tier == 2;
+        P.err_detail = L.err_detail;
         uint32_t lanes = t[tier].lanes;
         if (tier == 0) {  // persistent grid: the resident blocks (occupancy API), capped by the batch
             int per_cu = 0;

@@ -72,6 +72,7 @@ struct UParams {
     unsigned long long *counters;
     uint32_t last_tier;
     uint32_t live_lanes;  // lanes [live_lanes, 64) of every wave take no queries
+    uint32_t err_detail;
 };
 
 // word j (0..7) of the two consecutive windows v0, v1 -- selects, no scratch
@@ -170,6 +171,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 // root checkIsAllowed(node, d, false) (engine.go:214-249)
                 const NodeInfo ni = t_node_info(T, node);
                 if (ri_status(ni.ri) == REL_ERROR) {
+                    aux = t_relname(s, T, node, ni);
                     fin = 3;
                     break;
                 }
@@ -440,6 +442,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 // child checkIsAllowed(c, d, skipDirect=true) -> expandSubject(c, d-1) (engine.go:161)
                 const NodeInfo ni = t_node_info(T, c);
                 if (ri_status(ni.ri) == REL_ERROR) {
+                    aux = t_relname(s, T, c, ni);
                     fin = 3;
                     break;
                 }
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 }
             } else {
                 P.out_allowed[q] = fin == 1 ? 1 : 0;
-                P.out_err[q] = fin == 3 ? KETO_QERR_NO_RELATION : 0;
+                P.out_err[q] = fin == 3 ? (int32_t)(KETO_QERR_NO_RELATION | (P.err_detail ? aux << 8 : 0u)) : 0;
                 if (COUNT) {
                     c_rows += q_rows;
                     c_edges += q_edges;
@@ -571,6 +574,7 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         P.max_width = L.max_width;
         P.counters = st.counters + 8 * tier;
         P.last_tier = tier == 2;
+        P.err_detail = L.err_detail;
         uint32_t lanes = t[tier].lanes;
         if (tier == 0) {  // persistent grid: exactly the resident blocks (occupancy API), capped by the batch
             int per_cu = 0;

@@ -81,6 +81,12 @@ __device__ __forceinline__ NodeInfo t_node_info(const Tables &T, uint32_t node) 
     return r;
 }
 
+// relation name id of a node (error detail: the relation ASTRelationFor rejects)
+__device__ __forceinline__ uint32_t t_relname(const DevSnapshot &s, const Tables &T, uint32_t node, const NodeInfo &ni) {
+    if (node & VIRT_BIT) return node & 0xFFFFu;
+    return s.slot_rel[T.ns[ni.ns].slot_base + ni.slot];
+}
+
 // node of (same entity as `node`, relation `rel`): computed usersets / tuple-to-userset hops
 // Relation ids past the snapshot's name table (a caller-side id the snapshot never saw) are
 // clamped to the reserved last name, which no namespace declares: ASTRelationFor's

@@ -150,6 +150,7 @@ struct CheckLaunch {
     int32_t *out_err;
     int32_t max_depth, max_width;
     bool count;
+    bool err_detail;  // KETO_F_ERR_DETAIL: out_err carries the failing relation name id << 8
 };
 // resolve.hip: per-query start records, longest-first, into st.resolved
 void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth);

@@ -138,6 +138,12 @@ typedef struct keto_stream keto_stream;
 #define KETO_F_DEVICE_PTRS 0x1u  /* query / output pointers are device memory */
 #define KETO_F_ASYNC 0x2u        /* enqueue only; pair with keto_stream_sync */
 #define KETO_F_COUNT_WORK 0x4u   /* accumulate keto_work_counters on the stream */
+/* keto_check_batch: for KETO_QERR_NO_RELATION, out_err[i] = 1 | (relation name id << 8), the
+ * relation ASTRelationFor rejected -- not always the query's own (a subject set deeper in the
+ * walk can name it) -- so the shim can return the reference's exact
+ * `relation %q does not exist` (internal/namespace/definitions.go:61).  Without the flag
+ * out_err[i] is the bare code. */
+#define KETO_F_ERR_DETAIL 0x8u
 
 int keto_abi_version(void);
 /* copies the thread's last error message; returns its full length */
