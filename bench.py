@@ -233,10 +233,10 @@ def serving_probe(km, snap, q, wl, clients: int, req: int, seconds: float):
 
 
 def run_c5(args, rank, world, device, dist_on):
-    """configs[4]: a graph partitioned by object over the ranks (keto_mi355x/partition.py).
-    One step = one batch of this rank's Checks: closure exchange (RCCL all-to-all per BFS
-    level) -> device snapshot build of the closure -> the Check kernels.  Every phase is
-    inside the timed region."""
+    """configs[4]: a graph partitioned by object over the ranks (keto_partition_*, csrc/partition.hip).
+    One step = one batch of this rank's Checks: closure exchange (all-to-all per BFS level over
+    the job's collective) -> device snapshot build of the closure -> the Check kernels.  Every
+    phase is inside the timed region."""
     import torch
 
     import keto_mi355x as km
@@ -246,9 +246,14 @@ def run_c5(args, rank, world, device, dist_on):
     wl = synth.drive_scaled(args.scale, materialize=False)
     part = synth.drive_partition(wl, world, rank)
     n_part = len(part)
+    coll = None
+    if dist_on:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from torch_collective import TorchCollective  # keto_collective over the job's process group
+        coll = TorchCollective()
     eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
                                       device=device, max_read_depth=wl.max_depth, max_read_width=wl.max_width,
-                                      store_device=f"cuda:{device}")
+                                      collective=coll)
     del part
     setup_s = time.perf_counter() - t0
     log(f"[rank {rank}] partition {rank}/{world}: {n_part} of {wl.meta['n_tuples']} tuples, setup {setup_s:.1f}s")
@@ -261,7 +266,7 @@ def run_c5(args, rank, world, device, dist_on):
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
-    phases = {"closure_s": 0.0, "build_s": 0.0, "check_s": 0.0}
+    phases = {"closure_s": 0.0, "build_s": 0.0, "run_s": 0.0}
     t_start = time.perf_counter()
     for _ in range(args.steps):
         eng.check_batch(q)
@@ -285,6 +290,7 @@ def run_c5(args, rank, world, device, dist_on):
         "allowed_fraction": float(allowed.mean()),
         "phases_ms_per_step": {k: v / args.steps * 1e3 for k, v in phases.items()},
         "closure": {"tuples": eng.last["tuples"], "objects": eng.last["objects"], "levels": eng.last["levels"],
+                    "bytes_sent": eng.last["bytes_sent"],
                     "partition_tuples": n_part},
         "roofline": None, "cpu_baseline": None,
     }

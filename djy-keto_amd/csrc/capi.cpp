@@ -416,6 +416,49 @@ int keto_dispatcher_stats_get(keto_dispatcher *d, keto_dispatcher_stats *out) {
     return guarded([&] { keto::dispatcher_stats(d, out); });
 }
 
+int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
+                          const keto_collective *coll, const keto_limits *limits, keto_partition **out) {
+    if (!out) return fail(KETO_E_INVALID, "null output pointer");
+    *out = nullptr;
+    return guarded([&] {
+        *out = reinterpret_cast<keto_partition *>(
+            keto::partition_create(cfg, tuples, n, (flags & KETO_F_DEVICE_PTRS) != 0, coll, limits));
+    });
+}
+
+int keto_partition_check(keto_partition *p, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
+                         int32_t *out_err, uint32_t flags) {
+    if (!p) return fail(KETO_E_INVALID, "null partition");
+    if (n && (!queries || !out_allowed || !out_err)) return fail(KETO_E_INVALID, "null buffer");
+    return guarded([&] {
+        keto::partition_check(reinterpret_cast<keto::PartitionHandle *>(p), queries, n, out_allowed, out_err, flags);
+    });
+}
+
+int keto_partition_expand(keto_partition *p, const keto_subject_set *roots, uint64_t n, uint64_t *out_nodes_needed) {
+    if (!p || !out_nodes_needed) return fail(KETO_E_INVALID, "null argument");
+    if (n && !roots) return fail(KETO_E_INVALID, "null roots");
+    return guarded([&] { *out_nodes_needed = keto::partition_expand(reinterpret_cast<keto::PartitionHandle *>(p), roots, n); });
+}
+
+int keto_partition_expand_result(keto_partition *p, keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets,
+                                 int32_t *out_err) {
+    if (!p) return fail(KETO_E_INVALID, "null partition");
+    return guarded([&] {
+        keto::partition_expand_result(reinterpret_cast<keto::PartitionHandle *>(p), out_nodes, out_cap, out_offsets, out_err);
+    });
+}
+
+int keto_partition_stats_get(keto_partition *p, keto_partition_stats *out) {
+    if (!p || !out) return fail(KETO_E_INVALID, "null argument");
+    keto::partition_stats(reinterpret_cast<keto::PartitionHandle *>(p), out);
+    return KETO_OK;
+}
+
+int keto_partition_free(keto_partition *p) {
+    return guarded([&] { keto::partition_free(reinterpret_cast<keto::PartitionHandle *>(p)); });
+}
+
 int keto_store_create(int32_t device, const keto_tuple *tuples, uint64_t n, uint32_t flags, keto_store **out) {
     if (!out) return fail(KETO_E_INVALID, "null output pointer");
     *out = nullptr;

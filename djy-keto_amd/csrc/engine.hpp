@@ -194,4 +194,14 @@ Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg);
 void store_free(TupleStore *st);
 void store_info(const TupleStore &st, uint64_t *n, uint64_t *version);
 
+// partition.hip: graphs partitioned by object over the ranks of a job (keto_partition_*)
+struct PartitionHandle;
+PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
+                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits);
+void partition_check(PartitionHandle *p, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags);
+uint64_t partition_expand(PartitionHandle *p, const keto_subject_set *roots, uint64_t n);
+void partition_expand_result(PartitionHandle *p, keto_tree_node *nodes, uint64_t cap, uint64_t *offsets, int32_t *err);
+void partition_stats(PartitionHandle *p, keto_partition_stats *out);
+void partition_free(PartitionHandle *p);
+
 }  // namespace keto

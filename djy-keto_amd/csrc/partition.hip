@@ -1,0 +1,638 @@
+// Graphs larger than one GPU (BASELINE config 5): the relation-tuple graph
+// is partitioned by object over the ranks of a job -- every tuple of (ns, obj) lives on rank
+// keto_object_owner(ns, obj, world) -- so all relation slots of an object (its direct rows, the
+// rows its computed usersets reach, its tuple-to-userset row) are on one rank and crossing to
+// another object only happens along a subject-set edge.
+//
+// A batch (collective: every rank calls keto_partition_check / _expand together, each with its
+// own queries) runs in three steps, all on the device except the caller's collective:
+//  1. closure exchange.  The reference reads rows only of objects reachable from the query's
+//     object along subject-set edges, and only while the depth ledger allows (engine.go:214-249
+//     returns before any read at rest depth <= 0; the found-lookahead of traverser.go:73-80
+//     reads one level further), so max_read_depth + 1 levels of a level-synchronous object BFS
+//     collect every row any query of the batch can read.  Per level: the new objects (a device
+//     hash set drops the ones fetched before) are routed to their owners (counting scatter,
+//     one all-to-all of object keys), the owners gather those objects' tuples from their
+//     key-sorted partition (binary search + two-pass compaction) and send them back (second
+//     all-to-all).  The next frontier is the subject sets of the tuples received.
+//     Check batches also send every owner the batch's subject ids once: a subject-id tuple is
+//     only ever read by an EXISTS probe against the query's own subject (checkDirect
+//     engine.go:167-208, the found-lookahead traverser.go:73-80, the OR shortcut :143-172);
+//     expand-subject rows select subject sets only (traverser.go:87) and tuple-to-userset
+//     skips subject ids (rewrites.go:280).  So owners ship subject-set tuples plus only the
+//     subject-id tuples naming one of the batch's subjects -- the same decisions, a fraction
+//     of the bytes.  Expand batches ship every tuple (leaves are part of the tree).
+//  2. the closure (in shard order after the build's own sort) becomes an ordinary device
+//     snapshot (build_snapshot, the replicated path's builder);
+//  3. the unmodified Check / Expand kernels run on it.
+// The closure holds every row the reference engine could read for these queries, so the
+// kernels take exactly the decisions (and build exactly the trees) they would on the whole
+// graph; exactness needs no distributed version of the sequential walk.
+//
+// The collective is the caller's (keto_collective): a Go host passes its RCCL communicator's
+// all-to-all, the tests pass gloo.  coll == NULL runs one rank with no exchange.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "device_common.hpp"
+
+namespace keto {
+namespace {
+
+using build::DevBuf;
+constexpr uint32_t BLK = 256;
+constexpr uint32_t MAX_WORLD = 4096;
+
+inline dim3 grid_for(uint64_t n) {
+    return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + BLK - 1) / BLK, 1u << 16)));
+}
+__device__ __forceinline__ uint64_t gid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
+__device__ __forceinline__ uint64_t okey(uint32_t ns, uint32_t obj) { return ((uint64_t)ns << 32) | obj; }
+// keto_object_owner (include/keto_mi355x.h) on the device: the same hash of (ns << 32 | obj)
+__host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
+    return (uint32_t)(((key * 0x9E3779B97F4A7C15ull) >> 32) % world);
+}
+
+// ------------------------------------------------------------------ kernels
+
+__global__ __launch_bounds__(BLK) void k_tuple_keys(const keto_tuple *t, uint64_t n, uint64_t *keys, uint32_t *idx) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        keys[i] = okey(t[i].ns, t[i].obj);
+        idx[i] = (uint32_t)i;
+    }
+}
+__global__ __launch_bounds__(BLK) void k_gather_tuples(const keto_tuple *t, const uint32_t *idx, uint64_t n,
+                                                        keto_tuple *out) {
+    for (uint64_t i = gid(); i < n; i += gstride()) out[i] = t[idx[i]];
+}
+// run starts of the sorted keys: flag[i] = key[i] != key[i-1]
+__global__ __launch_bounds__(BLK) void k_run_flags(const uint64_t *k, uint64_t n, uint32_t *flag) {
+    for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+}
+// compacted runs: run r starts at the i with flag[i] and exclusive-scan pos[i] == r
+__global__ __launch_bounds__(BLK) void k_run_starts(const uint64_t *k, const uint32_t *flag, const uint64_t *pos,
+                                                     uint64_t n, uint64_t *ukeys, uint64_t *beg) {
+    for (uint64_t i = gid(); i < n; i += gstride())
+        if (flag[i]) {
+            ukeys[pos[i]] = k[i];
+            beg[pos[i]] = i;
+        }
+}
+__global__ __launch_bounds__(BLK) void k_query_keys(const keto_query *q, uint64_t n, uint64_t *keys, uint32_t *subj,
+                                                     unsigned long long *n_subj) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        keys[i] = okey(q[i].ns, q[i].obj);
+        if (q[i].subj_kind == 0) subj[atomicAdd(n_subj, 1ull)] = q[i].s_obj;
+    }
+}
+__global__ __launch_bounds__(BLK) void k_root_keys(const keto_subject_set *r, uint64_t n, uint64_t *keys) {
+    for (uint64_t i = gid(); i < n; i += gstride()) keys[i] = okey(r[i].ns, r[i].obj);
+}
+// seen-set insert: keys never asked for before go to `out` (each once)
+__global__ __launch_bounds__(BLK) void k_insert(const uint64_t *cand, uint64_t n, unsigned long long *table,
+                                                 uint64_t mask, uint64_t *out, unsigned long long *n_out) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        const unsigned long long k = cand[i] + 1;  // 0 = empty slot
+        uint64_t h = mix64(k) & mask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&table[h], 0ull, k);
+            if (prev == 0ull) {
+                out[atomicAdd(n_out, 1ull)] = k - 1;
+                break;
+            }
+            if (prev == k) break;
+            h = (h + 1) & mask;
+        }
+    }
+}
+__global__ __launch_bounds__(BLK) void k_rehash(const uint64_t *keys, uint64_t n, unsigned long long *table,
+                                                 uint64_t mask) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        const unsigned long long k = keys[i] + 1;
+        uint64_t h = mix64(k) & mask;
+        while (atomicCAS(&table[h], 0ull, k) != 0ull) h = (h + 1) & mask;
+    }
+}
+// routing: destination histogram, then a counting scatter (order within a destination is free)
+__global__ __launch_bounds__(BLK) void k_dest_hist(const uint64_t *keys, uint64_t n, uint32_t world,
+                                                    unsigned long long *hist) {
+    for (uint64_t i = gid(); i < n; i += gstride()) atomicAdd(&hist[owner_of(keys[i], world)], 1ull);
+}
+__global__ __launch_bounds__(BLK) void k_dest_scatter(const uint64_t *keys, uint64_t n, uint32_t world,
+                                                       unsigned long long *cursor, uint64_t *out) {
+    for (uint64_t i = gid(); i < n; i += gstride()) out[atomicAdd(&cursor[owner_of(keys[i], world)], 1ull)] = keys[i];
+}
+// owner side: tuples to ship for each requested key (all of them for Expand; subject sets plus
+// subject ids in the requester's subject list for Check)
+struct Lookup {
+    const uint64_t *ukeys, *beg;  // partition runs: ukeys[m], beg[m+1]
+    uint64_t m;
+    const keto_tuple *tuples;
+    const uint64_t *req;          // requested keys, grouped by source rank
+    const uint64_t *req_off;      // [world+1] request offsets per source
+    const uint32_t *subj;         // sorted subject lists of every source, concatenated
+    const uint64_t *subj_off;     // [world+1]
+    uint32_t world;
+    int filter;
+};
+__device__ __forceinline__ bool run_of(const Lookup &L, uint64_t key, uint64_t &b, uint64_t &e) {
+    uint64_t lo = 0, hi = L.m;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (L.ukeys[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= L.m || L.ukeys[lo] != key) return false;
+    b = L.beg[lo];
+    e = L.beg[lo + 1];
+    return true;
+}
+__device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
+    uint32_t lo = 0, hi = L.world;  // last source whose offset <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.req_off[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ bool keep(const Lookup &L, const keto_tuple &t, uint32_t src) {
+    if (!L.filter || t.subj_kind == 1) return true;
+    uint64_t lo = L.subj_off[src], hi = L.subj_off[src + 1];
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (L.subj[mid] < t.s_obj) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < L.subj_off[src + 1] && L.subj[lo] == t.s_obj;
+}
+__global__ __launch_bounds__(BLK) void k_lookup_count(Lookup L, uint64_t n, uint64_t *cnt) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        uint64_t b, e, c = 0;
+        if (run_of(L, L.req[i], b, e)) {
+            const uint32_t src = source_of(L, i);
+            for (uint64_t j = b; j < e; j++) c += keep(L, L.tuples[j], src) ? 1 : 0;
+        }
+        cnt[i] = c;
+    }
+}
+__global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const uint64_t *pos, keto_tuple *out) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        uint64_t b, e;
+        if (!run_of(L, L.req[i], b, e)) continue;
+        const uint32_t src = source_of(L, i);
+        uint64_t o = pos[i];
+        for (uint64_t j = b; j < e; j++)
+            if (keep(L, L.tuples[j], src)) out[o++] = L.tuples[j];
+    }
+}
+// next frontier: the subject-set objects of the tuples received
+__global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, uint64_t *cand,
+                                               unsigned long long *n_cand) {
+    for (uint64_t i = gid(); i < n; i += gstride())
+        if (t[i].subj_kind == 1) cand[atomicAdd(n_cand, 1ull)] = okey(t[i].s_ns, t[i].s_obj);
+}
+
+// ------------------------------------------------------------------ host side
+
+template <class T>
+T *dptr(const DevBuf &b) { return static_cast<T *>(b.p); }
+
+void ensure(DevBuf &b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return;
+    b = DevBuf(std::max<size_t>(bytes, 256));
+}
+
+struct Partition {
+    int device = 0;
+    bool have_coll = false;
+    keto_collective coll{};
+    uint32_t rank = 0, world = 1;
+    keto_limits limits{5, 100};
+    // snapshot configuration for the per-batch closure builds
+    std::vector<std::string> ns_names, rel_names;
+    std::vector<const char *> ns_ptr, rel_ptr;
+    std::string json;
+    keto_snapshot_config cfg{};
+    // this rank's partition, sorted by object key: tuples[n], run keys ukeys[m], beg[m+1]
+    DevBuf tuples, ukeys, beg;
+    uint64_t n = 0, m = 0;
+    hipStream_t hs = nullptr;
+    keto_stream *kstream = nullptr;
+    // per-batch workspace (grown on demand, reused)
+    DevBuf table, seen, cand, fresh, routed, req, req_off, subj, subj_off, cnt, pos, out, got, scratch, ctr, closure;
+    uint64_t table_mask = 0, n_seen = 0;
+    keto_partition_stats last{};
+    // Expand results between keto_partition_expand and keto_partition_expand_result
+    std::vector<keto_tree_node> xnodes;
+    std::vector<uint64_t> xoffs;
+    std::vector<int32_t> xerr;
+    ~Partition() {
+        if (kstream) keto_stream_destroy(kstream);
+        if (hs) (void)hipStreamDestroy(hs);
+    }
+};
+
+void sync(Partition &P) { KETO_HIP(hipStreamSynchronize(P.hs)); }
+
+template <class F>
+void cub_call(Partition &P, F &&f) {  // hipCUB two-phase call with the shared scratch buffer
+    size_t bytes = 0;
+    KETO_HIP(f(nullptr, bytes));
+    ensure(P.scratch, bytes);
+    KETO_HIP(f(P.scratch.p, bytes));
+}
+
+uint64_t d2h_u64(Partition &P, const void *d) {
+    uint64_t v = 0;
+    KETO_HIP(hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, P.hs));
+    sync(P);
+    return v;
+}
+
+void coll_check(int rc, const char *what) {
+    if (rc != 0) throw Error(KETO_E_DEVICE, std::string("collective ") + what + " failed with " + std::to_string(rc));
+}
+
+uint64_t allreduce_max(Partition &P, uint64_t v) {
+    if (!P.have_coll || P.world == 1) return v;
+    coll_check(P.coll.allreduce_max_u64(P.coll.ctx, &v), "allreduce_max_u64");
+    return v;
+}
+
+// all-to-all-v of device records grouped by destination (send_cnt[r] records of `rec` bytes
+// for rank r): received records land in `dst` (grown), grouped by source; returns per-source
+// counts.  Host-staged, so any collective (RCCL, gloo, MPI) can carry it.
+std::vector<uint64_t> exchange(Partition &P, const void *src, const std::vector<uint64_t> &send_cnt, size_t rec,
+                               DevBuf &dst, uint64_t &bytes_sent) {
+    const uint32_t W = P.world;
+    if (!P.have_coll || W == 1) {
+        ensure(dst, send_cnt[0] * rec);
+        if (send_cnt[0]) KETO_HIP(hipMemcpyAsync(dst.p, src, send_cnt[0] * rec, hipMemcpyDeviceToDevice, P.hs));
+        return send_cnt;
+    }
+    std::vector<uint64_t> recv_cnt(W, 0), sb(W), rb(W);
+    coll_check(P.coll.alltoall_u64(P.coll.ctx, send_cnt.data(), recv_cnt.data()), "alltoall_u64");
+    uint64_t ns = 0, nr = 0;
+    for (uint32_t r = 0; r < W; r++) {
+        sb[r] = send_cnt[r] * rec;
+        rb[r] = recv_cnt[r] * rec;
+        ns += sb[r];
+        nr += rb[r];
+        if (r != P.rank) bytes_sent += sb[r];
+    }
+    std::vector<uint8_t> hsend(ns), hrecv(nr);
+    if (ns) KETO_HIP(hipMemcpyAsync(hsend.data(), src, ns, hipMemcpyDeviceToHost, P.hs));
+    sync(P);
+    coll_check(P.coll.alltoallv(P.coll.ctx, hsend.data(), sb.data(), hrecv.data(), rb.data()), "alltoallv");
+    ensure(dst, nr);
+    if (nr) KETO_HIP(hipMemcpyAsync(dst.p, hrecv.data(), nr, hipMemcpyHostToDevice, P.hs));
+    sync(P);
+    return recv_cnt;
+}
+
+void ensure_table(Partition &P, uint64_t add) {
+    uint64_t cap = P.table_mask + 1;
+    if (P.table.p && 2 * (P.n_seen + add) <= cap) return;
+    while (2 * (P.n_seen + add) > cap || cap < (1u << 20)) cap *= 2;
+    if (cap < 2) cap = 1u << 20;
+    ensure(P.table, cap * 8);
+    P.table_mask = cap - 1;
+    KETO_HIP(hipMemsetAsync(P.table.p, 0, cap * 8, P.hs));
+    if (P.n_seen)
+        hipLaunchKernelGGL(k_rehash, grid_for(P.n_seen), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.seen), P.n_seen,
+                           dptr<unsigned long long>(P.table), P.table_mask);
+}
+
+// Closure of the objects keyed in `keys` (device, n_keys): appended into P.closure, count returned.
+// subj (device, sorted unique, n_subj) filters subject-id tuples (Check); null ships everything.
+uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint32_t *subj, uint64_t n_subj,
+                 bool filter, keto_partition_stats &st) {
+    const uint32_t W = P.world;
+    // every owner gets this rank's subject list once per batch
+    std::vector<uint64_t> subj_cnt(W, filter ? n_subj : 0);
+    DevBuf subj_src;
+    ensure(subj_src, std::max<uint64_t>(1, n_subj) * W * 4);
+    if (filter)
+        for (uint32_t r = 0; r < W; r++)
+            if (n_subj)
+                KETO_HIP(hipMemcpyAsync(dptr<uint32_t>(subj_src) + (uint64_t)r * n_subj, subj, n_subj * 4,
+                                        hipMemcpyDeviceToDevice, P.hs));
+    std::vector<uint64_t> subj_from = exchange(P, subj_src.p, subj_cnt, 4, P.subj, st.bytes_sent);
+    std::vector<uint64_t> soff(W + 1, 0);
+    for (uint32_t r = 0; r < W; r++) soff[r + 1] = soff[r] + subj_from[r];
+    ensure(P.subj_off, (W + 1) * 8);
+    KETO_HIP(hipMemcpyAsync(P.subj_off.p, soff.data(), (W + 1) * 8, hipMemcpyHostToDevice, P.hs));
+
+    // seen set: fresh per batch
+    P.n_seen = 0;
+    ensure_table(P, n_keys);
+    KETO_HIP(hipMemsetAsync(P.table.p, 0, (P.table_mask + 1) * 8, P.hs));
+    ensure(P.ctr, 64);
+    ensure(P.cand, std::max<uint64_t>(1, n_keys) * 8);
+    KETO_HIP(hipMemcpyAsync(P.cand.p, keys, n_keys * 8, hipMemcpyDeviceToDevice, P.hs));
+    uint64_t n_cand = n_keys, total = 0;
+    std::vector<std::pair<DevBuf, uint64_t>> parts;
+    const int levels = P.limits.max_read_depth + 1;
+    for (int level = 0; level < levels; level++) {
+        // new objects of this level: never asked for before (seen-set insert)
+        ensure_table(P, n_cand);
+        ensure(P.fresh, std::max<uint64_t>(1, n_cand) * 8);
+        unsigned long long *c = dptr<unsigned long long>(P.ctr);
+        KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
+        if (n_cand)
+            hipLaunchKernelGGL(k_insert, grid_for(n_cand), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.cand), n_cand,
+                               dptr<unsigned long long>(P.table), P.table_mask, dptr<uint64_t>(P.fresh), c);
+        const uint64_t n_new = d2h_u64(P, c);
+        if (allreduce_max(P, n_new) == 0) break;
+        st.levels++;
+        st.objects += n_new;
+        if (!P.seen.p || P.seen.bytes < (P.n_seen + n_new) * 8) {  // remembered for rehashing
+            DevBuf bigger(std::max<uint64_t>(1u << 20, (P.n_seen + n_new) * 16));
+            if (P.n_seen) KETO_HIP(hipMemcpyAsync(bigger.p, P.seen.p, P.n_seen * 8, hipMemcpyDeviceToDevice, P.hs));
+            P.seen = std::move(bigger);
+        }
+        if (n_new)
+            KETO_HIP(hipMemcpyAsync(dptr<uint64_t>(P.seen) + P.n_seen, P.fresh.p, n_new * 8, hipMemcpyDeviceToDevice,
+                                    P.hs));
+        P.n_seen += n_new;
+        // route the requests to their owners
+        std::vector<uint64_t> send(W, 0);
+        ensure(P.routed, std::max<uint64_t>(1, n_new) * 8);
+        if (W == 1) {
+            send[0] = n_new;
+            if (n_new) KETO_HIP(hipMemcpyAsync(P.routed.p, P.fresh.p, n_new * 8, hipMemcpyDeviceToDevice, P.hs));
+        } else {
+            DevBuf hist(W * 8);
+            KETO_HIP(hipMemsetAsync(hist.p, 0, W * 8, P.hs));
+            if (n_new)
+                hipLaunchKernelGGL(k_dest_hist, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new, W,
+                                   dptr<unsigned long long>(hist));
+            KETO_HIP(hipMemcpyAsync(send.data(), hist.p, W * 8, hipMemcpyDeviceToHost, P.hs));
+            sync(P);
+            std::vector<uint64_t> cur(W, 0);
+            for (uint32_t r = 1; r < W; r++) cur[r] = cur[r - 1] + send[r - 1];
+            KETO_HIP(hipMemcpyAsync(hist.p, cur.data(), W * 8, hipMemcpyHostToDevice, P.hs));
+            if (n_new)
+                hipLaunchKernelGGL(k_dest_scatter, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new,
+                                   W, dptr<unsigned long long>(hist), dptr<uint64_t>(P.routed));
+        }
+        std::vector<uint64_t> from = exchange(P, P.routed.p, send, 8, P.req, st.bytes_sent);
+        std::vector<uint64_t> roff(W + 1, 0);
+        for (uint32_t r = 0; r < W; r++) roff[r + 1] = roff[r] + from[r];
+        const uint64_t n_req = roff[W];
+        // owner side: count, scan, fill
+        ensure(P.req_off, (W + 1) * 8);
+        KETO_HIP(hipMemcpyAsync(P.req_off.p, roff.data(), (W + 1) * 8, hipMemcpyHostToDevice, P.hs));
+        Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<keto_tuple>(P.tuples),
+                 dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<uint32_t>(P.subj), dptr<uint64_t>(P.subj_off),
+                 W, filter ? 1 : 0};
+        ensure(P.cnt, (n_req + 1) * 8);
+        ensure(P.pos, (n_req + 1) * 8);
+        KETO_HIP(hipMemsetAsync(P.cnt.p, 0, (n_req + 1) * 8, P.hs));
+        if (n_req) hipLaunchKernelGGL(k_lookup_count, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, dptr<uint64_t>(P.cnt));
+        uint64_t *cntp = dptr<uint64_t>(P.cnt), *posp = dptr<uint64_t>(P.pos);
+        const int nn = (int)(n_req + 1);
+        cub_call(P, [&](void *tmp, size_t &b) {
+            return hipcub::DeviceScan::ExclusiveSum(tmp, b, cntp, posp, nn, P.hs);
+        });
+        // tuples per source = pos at the source boundaries
+        std::vector<uint64_t> pb(W + 1, 0);
+        for (uint32_t r = 0; r <= W; r++)
+            KETO_HIP(hipMemcpyAsync(&pb[r], posp + roff[r], 8, hipMemcpyDeviceToHost, P.hs));
+        sync(P);
+        const uint64_t n_out = pb[W];
+        ensure(P.out, std::max<uint64_t>(1, n_out) * sizeof(keto_tuple));
+        if (n_req)
+            hipLaunchKernelGGL(k_lookup_fill, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, posp,
+                               dptr<keto_tuple>(P.out));
+        std::vector<uint64_t> back(W);
+        for (uint32_t r = 0; r < W; r++) back[r] = pb[r + 1] - pb[r];
+        std::vector<uint64_t> recv = exchange(P, P.out.p, back, sizeof(keto_tuple), P.got, st.bytes_sent);
+        uint64_t n_got = 0;
+        for (uint64_t v : recv) n_got += v;
+        // keep them; next frontier = their subject sets
+        DevBuf keepb(std::max<uint64_t>(1, n_got) * sizeof(keto_tuple));
+        if (n_got) KETO_HIP(hipMemcpyAsync(keepb.p, P.got.p, n_got * sizeof(keto_tuple), hipMemcpyDeviceToDevice, P.hs));
+        ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
+        KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
+        if (n_got)
+            hipLaunchKernelGGL(k_next, grid_for(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(keepb), n_got,
+                               dptr<uint64_t>(P.cand), c);
+        n_cand = d2h_u64(P, c);
+        total += n_got;
+        parts.emplace_back(std::move(keepb), n_got);
+    }
+    ensure(P.closure, std::max<uint64_t>(1, total) * sizeof(keto_tuple));
+    uint64_t o = 0;
+    for (auto &pt : parts) {
+        if (pt.second)
+            KETO_HIP(hipMemcpyAsync(dptr<keto_tuple>(P.closure) + o, pt.first.p, pt.second * sizeof(keto_tuple),
+                                    hipMemcpyDeviceToDevice, P.hs));
+        o += pt.second;
+    }
+    sync(P);
+    st.tuples = total;
+    return total;
+}
+
+double secs(std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+}
+
+}  // namespace
+
+struct PartitionHandle : Partition {};
+
+PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
+                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits) {
+    if (!cfg) throw Error(KETO_E_INVALID, "null config");
+    if (n && !tuples) throw Error(KETO_E_INVALID, "null tuples");
+    if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "a partition holds at most 2^31 - 1 tuples");
+    auto P = std::make_unique<PartitionHandle>();
+    P->device = cfg->device;
+    KETO_HIP(hipSetDevice(P->device));
+    if (coll) {
+        if (coll->world < 1 || (uint32_t)coll->world > MAX_WORLD || coll->rank < 0 || coll->rank >= coll->world)
+            throw Error(KETO_E_INVALID, "collective rank / world out of range");
+        if (coll->world > 1 && (!coll->alltoall_u64 || !coll->alltoallv || !coll->allreduce_max_u64))
+            throw Error(KETO_E_INVALID, "collective callbacks missing");
+        P->have_coll = true;
+        P->coll = *coll;
+        P->rank = (uint32_t)coll->rank;
+        P->world = (uint32_t)coll->world;
+    }
+    if (limits) P->limits = *limits;
+    if (P->limits.max_read_depth < 1 || P->limits.max_read_depth > 65535 || P->limits.max_read_width < 1)
+        throw Error(KETO_E_INVALID, "limits out of range");
+    for (uint32_t i = 0; i < cfg->n_namespaces; i++)
+        P->ns_names.emplace_back(cfg->namespace_names && cfg->namespace_names[i] ? cfg->namespace_names[i] : "");
+    for (uint32_t i = 0; i < cfg->n_relations; i++)
+        P->rel_names.emplace_back(cfg->relation_names && cfg->relation_names[i] ? cfg->relation_names[i] : "");
+    for (auto &s : P->ns_names) P->ns_ptr.push_back(s.c_str());
+    for (auto &s : P->rel_names) P->rel_ptr.push_back(s.c_str());
+    P->json = cfg->namespaces_json ? cfg->namespaces_json : "";
+    P->cfg = *cfg;
+    P->cfg.namespace_names = P->ns_ptr.data();
+    P->cfg.relation_names = P->rel_ptr.data();
+    P->cfg.namespaces_json = P->json.c_str();
+    KETO_HIP(hipStreamCreateWithFlags(&P->hs, hipStreamNonBlocking));
+    if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
+    // the partition, grouped by object key (stable radix sort of (key, index), then a gather)
+    P->n = n;
+    DevBuf raw;
+    const keto_tuple *src = tuples;
+    if (!device_ptrs) {
+        raw = DevBuf(std::max<uint64_t>(1, n) * sizeof(keto_tuple));
+        if (n) KETO_HIP(hipMemcpyAsync(raw.p, tuples, n * sizeof(keto_tuple), hipMemcpyHostToDevice, P->hs));
+        src = static_cast<const keto_tuple *>(raw.p);
+    }
+    Partition &Q = *P;
+    DevBuf k0(std::max<uint64_t>(1, n) * 8), k1(std::max<uint64_t>(1, n) * 8), i0(std::max<uint64_t>(1, n) * 4),
+        i1(std::max<uint64_t>(1, n) * 4);
+    if (n) hipLaunchKernelGGL(k_tuple_keys, grid_for(n), dim3(BLK), 0, Q.hs, src, n, dptr<uint64_t>(k0), dptr<uint32_t>(i0));
+    const int ni = (int)n;
+    uint64_t *kin = dptr<uint64_t>(k0), *kout = dptr<uint64_t>(k1);
+    uint32_t *vin = dptr<uint32_t>(i0), *vout = dptr<uint32_t>(i1);
+    if (n)
+        cub_call(Q, [&](void *tmp, size_t &b) {
+            return hipcub::DeviceRadixSort::SortPairs(tmp, b, kin, kout, vin, vout, ni, 0, 64, Q.hs);
+        });
+    Q.tuples = DevBuf(std::max<uint64_t>(1, n) * sizeof(keto_tuple));
+    if (n) hipLaunchKernelGGL(k_gather_tuples, grid_for(n), dim3(BLK), 0, Q.hs, src, vout, n, dptr<keto_tuple>(Q.tuples));
+    sync(Q);
+    raw.reset();
+    // runs: one entry per object key
+    DevBuf flag(std::max<uint64_t>(1, n + 1) * 4), fpos(std::max<uint64_t>(1, n + 1) * 8);
+    KETO_HIP(hipMemsetAsync(flag.p, 0, (n + 1) * 4, Q.hs));
+    if (n) hipLaunchKernelGGL(k_run_flags, grid_for(n), dim3(BLK), 0, Q.hs, kout, n, dptr<uint32_t>(flag));
+    uint32_t *fl = dptr<uint32_t>(flag);
+    uint64_t *fp = dptr<uint64_t>(fpos);
+    const int nf = (int)(n + 1);
+    cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(tmp, b, fl, fp, nf, Q.hs); });
+    Q.m = d2h_u64(Q, fp + n);
+    Q.ukeys = DevBuf(std::max<uint64_t>(1, Q.m) * 8);
+    Q.beg = DevBuf((Q.m + 1) * 8);
+    if (n)
+        hipLaunchKernelGGL(k_run_starts, grid_for(n), dim3(BLK), 0, Q.hs, kout, fl, fp, n, dptr<uint64_t>(Q.ukeys),
+                           dptr<uint64_t>(Q.beg));
+    KETO_HIP(hipMemcpyAsync(dptr<uint64_t>(Q.beg) + Q.m, &Q.n, 8, hipMemcpyHostToDevice, Q.hs));
+    sync(Q);
+    return P.release();
+}
+
+namespace {
+// the batch's subject ids (kind 0), sorted and unique, into P.cand-independent storage
+uint64_t batch_keys(Partition &P, const keto_query *q, uint64_t n, DevBuf &keys, DevBuf &subj) {
+    DevBuf dq(std::max<uint64_t>(1, n) * sizeof(keto_query));
+    if (n) KETO_HIP(hipMemcpyAsync(dq.p, q, n * sizeof(keto_query), hipMemcpyHostToDevice, P.hs));
+    ensure(keys, std::max<uint64_t>(1, n) * 8);
+    DevBuf raw(std::max<uint64_t>(1, n) * 4), sorted(std::max<uint64_t>(1, n) * 4);
+    ensure(subj, std::max<uint64_t>(1, n) * 4 + 8);
+    ensure(P.ctr, 64);
+    unsigned long long *c = dptr<unsigned long long>(P.ctr);
+    KETO_HIP(hipMemsetAsync(c, 0, 16, P.hs));
+    if (n)
+        hipLaunchKernelGGL(k_query_keys, grid_for(n), dim3(BLK), 0, P.hs, dptr<keto_query>(dq), n, dptr<uint64_t>(keys),
+                           dptr<uint32_t>(raw), c);
+    const uint64_t ns = d2h_u64(P, c);
+    if (!ns) return 0;
+    uint32_t *rin = dptr<uint32_t>(raw), *rout = dptr<uint32_t>(sorted), *uo = dptr<uint32_t>(subj);
+    unsigned long long *nu = c + 1;
+    const int nsi = (int)ns;
+    cub_call(P, [&](void *tmp, size_t &b) { return hipcub::DeviceRadixSort::SortKeys(tmp, b, rin, rout, nsi, 0, 32, P.hs); });
+    cub_call(P, [&](void *tmp, size_t &b) { return hipcub::DeviceSelect::Unique(tmp, b, rout, uo, nu, nsi, P.hs); });
+    return d2h_u64(P, nu);
+}
+
+Snapshot *closure_snapshot(Partition &P, uint64_t n_tuples) {
+    return build_snapshot(&P.cfg, dptr<keto_tuple>(P.closure), n_tuples, true);
+}
+}  // namespace
+
+void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
+    Partition &P = *PH;
+    KETO_HIP(hipSetDevice(P.device));
+    keto_partition_stats st{};
+    st.batches = 1;
+    auto t0 = std::chrono::steady_clock::now();
+    DevBuf keys, subj;
+    const uint64_t n_subj = batch_keys(P, q, n, keys, subj);
+    const uint64_t nt = closure(P, dptr<uint64_t>(keys), n, dptr<uint32_t>(subj), n_subj, true, st);
+    st.closure_s = secs(t0);
+    t0 = std::chrono::steady_clock::now();
+    std::unique_ptr<Snapshot> snap(closure_snapshot(P, nt));
+    st.build_s = secs(t0);
+    t0 = std::chrono::steady_clock::now();
+    const int rc = keto_check_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, q, n, &P.limits, allowed, err,
+                                    flags & (KETO_F_COUNT_WORK | KETO_F_ERR_DETAIL));
+    if (rc != KETO_OK) {
+        char buf[512];
+        keto_last_error(buf, sizeof buf);
+        throw Error(rc, buf);
+    }
+    st.run_s = secs(t0);
+    P.last = st;
+}
+
+uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, uint64_t n) {
+    Partition &P = *PH;
+    KETO_HIP(hipSetDevice(P.device));
+    keto_partition_stats st{};
+    st.batches = 1;
+    auto t0 = std::chrono::steady_clock::now();
+    DevBuf dr(std::max<uint64_t>(1, n) * sizeof(keto_subject_set)), keys(std::max<uint64_t>(1, n) * 8);
+    if (n) KETO_HIP(hipMemcpyAsync(dr.p, roots, n * sizeof(keto_subject_set), hipMemcpyHostToDevice, P.hs));
+    if (n) hipLaunchKernelGGL(k_root_keys, grid_for(n), dim3(BLK), 0, P.hs, dptr<keto_subject_set>(dr), n, dptr<uint64_t>(keys));
+    const uint64_t nt = closure(P, dptr<uint64_t>(keys), n, nullptr, 0, false, st);
+    st.closure_s = secs(t0);
+    t0 = std::chrono::steady_clock::now();
+    std::unique_ptr<Snapshot> snap(closure_snapshot(P, nt));
+    st.build_s = secs(t0);
+    t0 = std::chrono::steady_clock::now();
+    P.xoffs.assign(n + 1, 0);
+    P.xerr.assign(std::max<uint64_t>(1, n), 0);
+    if (P.xnodes.empty()) P.xnodes.resize(1u << 16);
+    for (;;) {
+        const int rc = keto_expand_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, roots, n, &P.limits,
+                                         P.xnodes.data(), P.xnodes.size(), P.xoffs.data(), P.xerr.data());
+        if (rc == KETO_E_CAPACITY) {
+            P.xnodes.resize(P.xoffs[n]);
+            continue;
+        }
+        if (rc != KETO_OK) {
+            char buf[512];
+            keto_last_error(buf, sizeof buf);
+            throw Error(rc, buf);
+        }
+        break;
+    }
+    st.run_s = secs(t0);
+    P.last = st;
+    return P.xoffs[n];
+}
+
+void partition_expand_result(PartitionHandle *PH, keto_tree_node *nodes, uint64_t cap, uint64_t *offsets, int32_t *err) {
+    Partition &P = *PH;
+    const uint64_t n = P.xoffs.empty() ? 0 : P.xoffs.size() - 1;
+    const uint64_t total = n ? P.xoffs[n] : 0;
+    if (!offsets || (n && !err)) throw Error(KETO_E_INVALID, "null buffer");
+    if (total > cap || (total && !nodes)) throw Error(KETO_E_CAPACITY, "expand output needs " + std::to_string(total) + " nodes");
+    std::memcpy(offsets, P.xoffs.data(), (n + 1) * 8);
+    if (n) std::memcpy(err, P.xerr.data(), n * 4);
+    if (total) std::memcpy(nodes, P.xnodes.data(), total * sizeof(keto_tree_node));
+}
+
+void partition_stats(PartitionHandle *PH, keto_partition_stats *out) { *out = PH->last; }
+void partition_free(PartitionHandle *PH) { delete PH; }
+
+}  // namespace keto

@@ -16,7 +16,7 @@ if os.environ.get("KETO_MI355X_ALLOW_OVERRIDE") == "tools" and os.environ.get("K
 
 KETO_OK = 0
 KETO_E_INVALID, KETO_E_DEVICE, KETO_E_CAPACITY, KETO_E_LIMIT = -1, -2, -3, -4
-F_DEVICE_PTRS, F_ASYNC, F_COUNT_WORK = 0x1, 0x2, 0x4
+F_DEVICE_PTRS, F_ASYNC, F_COUNT_WORK, F_ERR_DETAIL = 0x1, 0x2, 0x4, 0x8
 QERR_NONE, QERR_NO_RELATION, QERR_INTERNAL, QERR_NOT_IMPLEMENTED = 0, 1, 2, 3
 
 TUPLE_DT = np.dtype([("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"), ("subj_kind", "<u4"), ("s_obj", "<u4"),
@@ -62,6 +62,20 @@ class DispatcherStats(ctypes.Structure):
                 ("max_batch_seen", ctypes.c_uint64)]
 
 
+class PartitionStats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("levels", ctypes.c_uint64), ("objects", ctypes.c_uint64),
+                ("tuples", ctypes.c_uint64), ("bytes_sent", ctypes.c_uint64), ("closure_s", ctypes.c_double),
+                ("build_s", ctypes.c_double), ("run_s", ctypes.c_double)]
+
+
+# keto_collective callbacks
+ALLTOALL_U64_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                   ctypes.POINTER(ctypes.c_uint64))
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+ALLREDUCE_MAX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
+
 class NameTables(ctypes.Structure):
     _fields_ = [("n_namespaces", ctypes.c_uint32), ("namespace_names", ctypes.POINTER(ctypes.c_char_p)),
                 ("n_relations", ctypes.c_uint32), ("relation_names", ctypes.POINTER(ctypes.c_char_p)),
@@ -101,6 +115,13 @@ SIGNATURES = {
     "keto_dispatcher_expand": (ctypes.c_int, [_VP, _VP, _U64, _VP, _U64, _VP, _VP]),
     "keto_dispatcher_set_snapshot": (ctypes.c_int, [_VP, _VP]),
     "keto_dispatcher_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherStats)]),
+    "keto_partition_create": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, _U32, _VP,
+                                             ctypes.POINTER(Limits), ctypes.POINTER(_VP)]),
+    "keto_partition_check": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP, _U32]),
+    "keto_partition_expand": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),
+    "keto_partition_expand_result": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP]),
+    "keto_partition_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(PartitionStats)]),
+    "keto_partition_free": (ctypes.c_int, [_VP]),
     "keto_trees_to_json": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
     "keto_trees_to_proto": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
 }

@@ -1,51 +1,31 @@
-"""Partitioned graphs: BASELINE config 5 (second half).
+"""Partitioned graphs: BASELINE config 5 (second half) over the C ABI.
 
 A graph too large to replicate is spread over the ranks of a job by object: every tuple of
-`(ns, obj)` lives on rank `keto_object_owner(ns, obj, world)` (include/keto_mi355x.h).  All
-relation slots of an object are therefore on one rank -- its direct rows, the rows its
-computed usersets reach and its tuple-to-userset (`parents`) row.  Crossing to another
-object only ever happens along a subject-set edge.
+`(ns, obj)` lives on rank `keto_object_owner(ns, obj, world)` (include/keto_mi355x.h).  Per
+batch the library (csrc/partition.hip, `keto_partition_*`) gathers the closure of the batch's
+objects from their owners -- one all-to-all pair per depth level, driven by device kernels
+(hash-set dedup, counting-scatter routing, binary-search gathers) -- builds it into a device
+snapshot and runs the unmodified kernels on it; see that file for why the result equals the
+whole graph's.  The collective is the caller's: `collective` is any object with
 
-How a batch runs (each rank checks its own queries):
+    rank, world
+    alltoall_u64(send: np.ndarray[world] uint64) -> np.ndarray[world] uint64
+    alltoallv(send: np.ndarray uint8, send_bytes: list, recv: np.ndarray uint8, recv_bytes: list) -> None
+    allreduce_max_u64(v: int) -> int
 
-1. **Closure exchange.**  The reference reads rows only of objects reachable from the
-   query's object along subject-set edges, and only up to the depth ledger
-   (`check/engine.go:214-249` returns before reading anything at rest depth <= 0; the
-   found-lookahead of `traverser.go:73-80` reads one level further).  So `max_depth + 1`
-   levels of a level-synchronous object BFS collect every tuple any query of the batch can
-   read.  Each level is two RCCL all-to-alls over xGMI: object requests go to their owners,
-   and the owners' tuples for them come back.  Objects already fetched are not asked for
-   again.
-2. **Local snapshot.**  The batch's closure is built into an ordinary device snapshot
-   (`keto_snapshot_build_device`, the same HIP builder as the replicated path).
-3. **Unmodified kernels.**  The Check / Expand kernels run on it.
-
-The closure holds every tuple of every object the reference engine could read for these
-queries, in the same `shard_id` order.  The kernels therefore take exactly the decisions
-(and build exactly the trees) they would take on the whole graph.  Exactness (H0-H6,
-SURVEY.md 8.0) comes for free, with no distributed version of the sequential DFS.
-`tests/test_partition.py` checks this against the oracle over the whole graph, on two gloo
-ranks.
-
-The exchange uses torch.distributed (RCCL on GPUs, gloo in the CPU tests) and torch tensor
-ops for the request routing.  That is plumbing; the data path is the HIP builder and
-kernels.
+(tests/torch_collective.py wraps torch.distributed: gloo in the tests, RCCL in bench.py; a Go
+host wraps its own communicator).  No collective = one rank.  This module imports no torch.
 """
 from __future__ import annotations
 
-import time
+import ctypes
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 from . import _abi
-from .engine import CheckEngine, DeviceBuffer, ExpandEngine, Snapshot, Stream
+from ._abi import check, lib
 
 _MULT = 0x9E3779B97F4A7C15
-_MULT_I64 = _MULT - (1 << 64)   # the same bits as a signed 64-bit multiplier
-W = _abi.TUPLE_DT.itemsize // 4  # int32 words per keto_tuple record
-F_NS, F_OBJ, F_KIND, F_SOBJ, F_SNS = 0, 1, 3, 4, 5
 
 
 def object_owner(ns: np.ndarray, obj: np.ndarray, nparts: int) -> np.ndarray:
@@ -56,199 +36,120 @@ def object_owner(ns: np.ndarray, obj: np.ndarray, nparts: int) -> np.ndarray:
     return ((h >> np.uint64(32)) % np.uint64(nparts)).astype(np.uint32)
 
 
-def _keys(ns: torch.Tensor, obj: torch.Tensor) -> torch.Tensor:
-    """object key (ns << 32 | obj) from int32 columns holding u32 bit patterns"""
-    return ((ns.to(torch.int64) & 0xFFFFFFFF) << 32) | (obj.to(torch.int64) & 0xFFFFFFFF)
+class _CCollective(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
+                ("alltoall_u64", _abi.ALLTOALL_U64_FN), ("alltoallv", _abi.ALLTOALLV_FN),
+                ("allreduce_max_u64", _abi.ALLREDUCE_MAX_FN)]
 
 
-def _owner(keys: torch.Tensor, nparts: int) -> torch.Tensor:
-    return (((keys * _MULT_I64) >> 32) & 0xFFFFFFFF) % nparts
+def _c_collective(coll):
+    """ctypes callbacks over a Python collective object (kept alive by the caller)."""
+    W = int(coll.world)
 
+    def a2a(_ctx, send, recv):
+        try:
+            s = np.ctypeslib.as_array(send, shape=(W,)).copy()
+            np.ctypeslib.as_array(recv, shape=(W,))[:] = coll.alltoall_u64(s)
+            return 0
+        except Exception:  # surfaced to the library as a failed collective
+            return -1
 
-def _as_rows(tuples, device) -> torch.Tensor:
-    if isinstance(tuples, torch.Tensor):
-        return tuples.view(torch.int32).reshape(-1, W).to(device)
-    a = np.ascontiguousarray(tuples, dtype=_abi.TUPLE_DT)
-    return torch.from_numpy(a.view(np.int32).reshape(-1, W)).to(device)
+    def a2av(_ctx, send, send_bytes, recv, recv_bytes):
+        try:
+            sb = [int(x) for x in np.ctypeslib.as_array(send_bytes, shape=(W,))]
+            rb = [int(x) for x in np.ctypeslib.as_array(recv_bytes, shape=(W,))]
+            s = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, sum(sb))).from_address(send or 0)) if sum(sb) \
+                else np.zeros(0, np.uint8)
+            r = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, sum(rb))).from_address(recv or 0)) if sum(rb) \
+                else np.zeros(0, np.uint8)
+            coll.alltoallv(s[:sum(sb)], sb, r[:sum(rb)], rb)
+            return 0
+        except Exception:
+            return -1
 
+    def amax(_ctx, v):
+        try:
+            v[0] = int(coll.allreduce_max_u64(int(v[0])))
+            return 0
+        except Exception:
+            return -1
 
-class ObjectStore:
-    """One rank's partition: its tuple records grouped by object key."""
-
-    def __init__(self, tuples, device):
-        t = _as_rows(tuples, device)
-        keys, perm = torch.sort(_keys(t[:, F_NS], t[:, F_OBJ]), stable=True)
-        self.tuples = t[perm]
-        del t, perm
-        self.keys, self.count = torch.unique_consecutive(keys, return_counts=True)
-        self.begin = torch.cumsum(self.count, 0) - self.count
-        self.device = torch.device(device)
-
-    def __len__(self):
-        return int(self.tuples.shape[0])
-
-    def rows_of(self, req: torch.Tensor):
-        """every tuple of each requested object, in request order; and the count per object"""
-        if len(self.keys) == 0 or len(req) == 0:
-            return self.tuples[:0], torch.zeros(len(req), dtype=torch.int64, device=self.device)
-        idx = torch.searchsorted(self.keys, req).clamp_(max=len(self.keys) - 1)
-        cnt = torch.where(self.keys[idx] == req, self.count[idx], 0)
-        beg = self.begin[idx]
-        total = int(cnt.sum())
-        rep = torch.repeat_interleave(torch.arange(len(req), device=self.device), cnt)
-        start = torch.cumsum(cnt, 0) - cnt
-        pos = beg[rep] + (torch.arange(total, device=self.device) - start[rep])
-        return self.tuples[pos], cnt
-
-
-class _Comm:
-    """all-to-all with variable splits over the job's process group (or none)."""
-
-    def __init__(self, group=None):
-        self.group = group
-        self.on = dist.is_available() and dist.is_initialized()
-        self.world = dist.get_world_size(group) if self.on else 1
-        self.rank = dist.get_rank(group) if self.on else 0
-        self.dev = "cuda" if self.on and dist.get_backend(group) == "nccl" else "cpu"
-        self.bytes_sent = 0
-
-    def a2a(self, x: torch.Tensor, send_counts: torch.Tensor):
-        """x: rows grouped by destination rank, send_counts[r] rows for rank r.  Returns the
-        rows received (grouped by source rank) and the count from each source."""
-        if self.world == 1:
-            return x, send_counts
-        sc = send_counts.to(self.dev)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)
-        sl, rl = sc.tolist(), rc.tolist()
-        xin = x.to(self.dev).contiguous()
-        out = torch.empty((sum(rl),) + tuple(x.shape[1:]), dtype=x.dtype, device=self.dev)
-        dist.all_to_all_single(out, xin, rl, sl, group=self.group)
-        self.bytes_sent += (sum(sl) - sl[self.rank]) * xin[:1].numel() * xin.element_size()
-        return out.to(x.device), rc.to(x.device)
-
-    def any_rank(self, n: int) -> bool:
-        if self.world == 1:
-            return n > 0
-        t = torch.tensor([n], dtype=torch.int64, device=self.dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return int(t.item()) > 0
-
-
-def closure(store: ObjectStore, comm: _Comm, root_keys: torch.Tensor, levels: int):
-    """Every tuple of every object within `levels` subject-set hops of the roots, gathered from
-    the objects' owners (level-synchronous; collective: all ranks call it together).
-    Returns (rows int32[n, W] on the store's device, stats)."""
-    dev = store.device
-    seen = torch.empty(0, dtype=torch.int64, device=dev)
-    front = torch.unique(root_keys.to(dev))
-    parts, st = [], {"levels": 0, "objects": 0, "tuples": 0}
-    for _ in range(levels):
-        if len(seen) and len(front):
-            front = front[~torch.isin(front, seen)]
-        if not comm.any_rank(len(front)):
-            break
-        st["levels"] += 1
-        st["objects"] += len(front)
-        seen = torch.sort(torch.cat([seen, front]))[0]
-        dest = _owner(front, comm.world)
-        order = torch.argsort(dest, stable=True)
-        asked, asked_counts = comm.a2a(front[order], torch.bincount(dest, minlength=comm.world))
-        rows, cnt = store.rows_of(asked)  # this rank's tuples for the objects asked of it
-        src = torch.repeat_interleave(torch.arange(comm.world, device=dev), asked_counts)
-        back = torch.zeros(comm.world, dtype=torch.int64, device=dev).index_add_(0, src, cnt)
-        got, _ = comm.a2a(rows, back)
-        parts.append(got)
-        ss = got[got[:, F_KIND] == 1]
-        front = torch.unique(_keys(ss[:, F_SNS], ss[:, F_SOBJ]))
-    out = torch.cat(parts) if parts else store.tuples[:0]
-    st["tuples"] = int(out.shape[0])
-    return out, st
+    fns = (_abi.ALLTOALL_U64_FN(a2a), _abi.ALLTOALLV_FN(a2av), _abi.ALLREDUCE_MAX_FN(amax))
+    c = _CCollective(None, int(coll.rank), W, *fns)
+    return c, fns
 
 
 class PartitionedEngine:
     """check.Engine / expand.Engine over a graph partitioned by object across the ranks of a
-    job: one rank per GPU, `part_tuples` = this rank's partition (keto_object_owner == rank).
-    Collective: every rank calls check_batch / expand_batch for each batch together."""
+    job: one rank per GPU, `part_tuples` = this rank's partition (keto_object_owner == rank),
+    host TUPLE_DT records or device_tuples=(pointer, count).  Collective: every rank calls
+    check_batch / expand_batch for each batch together."""
 
-    def __init__(self, namespaces, ns_names, rel_names, n_uuids: int, part_tuples, *, strict: bool = False,
-                 device: int = 0, max_read_depth: int = 5, max_read_width: int = 100, group=None,
-                 store_device: str | None = None):
-        self.namespaces, self.ns_names, self.rel_names = namespaces, list(ns_names), list(rel_names)
-        self.n_uuids, self.strict, self.device = n_uuids, strict, device
+    def __init__(self, namespaces, ns_names, rel_names, n_uuids: int, part_tuples=None, *, strict: bool = False,
+                 device: int = 0, max_read_depth: int = 5, max_read_width: int = 100, collective=None,
+                 device_tuples: tuple | None = None):
+        import json
+        if isinstance(namespaces, dict):
+            namespaces = json.dumps(namespaces)
+        self._ns = (ctypes.c_char_p * max(1, len(ns_names)))(*[n.encode() for n in ns_names])
+        self._rel = (ctypes.c_char_p * max(1, len(rel_names)))(*[r.encode() for r in rel_names])
+        self._json = namespaces.encode()
+        cfg = _abi.SnapshotConfig(len(ns_names), self._ns, len(rel_names), self._rel, n_uuids, self._json,
+                                  int(strict), device)
         self.max_read_depth, self.max_read_width = max_read_depth, max_read_width
-        self.comm = _Comm(group)
-        # the exchange runs where the process group's tensors live: on the GPU under RCCL, on
-        # the host under gloo (and for a single rank), where the closure is uploaded through
-        # the library's own allocator
-        if store_device is None:
-            store_device = f"cuda:{device}" if self.comm.dev == "cuda" else "cpu"
-        self.store = ObjectStore(part_tuples, store_device)
-        self.stream = None
+        lim = _abi.Limits(max_read_depth, max_read_width)
+        self._coll = None
+        if collective is not None and int(collective.world) > 1:
+            self._coll = _c_collective(collective)
+        h = ctypes.c_void_p()
+        if device_tuples is not None:
+            ptr, count = device_tuples
+            check(lib().keto_partition_create(ctypes.byref(cfg), ptr, count, _abi.F_DEVICE_PTRS,
+                                              ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
+                                              ctypes.byref(h)))
+        else:
+            t = np.ascontiguousarray(part_tuples, dtype=_abi.TUPLE_DT)
+            check(lib().keto_partition_create(ctypes.byref(cfg), t.ctypes.data if len(t) else None, len(t), 0,
+                                              ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
+                                              ctypes.byref(h)))
+        self.handle = h
         self.last = {}
 
     def levels(self) -> int:
-        # rows are read at rest depth >= 1 (max_read_depth - 1 hops); the found-lookahead
-        # probes one level beyond a row it expands
         return self.max_read_depth + 1
 
-    def closure_tuples(self, ns: np.ndarray, obj: np.ndarray):
-        keys = _keys(torch.from_numpy(np.ascontiguousarray(ns, np.uint32).view(np.int32)),
-                     torch.from_numpy(np.ascontiguousarray(obj, np.uint32).view(np.int32)))
-        return closure(self.store, self.comm, keys, self.levels())
+    def _stats(self):
+        st = _abi.PartitionStats()
+        check(lib().keto_partition_stats_get(self.handle, ctypes.byref(st)))
+        self.last = {k: getattr(st, k) for k, _ in st._fields_}
 
-    def _snapshot(self, rows: torch.Tensor) -> Snapshot:
-        n = int(rows.shape[0])
-        if rows.is_cuda:
-            rows = rows.contiguous()
-            torch.cuda.synchronize(rows.device)  # the builder reads them from its own stream
-            return Snapshot(self.namespaces, None, self.ns_names, self.rel_names, self.n_uuids, strict=self.strict,
-                            device=self.device, device_tuples=(rows.data_ptr(), n))
-        host = np.ascontiguousarray(rows.numpy()).view(_abi.TUPLE_DT).reshape(-1)
-        buf = DeviceBuffer(self.device, max(1, host.nbytes))
-        try:
-            if n:
-                buf.upload(self._stream(), host)
-            return Snapshot(self.namespaces, None, self.ns_names, self.rel_names, self.n_uuids, strict=self.strict,
-                            device=self.device, device_tuples=(buf.ptr, n))
-        finally:
-            buf.free()  # the build has finished reading the records
-
-    def _stream(self) -> Stream:
-        if self.stream is None:
-            self.stream = Stream(self.device)
-        return self.stream
-
-    def check_batch(self, queries: np.ndarray):
+    def check_batch(self, queries: np.ndarray, count_work: bool = False):
         """queries: QUERY_DT (this rank's) -> (allowed u8[n], err i32[n])"""
         q = np.ascontiguousarray(queries, dtype=_abi.QUERY_DT)
-        t0 = time.perf_counter()
-        rows, st = self.closure_tuples(q["ns"], q["obj"])
-        t1 = time.perf_counter()
-        snap = self._snapshot(rows)
-        t2 = time.perf_counter()
-        try:
-            eng = CheckEngine(snap, self._stream(), self.max_read_depth, self.max_read_width)
-            allowed, err = eng.check_batch(q)
-        finally:
-            snap.close()
-        t3 = time.perf_counter()
-        self.last = dict(st, closure_s=t1 - t0, build_s=t2 - t1, check_s=t3 - t2)
-        return allowed, err
+        allowed = np.zeros(len(q), np.uint8)
+        err = np.zeros(max(1, len(q)), np.int32)
+        check(lib().keto_partition_check(self.handle, q.ctypes.data if len(q) else None, len(q), allowed.ctypes.data,
+                                         err.ctypes.data, _abi.F_COUNT_WORK if count_work else 0))
+        self._stats()
+        return allowed, err[:len(q)]
 
     def expand_batch(self, roots: np.ndarray):
         """roots: SUBJSET_DT (this rank's) -> (nodes TREE_DT, offsets u64[n+1], err i32[n])"""
         r = np.ascontiguousarray(roots, dtype=_abi.SUBJSET_DT)
-        rows, st = self.closure_tuples(r["ns"], r["obj"])
-        snap = self._snapshot(rows)
-        try:
-            out = ExpandEngine(snap, self._stream(), self.max_read_depth).build_trees(r)
-        finally:
-            snap.close()
-        self.last = st
-        return out
+        need = ctypes.c_uint64()
+        check(lib().keto_partition_expand(self.handle, r.ctypes.data if len(r) else None, len(r), ctypes.byref(need)))
+        nodes = np.empty(max(1, need.value), dtype=_abi.TREE_DT)
+        offs = np.zeros(len(r) + 1, np.uint64)
+        err = np.zeros(max(1, len(r)), np.int32)
+        check(lib().keto_partition_expand_result(self.handle, nodes.ctypes.data, need.value, offs.ctypes.data,
+                                                 err.ctypes.data))
+        self._stats()
+        return nodes[:need.value], offs, err[:len(r)]
 
     def close(self):
-        if self.stream is not None:
-            self.stream.close()
-            self.stream = None
+        if getattr(self, "handle", None):
+            lib().keto_partition_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()

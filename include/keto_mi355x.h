@@ -258,12 +258,55 @@ int keto_trees_to_proto(const keto_tree_node *nodes, const uint64_t *offsets, ui
 /* Owner of an object in a graph partitioned over nparts GPUs (BASELINE config 5,
  * SURVEY.md 8.1 (e)): every tuple of (ns, obj) lives on one rank, so all relation slots of
  * an object -- its direct rows, computed usersets and tuple-to-userset rows -- are local to
- * one partition.  The loader selects a rank's tuples with it; keto_mi355x/partition.py
- * routes object requests with the same function. */
+ * one partition.  A loader selects a rank's tuples with it; keto_partition_* routes object
+ * requests with the same function. */
 static inline uint32_t keto_object_owner(uint32_t ns, uint32_t obj, uint32_t nparts) {
     const uint64_t h = ((((uint64_t)ns) << 32) | obj) * 0x9E3779B97F4A7C15ull;
     return (uint32_t)((h >> 32) % nparts);
 }
+
+/* Graphs larger than one GPU: the job's ranks each hold the tuples they own
+ * (keto_object_owner) and evaluate their own queries together.  Per batch the library runs a
+ * level-synchronous closure exchange (object requests to their owners, their tuples back, one
+ * all-to-all pair per depth level, max_read_depth + 1 levels), builds the closure into a device
+ * snapshot and runs the Check / Expand kernels on it: the decisions and trees of the whole
+ * graph.  There is no reference counterpart (Keto never partitions).
+ *
+ * The exchange goes through the caller's collective, host buffers only, every rank calling in
+ * the same order (a Go host wraps its RCCL communicator; the tests wrap gloo): */
+typedef struct keto_collective {
+    void *ctx;
+    int32_t rank, world;
+    /* send[r] -> rank r; recv[r] <- rank r (one value per rank) */
+    int (*alltoall_u64)(void *ctx, const uint64_t *send, uint64_t *recv);
+    /* send: the bytes for rank 0, 1, ... back to back (send_bytes[r] each); recv likewise,
+     * recv_bytes[r] from rank r (announced by the preceding alltoall_u64) */
+    int (*alltoallv)(void *ctx, const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes);
+    /* *value <- max over ranks */
+    int (*allreduce_max_u64)(void *ctx, uint64_t *value);
+} keto_collective;
+typedef struct keto_partition_stats {
+    uint64_t batches, levels, objects, tuples, bytes_sent;
+    double closure_s, build_s, run_s;
+} keto_partition_stats;
+typedef struct keto_partition keto_partition;
+/* tuples: this rank's partition (host, or device memory of cfg->device with
+ * KETO_F_DEVICE_PTRS); coll NULL = one rank, no exchange.  The collective is kept by value. */
+int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
+                          const keto_collective *coll, const keto_limits *limits, keto_partition **out);
+/* collective: this rank's queries (host) -> decisions, as keto_check_batch (flags: COUNT_WORK,
+ * ERR_DETAIL).  Check closures ship subject-set tuples plus only the subject-id tuples that
+ * name one of the batch's subjects: no other subject-id tuple is ever read by these queries. */
+int keto_partition_check(keto_partition *p, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
+                         int32_t *out_err, uint32_t flags);
+/* collective: expands this rank's roots; *out_nodes_needed = nodes of all the trees.  Then
+ * (local, no collective) keto_partition_expand_result copies them out, as keto_expand_batch. */
+int keto_partition_expand(keto_partition *p, const keto_subject_set *roots, uint64_t n, uint64_t *out_nodes_needed);
+int keto_partition_expand_result(keto_partition *p, keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets,
+                                 int32_t *out_err);
+/* the last batch's closure and phase times */
+int keto_partition_stats_get(keto_partition *p, keto_partition_stats *out);
+int keto_partition_free(keto_partition *p);
 
 /* device memory helpers (for callers without their own allocator) */
 int keto_device_alloc(int32_t device, uint64_t bytes, void **out);

@@ -1,6 +1,7 @@
-"""Config-5 partitioned path on the GPU: closure exchange -> device snapshot build -> the
-unmodified Check / Expand kernels, against the oracle over the whole graph (bit-exact), on
-one rank and on two gloo ranks sharing the box's GPU."""
+"""Config-5 partitioned path on the GPU through the C ABI (keto_partition_*): device closure
+exchange -> device snapshot build -> the unmodified Check / Expand kernels, against the oracle
+over the whole graph (bit-exact), on one rank and on two gloo ranks sharing the box's GPU.
+The device closure has exactly the size of the numpy restatement's (tests/closure_ref.py)."""
 import os
 import socket
 import sys
@@ -12,6 +13,7 @@ import torch.multiprocessing as mp
 
 import keto_mi355x as km
 import refsem
+from closure_ref import closure
 from keto_mi355x import partition, synth
 from product_helpers import queries_to_oracle, world_from_workload
 
@@ -34,6 +36,13 @@ def _roots(wl, rng, n):
     return r
 
 
+def _oracle(wl):
+    w, _ = world_from_workload(wl, with_tuples=False)
+    orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    return orc
+
+
 def test_single_rank_partitioned_matches_oracle():
     wl = _wl()
     q = synth.drive_queries(wl, 20_000, seed=31)
@@ -41,15 +50,21 @@ def test_single_rank_partitioned_matches_oracle():
     eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, wl.tuples,
                                       max_read_depth=wl.max_depth, max_read_width=wl.max_width)
     allowed, err = eng.check_batch(q)
+    ref = closure(wl.tuples, q["ns"], q["obj"], wl.max_depth + 1, subjects=q["s_obj"][q["subj_kind"] == 0])
+    assert eng.last["tuples"] == len(ref)
     assert 0 < eng.last["tuples"] < len(wl.tuples)
-    w, t = world_from_workload(wl)
-    orc = refsem.Oracle(w, t)
-    orc.set_limits(wl.max_depth, wl.max_width)
+    orc = _oracle(wl)
     dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=8)
     np.testing.assert_array_equal(err, oerr)
     np.testing.assert_array_equal(allowed, dec)
+    # a second batch on the same engine (workspace reuse)
+    q2 = synth.drive_queries(wl, 5000, seed=32)
+    a2, e2 = eng.check_batch(q2)
+    d2, _, _ = orc.check_batch(queries_to_oracle(q2), threads=8)
+    np.testing.assert_array_equal(a2, d2)
     roots = _roots(wl, np.random.default_rng(1), 256)
     nodes, offs, xerr = eng.expand_batch(roots)
+    assert eng.last["tuples"] == len(closure(wl.tuples, roots["ns"], roots["obj"], wl.max_depth + 1))
     assert (xerr == 0).all()
     for i, r in enumerate(roots):
         on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), wl.max_depth)
@@ -76,17 +91,25 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from torch_collective import TorchCollective
         wl = _wl()
         eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids,
                                           synth.drive_partition(wl, world, rank), max_read_depth=wl.max_depth,
-                                          max_read_width=wl.max_width)
+                                          max_read_width=wl.max_width, collective=TorchCollective())
         q = synth.drive_queries(wl, 8192, seed=40 + rank)
         allowed, err = eng.check_batch(q)
-        w, t = world_from_workload(wl)
-        orc = refsem.Oracle(w, t)
-        orc.set_limits(wl.max_depth, wl.max_width)
+        st = dict(eng.last)
+        orc = _oracle(wl)
         dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=4)
-        out[rank] = (int((allowed != dec).sum()), int((err != oerr).sum()), int(dec.sum()), eng.comm.bytes_sent)
+        roots = _roots(wl, np.random.default_rng(rank), 64)
+        nodes, offs, xerr = eng.expand_batch(roots)
+        tree_mis = 0
+        for i, r in enumerate(roots):
+            on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), wl.max_depth)
+            mine = nodes[int(offs[i]):int(offs[i + 1])]
+            tree_mis += len(mine) != len(on) or not (mine["s_obj"] == on["sid"]).all()
+        out[rank] = (int((allowed != dec).sum()), int((err != oerr).sum()), int(dec.sum()), st["bytes_sent"],
+                     tree_mis, int((xerr != 0).sum()))
         eng.close()
     finally:
         dist.destroy_process_group()
@@ -99,6 +122,6 @@ def test_two_rank_partitioned_matches_oracle():
         mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
         res = dict(out)
     for r in range(world):
-        dmis, emis, n_allowed, sent = res[r]
-        assert dmis == 0 and emis == 0
+        dmis, emis, n_allowed, sent, tree_mis, xerr = res[r]
+        assert dmis == 0 and emis == 0 and tree_mis == 0 and xerr == 0
         assert n_allowed > 0 and sent > 0

@@ -135,12 +135,14 @@ def test_c5_partitioned_one_rank(c4):
     wl, orc = c4
     t0 = time.perf_counter()
     eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, wl.tuples,
-                                      max_read_depth=wl.max_depth, max_read_width=wl.max_width,
-                                      store_device="cuda:0")
+                                      max_read_depth=wl.max_depth, max_read_width=wl.max_width)
     _log(f"C5 object store: {time.perf_counter() - t0:.1f} s")
     q = _batch(wl, 25)
     a, e = eng.check_batch(q)
     _log(f"C5 batch: {eng.last}")
+    a2, e2 = eng.check_batch(q)  # the second batch reuses the workspace: same answers
+    np.testing.assert_array_equal(a, a2)
+    _log(f"C5 batch 2: {eng.last}")
     assert 0 < eng.last["tuples"] < len(wl.tuples)
     idx = _sample(25)
     dec, err, _ = orc.check_batch(q[idx].view(refsem.QUERY_DT), threads=16)

@@ -1,14 +1,15 @@
-"""Config-5 partitioned path (keto_mi355x/partition.py) on the CPU: the object partition, the
-closure exchange over two gloo ranks, and the claim that makes it exact.  The claim is that
-the oracle over a batch's closure decides every query of the batch (and builds every Expand
-tree) exactly as the oracle over the whole graph does."""
+"""Config-5 partitioned path on the CPU: the object partition, the claim that makes the
+closure exchange exact -- the oracle over a batch's closure (tests/closure_ref.py, the numpy
+restatement of csrc/partition.hip) decides every query of the batch, and builds every Expand
+tree, exactly as the oracle over the whole graph; with the Check filter that ships only the
+batch's own subject ids -- and the keto_collective adapter over two gloo ranks."""
+import ctypes
 import os
 import socket
 import sys
 
 import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -18,7 +19,10 @@ for p in (ROOT, os.path.join(ROOT, "djy-keto_amd"), os.path.join(ROOT, "oracle")
         sys.path.insert(0, p)
 
 import keto_mi355x as km  # noqa: E402
+import refsem  # noqa: E402
+from closure_ref import closure  # noqa: E402
 from keto_mi355x import partition, synth  # noqa: E402
+from product_helpers import queries_to_oracle, world_from_workload  # noqa: E402
 
 
 def _small_drive(seed=4):
@@ -30,19 +34,19 @@ def _rows_sorted(t):
     return np.sort(np.ascontiguousarray(t).view(np.uint8).reshape(len(t), -1).view("V48").reshape(-1))
 
 
-def test_owner_numpy_and_torch_agree():
+def test_owner_matches_the_header_function():
+    # a fixed value, so the C inline function in the header and this mirror cannot drift apart
+    assert int(partition.object_owner(np.array([3], np.uint32), np.array([12345], np.uint32), 8)[0]) == \
+        (((((3 << 32) | 12345) * 0x9E3779B97F4A7C15) % (1 << 64)) >> 32) % 8
     rng = np.random.default_rng(1)
     ns = rng.integers(0, 64, 5000).astype(np.uint32)
     obj = rng.integers(0, 2**32, 5000, dtype=np.uint64).astype(np.uint32)
     for n in (1, 2, 3, 8):
         a = partition.object_owner(ns, obj, n)
-        k = partition._keys(torch.from_numpy(ns.view(np.int32)), torch.from_numpy(obj.view(np.int32)))
-        b = partition._owner(k, n).numpy()
-        np.testing.assert_array_equal(a, b)
+        b = np.array([(((((int(x) << 32) | int(y)) * 0x9E3779B97F4A7C15) % (1 << 64)) >> 32) % n
+                      for x, y in zip(ns[:200], obj[:200])])
+        np.testing.assert_array_equal(a[:200], b)
         assert a.max() < n
-    # a fixed value, so the C inline function in the header and this mirror cannot drift apart
-    assert int(partition.object_owner(np.array([3], np.uint32), np.array([12345], np.uint32), 8)[0]) == \
-        (((((3 << 32) | 12345) * 0x9E3779B97F4A7C15) % (1 << 64)) >> 32) % 8
 
 
 def test_partitions_cover_the_graph_exactly():
@@ -54,18 +58,43 @@ def test_partitions_cover_the_graph_exactly():
     np.testing.assert_array_equal(_rows_sorted(np.concatenate(parts)), _rows_sorted(w.tuples))
 
 
-def test_object_store_rows_of():
-    w = _small_drive()
-    st = partition.ObjectStore(w.tuples, "cpu")
-    objs = np.unique(w.tuples[["ns", "obj"]])[:50]
-    req = partition._keys(torch.from_numpy(objs["ns"].astype(np.uint32).view(np.int32)),
-                          torch.from_numpy(objs["obj"].astype(np.uint32).view(np.int32)))
-    req = torch.cat([req, torch.tensor([(7 << 32) | 99], dtype=torch.int64)])  # absent object
-    rows, cnt = st.rows_of(req)
-    assert int(cnt[-1]) == 0
-    want = w.tuples[np.isin(w.tuples[["ns", "obj"]], objs)]
-    assert int(cnt.sum()) == len(want)
-    np.testing.assert_array_equal(_rows_sorted(rows.numpy().view(synth.TUPLE_DT).reshape(-1)), _rows_sorted(want))
+@pytest.mark.parametrize("depth", [2, 3, 16])
+def test_closure_decides_like_the_whole_graph(depth):
+    """the exactness claim, Check (with the subject filter) and Expand; fewer levels than
+    max_read_depth + 1 do produce mismatches, so the comparison is not vacuous"""
+    wl = _small_drive()
+    q = synth.drive_queries(wl, 3000, seed=20)
+    q["max_depth"][:500] = np.random.default_rng(0).integers(1, 6, 500)
+    w, _ = world_from_workload(wl, with_tuples=False)
+    full = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+    full.set_limits(depth, wl.max_width)
+    d0, e0, _ = full.check_batch(queries_to_oracle(q), threads=4)
+    subj = q["s_obj"][q["subj_kind"] == 0]
+    rows = closure(wl.tuples, q["ns"], q["obj"], depth + 1, subjects=subj)
+    assert len(rows) < len(wl.tuples)
+    sub = refsem.Oracle(w, rows.view(refsem.TUPLE_DT), shard_bytes=True)
+    sub.set_limits(depth, wl.max_width)
+    d1, e1, _ = sub.check_batch(queries_to_oracle(q), threads=4)
+    np.testing.assert_array_equal(d0, d1)
+    np.testing.assert_array_equal(e0, e1)
+    if depth == 16:  # one level short: the found-lookahead beyond the last row is missing
+        short = refsem.Oracle(w, closure(wl.tuples, q["ns"], q["obj"], 3, subjects=subj).view(refsem.TUPLE_DT),
+                              shard_bytes=True)
+        short.set_limits(depth, wl.max_width)
+        assert (short.check_batch(queries_to_oracle(q), threads=4)[0] != d0).any()
+    rng = np.random.default_rng(5)
+    roots = np.zeros(100, dtype=km.SUBJSET_DT)
+    roots["ns"][:50], roots["rel"][:50] = 1, wl.rel_names.index("members")
+    roots["obj"][:50] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], 50)
+    roots["ns"][50:], roots["rel"][50:] = 2, wl.rel_names.index("viewers")
+    roots["obj"][50:] = rng.integers(0, wl.meta["folders_per_root"], 50)
+    xrows = closure(wl.tuples, roots["ns"], roots["obj"], depth + 1)
+    xsub = refsem.Oracle(w, xrows.view(refsem.TUPLE_DT), shard_bytes=True)
+    xsub.set_limits(depth, wl.max_width)
+    for r in roots:
+        a, _ = full.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), depth)
+        b, _ = xsub.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), depth)
+        assert a.tobytes() == b.tobytes()  # pre-order node arrays, child order included
 
 
 def _free_port():
@@ -80,57 +109,42 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        import refsem
-        from product_helpers import queries_to_oracle, world_from_workload
-
-        wl = _small_drive()
-        eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids,
-                                          synth.drive_partition(wl, world, rank), store_device="cpu")
-        q = synth.drive_queries(wl, 3000, seed=20 + rank)
-        rng = np.random.default_rng(rank)
-        q["max_depth"][:500] = rng.integers(1, 6, 500)  # request depths below the global one
-        roots = np.zeros(200, dtype=km.SUBJSET_DT)
-        roots["ns"][:100], roots["rel"][:100] = 1, wl.rel_names.index("members")
-        roots["obj"][:100] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], 100)
-        roots["ns"][100:], roots["rel"][100:] = 2, wl.rel_names.index("viewers")
-        roots["obj"][100:] = rng.integers(0, wl.meta["folders_per_root"], 100)
-        w, t_full = world_from_workload(wl)
-        full = refsem.Oracle(w, t_full)
-        res = {}
-        for depth in (2, 3, 16):
-            eng.max_read_depth = depth
-            full.set_limits(depth, wl.max_width)
-            rows, st = eng.closure_tuples(q["ns"], q["obj"])
-            sub = refsem.Oracle(w, rows.numpy().copy().view(refsem.TUPLE_DT).reshape(-1), shard_bytes=True)
-            sub.set_limits(depth, wl.max_width)
-            d0, e0, _ = full.check_batch(queries_to_oracle(q), threads=2)
-            d1, e1, _ = sub.check_batch(queries_to_oracle(q), threads=2)
-            xrows, _ = eng.closure_tuples(roots["ns"], roots["obj"])
-            xsub = refsem.Oracle(w, xrows.numpy().copy().view(refsem.TUPLE_DT).reshape(-1), shard_bytes=True)
-            xsub.set_limits(depth, wl.max_width)
-            tree_diff = 0
-            for r in roots:
-                a, _ = full.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), depth)
-                b, _ = xsub.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), depth)
-                tree_diff += a.tobytes() != b.tobytes()  # pre-order node arrays, child order included
-            res[depth] = (int((d0 != d1).sum()), int((e0 != e1).sum()), int(d0.sum()), st["tuples"], st["levels"],
-                          tree_diff)
-        out[rank] = (res, len(wl.tuples), eng.comm.bytes_sent)
+        from torch_collective import TorchCollective
+        coll = TorchCollective()
+        # the adapter itself
+        got = coll.alltoall_u64(np.array([10 * rank + r for r in range(world)], np.uint64))
+        send_bytes = [r + 1 + rank for r in range(world)]
+        send = np.concatenate([np.full(b, 16 * rank + r, np.uint8) for r, b in enumerate(send_bytes)])
+        recv_bytes = [r + 1 + rank for r in range(world)]  # rank r sent rank+1+r bytes to me
+        recv_bytes = [rank + 1 + r for r in range(world)]
+        recv = np.zeros(sum(recv_bytes), np.uint8)
+        coll.alltoallv(send, send_bytes, recv, recv_bytes)
+        mx = coll.allreduce_max_u64(100 + rank)
+        # and through the C callbacks the library calls
+        c, fns = partition._c_collective(coll)
+        a = (ctypes.c_uint64 * world)(*[7 * rank + r for r in range(world)])
+        b = (ctypes.c_uint64 * world)()
+        rc1 = c.alltoall_u64(None, a, b)
+        v = (ctypes.c_uint64 * 1)(5 + rank)
+        rc2 = c.allreduce_max_u64(None, v)
+        out[rank] = (got.tolist(), recv.tolist(), recv_bytes, mx, rc1, list(b), rc2, v[0])
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_closure_decides_like_the_whole_graph():
+def test_collective_adapter_two_gloo_ranks():
     world = 2
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
         res = dict(out)
     for rank in range(world):
-        per_depth, n_total, sent = res[rank]
-        assert sent > 0  # the other rank's objects really came over the exchange
-        for depth, (dmis, emis, n_allowed, n_closure, levels, tree_diff) in per_depth.items():
-            assert dmis == 0 and emis == 0 and tree_diff == 0, (rank, depth)
-            assert 0 < n_allowed < 3000
-            assert 0 < n_closure < n_total
-            assert levels <= depth + 1
+        got, recv, recv_bytes, mx, rc1, b, rc2, v = res[rank]
+        assert got == [10 * r + rank for r in range(world)]
+        want = []
+        for r in range(world):
+            want += [16 * r + rank] * recv_bytes[r]
+        assert recv == want
+        assert mx == 100 + world - 1
+        assert rc1 == 0 and b == [7 * r + rank for r in range(world)]
+        assert rc2 == 0 and v == 5 + world - 1

@@ -1,0 +1,15 @@
+// TEST/DEBUG TOOL ONLY: the CPU emulation build has no hipCUB, so keto_partition_* (csrc/partition.hip)
+// is not emulated; its entry points fail loudly here.
+#include "../../djy-keto_amd/csrc/engine.hpp"
+
+namespace keto {
+struct PartitionHandle {};
+[[noreturn]] static void unavailable() { throw Error(KETO_E_DEVICE, "keto_partition_* is not part of the CPU emulation"); }
+PartitionHandle *partition_create(const keto_snapshot_config *, const keto_tuple *, uint64_t, bool, const keto_collective *,
+                                  const keto_limits *) { unavailable(); }
+void partition_check(PartitionHandle *, const keto_query *, uint64_t, uint8_t *, int32_t *, uint32_t) { unavailable(); }
+uint64_t partition_expand(PartitionHandle *, const keto_subject_set *, uint64_t) { unavailable(); }
+void partition_expand_result(PartitionHandle *, keto_tree_node *, uint64_t, uint64_t *, int32_t *) { unavailable(); }
+void partition_stats(PartitionHandle *, keto_partition_stats *) { unavailable(); }
+void partition_free(PartitionHandle *) {}
+}  // namespace keto
