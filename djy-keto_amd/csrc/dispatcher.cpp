@@ -81,7 +81,7 @@ struct Slot {
 struct Dispatcher {
     keto_snapshot *snap = nullptr;
     keto_limits limits{5, 100};
-    uint32_t max_batch = 1u << 16, max_wait_us = 0;
+    uint32_t max_batch = 1u << 16, max_wait_us = 0, flags = 0;
     int device = 0;
     std::mutex m;                // queues, stats, snapshot pointer and its users
     std::condition_variable cv_in;
@@ -101,7 +101,8 @@ int Slot::launch(keto_snapshot *snap, uint64_t n, std::string &msg) {
     try {
         KETO_HIP(hipMemcpyAsync(dq, hq, n * sizeof(keto_query), hipMemcpyHostToDevice, hs));
         rc = keto_check_batch(snap, stream, static_cast<const keto_query *>(dq), n, &d->limits,
-                              static_cast<uint8_t *>(da), static_cast<int32_t *>(de), KETO_F_DEVICE_PTRS | KETO_F_ASYNC);
+                              static_cast<uint8_t *>(da), static_cast<int32_t *>(de),
+                              KETO_F_DEVICE_PTRS | KETO_F_ASYNC | d->flags);
         if (rc == KETO_OK) {
             KETO_HIP(hipMemcpyAsync(ha, da, n, hipMemcpyDeviceToHost, hs));
             KETO_HIP(hipMemcpyAsync(he, de, n * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
@@ -224,7 +225,7 @@ void Slot::run() {
             rc = launch(snap, n, msg);
         } else {  // a single request larger than the staging: the host-pointer path
             Request *r = take[0];
-            rc = keto_check_batch(snap, stream, r->q, r->n, &d->limits, r->allowed, r->err, 0);
+            rc = keto_check_batch(snap, stream, r->q, r->n, &d->limits, r->allowed, r->err, d->flags);
             if (rc != KETO_OK) {
                 char buf[512];
                 keto_last_error(buf, sizeof(buf));
@@ -290,6 +291,7 @@ void dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, k
     d->limits = l;
     d->max_batch = cfg->max_batch;
     d->max_wait_us = cfg->max_wait_us;
+    d->flags = cfg->flags & KETO_F_ERR_DETAIL;
     d->device = reinterpret_cast<Snapshot *>(snap)->device;
     try {
         KETO_HIP(hipSetDevice(d->device));

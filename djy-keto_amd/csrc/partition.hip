@@ -131,11 +131,25 @@ __global__ __launch_bounds__(BLK) void k_dest_scatter(const uint64_t *keys, uint
                                                        unsigned long long *cursor, uint64_t *out) {
     for (uint64_t i = gid(); i < n; i += gstride()) out[atomicAdd(&cursor[owner_of(keys[i], world)], 1ull)] = keys[i];
 }
+// object-key index of the partition: open addressing, {key lo, key hi, run, 0} per slot
+__global__ __launch_bounds__(BLK) void k_index_fill(const uint64_t *ukeys, uint64_t m, uint4 *slots, uint64_t mask) {
+    for (uint64_t r = gid(); r < m; r += gstride()) {
+        const uint64_t k = ukeys[r];
+        uint64_t h = mix64(k + 1) & mask;
+        // claim a slot by its run word (NONE32 = empty), then publish the key
+        while (atomicCAS(&slots[h].z, NONE32, (uint32_t)r) != NONE32) h = (h + 1) & mask;
+        slots[h].x = (uint32_t)k;
+        slots[h].y = (uint32_t)(k >> 32);
+    }
+}
+
 // owner side: tuples to ship for each requested key (all of them for Expand; subject sets plus
 // subject ids in the requester's subject list for Check)
 struct Lookup {
     const uint64_t *ukeys, *beg;  // partition runs: ukeys[m], beg[m+1]
     uint64_t m;
+    const uint4 *index;           // k_index_fill table
+    uint64_t index_mask;
     const keto_tuple *tuples;
     const uint64_t *req;          // requested keys, grouped by source rank
     const uint64_t *req_off;      // [world+1] request offsets per source
@@ -145,16 +159,17 @@ struct Lookup {
     int filter;
 };
 __device__ __forceinline__ bool run_of(const Lookup &L, uint64_t key, uint64_t &b, uint64_t &e) {
-    uint64_t lo = 0, hi = L.m;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (L.ukeys[mid] < key) lo = mid + 1;
-        else hi = mid;
+    uint64_t h = mix64(key + 1) & L.index_mask;
+    for (;;) {  // one 16-byte probe per step; the table is at most half full
+        const uint4 sl = L.index[h];
+        if (sl.z == NONE32) return false;
+        if (sl.x == (uint32_t)key && sl.y == (uint32_t)(key >> 32)) {
+            b = L.beg[sl.z];
+            e = L.beg[sl.z + 1];
+            return true;
+        }
+        h = (h + 1) & L.index_mask;
     }
-    if (lo >= L.m || L.ukeys[lo] != key) return false;
-    b = L.beg[lo];
-    e = L.beg[lo + 1];
-    return true;
 }
 __device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
     uint32_t lo = 0, hi = L.world;  // last source whose offset <= i
@@ -224,8 +239,8 @@ struct Partition {
     std::string json;
     keto_snapshot_config cfg{};
     // this rank's partition, sorted by object key: tuples[n], run keys ukeys[m], beg[m+1]
-    DevBuf tuples, ukeys, beg;
-    uint64_t n = 0, m = 0;
+    DevBuf tuples, ukeys, beg, index;
+    uint64_t n = 0, m = 0, index_mask = 0;
     hipStream_t hs = nullptr;
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
@@ -300,6 +315,15 @@ std::vector<uint64_t> exchange(Partition &P, const void *src, const std::vector<
     return recv_cnt;
 }
 
+// grow the closure buffer keeping its content (capacity doubles: few copies per batch)
+void reserve_closure(Partition &P, uint64_t keep, uint64_t n) {
+    const size_t need = std::max<uint64_t>(1, n) * sizeof(keto_tuple);
+    if (P.closure.p && P.closure.bytes >= need) return;
+    DevBuf b(std::max<size_t>(need * 2, 64u << 20));
+    if (keep) KETO_HIP(hipMemcpyAsync(b.p, P.closure.p, keep * sizeof(keto_tuple), hipMemcpyDeviceToDevice, P.hs));
+    P.closure = std::move(b);
+}
+
 void ensure_table(Partition &P, uint64_t add) {
     uint64_t cap = P.table_mask + 1;
     if (P.table.p && 2 * (P.n_seen + add) <= cap) return;
@@ -341,7 +365,6 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
     ensure(P.cand, std::max<uint64_t>(1, n_keys) * 8);
     KETO_HIP(hipMemcpyAsync(P.cand.p, keys, n_keys * 8, hipMemcpyDeviceToDevice, P.hs));
     uint64_t n_cand = n_keys, total = 0;
-    std::vector<std::pair<DevBuf, uint64_t>> parts;
     const int levels = P.limits.max_read_depth + 1;
     for (int level = 0; level < levels; level++) {
         // new objects of this level: never asked for before (seen-set insert)
@@ -393,7 +416,8 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         // owner side: count, scan, fill
         ensure(P.req_off, (W + 1) * 8);
         KETO_HIP(hipMemcpyAsync(P.req_off.p, roff.data(), (W + 1) * 8, hipMemcpyHostToDevice, P.hs));
-        Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<keto_tuple>(P.tuples),
+        Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
+                 dptr<keto_tuple>(P.tuples),
                  dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<uint32_t>(P.subj), dptr<uint64_t>(P.subj_off),
                  W, filter ? 1 : 0};
         ensure(P.cnt, (n_req + 1) * 8);
@@ -411,34 +435,35 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             KETO_HIP(hipMemcpyAsync(&pb[r], posp + roff[r], 8, hipMemcpyDeviceToHost, P.hs));
         sync(P);
         const uint64_t n_out = pb[W];
-        ensure(P.out, std::max<uint64_t>(1, n_out) * sizeof(keto_tuple));
-        if (n_req)
-            hipLaunchKernelGGL(k_lookup_fill, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, posp,
-                               dptr<keto_tuple>(P.out));
-        std::vector<uint64_t> back(W);
-        for (uint32_t r = 0; r < W; r++) back[r] = pb[r + 1] - pb[r];
-        std::vector<uint64_t> recv = exchange(P, P.out.p, back, sizeof(keto_tuple), P.got, st.bytes_sent);
         uint64_t n_got = 0;
-        for (uint64_t v : recv) n_got += v;
-        // keep them; next frontier = their subject sets
-        DevBuf keepb(std::max<uint64_t>(1, n_got) * sizeof(keto_tuple));
-        if (n_got) KETO_HIP(hipMemcpyAsync(keepb.p, P.got.p, n_got * sizeof(keto_tuple), hipMemcpyDeviceToDevice, P.hs));
+        if (W == 1) {  // one rank: the owner's gather lands in the closure directly
+            reserve_closure(P, total, total + n_out);
+            if (n_req)
+                hipLaunchKernelGGL(k_lookup_fill, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, posp,
+                                   dptr<keto_tuple>(P.closure) + total);
+            n_got = n_out;
+        } else {
+            ensure(P.out, std::max<uint64_t>(1, n_out) * sizeof(keto_tuple));
+            if (n_req)
+                hipLaunchKernelGGL(k_lookup_fill, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, posp,
+                                   dptr<keto_tuple>(P.out));
+            std::vector<uint64_t> back(W);
+            for (uint32_t r = 0; r < W; r++) back[r] = pb[r + 1] - pb[r];
+            std::vector<uint64_t> recv = exchange(P, P.out.p, back, sizeof(keto_tuple), P.got, st.bytes_sent);
+            for (uint64_t v : recv) n_got += v;
+            reserve_closure(P, total, total + n_got);
+            if (n_got)
+                KETO_HIP(hipMemcpyAsync(dptr<keto_tuple>(P.closure) + total, P.got.p, n_got * sizeof(keto_tuple),
+                                        hipMemcpyDeviceToDevice, P.hs));
+        }
+        // next frontier: the subject sets of the tuples received
         ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
         KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
         if (n_got)
-            hipLaunchKernelGGL(k_next, grid_for(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(keepb), n_got,
+            hipLaunchKernelGGL(k_next, grid_for(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total, n_got,
                                dptr<uint64_t>(P.cand), c);
         n_cand = d2h_u64(P, c);
         total += n_got;
-        parts.emplace_back(std::move(keepb), n_got);
-    }
-    ensure(P.closure, std::max<uint64_t>(1, total) * sizeof(keto_tuple));
-    uint64_t o = 0;
-    for (auto &pt : parts) {
-        if (pt.second)
-            KETO_HIP(hipMemcpyAsync(dptr<keto_tuple>(P.closure) + o, pt.first.p, pt.second * sizeof(keto_tuple),
-                                    hipMemcpyDeviceToDevice, P.hs));
-        o += pt.second;
     }
     sync(P);
     st.tuples = total;
@@ -526,6 +551,14 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
         hipLaunchKernelGGL(k_run_starts, grid_for(n), dim3(BLK), 0, Q.hs, kout, fl, fp, n, dptr<uint64_t>(Q.ukeys),
                            dptr<uint64_t>(Q.beg));
     KETO_HIP(hipMemcpyAsync(dptr<uint64_t>(Q.beg) + Q.m, &Q.n, 8, hipMemcpyHostToDevice, Q.hs));
+    uint64_t cap = 1u << 10;
+    while (cap < 2 * Q.m) cap *= 2;
+    Q.index = DevBuf(cap * 16);
+    Q.index_mask = cap - 1;
+    KETO_HIP(hipMemsetAsync(Q.index.p, 0xFF, cap * 16, Q.hs));
+    if (Q.m)
+        hipLaunchKernelGGL(k_index_fill, grid_for(Q.m), dim3(BLK), 0, Q.hs, dptr<uint64_t>(Q.ukeys), Q.m,
+                           dptr<uint4>(Q.index), Q.index_mask);
     sync(Q);
     return P.release();
 }

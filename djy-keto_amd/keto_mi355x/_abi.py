@@ -54,7 +54,7 @@ class WorkCounters(ctypes.Structure):
 
 class DispatcherConfig(ctypes.Structure):
     _fields_ = [("limits", Limits), ("max_batch", ctypes.c_uint32), ("max_wait_us", ctypes.c_uint32),
-                ("inflight", ctypes.c_uint32)]
+                ("inflight", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
 class DispatcherStats(ctypes.Structure):

@@ -202,12 +202,13 @@ class CheckEngine:
         self.stream = stream or Stream(snapshot.device)
         self.limits = _abi.Limits(max_read_depth, max_read_width)
 
-    def check_batch(self, queries: np.ndarray, count_work: bool = False):
-        """queries: QUERY_DT array (host).  Returns (allowed uint8[n], err int32[n])."""
+    def check_batch(self, queries: np.ndarray, count_work: bool = False, err_detail: bool = False):
+        """queries: QUERY_DT array (host).  Returns (allowed uint8[n], err int32[n]); with
+        err_detail, err = 1 | relation-name id << 8 for `relation %q does not exist`."""
         q = np.ascontiguousarray(queries, dtype=_abi.QUERY_DT)
         allowed = np.zeros(len(q), dtype=np.uint8)
         err = np.zeros(len(q), dtype=np.int32)
-        flags = _abi.F_COUNT_WORK if count_work else 0
+        flags = (_abi.F_COUNT_WORK if count_work else 0) | (_abi.F_ERR_DETAIL if err_detail else 0)
         check(lib().keto_check_batch(self.snapshot.handle, self.stream.handle, q.ctypes.data, len(q),
                                      ctypes.byref(self.limits), allowed.ctypes.data, err.ctypes.data, flags))
         return allowed, err
@@ -224,10 +225,19 @@ class CheckEngine:
         return bool(a[0]), int(e[0])
 
     def check_is_member(self, query_rec: np.ndarray) -> bool:
-        a, e = self.check_relation_tuple(query_rec)
-        if e:
-            raise KetoError(e, "relation does not exist" if e == _abi.QERR_NO_RELATION else "check failed")
-        return a
+        """CheckIsMember (engine.go:65-71): the bool, or the reference's error -- for an
+        undeclared relation its exact text `relation %q does not exist`
+        (namespace/definitions.go:61), naming the relation the walk rejected."""
+        a, e = self.check_batch(np.atleast_1d(query_rec), err_detail=True)
+        code, rel = int(e[0]) & 0xFF, int(e[0]) >> 8
+        if code == _abi.QERR_NO_RELATION:
+            names = self.snapshot.rel_names
+            name = names[rel] if rel < len(names) else names[int(np.atleast_1d(query_rec)["rel"][0])] \
+                if int(np.atleast_1d(query_rec)["rel"][0]) < len(names) else ""
+            raise KetoError(code, f"relation {json.dumps(name)} does not exist")
+        if code:
+            raise KetoError(code, "not implemented" if code == _abi.QERR_NOT_IMPLEMENTED else "check failed")
+        return bool(a[0])
 
 
 class ExpandEngine:
@@ -272,8 +282,9 @@ class Dispatcher:
     GIL for the blocking call, so Python threads coalesce like goroutines in the Go shim."""
 
     def __init__(self, snapshot: Snapshot, max_read_depth: int = 5, max_read_width: int = 100,
-                 max_batch: int = 1 << 16, max_wait_us: int = 0, inflight: int = 4):
-        cfg = _abi.DispatcherConfig(_abi.Limits(max_read_depth, max_read_width), max_batch, max_wait_us, inflight)
+                 max_batch: int = 1 << 16, max_wait_us: int = 0, inflight: int = 4, err_detail: bool = False):
+        cfg = _abi.DispatcherConfig(_abi.Limits(max_read_depth, max_read_width), max_batch, max_wait_us, inflight,
+                                    _abi.F_ERR_DETAIL if err_detail else 0)
         h = ctypes.c_void_p()
         check(lib().keto_dispatcher_create(snapshot.handle, ctypes.byref(cfg), ctypes.byref(h)))
         self.handle = h

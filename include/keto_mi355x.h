@@ -206,6 +206,7 @@ typedef struct keto_dispatcher_config {
     uint32_t max_batch;   /* queries per launch (staging size); a larger request runs alone */
     uint32_t max_wait_us; /* 0: launch as soon as a slot is free with whatever is queued */
     uint32_t inflight;    /* batches in flight on their own streams (0 -> 4, at most 16) */
+    uint32_t flags;       /* KETO_F_ERR_DETAIL: out_err as keto_check_batch with that flag */
 } keto_dispatcher_config;
 typedef struct keto_dispatcher_stats {
     uint64_t batches, requests, queries, max_batch_seen;

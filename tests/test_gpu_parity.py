@@ -328,3 +328,37 @@ def test_sqlite_to_api_tree_on_gpu(stream, tmp_path):
     out = api.trees_to_json(nodes, offs, store.name_tables())
     with open(os.path.join(GOLDEN, "api", "docs_expand_beach_expected_output.json")) as f:
         assert _canon(json.loads(out[0])) == _canon(json.load(f))
+
+
+def test_relation_error_detail_and_out_of_range_ids(stream):
+    """`relation %q does not exist` (namespace/definitions.go:61) names the relation the walk
+    rejected -- here one reached through a subject set, not the query's own -- and relation ids
+    outside the snapshot's name table resolve like any undeclared relation (configured
+    namespace: the error; legacy namespace: nil, not a member) instead of reading past a table."""
+    ns = {"doc": [{"name": "viewer", "types": [{"namespace": "grp", "relation": "member"}]}],
+          "grp": [{"name": "member", "types": [{"namespace": "user"}]}], "user": []}
+    w = refsem.World(namespaces=ns)
+    t = w.tuple_array(["doc:d#viewer@(grp:g#nope)", "grp:h#member@alice", "doc:e#viewer@(grp:h#member)"])
+    q = w.query_array(["doc:d#viewer@alice", "doc:d#bogus@alice", "doc:e#viewer@alice", "user:u#x@alice"])
+    snap = product_snapshot(w, t)
+    eng = km.CheckEngine(snap, stream, max_read_depth=5)
+    pq = queries_to_product(q)
+    a, e = eng.check_batch(pq)
+    orc = refsem.Oracle(w, t)
+    mem, oerr, _ = orc.check(q)
+    np.testing.assert_array_equal(e, oerr)
+    assert list(e) == [1, 1, 0, 0] and list(a) == [0, 0, 1, 0]
+    a2, e2 = eng.check_batch(pq, err_detail=True)
+    np.testing.assert_array_equal(a2, a)
+    assert w.rel_names.names[int(e2[0]) >> 8] == "nope"
+    assert w.rel_names.names[int(e2[1]) >> 8] == "bogus"
+    with pytest.raises(km.KetoError, match='relation "nope" does not exist'):
+        eng.check_is_member(pq[0])
+    assert eng.check_is_member(pq[2]) is True
+    # ids past the name table: 9999 and 70000 (which would alias a real id if truncated to 16 bits)
+    bad = pq.copy()
+    bad["rel"][0] = 9999
+    bad["rel"][1] = 70000 + int(pq["rel"][0])
+    bad["rel"][3] = 123456
+    a3, e3 = eng.check_batch(bad)
+    assert list(e3) == [1, 1, 0, 0] and list(a3) == [0, 0, 1, 0]
