@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.hpp"
 
@@ -177,756 +178,187 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
             c_lsteps += st != S_IDLE ? 1 : 0;
         }
         if (st == S_IDLE) continue;
-
-        // fin: 0 running, 1 finished (res), 2 scratch outgrown
-        uint32_t fin = 0;
-        // At most KETO_GUARD transitions per step; the rest carry over to the next step.  S_FSCAN
-        // entered by a transition reads its window from v0 (set to the cached `ew`), which does
-        // not survive the step boundary: such a lane always runs it before leaving.
-        for (int guard = 0; (guard < KETO_GUARD || st == S_FSCAN) && ln == 0 && fin == 0; guard++) {
-            const uint32_t w = top.w;
-            const uint32_t d = f_d(w);
-#ifdef KETO_PROF_STATES  // profiling builds only (tools/ab_build.sh, tools/prof_states.py)
-            if (COUNT) {     // tiers 1-2 counter slots <- per dispatch key: rounds a wave runs it (1) or lanes in it (2)
-                const int lead = __ffsll((long long)__ballot(true)) - 1;
-                const uint32_t key = st == S_RUN ? 17 + f_type(w) : st;  // slots 7 and 15 are not exported
-                const uint32_t keys[16] = {S_RET, S_POP, S_ROWOFF, S_FSCAN, S_ESDONE, S_CNEXT, S_VIS, S_CEDGE,
-                                           S_TNEXT, 17, 18, 19, 20, 21, 22, S_TEDGE};
-                for (uint32_t k = 0; k < 16; k++) {
-                    const unsigned long long b = __ballot(key == keys[k]);
-                    const unsigned long long v = KETO_PROF_STATES == 1 ? (b != 0) : (unsigned long long)__popcll(b);
-                    if ((int)lane == lead && v) atomicAdd(&P.counters[8 + k], v);
-                }
-            }
+#ifdef KETO_EMU_TRACE
+        keto_emu_trace_step(st == S_START ? pos : NONE32);
 #endif
-            switch (st) {
-            // ---------------------------------------------------------------- query entry
-            case S_START:
-                q = v0.w;
-                sidx = v0.y;
-                heavy = (v0.z & START_HEAVY) != 0;
-                R0 = v1.x;
-                R1 = v1.y;
-                R2 = v1.z;
-                R3 = v1.w;
-                top = make_uint4(v0.x, 0, 0, fw(F_IA, v0.z & 0xFFFFu));  // checkIsAllowed(root, d, false)
-                sp = 0;
-                have_res = false;
-                scope = false;
-                st = S_RUN;
-                break;
-            // ---------------------------------------------------------------- returns
-            case S_RET:
-                if (sp == 0) {
-                    fin = 1;  // CheckIsMember (engine.go:65-71)
-                    break;
-                }
-                la0 = stk + (sp - 1);
-                ln = 1;
-                st = S_POP;
-                break;
-            case S_POP:
-                top = v0;
-                sp--;
-                have_res = true;
-                st = S_RUN;
-                break;
-            // ---------------------------------------------------------------- loads of frames
-            case S_DPROBE: {  // checkDirect via the probe hash (engine.go:167-208)
-                const uint32_t r = probe_check(v0, (((uint64_t)sidx << 32) | top.x) + 1);
-                if (r == 2) {
-                    aux = (aux + 1) & s.probe_mask;
-                    la0 = s.probe + aux;
-                    ln = 1;
-                    break;
-                }
-                if (r == 1) {
-                    res = M_IS;
-                    st = S_RET;
-                    break;
-                }
-                top.w = set_phase(w, 3);
-                st = S_RUN;
-                break;
-            }
-            case S_ROWOFF: {
-                const bool is_es = f_type(w) == F_ES;
-                const uint32_t b = v0.x, e = v0.y;
-                if (b == e) {
-                    res = M_NOT;
-                    st = S_RET;
-                    break;
-                }
-                ew = make_uint4(v0.z, v0.w, NONE32, NONE32);  // the row's first two edges, inline
-                ew_lo = b;
-                ew_hi = b + 2;
-                if (is_es) {
-                    top = make_uint4(b, b, e, set_phase(w, 2) | FL_INLINE);  // x = row begin, y = cursor, z = end
-                    v0 = ew;
-                    st = S_FSCAN;
-                } else {
-                    top = make_uint4(top.x, b, e, set_phase(w, 2));  // x = computed relation
-                    st = S_TNEXT;
-                }
-                break;
-            }
-            case S_FSCAN: {  // found-lookahead over one edge window (traverser.go:73-80, 109-111)
-                ew = v0;
-                uint32_t cur = top.y;
-                const uint32_t e = top.z;
-                if (w & FL_INLINE) {  // the row descriptor's edges (entered from S_ROWOFF)
-                    top.w &= ~FL_INLINE;
-                    ew_lo = cur;
-                    ew_hi = cur + 2;
-                } else {
-                    ew_lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + cur) >> 2) & 3);
-                    ew_hi = ew_lo + 4;
-                }
-                if (!heavy) {
-                    bool found = false;
-                    while (cur < e && cur < ew_hi) {
-                        const uint32_t c = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
-                        cur++;
-                        if (COUNT) {
-                            q_edges++;
-                            q_probes++;
-                        }
-                        if (R0 == c || R1 == c || R2 == c || R3 == c) {
-                            found = true;
-                            break;
-                        }
-                    }
-                    top.y = cur;
-                    if (found) {
-                        res = M_IS;
-                        st = S_RET;
-                        break;
-                    }
-                } else if (cur < e) {  // up to two probes per step, in edge order
-                    pc0 = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
-                    aux = (uint32_t)mix64((((uint64_t)sidx << 32) | pc0) + 1) & s.probe_mask;
-                    la0 = s.probe + aux;
-                    ln = 1;
-                    pn = 1;
-                    if (cur + 1 < e && cur + 1 < ew_hi) {
-                        pc1 = wword(ew, cur + 1 - ew_lo) & ~EDGE_ALIAS;
-                        aux2 = (uint32_t)mix64((((uint64_t)sidx << 32) | pc1) + 1) & s.probe_mask;
-                        la1 = s.probe + aux2;
-                        ln = 2;
-                        pn = 2;
-                    }
-                    st = S_FPROBE;
-                    break;
-                }
-                if (cur < e) {
-                    la0 = win(s.set_dst, cur);
-                    ln = 1;
-                    break;  // next window, stay S_FSCAN
-                }
-                st = S_ESDONE;
-                break;
-            }
-            case S_FPROBE: {
-                const uint32_t r0 = probe_check(v0, (((uint64_t)sidx << 32) | pc0) + 1);
-                const uint32_t r1 = pn > 1 ? probe_check(v1, (((uint64_t)sidx << 32) | pc1) + 1) : 0;
-                if (r0 == 2 || r1 == 2) {  // full buckets: follow them (rare)
-                    if (r0 == 2) aux = (aux + 1) & s.probe_mask;
-                    la0 = s.probe + aux;
-                    ln = 1;
-                    if (pn > 1) {
-                        if (r1 == 2) aux2 = (aux2 + 1) & s.probe_mask;
-                        la1 = s.probe + aux2;
-                        ln = 2;
-                    }
-                    break;
-                }
-                if (COUNT) {
-                    q_edges++;
-                    q_probes++;
-                }
-                if (r0 == 1) {
-                    res = M_IS;
-                    st = S_RET;
-                    break;
-                }
-                top.y++;
-                if (pn > 1) {
-                    if (COUNT) {
-                        q_edges++;
-                        q_probes++;
-                    }
-                    if (r1 == 1) {
-                        res = M_IS;
-                        st = S_RET;
-                        break;
-                    }
-                    top.y++;
-                }
-                if (top.y < top.z) {
-                    if (top.y < ew_hi) {
-                        v0 = ew;  // rest of the cached window
-                        st = S_FSCAN;
-                        break;
-                    }
-                    la0 = win(s.set_dst, top.y);
-                    ln = 1;
-                    st = S_FSCAN;
-                    break;
-                }
-                st = S_ESDONE;
-                break;
-            }
-            case S_ESDONE: {  // width truncation, visited scope, child loop (engine.go:141-162)
-                const uint32_t b = top.x;
-                uint32_t e = top.z;
-                if (e - b > W) e = b + (W > 0 ? W - 1 : 0);  // results[:maxWidth-1]
-                uint32_t flags = 0;
-                if (!scope) {  // graph.InitVisited (graph_utils.go:38-43)
-                    scope = true;
-                    epoch++;
-                    vcount = 0;
-                    flags = FL_OWNER;
-                }
-                top = make_uint4(b, e, NONE32, fw(F_ES, d, 3, flags));  // x = cursor, y = end, z = pending
-                st = S_CNEXT;
-                break;
-            }
-            case S_CNEXT: {  // advance: mark the next children until one was not visited (engine.go:151-160)
-                const uint32_t cur = top.x;
-                if (cur >= top.y) {
-                    cc = NONE32;
-                    st = S_CDISP;
-                    break;
-                }
-                if (cur < ew_lo || cur >= ew_hi) {
-                    la0 = win(s.set_dst, cur);
-                    ln = 1;
-                    st = S_CEDGE;
-                    break;
-                }
-                const uint32_t raw = wword(ew, cur - ew_lo);
-                top.x = cur + 1;
-                cc = raw & ~EDGE_ALIAS;
-                if (raw & EDGE_ALIAS) {
-                    la0 = win(s.vkey, cc);
-                    ln = 1;
-                    st = S_VKEY;
-                    break;
-                }
-                vk = cc;
-                aux = (uint32_t)mix64(vk) & pmask;
-                la0 = reinterpret_cast<const uint4 *>(vis + 2 * aux);
-                ln = 1;
-                st = S_VIS;
-                break;
-            }
-            case S_CEDGE:
-                ew = v0;
-                ew_lo = top.x - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + top.x) >> 2) & 3);
-                ew_hi = ew_lo + 4;
-                st = S_CNEXT;
-                break;
-            case S_VKEY:
-                vk = pick(s.vkey, cc, v0);
-                aux = (uint32_t)mix64(vk) & pmask;
-                la0 = reinterpret_cast<const uint4 *>(vis + 2 * aux);
-                ln = 1;
-                st = S_VIS;
-                break;
-            case S_VIS: {  // CheckAndAddVisited (graph_utils.go:45-53), epoch-tagged slots
-                const unsigned long long tag = ((unsigned long long)epoch << 32) | vk;
-                const unsigned long long s0 = (unsigned long long)v0.x | ((unsigned long long)v0.y << 32);
-                const unsigned long long s1 = (unsigned long long)v0.z | ((unsigned long long)v0.w << 32);
-                const bool e0 = (uint32_t)(s0 >> 32) != epoch, e1 = (uint32_t)(s1 >> 32) != epoch;
-                if (s0 == tag || (!e0 && s1 == tag)) {
-                    st = S_CNEXT;  // already visited (engine.go:157-160)
-                    break;
-                }
-                if (!e0 && !e1) {
-                    aux = (aux + 1) & pmask;
-                    la0 = reinterpret_cast<const uint4 *>(vis + 2 * aux);
-                    ln = 1;
-                    break;
-                }
-                if (2 * (vcount + 1) > P.vcap) {
-                    fin = 2;
-                    break;
-                }
-                vis[2 * aux + (e0 ? 0 : 1)] = tag;
-                vcount++;
-                st = S_CDISP;
-                break;
-            }
-            case S_CDISP: {
-                if (f_phase(w) == 4) {  // draining after a decisive child: mark, never run
-                    if (cc == NONE32) st = S_RET;  // `res` still holds the decisive result
-                    else st = S_CNEXT;
-                    break;
-                }
-                const uint32_t c = top.z;
-                top.z = cc;
-                if (c == NONE32) {  // nothing was pending: the loop's first child, or none left
-                    if (cc == NONE32) {
-                        if (w & FL_OWNER) scope = false;
-                        res = M_NOT;
-                        st = S_RET;
-                    } else {
-                        st = S_CNEXT;  // find its successor before it runs
-                    }
-                    break;
-                }
-                // run the pending child checkIsAllowed(c, d, skipDirect=true) (engine.go:161)
-                const NodeInfo ni = t_node_info(T, c);
-                if (ri_status(ni.ri) == REL_ERROR) {  // engine.go:228-232: decisive
-                    res = mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16);
-                    if (w & FL_OWNER) {
-                        scope = false;
-                        st = S_RET;
-                    } else {
-                        top.w = set_phase(w, 4);
-                        st = cc == NONE32 ? S_RET : S_CNEXT;
-                    }
-                    break;
-                }
-                const bool rw = ri_rw(ni.ri);
-                if (!rw && (!ri_ss(ni.ri) || d <= 1)) {  // empty group / Unknown -> not a member
-                    if (cc == NONE32) {
-                        if (w & FL_OWNER) scope = false;
-                        res = M_NOT;
-                        st = S_RET;
-                    } else {
-                        st = S_CNEXT;
-                    }
-                    break;
-                }
-                if (sp + 1 >= P.scap) {
-                    fin = 2;
-                    break;
-                }
-                stk[sp++] = top;
-                // without a rewrite the child's group is just expandSubject(c, d-1)
-                top = rw ? make_uint4(c, 0, 0, fw(F_IA, d, 0, FL_SKIP)) : make_uint4(c, 0, 0, fw(F_ES, d - 1));
-                have_res = false;
-                st = S_RUN;
-                break;
-            }
-            case S_TNEXT: {  // TTU: next parent (rewrites.go:279-288)
-                const uint32_t cur = top.y;
-                if (cur >= top.z) {
-                    res = M_NOT;
-                    st = S_RET;
-                    break;
-                }
-                if (cur < ew_lo || cur >= ew_hi) {
-                    la0 = win(s.set_dst, cur);
-                    ln = 1;
-                    st = S_TEDGE;
-                    break;
-                }
-                const uint32_t c = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
-                top.y = cur + 1;
-                if (COUNT) q_edges++;
-                if (d <= 1) break;  // checkIsAllowed(..., <= 0) -> Unknown: next parent
-                const NodeInfo ci = t_node_info(T, c);
-                if (sp + 1 >= P.scap) {
-                    fin = 2;
-                    break;
-                }
-                stk[sp++] = top;
-                top = make_uint4(t_sibling(T, c, ci, top.x), 0, 0, fw(F_IA, d - 1));
-                have_res = false;
-                st = S_RUN;
-                break;
-            }
-            case S_TEDGE:
-                ew = v0;
-                ew_lo = top.y - (uint32_t)((reinterpret_cast<uintptr_t>(s.set_dst + top.y) >> 2) & 3);
-                ew_hi = ew_lo + 4;
-                st = S_TNEXT;
-                break;
-            case S_SPROBE: {  // OR shortcut `relation IN (...) LIMIT 1` (traverser.go:143-172)
-                const uint32_t r0 = probe_check(v0, (((uint64_t)sidx << 32) | pc0) + 1);
-                const uint32_t r1 = pn > 1 ? probe_check(v1, (((uint64_t)sidx << 32) | pc1) + 1) : 0;
-                if (r0 == 2 || r1 == 2) {
-                    if (r0 == 2) aux = (aux + 1) & s.probe_mask;
-                    la0 = s.probe + aux;
-                    ln = 1;
-                    if (pn > 1) {
-                        if (r1 == 2) aux2 = (aux2 + 1) & s.probe_mask;
-                        la1 = s.probe + aux2;
-                        ln = 2;
-                    }
-                    break;
-                }
-                if (COUNT) q_probes++;
-                if (r0 == 1) {
-                    res = M_IS;
-                    st = S_RET;
-                    break;
-                }
-                if (pn > 1) {
-                    if (COUNT) q_probes++;
-                    if (r1 == 1) {
-                        res = M_IS;
-                        st = S_RET;
-                        break;
-                    }
-                }
-                st = S_RUN;  // the RW frame continues from its cursor (phase 1)
-                break;
-            }
-            // ---------------------------------------------------------------- frame execution
-            case S_RUN: {
-                uint32_t action = 0;  // 1 call `callee`, 2 return `res`
-                uint4 callee = make_uint4(0, 0, 0, 0);
-                switch (f_type(w)) {
-                case F_IA: {  // checkIsAllowed (engine.go:214-249)
-                    const uint32_t node = top.x;
-                    uint32_t phase = f_phase(w);
-                    if (phase == 0) {
-                        if (d == 0) {  // :215-220
-                            res = M_UNK;
-                            action = 2;
-                            break;
-                        }
-                        const NodeInfo ni = t_node_info(T, node);
-                        top.y = ni.ri;
-                        if (ri_status(ni.ri) == REL_ERROR) {  // :228-232
-                            res = mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, node, ni) << 16);
-                            action = 2;
-                            break;
-                        }
-                        if (ri_rw(ni.ri)) {  // :236-238
-                            top.w = set_phase(w, 1);
-                            callee = make_uint4(node, ri_op(ni.ri), 0, fw(F_RW, d));
-                            action = 1;
-                            break;
-                        }
-                        phase = 2;  // no rewrite: straight to the direct check
-                    } else if (phase == 1) {  // the rewrite returned
-                        have_res = false;
-                        if (decisive(res)) {
-                            action = 2;
-                            break;
-                        }
-                        phase = 2;
-                    }
-                    const uint32_t ri = top.y;
-                    if (phase == 2 && (!s.strict || !ri_rw(ri)) && !(w & FL_SKIP) && d > 1) {  // :239-243
-                        if (COUNT) q_probes++;  // checkDirect(d-1) (:167-208)
-                        if (!(node & VIRT_BIT)) {
-                            if (!heavy) {
-                                if (R0 == node || R1 == node || R2 == node || R3 == node) {
-                                    res = M_IS;
-                                    action = 2;
-                                    break;
-                                }
-                            } else {
-                                top.w = set_phase(w, 2);
-                                aux = (uint32_t)mix64((((uint64_t)sidx << 32) | node) + 1) & s.probe_mask;
-                                la0 = s.probe + aux;
-                                ln = 1;
-                                st = S_DPROBE;
-                                break;
-                            }
-                        }
-                    }
-                    // expand-subject(d-1) as a tail call (:244-246); Unknown or no group -> NotMember
-                    if (ri_ss(ri) && d > 1) {
-                        top = make_uint4(node, 0, 0, fw(F_ES, d - 1));
-                        break;
-                    }
-                    res = M_NOT;
-                    action = 2;
-                    break;
-                }
-                case F_ES:  // checkExpandSubject (engine.go:102-164)
-                    if (f_phase(w) == 0) {
-                        if (COUNT) q_rows++;
-                        if (top.x & VIRT_BIT) {
-                            res = M_NOT;
-                            action = 2;
-                            break;
-                        }
-                        la0 = s.set_row + top.x;
-                        ln = 1;
-                        top.w = set_phase(w, 1);
-                        st = S_ROWOFF;
-                        break;
-                    }
-                    have_res = false;  // phase 3: a child returned
-                    ew_lo = 1;         // the edge window did not survive the child
-                    ew_hi = 0;
-                    if (decisive(res)) {
-                        if (w & FL_OWNER) {  // the scope dies with this frame: no marks needed
-                            scope = false;
-                            action = 2;
-                            break;
-                        }
-                        top.w = set_phase(w, 4);  // mark the remaining siblings, then return res
-                        if (top.z == NONE32) {
-                            action = 2;
-                            break;
-                        }
-                        st = S_CNEXT;
-                        break;
-                    }
-                    if (top.z == NONE32) {  // no sibling pending: the loop is done
-                        if (w & FL_OWNER) scope = false;
-                        res = M_NOT;
-                        action = 2;
-                        break;
-                    }
-                    st = S_CNEXT;  // find the pending sibling's successor, then run it
-                    break;
-                case F_RW: {  // checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73)
-                    const uint32_t node = top.x;
-                    const Op op = T.ops[top.y];
-                    const uint32_t kind = (op.type_kind >> 8) & 0xFFu;
-                    const bool is_or = kind == OPK_OR;
-                    uint32_t phase = f_phase(w);
-                    if (phase == 0) {
-                        if (d == 0) {  // :39-42
-                            res = M_UNK;
-                            action = 2;
-                            break;
-                        }
-                        if (kind == OPK_BAD) {  // :58-59
-                            res = mk_err(KETO_QERR_NOT_IMPLEMENTED);
-                            action = 2;
-                            break;
-                        }
-                        phase = (is_or && ((op.type_kind >> 16) & 1u)) ? 1 : 3;
-                        top.z = 0;
-                    } else if (phase == 2) {  // shortcut candidates returned
-                        have_res = false;
-                        if (decisive(res)) {
-                            action = 2;
-                            break;
-                        }
-                        phase = 3;
-                        top.z = 0;
-                    } else if (phase == 4) {  // a child check returned
-                        have_res = false;
-                        if (is_or) {
-                            if (decisive(res)) {  // binop.go:23-26
-                                action = 2;
-                                break;
-                            }
-                        } else if ((res >> 8) != 0 || (res & 3u) != M_IS) {  // binop.go:52-54
-                            res = (res & ~3u) | M_NOT;
-                            action = 2;
-                            break;
-                        }
-                        phase = 3;
-                    }
-                    top.w = set_phase(w, phase);
-                    const NodeInfo ni = t_node_info(T, node);
-                    if (phase == 1) {  // shortcut IN probes in AST order (rewrites.go:62-92)
-                        uint32_t k = top.z;
-                        bool found = false;
-                        pn = 0;
-                        while (k < op.child_count && pn < 2 && !found) {
-                            const Op ch = T.ops[T.op_children[op.child_begin + k]];
-                            if ((ch.type_kind & 0xFFu) != OP_CSS) {
-                                k++;
-                                continue;
-                            }
-                            const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
-                            if (s.strict && !(t & VIRT_BIT)) {  // traverser.go:137-139
-                                const NodeInfo ti = t_node_info(T, t);
-                                if (ri_status(ti.ri) == REL_DECLARED && ri_rw(ti.ri)) {
-                                    k++;
-                                    continue;
-                                }
-                            }
-                            if (heavy && !(t & VIRT_BIT)) {
-                                if (pn == 0) pc0 = t;
-                                else pc1 = t;
-                                pn++;
-                                k++;
-                                continue;
-                            }
-                            if (pn) break;  // keep probe order: resolve the pending hash probes first
-                            if (COUNT) q_probes++;
-                            if (!(t & VIRT_BIT) && (R0 == t || R1 == t || R2 == t || R3 == t)) found = true;
-                            k++;
-                        }
-                        top.z = k;
-                        if (found) {
-                            res = M_IS;
-                            action = 2;
-                            break;
-                        }
-                        if (pn) {
-                            aux = (uint32_t)mix64((((uint64_t)sidx << 32) | pc0) + 1) & s.probe_mask;
-                            la0 = s.probe + aux;
-                            ln = 1;
-                            if (pn > 1) {
-                                aux2 = (uint32_t)mix64((((uint64_t)sidx << 32) | pc1) + 1) & s.probe_mask;
-                                la1 = s.probe + aux2;
-                                ln = 2;
-                            }
-                            st = S_SPROBE;
-                            break;
-                        }
-                        if (k < op.child_count) break;  // more CSS children: next step
-                        // no direct member: candidates checkIsAllowed(c, d-1, true) (rewrites.go:88-90)
-                        top.w = set_phase(w, 2);
-                        callee = make_uint4(node, top.y, 0, fw(F_SC, d));
-                        action = 1;
-                        break;
-                    }
-                    // phase 3: next non-CSS (OR) / any (AND) child
-                    uint32_t k = top.z;
-                    while (k < op.child_count) {
-                        const uint32_t ci = T.op_children[op.child_begin + k];
-                        k++;
-                        const Op ch = T.ops[ci];
-                        const uint32_t ct = ch.type_kind & 0xFFu;
-                        if (is_or && ct == OP_CSS) continue;  // handled by the shortcut (:95-98)
-                        top.z = k;
-                        top.w = set_phase(w, 4);
-                        if (ct == OP_TTU) callee = make_uint4(node, ci, 0, fw(F_TTU, d));
-                        else if (ct == OP_CSS)
-                            callee = make_uint4(t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), 0, 0, fw(F_IA, d));
-                        else if (ct == OP_REWRITE) callee = make_uint4(node, ci, 0, fw(F_RW, d - 1));  // :118
-                        else callee = make_uint4(node, ci, 0, fw(F_INV, d));
-                        action = 1;
-                        break;
-                    }
-                    if (action == 1) break;
-                    res = (!is_or && op.child_count > 0) ? M_IS : M_NOT;  // binop.go:19-21,38,42-44,62-65
-                    action = 2;
-                    break;
-                }
-                case F_SC: {  // shortcut candidates (rewrites.go:88-90)
-                    if (have_res) {
-                        have_res = false;
-                        if (decisive(res)) {
-                            action = 2;
-                            break;
-                        }
-                    }
-                    const uint32_t node = top.x;
-                    const Op op = T.ops[top.y];
-                    const NodeInfo ni = t_node_info(T, node);
-                    uint32_t k = top.z;
-                    while (k < op.child_count) {
-                        const Op ch = T.ops[T.op_children[op.child_begin + k]];
-                        k++;
-                        if ((ch.type_kind & 0xFFu) != OP_CSS || d <= 1) continue;  // d-1 <= 0 -> Unknown
-                        top.z = k;
-                        callee = make_uint4(t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), 0, 0,
-                                            fw(F_IA, d - 1, 0, FL_SKIP));
-                        action = 1;
-                        break;
-                    }
-                    if (action == 1) break;
-                    res = M_NOT;
-                    action = 2;
-                    break;
-                }
-                case F_TTU:  // checkTupleToSubjectSet (rewrites.go:242-293)
-                    if (f_phase(w) == 0) {
-                        const Op op = T.ops[top.y];
-                        const NodeInfo ni = t_node_info(T, top.x);
-                        const uint32_t ts = t_sibling(T, top.x, ni, op.rel_computed & 0xFFFFu);
-                        if (COUNT) q_rows++;
-                        if (ts & VIRT_BIT) {
-                            res = M_NOT;
-                            action = 2;
-                            break;
-                        }
-                        top = make_uint4(op.rel_computed >> 16, ts, 0, set_phase(w, 1));
-                        la0 = s.set_row + ts;
-                        ln = 1;
-                        st = S_ROWOFF;
-                        break;
-                    }
-                    have_res = false;  // a parent's check returned
-                    if (decisive(res)) {
-                        action = 2;
-                        break;
-                    }
-                    ew_lo = 1;  // window unknown after the child: reload
-                    ew_hi = 0;
-                    st = S_TNEXT;
-                    break;
-                case F_INV: {  // checkInverted (rewrites.go:136-200)
-                    if (have_res) {
-                        have_res = false;
-                        const uint32_t m = res & 3u;
-                        if (m == M_IS) res = (res & ~3u) | M_NOT;
-                        else if (m == M_NOT) res = (res & ~3u) | M_IS;
-                        action = 2;
-                        break;
-                    }
-                    const Op op = T.ops[top.y];
-                    if (op.child_count != 1) {
-                        res = mk_err(KETO_QERR_NOT_IMPLEMENTED);
-                        action = 2;
-                        break;
-                    }
-                    const uint32_t ci = T.op_children[op.child_begin];
-                    const Op ch = T.ops[ci];
-                    const uint32_t ct = ch.type_kind & 0xFFu;
-                    const uint32_t node = top.x;
-                    top.w = set_phase(w, 1);
-                    if (ct == OP_TTU) callee = make_uint4(node, ci, 0, fw(F_TTU, d));
-                    else if (ct == OP_CSS) {
-                        const NodeInfo ni = t_node_info(T, node);
-                        callee = make_uint4(t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), 0, 0, fw(F_IA, d));
-                    } else if (ct == OP_REWRITE) callee = make_uint4(node, ci, 0, fw(F_RW, d));  // keeps depth (:171)
-                    else callee = make_uint4(node, ci, 0, fw(F_INV, d));
-                    action = 1;
-                    break;
-                }
-                default:
-                    res = mk_err(KETO_QERR_INTERNAL);
-                    action = 2;
-                }
-                if (action == 1) {  // call: push the caller, run the callee
-                    if (sp + 1 >= P.scap) {
-                        fin = 2;
-                        break;
-                    }
-                    stk[sp++] = top;
-                    top = callee;
-                    have_res = false;
-                } else if (action == 2) {
-                    st = S_RET;
-                }
-                break;
-            }
-            default:
-                fin = 2;
-            }
-        }
-        if (fin) {
-            if (fin == 2) {  // scratch outgrown: hand the query to the next tier
-                if (P.last_tier) {
-                    P.out_allowed[q] = 0;
-                    P.out_err[q] = KETO_QERR_INTERNAL;
-                } else {
-                    P.ovf_list[atomicAdd(P.ovf_count, 1u)] = pos;
-                }
-            } else {
-                const uint32_t err = res >> 8;  // code | relation name id << 8 (KETO_F_ERR_DETAIL)
-                P.out_allowed[q] = (err == 0 && (res & 3u) == M_IS) ? 1 : 0;
-                P.out_err[q] = (int32_t)(P.err_detail ? err : err & 0xFFu);
-                if (COUNT) {
-                    c_rows += q_rows;
-                    c_edges += q_edges;
-                    c_probes += q_probes;
-                    c_q++;
-                }
-            }
-            st = S_IDLE;
-            ln = 0;
-        }
+
+#include "check_step.inc"
     }
     P.epochs[gl] = epoch;
+    if (COUNT) {
+        for (int off = 32; off > 0; off >>= 1) {
+            c_rows += __shfl_down(c_rows, off);
+            c_edges += __shfl_down(c_edges, off);
+            c_probes += __shfl_down(c_probes, off);
+            c_q += __shfl_down(c_q, off);
+            c_lsteps += __shfl_down(c_lsteps, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&P.counters[0], c_rows);
+            atomicAdd(&P.counters[1], c_edges);
+            atomicAdd(&P.counters[2], c_probes);
+            atomicAdd(&P.counters[4], c_q);
+            atomicAdd(&P.counters[5], c_wsteps);
+            atomicAdd(&P.counters[6], c_lsteps);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Block-regrouped interpreter (tier 0 of large batches).
+//
+// A wave-step costs one pass over every distinct case body its 64 lanes are in, and lanes that
+// each own one query sit in ~20 different bodies per step.  Here a block's
+// queries live in LDS slots instead of lanes: every step, each lane loads the slot it was dealt,
+// issues the slot's load, runs the same transitions as check_kernel (check_step.inc), stores
+// the slot back, and then the block counting-sorts its slots by the dispatch key they stopped
+// at -- so at the next step the lanes of one wave hold queries in the same few states.
+// tools/sim_regroup.py (CPU-emulation traces of the Drive workload) puts the case bodies per
+// lane-step at 1.8x (256 slots) to 2.5x (1024 slots) fewer.  Visited tables, frame stacks and
+// epochs belong to the slot, so a query may run on a different lane every step.
+#ifndef KETO_RG_BLOCK
+#define KETO_RG_BLOCK 512
+#endif
+constexpr uint32_t RG = KETO_RG_BLOCK;
+constexpr uint32_t RG_KEYS = 64;
+constexpr uint32_t RG_GROUPS = 8;  // 16-byte state groups per slot (+1 with work counting)
+
+__host__ __device__ constexpr size_t rg_state_bytes(bool count) { return (size_t)RG * 16 * (RG_GROUPS + (count ? 1 : 0)); }
+__host__ __device__ constexpr size_t rg_extra_bytes() { return (size_t)RG * 2 + 3 * RG_KEYS * 4 + 16; }
+
+__device__ __forceinline__ uint32_t rg_key(uint32_t st, uint32_t w) {
+    if (st != S_RUN) return st;  // S_IDLE = 0 sorts first: the lanes that refill are contiguous
+    const uint32_t ph = f_phase(w) < 3 ? f_phase(w) : 3u;
+    return 32 + f_type(w) * 4 + ph;
+}
+
+template <bool COUNT, bool LDS_TABLES>
+__global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const DevSnapshot &s = P.s;
+    const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
+    const size_t tab = LDS_TABLES ? ((size_t)s.lds_bytes + 15) / 16 * 16 : 0;
+    uint4 *G = reinterpret_cast<uint4 *>(lds + tab);  // group g of slot k at G[g * RG + k]
+    uint16_t *perm = reinterpret_cast<uint16_t *>(lds + tab + rg_state_bytes(COUNT));
+    uint32_t *hist = reinterpret_cast<uint32_t *>(perm + RG);  // [2][RG_KEYS]
+    uint32_t *pref = hist + 2 * RG_KEYS;
+    uint32_t *flags = pref + RG_KEYS;  // [0] queue exhausted, [1] block done
+    const uint32_t tid = threadIdx.x;
+    const uint32_t base = blockIdx.x * RG;
+    const uint32_t nq = P.qlist ? *P.qlist_count : P.n;
+    const uint32_t pmask = (P.vcap >> 1) - 1;
+    const uint32_t W = (uint32_t)P.max_width;
+    const uint32_t lane = __lane_id();
+    unsigned long long c_rows = 0, c_edges = 0, c_probes = 0, c_q = 0, c_wsteps = 0, c_lsteps = 0;
+
+    // every slot starts idle, with its epoch
+    G[0 * RG + tid] = make_uint4(0, 0, 0, 0);
+    G[1 * RG + tid] = make_uint4(0, 0, 0, 0);
+    G[2 * RG + tid] = make_uint4(0, 0, NONE32, S_IDLE);
+    G[3 * RG + tid] = make_uint4(NONE32, NONE32, NONE32, NONE32);
+    G[4 * RG + tid] = make_uint4(0, 0, P.epochs[base + tid], 0);
+    G[5 * RG + tid] = make_uint4(1, 0, 0, 0);
+    G[6 * RG + tid] = make_uint4(0, 0, 0, 0);
+    G[7 * RG + tid] = make_uint4(0, 0, 0, 0);
+    if (COUNT) G[8 * RG + tid] = make_uint4(0, 0, 0, 0);
+    perm[tid] = (uint16_t)tid;
+    if (tid < 2 * RG_KEYS) hist[tid] = 0;
+    if (tid < 4) flags[tid] = 0;
+    __syncthreads();
+    uint32_t cur = 0;
+    for (;;) {
+        const uint32_t slot = perm[tid];
+        unsigned long long *vis = P.vis + (size_t)(base + slot) * P.vcap;
+        uint4 *stk = P.stack + (size_t)(base + slot) * P.scap;
+        // ---- the slot's query state
+        uint4 top = G[0 * RG + slot];
+        uint4 ew = G[1 * RG + slot];
+        const uint4 g2 = G[2 * RG + slot], g3 = G[3 * RG + slot], g4 = G[4 * RG + slot], g5 = G[5 * RG + slot],
+                    g6 = G[6 * RG + slot], g7 = G[7 * RG + slot];
+        uint32_t q = g2.x, pos = g2.y, sidx = g2.z;
+        uint32_t st = g2.w & 63u, pn = (g2.w >> 9) & 3u, ln = (g2.w >> 11) & 3u;
+        bool heavy = (g2.w >> 6) & 1u, have_res = (g2.w >> 7) & 1u, scope = (g2.w >> 8) & 1u;
+        uint32_t R0 = g3.x, R1 = g3.y, R2 = g3.z, R3 = g3.w;
+        uint32_t res = g4.x, vcount = g4.y, epoch = g4.z, sp = g4.w;
+        uint32_t ew_lo = g5.x, ew_hi = g5.y, aux = g5.z, aux2 = g5.w;
+        uint32_t cc = g6.x, vk = g6.y, pc0 = g6.z, pc1 = g6.w;
+        const uint4 *la0 = reinterpret_cast<const uint4 *>((uintptr_t)g7.x | ((uintptr_t)g7.y << 32));
+        const uint4 *la1 = reinterpret_cast<const uint4 *>((uintptr_t)g7.z | ((uintptr_t)g7.w << 32));
+        uint32_t q_rows = 0, q_edges = 0, q_probes = 0;
+        if (COUNT) {
+            const uint4 g8 = G[8 * RG + slot];
+            q_rows = g8.x;
+            q_edges = g8.y;
+            q_probes = g8.z;
+        }
+        // ---- refill idle slots: one atomic per wavefront (ballot + mbcnt)
+        const bool need = (st == S_IDLE) && flags[0] == 0;
+        const unsigned long long mask = __ballot(need);
+        if (mask) {
+            const int leader = __ffsll((long long)mask) - 1;
+            uint32_t b0 = 0;
+            if ((int)lane == leader) b0 = atomicAdd(P.next, (uint32_t)__popcll(mask));
+            b0 = __shfl(b0, leader);
+            if (need) {
+                const uint32_t my = b0 + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                if (my >= nq) flags[0] = 1;
+                else {
+                    pos = P.qlist ? P.qlist[my] : my;
+                    st = S_START;
+                    la0 = P.start + 2 * (size_t)pos;
+                    la1 = la0 + 1;
+                    ln = 2;
+                    q_rows = q_edges = q_probes = 0;
+                }
+            }
+        }
+        // ---- the load slot, then the transitions (the same state machine as check_kernel)
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+        if (ln > 0) v0 = *la0;
+        if (ln > 1) v1 = *la1;
+        ln = 0;
+        if (COUNT) {
+            c_wsteps += lane == 0 ? 1 : 0;
+            c_lsteps += st != S_IDLE ? 1 : 0;
+        }
+        if (st != S_IDLE) {
+#include "check_step.inc"
+        }
+        // ---- store the slot back
+        G[0 * RG + slot] = top;
+        G[1 * RG + slot] = ew;
+        G[2 * RG + slot] = make_uint4(q, pos, sidx, st | (uint32_t(heavy) << 6) | (uint32_t(have_res) << 7) |
+                                                         (uint32_t(scope) << 8) | (pn << 9) | (ln << 11));
+        G[3 * RG + slot] = make_uint4(R0, R1, R2, R3);
+        G[4 * RG + slot] = make_uint4(res, vcount, epoch, sp);
+        G[5 * RG + slot] = make_uint4(ew_lo, ew_hi, aux, aux2);
+        G[6 * RG + slot] = make_uint4(cc, vk, pc0, pc1);
+        G[7 * RG + slot] = make_uint4((uint32_t)(uintptr_t)la0, (uint32_t)((uintptr_t)la0 >> 32), (uint32_t)(uintptr_t)la1,
+                                      (uint32_t)((uintptr_t)la1 >> 32));
+        if (COUNT) G[8 * RG + slot] = make_uint4(q_rows, q_edges, q_probes, 0);
+        // ---- regroup: counting sort of the slots by the key they stopped at
+        const uint32_t key = rg_key(st, top.w);
+        const uint32_t rank = atomicAdd(&hist[cur * RG_KEYS + key], 1u);
+        __syncthreads();
+        if (tid < RG_KEYS) {  // wave 0: exclusive scan of the histogram
+            const uint32_t h = hist[cur * RG_KEYS + tid];
+            uint32_t incl = h;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if ((int)lane >= o) incl += t;
+            }
+            pref[tid] = incl - h;
+            hist[(cur ^ 1) * RG_KEYS + tid] = 0;
+            if (tid == RG_KEYS - 1) flags[1] = (incl - hist[cur * RG_KEYS] == 0 && flags[0] != 0) ? 1u : 0u;
+        }
+        __syncthreads();
+        perm[pref[key] + rank] = (uint16_t)slot;
+        const bool done = flags[1] != 0;
+        __syncthreads();
+        if (done) break;
+        cur ^= 1;
+    }
+    P.epochs[base + tid] = G[4 * RG + tid].z;
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
             c_rows += __shfl_down(c_rows, off);
@@ -971,6 +403,28 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
     const size_t lds = lds_tables ? s.dev.lds_bytes : 0;
     KETO_HIP(hipMemsetAsync(sc.ctrl, 0, 64, st.stream));
+    // Large batches run tier 0 on the block-regrouped interpreter: RG-slot blocks, as many as
+    // are resident (LDS-bound), when the batch fills them several times over -- small (latency)
+    // batches keep the spread lane kernel.  KETO_REGROUP=0 never uses it, =force always (tests).
+#ifdef KETO_CPUEMU
+    const bool rg_on = false, rg_force = false;  // the CPU emulation runs one-lane waves
+#else
+    const char *rge = getenv("KETO_REGROUP");
+    const bool rg_on = !(rge && rge[0] == '0'), rg_force = rge && rge[0] == 'f';
+#endif
+    const bool rg_tables = s.dev.lds_bytes <= 16 * 1024;
+    uint32_t rg_blocks = 0;
+    if (rg_on) {
+        int per_cu = 0;
+        const size_t rl = (rg_tables ? (s.dev.lds_bytes + 15) / 16 * 16 : 0) + rg_state_bytes(L.count) + rg_extra_bytes();
+        const void *kf = rg_tables ? reinterpret_cast<const void *>(&check_kernel_rg<false, true>)
+                                   : reinterpret_cast<const void *>(&check_kernel_rg<false, false>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, RG, rl) != hipSuccess || per_cu <= 0) per_cu = 1;
+        per_cu = std::min(per_cu, 2);
+        rg_blocks = (uint32_t)per_cu * cus;
+    }
+    const bool rg = rg_on && (rg_force || (uint64_t)L.n >= 4ull * rg_blocks * RG);
+    if (rg) rg_blocks = (uint32_t)std::min<uint64_t>(rg_blocks, (L.n + RG - 1) / RG);
     for (int tier = 0; tier < 3; tier++) {
         CheckParams P{};
         P.s = s.dev;
@@ -1014,7 +468,17 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);  // every launched lane owns scratch
         dim3 grid(lanes / bs), block(bs);
         if (tier == 0) st.mark_begin();
-        if (lds_tables) {
+        if (tier == 0 && rg) {  // the block-regrouped interpreter: resident blocks of RG slots
+            const size_t rl = (rg_tables ? (s.dev.lds_bytes + 15) / 16 * 16 : 0) + rg_state_bytes(L.count) + rg_extra_bytes();
+            dim3 g(rg_blocks), b(RG);
+            if (rg_tables) {
+                if (L.count) hipLaunchKernelGGL((check_kernel_rg<true, true>), g, b, rl, st.stream, P);
+                else hipLaunchKernelGGL((check_kernel_rg<false, true>), g, b, rl, st.stream, P);
+            } else {
+                if (L.count) hipLaunchKernelGGL((check_kernel_rg<true, false>), g, b, rl, st.stream, P);
+                else hipLaunchKernelGGL((check_kernel_rg<false, false>), g, b, rl, st.stream, P);
+            }
+        } else if (lds_tables) {
             if (L.count) hipLaunchKernelGGL((check_kernel<true, true>), grid, block, lds, st.stream, P);
             else hipLaunchKernelGGL((check_kernel<false, true>), grid, block, lds, st.stream, P);
         } else {

@@ -362,3 +362,53 @@ def test_relation_error_detail_and_out_of_range_ids(stream):
     bad["rel"][3] = 123456
     a3, e3 = eng.check_batch(bad)
     assert list(e3) == [1, 1, 0, 0] and list(a3) == [0, 0, 1, 0]
+
+
+@pytest.fixture
+def regroup_forced():
+    """tier 0 on the block-regrouped interpreter whatever the batch size (check.hip
+    check_kernel_rg; by default only batches that fill its resident blocks 4x use it)"""
+    import os
+    old = os.environ.get("KETO_REGROUP")
+    os.environ["KETO_REGROUP"] = "force"
+    yield
+    if old is None:
+        del os.environ["KETO_REGROUP"]
+    else:
+        os.environ["KETO_REGROUP"] = old
+
+
+@pytest.mark.parametrize("seed", list(range(0, 60, 3)))
+def test_regrouped_interpreter_random_worlds(stream, regroup_forced, seed):
+    w, t, q, _ = random_world(seed, rewrites=True)
+    orc = refsem.Oracle(w, t)
+    snap = product_snapshot(w, t)
+    dec, err, st = _oracle_decisions(orc, q, w.max_depth, w.max_width)
+    eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+    stream.counters(reset=True)
+    allowed, gerr = eng.check_batch(queries_to_product(q), count_work=True)
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    c = stream.counters(reset=True)
+    if (err == 0).all():
+        assert (c["rows"], c["edges"], c["probes"]) == (st.rows, st.edges, st.probes)
+
+
+def test_regrouped_interpreter_drive(stream, regroup_forced):
+    from keto_mi355x import synth
+    wl = synth.drive(depth=6, n_groups=5000, n_users=20000, seed=11)
+    q = synth.drive_queries(wl, 1 << 17, seed=4)
+    q["max_depth"][:1000] = np.random.default_rng(0).integers(1, 5, 1000)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    stream.counters(reset=True)
+    a, e = eng.check_batch(q, count_work=True)
+    c = stream.counters(reset=True)
+    w, _ = world_from_workload(wl, with_tuples=False)
+    orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    dec, err, st = orc.check_batch(q.view(refsem.QUERY_DT), threads=8)
+    np.testing.assert_array_equal(a, dec)
+    np.testing.assert_array_equal(e, err)
+    assert (c["rows"], c["edges"], c["probes"]) == (st.rows, st.edges, st.probes)
+    assert c["per_tier"]["queries"][0] > 0

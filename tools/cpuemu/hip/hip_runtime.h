@@ -76,6 +76,7 @@ inline uint32_t __lane_id() { return 0; }
 inline unsigned long long __ballot(int p) { return p ? 1ull : 0ull; }
 template <class T> inline T __shfl(T v, int) { return v; }
 template <class T> inline T __shfl_down(T, int) { return T(0); }
+template <class T> inline T __shfl_up(T, int) { return T(0); }
 inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
