@@ -86,6 +86,48 @@ def schedule_report(orc, q, gpu_allowed, n: int, cores: int):
                          "pruned occurrences at different rest depths plus depth truncation (oracle/refsem.c)"}
 
 
+def _sql_worker(args):
+    """one host core of the SQL-mode baseline: load the rows its queries can read into an
+    in-memory SQLite store (untimed), then run the restated engine (oracle/refsql.py)"""
+    orc, wl, q, max_depth, max_width = args
+    import refsql
+    rows = refsql.closure_rows(orc, q["ns"], q["obj"], max_depth + 1)
+    eng = refsql.SqlEngine(rows, wl.namespaces, wl.ns_names, wl.rel_names, max_depth=max_depth, max_width=max_width,
+                           strict=wl.strict)
+    dec = np.zeros(len(q), np.uint8)
+    t0 = time.perf_counter()
+    for i, r in enumerate(q):
+        subj = (0, int(r["sid"])) if r["kind"] == 0 else (1, wl.ns_names[r["sns"]], int(r["sid"]), wl.rel_names[r["srel"]])
+        m, e = eng.check(wl.ns_names[r["ns"]], int(r["obj"]), wl.rel_names[r["rel"]], subj, int(r["depth"]))
+        dec[i] = e == 0 and m == refsql.IS_MEMBER
+    return dec, time.perf_counter() - t0, eng.statements, len(rows)
+
+
+def sql_baseline(orc, wl, q, max_depth, max_width, cores, per_core=512):
+    """"restated reference (SQL mode)": the engine recursion issuing the reference's four read
+    statements per hop (traverser.go:68-92,146-154; relationtuples.go:216-227,253-260) against
+    in-memory SQLite -- the cost model of Keto with its in-memory SQLite persister -- on the
+    host cores, one process per core, each over the rows its share of the sample can read
+    (per_core queries each: a few seconds in all, store loading included)"""
+    import multiprocessing as mp
+    n = min(len(q), per_core * cores)
+    parts = [q[i:n:cores] for i in range(cores)]
+    with mp.get_context("fork").Pool(cores) as pool:
+        res = pool.map(_sql_worker, [(orc, wl, p, max_depth, max_width) for p in parts])
+    dt = max(r[1] for r in res)
+    dec = np.zeros(n, np.uint8)
+    for i in range(cores):
+        dec[i:n:cores] = res[i][0]
+    stmts = sum(r[2] for r in res)
+    return {"value": n / dt, "unit": "checks/s", "cores": cores, "kind": "port",
+            "label": "restated reference (SQL mode)",
+            "sample": f"first {n} of the {len(q)}-query batch, oracle/refsql.py: the engine recursion issuing the "
+                      f"reference's 4 SQL statements per hop against in-memory SQLite (python sqlite3 "
+                      f"{__import__('sqlite3').sqlite_version}), {cores} processes, slowest {dt:.2f} s; "
+                      f"{stmts / n:.1f} statements/check; store = the {sum(r[3] for r in res)} rows the sample can "
+                      f"read (loaded untimed)"}, dec
+
+
 def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0, gpu_allowed=None):
     """The oracle (C restatement of the reference, oracle/refsem.c) on the host cores, on a
     bounded sample of the same batch over the same graph -- reported beside the GPU, never
@@ -119,7 +161,17 @@ def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0, gpu_allowed=N
         t0 = time.perf_counter()
         sched = schedule_report(orc, q, gpu_allowed, max(1 << 12, min(n, 1 << 16)), cores)
         log(f"schedule report ({sched['n']} queries): {time.perf_counter() - t0:.1f}s")
+    sql = None
+    try:
+        t0 = time.perf_counter()
+        sql, sdec = sql_baseline(orc, wl, q, max_depth, max_width, cores)
+        ns = len(sdec)
+        sql["parity_vs_port"] = {"n": ns, "mismatches": int((sdec != dec[:ns]).sum()) if ns <= len(dec) else None}
+        log(f"sql-mode baseline: {sql['value']:.0f} checks/s ({time.perf_counter() - t0:.1f}s)")
+    except Exception as e:  # reported, never fatal to the bench line
+        sql = {"error": repr(e)}
     orc.close()
+    cpu_baseline.sql = sql
     return sched, {"value": n / dt, "unit": "checks/s", "cores": cores, "kind": "port",
             "sample": f"first {n} of the {len(q)}-query batch over the full {len(wl.tuples)}-tuple graph, "
                       f"oracle/refsem.c (C restatement of internal/check + persistence/sql read path), "
@@ -466,6 +518,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sched, cb, dec = cpu_baseline(wl, q, wl.max_depth, wl.max_width, args.cpu_budget, gpu_allowed=allowed)
         out["cpu_baseline"] = cb
+        out["cpu_baseline_sql_mode"] = getattr(cpu_baseline, "sql", None)
         ns = len(dec)
         out["cpu_parity_sample"] = {"n": ns, "mismatches": int((dec != allowed[:ns]).sum())}
         out["schedule_sensitivity"] = sched

@@ -100,6 +100,14 @@ struct CheckParams {
 #ifndef KETO_T0_BLOCKS_PER_CU
 #define KETO_T0_BLOCKS_PER_CU 5
 #endif
+// one-frame register cache of the stack top (0: every return reloads its parent frame)
+#ifndef KETO_PCACHE
+#define KETO_PCACHE 1
+#endif
+// Tier-0 visited slots per lane (two per 16-byte probe): ~500 nodes per query scope
+#ifndef KETO_T0_VCAP
+#define KETO_T0_VCAP 1024
+#endif
 
 __device__ __forceinline__ uint32_t w8(const uint4 &v0, const uint4 &v1, uint32_t j) {
     return j < 4 ? wword(v0, j) : wword(v1, j - 4);
@@ -133,6 +141,10 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
     uint32_t R0 = NONE32, R1 = NONE32, R2 = NONE32, R3 = NONE32;
     // interpreter
     uint4 top = make_uint4(0, 0, 0, 0);
+    // one-frame register cache of the stack top (write-back): a call's frame is written to the
+    // scratch stack only when a deeper call evicts it, so a leaf call + return costs no memory
+    uint4 pcache = make_uint4(0, 0, 0, 0);
+    bool pc_ok = false;
     uint32_t sp = 0, res = 0, vcount = 0;
     bool have_res = false, scope = false;
     uint4 ew = make_uint4(0, 0, 0, 0);
@@ -221,7 +233,7 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
 #endif
 constexpr uint32_t RG = KETO_RG_BLOCK;
 constexpr uint32_t RG_KEYS = 64;
-constexpr uint32_t RG_GROUPS = 8;  // 16-byte state groups per slot (+1 with work counting)
+constexpr uint32_t RG_GROUPS = 9;  // 16-byte state groups per slot (+1 with work counting)
 
 __host__ __device__ constexpr size_t rg_state_bytes(bool count) { return (size_t)RG * 16 * (RG_GROUPS + (count ? 1 : 0)); }
 __host__ __device__ constexpr size_t rg_extra_bytes() { return (size_t)RG * 2 + 3 * RG_KEYS * 4 + 16; }
@@ -260,7 +272,8 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
     G[5 * RG + tid] = make_uint4(1, 0, 0, 0);
     G[6 * RG + tid] = make_uint4(0, 0, 0, 0);
     G[7 * RG + tid] = make_uint4(0, 0, 0, 0);
-    if (COUNT) G[8 * RG + tid] = make_uint4(0, 0, 0, 0);
+    G[8 * RG + tid] = make_uint4(0, 0, 0, 0);
+    if (COUNT) G[9 * RG + tid] = make_uint4(0, 0, 0, 0);
     perm[tid] = (uint16_t)tid;
     if (tid < 2 * RG_KEYS) hist[tid] = 0;
     if (tid < 4) flags[tid] = 0;
@@ -278,6 +291,8 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
         uint32_t q = g2.x, pos = g2.y, sidx = g2.z;
         uint32_t st = g2.w & 63u, pn = (g2.w >> 9) & 3u, ln = (g2.w >> 11) & 3u;
         bool heavy = (g2.w >> 6) & 1u, have_res = (g2.w >> 7) & 1u, scope = (g2.w >> 8) & 1u;
+        bool pc_ok = (g2.w >> 13) & 1u;
+        uint4 pcache = G[8 * RG + slot];
         uint32_t R0 = g3.x, R1 = g3.y, R2 = g3.z, R3 = g3.w;
         uint32_t res = g4.x, vcount = g4.y, epoch = g4.z, sp = g4.w;
         uint32_t ew_lo = g5.x, ew_hi = g5.y, aux = g5.z, aux2 = g5.w;
@@ -286,10 +301,10 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
         const uint4 *la1 = reinterpret_cast<const uint4 *>((uintptr_t)g7.z | ((uintptr_t)g7.w << 32));
         uint32_t q_rows = 0, q_edges = 0, q_probes = 0;
         if (COUNT) {
-            const uint4 g8 = G[8 * RG + slot];
-            q_rows = g8.x;
-            q_edges = g8.y;
-            q_probes = g8.z;
+            const uint4 g9 = G[9 * RG + slot];
+            q_rows = g9.x;
+            q_edges = g9.y;
+            q_probes = g9.z;
         }
         // ---- refill idle slots: one atomic per wavefront (ballot + mbcnt)
         const bool need = (st == S_IDLE) && flags[0] == 0;
@@ -328,14 +343,16 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
         G[0 * RG + slot] = top;
         G[1 * RG + slot] = ew;
         G[2 * RG + slot] = make_uint4(q, pos, sidx, st | (uint32_t(heavy) << 6) | (uint32_t(have_res) << 7) |
-                                                         (uint32_t(scope) << 8) | (pn << 9) | (ln << 11));
+                                                         (uint32_t(scope) << 8) | (pn << 9) | (ln << 11) |
+                                                         (uint32_t(pc_ok) << 13));
         G[3 * RG + slot] = make_uint4(R0, R1, R2, R3);
         G[4 * RG + slot] = make_uint4(res, vcount, epoch, sp);
         G[5 * RG + slot] = make_uint4(ew_lo, ew_hi, aux, aux2);
         G[6 * RG + slot] = make_uint4(cc, vk, pc0, pc1);
         G[7 * RG + slot] = make_uint4((uint32_t)(uintptr_t)la0, (uint32_t)((uintptr_t)la0 >> 32), (uint32_t)(uintptr_t)la1,
                                       (uint32_t)((uintptr_t)la1 >> 32));
-        if (COUNT) G[8 * RG + slot] = make_uint4(q_rows, q_edges, q_probes, 0);
+        G[8 * RG + slot] = pcache;
+        if (COUNT) G[9 * RG + slot] = make_uint4(q_rows, q_edges, q_probes, 0);
         // ---- regroup: counting sort of the slots by the key they stopped at
         const uint32_t key = rg_key(st, top.w);
         const uint32_t rank = atomicAdd(&hist[cur * RG_KEYS + key], 1u);
@@ -393,7 +410,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     // tier 1 ~4k, tier 2 ~500k.
     // Tier 0 is sized to the persistent grid it can ever launch (KETO_T0_BLOCKS_PER_CU resident
     // blocks per CU): 1.3k lanes x 9 KiB per CU, ~3 GiB per stream on 256 CUs.
-    const Tier t[3] = {Tier{cus * KETO_T0_BLOCKS_PER_CU * 256, 1024, 64},  // the common case
+    const Tier t[3] = {Tier{cus * KETO_T0_BLOCKS_PER_CU * 256, KETO_T0_VCAP, 64},  // the common case
                        Tier{cus * 64, 1u << 13, 1024},                      // wide visited scopes
                        Tier{64, 1u << 20, 1u << 14}};   // huge scopes / deep recursion
     ensure_scratch(st.check_scratch, t);

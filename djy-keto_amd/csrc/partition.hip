@@ -37,6 +37,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -245,6 +247,8 @@ struct Partition {
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
     DevBuf table, seen, cand, fresh, routed, req, req_off, subj, subj_off, cnt, pos, out, got, scratch, ctr, closure;
+    DevBuf bq, braw, bsorted, bkeys, bsubj, bsubj_src, bhist;  // per-batch inputs, reused
+    bool verbose = false;
     uint64_t table_mask = 0, n_seen = 0;
     keto_partition_stats last{};
     // Expand results between keto_partition_expand and keto_partition_expand_result
@@ -344,14 +348,18 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
     const uint32_t W = P.world;
     // every owner gets this rank's subject list once per batch
     std::vector<uint64_t> subj_cnt(W, filter ? n_subj : 0);
-    DevBuf subj_src;
-    ensure(subj_src, std::max<uint64_t>(1, n_subj) * W * 4);
-    if (filter)
-        for (uint32_t r = 0; r < W; r++)
-            if (n_subj)
-                KETO_HIP(hipMemcpyAsync(dptr<uint32_t>(subj_src) + (uint64_t)r * n_subj, subj, n_subj * 4,
-                                        hipMemcpyDeviceToDevice, P.hs));
-    std::vector<uint64_t> subj_from = exchange(P, subj_src.p, subj_cnt, 4, P.subj, st.bytes_sent);
+    DevBuf &subj_src = P.bsubj_src;
+    const void *subj_send = subj;
+    if (W > 1) {
+        ensure(subj_src, std::max<uint64_t>(1, n_subj) * W * 4);
+        if (filter)
+            for (uint32_t r = 0; r < W; r++)
+                if (n_subj)
+                    KETO_HIP(hipMemcpyAsync(dptr<uint32_t>(subj_src) + (uint64_t)r * n_subj, subj, n_subj * 4,
+                                            hipMemcpyDeviceToDevice, P.hs));
+        subj_send = subj_src.p;
+    }
+    std::vector<uint64_t> subj_from = exchange(P, subj_send, subj_cnt, 4, P.subj, st.bytes_sent);
     std::vector<uint64_t> soff(W + 1, 0);
     for (uint32_t r = 0; r < W; r++) soff[r + 1] = soff[r] + subj_from[r];
     ensure(P.subj_off, (W + 1) * 8);
@@ -366,7 +374,15 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
     KETO_HIP(hipMemcpyAsync(P.cand.p, keys, n_keys * 8, hipMemcpyDeviceToDevice, P.hs));
     uint64_t n_cand = n_keys, total = 0;
     const int levels = P.limits.max_read_depth + 1;
+    auto tl = std::chrono::steady_clock::now();
     for (int level = 0; level < levels; level++) {
+        if (P.verbose) {
+            sync(P);
+            fprintf(stderr, "[keto partition] level %d: %llu candidates, prev level %.3f ms\n", level,
+                    (unsigned long long)n_cand,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count());
+            tl = std::chrono::steady_clock::now();
+        }
         // new objects of this level: never asked for before (seen-set insert)
         ensure_table(P, n_cand);
         ensure(P.fresh, std::max<uint64_t>(1, n_cand) * 8);
@@ -395,7 +411,8 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             send[0] = n_new;
             if (n_new) KETO_HIP(hipMemcpyAsync(P.routed.p, P.fresh.p, n_new * 8, hipMemcpyDeviceToDevice, P.hs));
         } else {
-            DevBuf hist(W * 8);
+            DevBuf &hist = P.bhist;
+            ensure(hist, W * 8);
             KETO_HIP(hipMemsetAsync(hist.p, 0, W * 8, P.hs));
             if (n_new)
                 hipLaunchKernelGGL(k_dest_hist, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new, W,
@@ -511,6 +528,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     P->cfg.relation_names = P->rel_ptr.data();
     P->cfg.namespaces_json = P->json.c_str();
     KETO_HIP(hipStreamCreateWithFlags(&P->hs, hipStreamNonBlocking));
+    P->verbose = getenv("KETO_PART_VERBOSE") != nullptr;
     if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
     // the partition, grouped by object key (stable radix sort of (key, index), then a gather)
     P->n = n;
@@ -566,10 +584,12 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
 namespace {
 // the batch's subject ids (kind 0), sorted and unique, into P.cand-independent storage
 uint64_t batch_keys(Partition &P, const keto_query *q, uint64_t n, DevBuf &keys, DevBuf &subj) {
-    DevBuf dq(std::max<uint64_t>(1, n) * sizeof(keto_query));
+    DevBuf &dq = P.bq, &raw = P.braw, &sorted = P.bsorted;
+    ensure(dq, std::max<uint64_t>(1, n) * sizeof(keto_query));
     if (n) KETO_HIP(hipMemcpyAsync(dq.p, q, n * sizeof(keto_query), hipMemcpyHostToDevice, P.hs));
     ensure(keys, std::max<uint64_t>(1, n) * 8);
-    DevBuf raw(std::max<uint64_t>(1, n) * 4), sorted(std::max<uint64_t>(1, n) * 4);
+    ensure(raw, std::max<uint64_t>(1, n) * 4);
+    ensure(sorted, std::max<uint64_t>(1, n) * 4);
     ensure(subj, std::max<uint64_t>(1, n) * 4 + 8);
     ensure(P.ctr, 64);
     unsigned long long *c = dptr<unsigned long long>(P.ctr);
@@ -598,8 +618,9 @@ void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8
     keto_partition_stats st{};
     st.batches = 1;
     auto t0 = std::chrono::steady_clock::now();
-    DevBuf keys, subj;
+    DevBuf &keys = P.bkeys, &subj = P.bsubj;
     const uint64_t n_subj = batch_keys(P, q, n, keys, subj);
+    if (P.verbose) fprintf(stderr, "[keto partition] batch keys + %llu subjects: %.3f ms\n", (unsigned long long)n_subj, secs(t0) * 1e3);
     const uint64_t nt = closure(P, dptr<uint64_t>(keys), n, dptr<uint32_t>(subj), n_subj, true, st);
     st.closure_s = secs(t0);
     t0 = std::chrono::steady_clock::now();

@@ -928,6 +928,64 @@ void rs_check_batch_ex(rs_db *db, const rs_query *q, size_t n, int threads, uint
 }
 
 /* ------------------------------------------------------------------ */
+/* closure (bench helper for the SQL-mode baseline, oracle/refsql.py): every row of every    */
+/* object within `levels` subject-set hops of the given objects, in index order (so rows of */
+/* one (ns, obj, rel) keep their shard order; `pos` is the row's rank in it)                 */
+
+static void obj_rows(const rs_db *db, uint32_t ns, uint32_t obj, size_t *lo, size_t *hi) {
+    size_t a = 0, b = db->n;
+    while (a < b) {
+        size_t m = (a + b) / 2;
+        const key7 *t = &db->rt[m];
+        if (t->ns < ns || (t->ns == ns && t->obj < obj)) a = m + 1;
+        else b = m;
+    }
+    *lo = a;
+    b = db->n;
+    while (a < b) {
+        size_t m = (a + b) / 2;
+        const key7 *t = &db->rt[m];
+        if (t->ns < ns || (t->ns == ns && t->obj <= obj)) a = m + 1;
+        else b = m;
+    }
+    *hi = a;
+}
+
+size_t rs_closure(rs_db *db, const uint32_t *ns, const uint32_t *obj, size_t n, int levels, rs_row *out, size_t cap) {
+    vset *seen = vset_new();
+    size_t fcap = n ? n : 1, fn = 0, total = 0;
+    uint64_t *front = malloc(fcap * sizeof *front);
+    for (size_t i = 0; i < n; i++) front[fn++] = ((uint64_t)ns[i] << 32) | obj[i];
+    for (int level = 0; level < levels && fn; level++) {
+        size_t ncap = 16, nn = 0;
+        uint64_t *next = malloc(ncap * sizeof *next);
+        for (size_t i = 0; i < fn; i++) {
+            if (vset_add(seen, front[i])) continue;
+            size_t lo, hi;
+            obj_rows(db, (uint32_t)(front[i] >> 32), (uint32_t)front[i], &lo, &hi);
+            for (size_t j = lo; j < hi; j++) {
+                const key7 *t = &db->rt[j];
+                if (total < cap) {
+                    rs_row r = {t->ns, t->obj, t->rel, t->kind, t->sid, t->sns, t->srel, 0, (uint64_t)j};
+                    out[total] = r;
+                }
+                total++;
+                if (t->kind == 1) {
+                    if (nn == ncap) next = realloc(next, (ncap *= 2) * sizeof *next);
+                    next[nn++] = ((uint64_t)t->sns << 32) | t->sid;
+                }
+            }
+        }
+        free(front);
+        front = next;
+        fn = nn;
+    }
+    free(front);
+    vset_free(seen);
+    return total;
+}
+
+/* ------------------------------------------------------------------ */
 /* Expand (internal/expand/engine.go:43-124)                            */
 
 typedef struct {

@@ -128,6 +128,15 @@ int rs_check_ex(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, uint32
 void rs_check_batch_ex(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t *decision,
                        int32_t *err, uint32_t *flags, rs_stats *st);
 
+/* Rows of every object within `levels` subject-set hops of (ns[i], obj[i]) (the SQL-mode
+ * baseline's store, oracle/refsql.py): pos = the row's rank in the index, which keeps every
+ * (ns, obj, rel)'s shard order.  Returns the count; only the first cap are written. */
+typedef struct {
+    uint32_t ns, obj, rel, kind, sid, sns, srel, pad;
+    uint64_t pos;
+} rs_row;
+size_t rs_closure(rs_db *db, const uint32_t *ns, const uint32_t *obj, size_t n, int levels, rs_row *out, size_t cap);
+
 /* Expand: returns number of nodes written (0 = nil tree), -1 if cap too small. */
 long rs_expand(rs_db *db, uint32_t kind, uint32_t sid, uint32_t sns, uint32_t srel,
                int32_t depth, rs_tree_node *out, size_t cap, rs_stats *st);
