@@ -102,7 +102,7 @@ struct CheckParams {
 #endif
 // one-frame register cache of the stack top (0: every return reloads its parent frame)
 #ifndef KETO_PCACHE
-#define KETO_PCACHE 1
+#define KETO_PCACHE 0
 #endif
 // Tier-0 visited slots per lane (two per 16-byte probe): ~500 nodes per query scope
 #ifndef KETO_T0_VCAP
@@ -231,12 +231,15 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
 #ifndef KETO_RG_BLOCK
 #define KETO_RG_BLOCK 512
 #endif
+#ifndef KETO_RG_MAX_BLOCKS_PER_CU  // resident blocks per CU (LDS-bound below this)
+#define KETO_RG_MAX_BLOCKS_PER_CU 8
+#endif
 constexpr uint32_t RG = KETO_RG_BLOCK;
 constexpr uint32_t RG_KEYS = 64;
-constexpr uint32_t RG_GROUPS = 9;  // 16-byte state groups per slot (+1 with work counting)
+constexpr uint32_t RG_GROUPS = 8 + KETO_PCACHE;  // 16-byte state groups per slot (+1 with work counting)
 
 __host__ __device__ constexpr size_t rg_state_bytes(bool count) { return (size_t)RG * 16 * (RG_GROUPS + (count ? 1 : 0)); }
-__host__ __device__ constexpr size_t rg_extra_bytes() { return (size_t)RG * 2 + 3 * RG_KEYS * 4 + 16; }
+__host__ __device__ constexpr size_t rg_extra_bytes() { return (size_t)RG * 4 + 2 * RG_KEYS * 4 + 16; }
 
 __device__ __forceinline__ uint32_t rg_key(uint32_t st, uint32_t w) {
     if (st != S_RUN) return st;  // S_IDLE = 0 sorts first: the lanes that refill are contiguous
@@ -251,10 +254,9 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
     const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
     const size_t tab = LDS_TABLES ? ((size_t)s.lds_bytes + 15) / 16 * 16 : 0;
     uint4 *G = reinterpret_cast<uint4 *>(lds + tab);  // group g of slot k at G[g * RG + k]
-    uint16_t *perm = reinterpret_cast<uint16_t *>(lds + tab + rg_state_bytes(COUNT));
-    uint32_t *hist = reinterpret_cast<uint32_t *>(perm + RG);  // [2][RG_KEYS]
-    uint32_t *pref = hist + 2 * RG_KEYS;
-    uint32_t *flags = pref + RG_KEYS;  // [0] queue exhausted, [1] block done
+    uint16_t *perm = reinterpret_cast<uint16_t *>(lds + tab + rg_state_bytes(COUNT));  // [2][RG]: lane -> slot
+    uint32_t *hist = reinterpret_cast<uint32_t *>(perm + 2 * RG);                    // [2][RG_KEYS]
+    uint32_t *flags = hist + 2 * RG_KEYS;  // [0] queue exhausted
     const uint32_t tid = threadIdx.x;
     const uint32_t base = blockIdx.x * RG;
     const uint32_t nq = P.qlist ? *P.qlist_count : P.n;
@@ -272,15 +274,15 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
     G[5 * RG + tid] = make_uint4(1, 0, 0, 0);
     G[6 * RG + tid] = make_uint4(0, 0, 0, 0);
     G[7 * RG + tid] = make_uint4(0, 0, 0, 0);
-    G[8 * RG + tid] = make_uint4(0, 0, 0, 0);
-    if (COUNT) G[9 * RG + tid] = make_uint4(0, 0, 0, 0);
+    if (KETO_PCACHE) G[8 * RG + tid] = make_uint4(0, 0, 0, 0);
+    if (COUNT) G[RG_GROUPS * RG + tid] = make_uint4(0, 0, 0, 0);
     perm[tid] = (uint16_t)tid;
     if (tid < 2 * RG_KEYS) hist[tid] = 0;
     if (tid < 4) flags[tid] = 0;
     __syncthreads();
     uint32_t cur = 0;
     for (;;) {
-        const uint32_t slot = perm[tid];
+        const uint32_t slot = perm[cur * RG + tid];
         unsigned long long *vis = P.vis + (size_t)(base + slot) * P.vcap;
         uint4 *stk = P.stack + (size_t)(base + slot) * P.scap;
         // ---- the slot's query state
@@ -291,8 +293,8 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
         uint32_t q = g2.x, pos = g2.y, sidx = g2.z;
         uint32_t st = g2.w & 63u, pn = (g2.w >> 9) & 3u, ln = (g2.w >> 11) & 3u;
         bool heavy = (g2.w >> 6) & 1u, have_res = (g2.w >> 7) & 1u, scope = (g2.w >> 8) & 1u;
-        bool pc_ok = (g2.w >> 13) & 1u;
-        uint4 pcache = G[8 * RG + slot];
+        bool pc_ok = KETO_PCACHE && ((g2.w >> 13) & 1u);
+        uint4 pcache = KETO_PCACHE ? G[8 * RG + slot] : make_uint4(0, 0, 0, 0);
         uint32_t R0 = g3.x, R1 = g3.y, R2 = g3.z, R3 = g3.w;
         uint32_t res = g4.x, vcount = g4.y, epoch = g4.z, sp = g4.w;
         uint32_t ew_lo = g5.x, ew_hi = g5.y, aux = g5.z, aux2 = g5.w;
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
         const uint4 *la1 = reinterpret_cast<const uint4 *>((uintptr_t)g7.z | ((uintptr_t)g7.w << 32));
         uint32_t q_rows = 0, q_edges = 0, q_probes = 0;
         if (COUNT) {
-            const uint4 g9 = G[9 * RG + slot];
+            const uint4 g9 = G[RG_GROUPS * RG + slot];
             q_rows = g9.x;
             q_edges = g9.y;
             q_probes = g9.z;
@@ -351,26 +353,22 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
         G[6 * RG + slot] = make_uint4(cc, vk, pc0, pc1);
         G[7 * RG + slot] = make_uint4((uint32_t)(uintptr_t)la0, (uint32_t)((uintptr_t)la0 >> 32), (uint32_t)(uintptr_t)la1,
                                       (uint32_t)((uintptr_t)la1 >> 32));
-        G[8 * RG + slot] = pcache;
-        if (COUNT) G[9 * RG + slot] = make_uint4(q_rows, q_edges, q_probes, 0);
-        // ---- regroup: counting sort of the slots by the key they stopped at
+        if (KETO_PCACHE) G[8 * RG + slot] = pcache;
+        if (COUNT) G[RG_GROUPS * RG + slot] = make_uint4(q_rows, q_edges, q_probes, 0);
+        // ---- regroup: counting sort of the slots by the key they stopped at (two barriers)
         const uint32_t key = rg_key(st, top.w);
         const uint32_t rank = atomicAdd(&hist[cur * RG_KEYS + key], 1u);
+        if (tid < RG_KEYS) hist[(cur ^ 1) * RG_KEYS + tid] = 0;  // the next step's histogram
         __syncthreads();
-        if (tid < RG_KEYS) {  // wave 0: exclusive scan of the histogram
-            const uint32_t h = hist[cur * RG_KEYS + tid];
-            uint32_t incl = h;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(incl, o);
-                if ((int)lane >= o) incl += t;
-            }
-            pref[tid] = incl - h;
-            hist[(cur ^ 1) * RG_KEYS + tid] = 0;
-            if (tid == RG_KEYS - 1) flags[1] = (incl - hist[cur * RG_KEYS] == 0 && flags[0] != 0) ? 1u : 0u;
+        uint32_t pre = 0;  // slots in smaller keys: the histogram read 4 keys per load
+        const uint4 *h4 = reinterpret_cast<const uint4 *>(hist + cur * RG_KEYS);
+        for (uint32_t k4 = 0; k4 < RG_KEYS / 4; k4++) {
+            const uint4 h = h4[k4];
+            const uint32_t k = 4 * k4;
+            pre += (k < key ? h.x : 0u) + (k + 1 < key ? h.y : 0u) + (k + 2 < key ? h.z : 0u) + (k + 3 < key ? h.w : 0u);
         }
-        __syncthreads();
-        perm[pref[key] + rank] = (uint16_t)slot;
-        const bool done = flags[1] != 0;
+        perm[(cur ^ 1) * RG + pre + rank] = (uint16_t)slot;
+        const bool done = hist[cur * RG_KEYS] == RG && flags[0] != 0;  // every slot idle, queue drained
         __syncthreads();
         if (done) break;
         cur ^= 1;
@@ -420,14 +418,16 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
     const size_t lds = lds_tables ? s.dev.lds_bytes : 0;
     KETO_HIP(hipMemsetAsync(sc.ctrl, 0, 64, st.stream));
-    // Large batches run tier 0 on the block-regrouped interpreter: RG-slot blocks, as many as
-    // are resident (LDS-bound), when the batch fills them several times over -- small (latency)
-    // batches keep the spread lane kernel.  KETO_REGROUP=0 never uses it, =force always (tests).
+    // The block-regrouped interpreter is opt-in: it halves the issued instructions on C4 but
+    // measured 7-23% slower than the lane kernel on MI355X (every step ends
+    // in a block barrier, which exposes the memory latency the lane kernel hides across waves).
+    // KETO_REGROUP=1 uses it for batches that fill the resident blocks several times over,
+    // =force for every batch (tests).
 #ifdef KETO_CPUEMU
     const bool rg_on = false, rg_force = false;  // the CPU emulation runs one-lane waves
 #else
     const char *rge = getenv("KETO_REGROUP");
-    const bool rg_on = !(rge && rge[0] == '0'), rg_force = rge && rge[0] == 'f';
+    const bool rg_on = rge && (rge[0] == '1' || rge[0] == 'f'), rg_force = rge && rge[0] == 'f';
 #endif
     const bool rg_tables = s.dev.lds_bytes <= 16 * 1024;
     uint32_t rg_blocks = 0;
@@ -437,7 +437,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         const void *kf = rg_tables ? reinterpret_cast<const void *>(&check_kernel_rg<false, true>)
                                    : reinterpret_cast<const void *>(&check_kernel_rg<false, false>);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, RG, rl) != hipSuccess || per_cu <= 0) per_cu = 1;
-        per_cu = std::min(per_cu, 2);
+        per_cu = std::min(per_cu, KETO_RG_MAX_BLOCKS_PER_CU);
         rg_blocks = (uint32_t)per_cu * cus;
     }
     const bool rg = rg_on && (rg_force || (uint64_t)L.n >= 4ull * rg_blocks * RG);
