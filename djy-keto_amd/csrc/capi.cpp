@@ -50,6 +50,8 @@ Stream::~Stream() {
     if (check_scratch.mem) (void)hipFree(check_scratch.mem);
     if (expand_scratch.mem) (void)hipFree(expand_scratch.mem);
     if (union_scratch.mem) (void)hipFree(union_scratch.mem);
+    if (frontier.mem) (void)hipFree(frontier.mem);
+    if (frontier.host_ctrl) (void)hipHostFree(frontier.host_ctrl);
     if (lists) (void)hipFree(lists);
     if (qbuf) (void)hipFree(qbuf);
     if (obuf) (void)hipFree(obuf);
@@ -219,6 +221,15 @@ int keto_stream_counters(keto_stream *hs, keto_work_counters *out, int32_t reset
             KETO_HIP(hipMemsetAsync(s->counters, 0, sizeof c, s->stream));
             KETO_HIP(hipStreamSynchronize(s->stream));
         }
+    });
+}
+
+int keto_stream_frontier_stats(keto_stream *hs, keto_frontier_stats *out, int32_t reset) {
+    keto::Stream *s = ST(hs);
+    if (!s) return fail(KETO_E_INVALID, "null stream");
+    return guarded([&] {
+        if (out) *out = s->frontier.stats;
+        if (reset) s->frontier.stats = keto_frontier_stats{};
     });
 }
 

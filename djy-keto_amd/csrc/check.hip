@@ -398,9 +398,10 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
 // --------------------------------------------------------------------------------------
 // host launcher
 
-void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
-    if (L.n == 0) return;
-    if (L.n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
+// The DFS interpreter over the resolved batch, or over the `nl` positions of the device list
+// `list` (queries the frontier engine routed here).  Tier 0's kernel is timed when `timed`.
+static void run_dfs(const Snapshot &s, Stream &st, const CheckLaunch &L, const uint32_t *list, const uint32_t *list_count,
+                    uint64_t nl, bool timed) {
     constexpr uint32_t BLOCK = 256;
     const uint32_t cus = (uint32_t)num_cus(s.device);
     // Queries that outgrow a tier's scratch go to the next (lanes, visited slots per lane,
@@ -412,9 +413,8 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
                        Tier{cus * 64, 1u << 13, 1024},                      // wide visited scopes
                        Tier{64, 1u << 20, 1u << 14}};   // huge scopes / deep recursion
     ensure_scratch(st.check_scratch, t);
-    run_resolve(s, st, L.queries, L.n, L.max_depth);
     Scratch &sc = st.check_scratch;
-    uint32_t *list[2] = {st.lists, st.lists + st.list_cap};
+    uint32_t *lists[2] = {st.lists, st.lists + st.list_cap};
     const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
     const size_t lds = lds_tables ? s.dev.lds_bytes : 0;
     KETO_HIP(hipMemsetAsync(sc.ctrl, 0, 64, st.stream));
@@ -440,19 +440,19 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         per_cu = std::min(per_cu, KETO_RG_MAX_BLOCKS_PER_CU);
         rg_blocks = (uint32_t)per_cu * cus;
     }
-    const bool rg = rg_on && (rg_force || (uint64_t)L.n >= 4ull * rg_blocks * RG);
-    if (rg) rg_blocks = (uint32_t)std::min<uint64_t>(rg_blocks, (L.n + RG - 1) / RG);
+    const bool rg = rg_on && (rg_force || nl >= 4ull * rg_blocks * RG);
+    if (rg) rg_blocks = (uint32_t)std::min<uint64_t>(rg_blocks, (nl + RG - 1) / RG);
     for (int tier = 0; tier < 3; tier++) {
         CheckParams P{};
         P.s = s.dev;
         P.start = st.resolved;
-        P.qlist = tier == 0 ? nullptr : list[tier - 1];
-        P.qlist_count = tier == 0 ? nullptr : &sc.ctrl[3 + tier - 1];
+        P.qlist = tier == 0 ? list : lists[tier - 1];
+        P.qlist_count = tier == 0 ? list_count : &sc.ctrl[3 + tier - 1];
         P.n = (uint32_t)L.n;
         P.out_allowed = L.out_allowed;
         P.out_err = L.out_err;
         P.next = &sc.ctrl[tier];
-        P.ovf_list = tier < 2 ? list[tier] : nullptr;
+        P.ovf_list = tier < 2 ? lists[tier] : nullptr;
         P.ovf_count = tier < 2 ? &sc.ctrl[3 + tier] : nullptr;
         P.vis = sc.vis[tier];
         P.stack = sc.stack[tier];
@@ -476,15 +476,15 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             // lanes each: a wave-step then runs fewer distinct interpreter states, which is what
             // sets the step time (and so a small batch's latency).
             const uint64_t waves = lanes / 64;
-            P.live_lanes = (uint32_t)std::min<uint64_t>(64, (L.n + waves - 1) / waves);
-            const uint64_t need = (L.n + P.live_lanes - 1) / P.live_lanes * 64;
+            P.live_lanes = (uint32_t)std::min<uint64_t>(64, (nl + waves - 1) / waves);
+            const uint64_t need = (nl + P.live_lanes - 1) / P.live_lanes * 64;
             lanes = (uint32_t)std::min<uint64_t>(lanes, (need + BLOCK - 1) / BLOCK * BLOCK);
         } else {
             P.live_lanes = 64;
         }
         const uint32_t bs = std::min<uint32_t>(BLOCK, lanes);  // every launched lane owns scratch
         dim3 grid(lanes / bs), block(bs);
-        if (tier == 0) st.mark_begin();
+        if (tier == 0 && timed) st.mark_begin();
         if (tier == 0 && rg) {  // the block-regrouped interpreter: resident blocks of RG slots
             const size_t rl = (rg_tables ? (s.dev.lds_bytes + 15) / 16 * 16 : 0) + rg_state_bytes(L.count) + rg_extra_bytes();
             dim3 g(rg_blocks), b(RG);
@@ -503,8 +503,28 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             else hipLaunchKernelGGL((check_kernel<false, false>), grid, block, 0, st.stream, P);
         }
         KETO_HIP(hipGetLastError());
-        if (tier == 0) st.mark_end();
+        if (tier == 0 && timed) st.mark_end();
     }
+}
+
+// Check over a resolved batch: the frontier engine (frontier.hip) answers every query whose
+// result cannot depend on visited pruning and routes the rest here; KETO_FRONTIER=0 (A/B) and
+// work-counting launches run the DFS interpreter on the whole batch.  The timed region is the
+// whole device path of the batch after the resolve pass.
+void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
+    if (L.n == 0) return;
+    if (L.n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
+    run_resolve(s, st, L.queries, L.n, L.max_depth);
+    const char *fe = getenv("KETO_FRONTIER");
+    const bool frontier = !L.count && !(fe && fe[0] == '0');
+    if (!frontier) {
+        run_dfs(s, st, L, nullptr, nullptr, L.n, true);
+        return;
+    }
+    st.mark_begin();
+    const uint32_t routed = run_frontier(s, st, L);
+    if (routed) run_dfs(s, st, L, st.frontier.fb_list, st.frontier.fb_count, routed, false);
+    st.mark_end();
 }
 
 }  // namespace keto

@@ -110,6 +110,22 @@ struct Scratch {
     uint4 *stack[3]{};
 };
 
+// per-stream arena of the frontier engine (frontier.hip)
+struct FrontierScratch {
+    void *mem = nullptr;
+    uint64_t cap = 0, ncap = 0, tcap = 0;  // goals, queries, scope-key table slots
+    uint32_t *ctrl = nullptr;              // [gbase | gcount | fallback count]
+    uint32_t *qgoals = nullptr, *qroute = nullptr, *fb_list = nullptr, *fb_count = nullptr;
+    uint4 *g0 = nullptr;
+    uint2 *gfn = nullptr;
+    uint32_t *gval = nullptr;
+    unsigned long long *tkeys = nullptr;
+    uint8_t *trep = nullptr;
+    uint32_t *host_ctrl = nullptr;  // pinned
+    uint32_t last_gens = 0, last_goals = 0, last_routed = 0;
+    keto_frontier_stats stats{};
+};
+
 struct Stream {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -124,6 +140,7 @@ struct Stream {
     void harvest();     // accumulate every completed pair (call after a stream sync)
     // device workspace (allocated on first use, never inside a launch sequence)
     Scratch check_scratch, union_scratch, expand_scratch;
+    FrontierScratch frontier;
     // per-batch workspace of list_cap queries, one allocation:
     uint32_t *lists = nullptr;       // two overflow hand-off lists (of start-record positions)
     uint4 *resolved = nullptr;       // 2 x 16 B start record per query, longest-first (resolve.hip)
@@ -156,6 +173,9 @@ struct CheckLaunch {
 void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth);
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
 void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // rewrite-free snapshots
+// frontier.hip: the batch (already resolved) breadth-first; returns the number of queries routed
+// to the DFS interpreter (positions in st.frontier.fb_list)
+uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L);
 
 struct ExpandLaunch {
     const keto_subject_set *roots;  // device

@@ -1,0 +1,661 @@
+// gfx950 frontier engine for batched Check with OPL rewrites.
+//
+// The reference evaluates one Check as a recursion of goroutines, one SQL statement per hop
+// (internal/check/{engine,rewrites,binop}.go).  Its answer depends on sibling order only
+// through the visited set (engine.go:151-162, graph_utils.go:38-53): a child already marked
+// in the scope is skipped.  Evaluated without that pruning the recursion is a pure function
+// of the snapshot -- "U", oracle/refsem.c "Frontier semantics" -- and U equals the eager
+// DFS (check.hip) on every query where no repeated key of a scope has a decisive occurrence
+// (the proof is in refsem.c).  So U can be evaluated breadth-first, a goal per check:
+//
+//   generation k --fr_expand--> generation k+1 --...-->  (until a generation is empty)
+//   generation k <--fr_reduce-- generation k+1 <--...    (first-decisive / AND / NOT, add order)
+//
+// Every goal is one lane: no per-query state machine, no divergence across interpreter
+// states, no frame stack.  A goal reads what its hop needs (its row, the subject's probe),
+// decides what it can on the spot (a direct tuple, the OR shortcut's IN query, the
+// found-lookahead), and writes its children contiguously into the next generation.  ES
+// children are counted per (scope, visited key) in a device hash table; a decisive
+// occurrence of a repeated key routes the query to the DFS interpreter, as do queries that
+// spawn more than `budget` goals, run past MAX_GEN generations or overflow the arena.
+//
+// Goal records (HBM, one arena per stream, structure of arrays; 28 bytes per goal):
+//   g0[i]   = {node, query position, word, scope}   16 B, written by the parent at spawn
+//   gfn[i]  = {first child, children | reduce op}    8 B, written by fr_expand
+//   gval[i] = value (or the partial fr_reduce folds)  4 B, fr_expand, then fr_reduce
+// word: bits 0-11 rest depth, 12-14 kind, 15 skip_direct, 16-31 rewrite op (RW / TTU / INV);
+// an IA goal an ES spawned keeps bit 16 (its key went into the scope table) and bit 17 (the
+// key is the node's visited alias).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+#include "device_common.hpp"
+
+namespace keto {
+namespace {
+
+constexpr uint32_t M_UNK = 0, M_IS = 1, M_NOT = 2;
+__device__ __forceinline__ uint32_t mk_err(uint32_t e) { return e << 8; }
+__device__ __forceinline__ bool decisive(uint32_t r) { return (r >> 8) != 0 || (r & 3u) == M_IS; }
+
+enum GoalKind : uint32_t { G_IA = 0, G_ES = 1, G_RW = 2, G_TTU = 3, G_INV = 4, G_DEAD = 7 };
+constexpr uint32_t GD_MAX = 0xFFFu;
+constexpr uint32_t GF_SKIP = 1u << 15, GF_ESCHILD = 1u << 16, GF_ALIAS = 1u << 17;
+// gfn.y: children (< 2^24) | reduce op << 24
+enum ReduceOp : uint32_t { R_FIRST = 0, R_AND = 1, R_NOT = 2 };
+constexpr uint32_t NC_MAX = (1u << 24) - 1;
+constexpr uint32_t MAX_GEN = 192;
+// ctrl: gbase[MAX_GEN + 2] | gcount[MAX_GEN + 2] | fallback count (+3)
+constexpr size_t FR_CTRL_BYTES = (2 * (MAX_GEN + 2) + 4) * 4;
+__device__ __forceinline__ uint32_t gword(uint32_t kind, uint32_t d, uint32_t op = 0, uint32_t flags = 0) {
+    return (d & GD_MAX) | (kind << 12) | flags | (op << 16);
+}
+
+struct FrontierParams {
+    DevSnapshot s;
+    const uint4 *start;  // resolve records: 2 per query position (resolve.hip)
+    uint32_t n;
+    uint4 *g0;
+    uint2 *gfn;
+    uint32_t *gval;
+    uint32_t cap;                // arena goals
+    uint32_t *gbase, *gcount;    // [MAX_GEN + 1] per generation
+    uint32_t gen;
+    uint32_t *qgoals, *qroute;   // [n] per query position
+    uint32_t budget;
+    unsigned long long *tkeys;   // (scope, visited key) table
+    uint8_t *trep;               // slot received its key more than once
+    uint32_t tmask;
+    uint32_t max_width;
+    uint8_t *out_allowed;
+    int32_t *out_err;
+    uint32_t err_detail;
+    uint32_t *fb_list, *fb_count;  // routed positions, for the DFS interpreter
+};
+
+// the query subject's membership test (checkDirect / the found-lookahead / the IN shortcut):
+// a short reverse row sits in the start record, a long one is answered by the probe hash
+struct Subject {
+    uint32_t sidx;
+    bool heavy;
+    uint4 R;
+};
+__device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_t pos) {
+    const uint4 b = P.start[2 * (size_t)pos + 1];  // one load: resolve.hip packs a heavy subject here too
+    return Subject{b.x, b.y == START_R_HEAVY, b};
+}
+__device__ __forceinline__ bool member(const DevSnapshot &s, const Subject &q, uint32_t c) {
+    if (!q.heavy) return c == q.R.x || c == q.R.y || c == q.R.z || c == q.R.w;
+    const uint64_t key = (((uint64_t)q.sidx << 32) | c) + 1;
+    uint32_t b = (uint32_t)mix64(key) & s.probe_mask;
+    for (;;) {  // the table keeps empty slots: every probe sequence ends
+        const uint4 v = s.probe[b];
+        const uint64_t k0 = (uint64_t)v.x | ((uint64_t)v.y << 32), k1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+        if (k0 == key || k1 == key) return true;
+        if (k0 == 0 || k1 == 0) return false;
+        b = (b + 1) & s.probe_mask;
+    }
+}
+
+// the edges [cur, end) of a subject-set row in shard order, through 16-byte windows; the
+// row descriptor holds its first two edges
+struct Edges {
+    const uint32_t *dst;
+    uint32_t cur, end, lo, hi;
+    uint4 w;
+    __device__ __forceinline__ Edges(const DevSnapshot &s, const uint4 &row)
+        : dst(s.set_dst), cur(row.x), end(row.y), lo(row.x), hi(row.x + 2), w(make_uint4(row.z, row.w, 0, 0)) {}
+    __device__ __forceinline__ uint32_t next() {  // caller checks cur < end
+        if (cur < lo || cur >= hi) {
+            w = *win(dst, cur);
+            lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(dst + cur) >> 2) & 3);
+            hi = lo + 4;
+        }
+        return wword(w, cur++ - lo);
+    }
+};
+
+__device__ __forceinline__ unsigned long long tab_key(uint32_t scope, uint32_t vk) {
+    return (((unsigned long long)scope << 32) | vk) + 1ull;
+}
+
+// claim (scope, key) or find it; a second occurrence raises the slot's repeat flag
+__device__ __forceinline__ uint32_t tab_insert(const FrontierParams &P, uint32_t scope, uint32_t vk) {
+    const unsigned long long key = tab_key(scope, vk);
+    uint32_t h = (uint32_t)mix64(key) & P.tmask;
+    for (int probe = 0; probe < 64; probe++) {
+        const unsigned long long old = atomicCAS(&P.tkeys[h], 0ull, key);
+        if (old == 0ull) return h;
+        if (old == key) {
+            P.trep[h] = 1;
+            return h;
+        }
+        h = (h + 1) & P.tmask;
+    }
+    return NONE32;  // crowded: the caller routes the query
+}
+
+// a routed query also saturates its goal count, so the budget atomic of any later spawn refuses
+constexpr uint32_t QG_ROUTED = 0x40000000u;
+__device__ __forceinline__ void route(const FrontierParams &P, uint32_t pos) {
+    P.qroute[pos] = 1;
+    P.qgoals[pos] = QG_ROUTED;
+}
+
+__device__ __forceinline__ void spawn(const FrontierParams &P, uint32_t c, uint32_t node, uint32_t pos, uint32_t word,
+                                      uint32_t scope) {
+    P.g0[c] = make_uint4(node, pos, word, scope);
+}
+
+
+// wave-wide exclusive prefix sum of v; *total = the wave's sum
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t &total) {
+    uint32_t x = v;
+    const uint32_t lane = __lane_id();
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    total = __shfl(x, 63);
+    return x - v;
+}
+
+__global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        P.gbase[0] = 0;
+        P.gcount[0] = P.n;
+    }
+    if (i >= P.n) return;
+    const uint4 r0 = P.start[2 * (size_t)i];
+    const uint32_t d = r0.z & 0xFFFFu;
+    spawn(P, i, r0.x, i, gword(G_IA, d), NONE32);
+    P.qgoals[i] = d > GD_MAX ? QG_ROUTED : 1u;
+    P.qroute[i] = d > GD_MAX ? 1u : 0u;
+}
+
+// One generation: every goal decides what it can and spawns its children into the next.
+template <bool LDS_TABLES>
+__global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const DevSnapshot &s = P.s;
+    const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
+    const uint32_t k = P.gen;
+    const uint32_t base = P.gbase[k];
+    const uint32_t cnt = std::min(P.gcount[k], P.cap - std::min(base, P.cap));
+    const uint32_t nbase = base + cnt;
+    if (blockIdx.x == 0 && threadIdx.x == 0) P.gbase[k + 1] = nbase;
+    const bool last = k + 1 >= MAX_GEN;
+    const uint32_t W = P.max_width;
+    for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
+        const uint32_t j = j0 + threadIdx.x;
+        // goals of queries routed meanwhile still run (rare); they can no longer spawn
+        const bool live = j < cnt;
+        const uint32_t i = base + j;
+        const uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
+        const uint32_t node = g.x, pos = g.y, w = g.z, scope = g.w;
+        const uint32_t d = w & GD_MAX, kind = (w >> 12) & 7u, op = w >> 16;
+        // ---- phase A: decide, or count the children -------------------------------------------
+        uint32_t nc = 0, val = M_NOT;  // value if nc == 0, else the partial (tail) for fr_reduce
+        uint32_t rop = kind == G_INV ? R_NOT : R_FIRST;
+        uint32_t pat = 0;              // per kind: which children (phase B regenerates them)
+        uint4 row = make_uint4(0, 0, 0, 0);
+        uint32_t sc = scope, xrel = 0;
+        if (live) {
+            switch (kind) {
+            case G_IA: {  // checkIsAllowed (engine.go:214-249)
+                if (d == 0) {
+                    val = M_UNK;
+                    break;
+                }
+                const NodeInfo ni = t_node_info(T, node);
+                if (ri_status(ni.ri) == REL_ERROR) {  // :228-232
+                    val = mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, node, ni) << 16);
+                    break;
+                }
+                const bool rw = ri_rw(ni.ri);
+                bool direct = false;
+                if ((!s.strict || !rw) && !(w & GF_SKIP) && d > 1 && !(node & VIRT_BIT))  // :239-243
+                    direct = member(s, load_subject(P, pos), node);
+                const bool es = ri_ss(ni.ri) && d > 1 && !direct;  // :244-246
+                pat = (rw ? 1u : 0u) | (es ? 2u : 0u);
+                xrel = ri_op(ni.ri);
+                nc = (rw ? 1u : 0u) + (es ? 1u : 0u);
+                val = nc == 0 ? (direct ? M_IS : M_NOT) : (direct ? M_IS : NONE32);
+                break;
+            }
+            case G_ES: {  // checkExpandSubject (engine.go:102-164)
+                if (node & VIRT_BIT) break;
+                row = s.set_row[node];
+                if (row.x == row.y) break;
+                const Subject q = load_subject(P, pos);
+                Edges it(s, row);
+                bool found = false;  // found-lookahead over every row (traverser.go:73-80, 109-111)
+                while (it.cur < it.end && !found) found = member(s, q, it.next() & ~EDGE_ALIAS);
+                if (found) {
+                    val = M_IS;
+                    break;
+                }
+                uint32_t keep = row.y - row.x;
+                if (keep > W) keep = W > 0 ? W - 1 : 0;  // results[:maxWidth-1] (engine.go:141-150)
+                if (scope == NONE32) sc = i;              // graph.InitVisited (graph_utils.go:38-43)
+                nc = keep;
+                val = keep ? NONE32 : M_NOT;
+                break;
+            }
+            case G_RW: {  // checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73)
+                if (d == 0) {
+                    val = M_UNK;
+                    break;
+                }
+                const Op o = T.ops[op];
+                const uint32_t okind = (o.type_kind >> 8) & 0xFFu;
+                if (okind == OPK_BAD) {  // :58-59
+                    val = mk_err(KETO_QERR_NOT_IMPLEMENTED);
+                    break;
+                }
+                const bool is_or = okind == OPK_OR;
+                if (!is_or) rop = R_AND;
+                const NodeInfo ni = t_node_info(T, node);
+                uint32_t ncss = 0;
+                if (is_or && ((o.type_kind >> 16) & 1u)) {  // the IN shortcut (rewrites.go:62-92)
+                    const Subject q = load_subject(P, pos);
+                    bool found = false;
+                    for (uint32_t c = 0; c < o.child_count && !found; c++) {
+                        const Op ch = T.ops[T.op_children[o.child_begin + c]];
+                        if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
+                        ncss++;
+                        const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
+                        if (t & VIRT_BIT) continue;
+                        if (s.strict) {  // traverser.go:137-139
+                            const NodeInfo ti = t_node_info(T, t);
+                            if (ri_status(ti.ri) == REL_DECLARED && ri_rw(ti.ri)) continue;
+                        }
+                        found = member(s, q, t);
+                    }
+                    if (found) {
+                        val = M_IS;
+                        break;
+                    }
+                    if (d <= 1) ncss = 0;  // candidates checkIsAllowed(c, d-1 <= 0) are Unknown
+                }
+                // the other children in AST order, up to a leaf that decides the group
+                uint32_t kend = o.child_count, tail = NONE32, ns = 0;
+                for (uint32_t c = 0; c < o.child_count; c++) {
+                    const uint32_t ct = T.ops[T.op_children[o.child_begin + c]].type_kind & 0xFFu;
+                    if (is_or && ct == OP_CSS) continue;
+                    if (ct == OP_REWRITE && d <= 1) {  // nested rewrite at d-1 <= 0: Unknown (:39-42)
+                        if (is_or) continue;
+                        tail = M_NOT;  // AND: the first non-member decides (binop.go:52-54)
+                        kend = c;
+                        break;
+                    }
+                    ns++;
+                }
+                nc = ncss + ns;
+                pat = kend;
+                xrel = ncss;
+                if (nc == 0) val = tail != NONE32 ? tail : ((!is_or && o.child_count > 0) ? M_IS : M_NOT);
+                else val = tail;
+                break;
+            }
+            case G_TTU: {  // checkTupleToSubjectSet (rewrites.go:242-293)
+                const Op o = T.ops[op];
+                const NodeInfo ni = t_node_info(T, node);
+                const uint32_t ts = t_sibling(T, node, ni, o.rel_computed & 0xFFFFu);
+                if ((ts & VIRT_BIT) || d <= 1) break;  // no rows, or every parent check is Unknown
+                row = s.set_row[ts];
+                nc = row.y - row.x;
+                xrel = o.rel_computed >> 16;
+                val = nc ? NONE32 : M_NOT;
+                break;
+            }
+            case G_INV: {  // checkInverted (rewrites.go:136-200)
+                const Op o = T.ops[op];
+                if (o.child_count != 1) {
+                    val = mk_err(KETO_QERR_NOT_IMPLEMENTED);
+                    break;
+                }
+                const uint32_t ct = T.ops[T.op_children[o.child_begin]].type_kind & 0xFFu;
+                if ((ct == OP_CSS || ct == OP_REWRITE) && d == 0) {  // the child is Unknown: NOT keeps it
+                    val = M_UNK;
+                    break;
+                }
+                nc = 1;
+                val = NONE32;
+                break;
+            }
+            default:
+                val = mk_err(KETO_QERR_INTERNAL);
+            }
+        }
+        if (nc > NC_MAX) {  // a row too long for the record: the DFS interpreter takes the query
+            route(P, pos);
+            nc = 0;
+        }
+        // ---- budget and generation cap: one atomic per run of lanes holding goals of one query
+        // (a parent's children are contiguous, so siblings share a run) -----------------------------
+        const uint32_t lane = __lane_id();
+        {
+            const uint32_t key = live ? pos : NONE32;
+            const uint32_t prev = __shfl_up(key, 1);
+            const unsigned long long heads = __ballot(lane == 0 || prev != key);
+            const uint32_t wl = (uint32_t)warpSize - 1u;  // last lane of the wave
+            const uint32_t hl = 63u - (uint32_t)__clzll((long long)(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
+            uint32_t x = nc;  // segmented inclusive sum within the run
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o && lane - o >= hl) x += y;
+            }
+            const unsigned long long after = lane == 63 ? 0ull : (heads >> (lane + 1));
+            const uint32_t tl = after ? lane + (uint32_t)__ffsll((long long)after) - 1u : wl;
+            uint32_t over = 0;
+            if (lane == tl && x) {
+                over = (atomicAdd(&P.qgoals[pos], x) + x > P.budget || last) ? 1u : 0u;
+                if (over) route(P, pos);
+            }
+            if (__shfl(over, tl)) nc = 0;
+        }
+        // ---- allocation: one atomic per block iteration -------------------------------------------
+        __shared__ uint32_t s_woff[2][4], s_base[2];
+        const uint32_t par = (j0 / (gridDim.x * blockDim.x)) & 1u, wid = threadIdx.x >> 6;
+        uint32_t wtot = 0;
+        const uint32_t off = wave_excl(nc, wtot);
+        if (lane == 0) s_woff[par][wid] = wtot;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t sum = 0;
+            for (uint32_t q = 0; q < (blockDim.x + 63) / 64; q++) {
+                const uint32_t t = s_woff[par][q];
+                s_woff[par][q] = sum;
+                sum += t;
+            }
+            s_base[par] = sum ? atomicAdd(&P.gcount[k + 1], sum) : 0u;
+        }
+        __syncthreads();
+        const uint32_t cb = nbase + s_base[par] + s_woff[par][wid] + off;
+        if (nc && (uint64_t)cb + nc > P.cap) {  // arena full: route; fill the allocated slots that exist
+            route(P, pos);
+            for (uint32_t c = cb; c < P.cap && c < cb + nc; c++) spawn(P, c, 0, pos, gword(G_DEAD, 0), NONE32);
+            nc = 0;
+            val = M_NOT;
+        }
+        if (live) {
+            P.gfn[i] = make_uint2(cb, nc | (rop << 24));
+            P.gval[i] = val;
+        }
+        if (!nc) continue;
+        // ---- phase B: write the children ---------------------------------------------------------
+        switch (kind) {
+        case G_IA:
+            if (pat & 1u) spawn(P, cb, node, pos, gword(G_RW, d, xrel), scope);
+            if (pat & 2u) spawn(P, cb + ((pat & 1u) ? 1 : 0), node, pos, gword(G_ES, d - 1), scope);
+            break;
+        case G_ES: {
+            Edges it(s, row);
+            for (uint32_t c = 0; c < nc; c++) {
+                const uint32_t raw = it.next(), cn = raw & ~EDGE_ALIAS;
+                const bool alias = (raw & EDGE_ALIAS) != 0;
+                // CheckAndAddVisited (engine.go:157-160); then checkIsAllowed(c, d, skipDirect) (:161)
+                if (tab_insert(P, sc, alias ? s.vkey[cn] : cn) == NONE32) route(P, pos);
+                spawn(P, cb + c, cn, pos, gword(G_IA, d, 0, GF_SKIP | GF_ESCHILD | (alias ? GF_ALIAS : 0u)), sc);
+            }
+            break;
+        }
+        case G_RW: {
+            const Op o = T.ops[op];
+            const NodeInfo ni = t_node_info(T, node);
+            const bool is_or = ((o.type_kind >> 8) & 0xFFu) == OPK_OR;
+            uint32_t c = cb;
+            if (xrel)  // shortcut candidates checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
+                for (uint32_t k2 = 0; k2 < o.child_count; k2++) {
+                    const Op ch = T.ops[T.op_children[o.child_begin + k2]];
+                    if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
+                    spawn(P, c++, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), pos, gword(G_IA, d - 1, 0, GF_SKIP), scope);
+                }
+            for (uint32_t k2 = 0; k2 < pat; k2++) {  // rewrites.go:95-129
+                const uint32_t ci = T.op_children[o.child_begin + k2];
+                const Op ch = T.ops[ci];
+                const uint32_t ct = ch.type_kind & 0xFFu;
+                if (is_or && ct == OP_CSS) continue;
+                if (ct == OP_REWRITE && d <= 1) continue;  // (OR only: an AND stopped at kend)
+                if (ct == OP_TTU) spawn(P, c++, node, pos, gword(G_TTU, d, ci), scope);
+                else if (ct == OP_CSS)
+                    spawn(P, c++, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), pos, gword(G_IA, d), scope);
+                else if (ct == OP_REWRITE) spawn(P, c++, node, pos, gword(G_RW, d - 1, ci), scope);  // :118
+                else spawn(P, c++, node, pos, gword(G_INV, d, ci), scope);
+            }
+            break;
+        }
+        case G_TTU: {
+            Edges it(s, row);
+            for (uint32_t c = 0; c < nc; c++) {  // each parent: checkIsAllowed(S#computed, d-1) (:279-288)
+                const uint32_t pn = it.next() & ~EDGE_ALIAS;
+                const NodeInfo pi = t_node_info(T, pn);
+                spawn(P, cb + c, t_sibling(T, pn, pi, xrel), pos, gword(G_IA, d - 1), scope);
+            }
+            break;
+        }
+        case G_INV: {
+            const Op o = T.ops[op];
+            const uint32_t ci = T.op_children[o.child_begin];
+            const Op ch = T.ops[ci];
+            const uint32_t ct = ch.type_kind & 0xFFu;
+            if (ct == OP_TTU) spawn(P, cb, node, pos, gword(G_TTU, d, ci), scope);
+            else if (ct == OP_CSS) {
+                const NodeInfo ni = t_node_info(T, node);
+                spawn(P, cb, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), pos, gword(G_IA, d), scope);
+            } else if (ct == OP_REWRITE) spawn(P, cb, node, pos, gword(G_RW, d, ci), scope);  // keeps depth (:171)
+            else spawn(P, cb, node, pos, gword(G_INV, d, ci), scope);
+            break;
+        }
+        default:
+            break;
+        }
+    }
+}
+
+// One generation, bottom-up: each goal reduces its children in add order (checkgroup H0,
+// binop.go, rewrites.go:183-199); a decisive occurrence of a repeated scope key routes the
+// query; generation 0 writes the decisions.  Every goal of the generation was expanded in
+// this batch, so its children range is always this batch's.
+__global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
+    const DevSnapshot &s = P.s;
+    const uint32_t k = P.gen;
+    const uint32_t base = P.gbase[k];
+    const uint32_t cnt = std::min(P.gcount[k], P.cap - std::min(base, P.cap));
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
+        const uint32_t i = base + j;
+        const uint2 fn = P.gfn[i];
+        uint32_t val = P.gval[i];
+        const uint32_t nc = fn.y & NC_MAX, rop = fn.y >> 24;
+        if (nc) {
+            uint32_t res = NONE32;
+            for (uint32_t c = fn.x; c < fn.x + nc; c++) {
+                const uint32_t cv = P.gval[c];
+                if (rop == R_FIRST) {  // first Err / IsMember
+                    if (decisive(cv)) {
+                        res = cv;
+                        break;
+                    }
+                } else if (rop == R_AND) {  // AND: the first non-member, keeping its error
+                    if ((cv >> 8) != 0 || (cv & 3u) != M_IS) {
+                        res = (cv & ~3u) | M_NOT;
+                        break;
+                    }
+                } else {  // NOT swaps IsMember / NotMember, keeps Unknown and the error
+                    const uint32_t m = cv & 3u;
+                    res = m == M_IS ? ((cv & ~3u) | M_NOT) : (m == M_NOT ? ((cv & ~3u) | M_IS) : cv);
+                }
+            }
+            if (res == NONE32) res = val != NONE32 ? val : (rop == R_AND ? M_IS : M_NOT);
+            val = res;
+            P.gval[i] = val;
+        }
+        if (k > 0 && decisive(val)) {  // an ES child: was its key repeated in the scope?
+            const uint4 g = P.g0[i];
+            if (((g.z >> 12) & 7u) == G_IA && (g.z & GF_ESCHILD)) {  // (other kinds hold an op there)
+                const unsigned long long key = tab_key(g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x);
+                uint32_t h = (uint32_t)mix64(key) & P.tmask;
+                for (int probe = 0; probe < 64; probe++) {
+                    const unsigned long long kk = P.tkeys[h];
+                    if (kk == key) {
+                        if (P.trep[h]) route(P, g.y);
+                        break;
+                    }
+                    if (kk == 0ull) break;  // not inserted (crowded): the query was routed then
+                    h = (h + 1) & P.tmask;
+                }
+            }
+        }
+        if (k == 0) {  // generation 0 holds query position j
+            if (P.qroute[j]) {
+                P.fb_list[atomicAdd(P.fb_count, 1u)] = j;
+                continue;
+            }
+            const uint32_t q = P.start[2 * (size_t)j].w;
+            const uint32_t err = val >> 8;
+            P.out_allowed[q] = (err == 0 && (val & 3u) == M_IS) ? 1 : 0;
+            P.out_err[q] = (int32_t)(P.err_detail ? err : err & 0xFFu);
+        }
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// host
+
+static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+
+#ifndef KETO_FR_GOALS_PER_QUERY
+#define KETO_FR_GOALS_PER_QUERY 256
+#endif
+
+void ensure_frontier(FrontierScratch &f, uint64_t n) {
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n * KETO_FR_GOALS_PER_QUERY, 1u << 20), 1ull << 29);
+    if (f.mem && f.cap >= want && f.ncap >= n) return;
+    if (f.mem) KETO_HIP(hipFree(f.mem));
+    f.mem = nullptr;
+    const uint64_t cap = std::max<uint64_t>(want, f.cap);
+    const uint64_t ncap = std::max<uint64_t>(n, f.ncap);
+    uint64_t tcap = 1;
+    while (tcap < cap / 2) tcap <<= 1;
+    const size_t ctrl = al256(FR_CTRL_BYTES);
+    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 4) + al256(tcap * 9);
+    KETO_HIP(hipMalloc(&f.mem, bytes));
+    char *p = static_cast<char *>(f.mem);
+    f.ctrl = reinterpret_cast<uint32_t *>(p);
+    f.fb_count = f.ctrl + 2 * (MAX_GEN + 2);
+    p += ctrl;
+    f.qgoals = reinterpret_cast<uint32_t *>(p);
+    f.qroute = f.qgoals + ncap;
+    f.fb_list = f.qroute + ncap;
+    p += al256(ncap * 12);
+    f.g0 = reinterpret_cast<uint4 *>(p);
+    p += al256(cap * 16);
+    f.gfn = reinterpret_cast<uint2 *>(p);
+    p += al256(cap * 8);
+    f.gval = reinterpret_cast<uint32_t *>(p);
+    p += al256(cap * 4);
+    f.tkeys = reinterpret_cast<unsigned long long *>(p);
+    f.trep = reinterpret_cast<uint8_t *>(f.tkeys + tcap);
+    // the table starts empty and is emptied after every batch
+    KETO_HIP(hipMemset(f.tkeys, 0, tcap * 9));
+    KETO_HIP(hipDeviceSynchronize());
+    f.cap = cap;
+    f.ncap = ncap;
+    f.tcap = tcap;
+    if (!f.host_ctrl) KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&f.host_ctrl), 2 * (MAX_GEN + 2) * 4 + 16, 0));
+}
+
+uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
+    FrontierScratch &f = st.frontier;
+    ensure_frontier(f, L.n);
+    const uint32_t cus = (uint32_t)num_cus(s.device);
+    const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
+    const size_t lds = lds_tables ? s.dev.lds_bytes : 0;
+    uint32_t *gbase = f.ctrl, *gcount = f.ctrl + (MAX_GEN + 2), *fb_count = f.fb_count;
+    KETO_HIP(hipMemsetAsync(f.ctrl, 0, FR_CTRL_BYTES, st.stream));
+    FrontierParams P{};
+    P.s = s.dev;
+    P.start = st.resolved;
+    P.n = (uint32_t)L.n;
+    P.g0 = f.g0;
+    P.gfn = f.gfn;
+    P.gval = f.gval;
+    P.cap = (uint32_t)f.cap;
+    P.gbase = gbase;
+    P.gcount = gcount;
+    P.qgoals = f.qgoals;
+    P.qroute = f.qroute;
+    const char *be = getenv("KETO_FR_BUDGET");
+    P.budget = be ? (uint32_t)std::max(1, atoi(be)) : 1024u;
+    P.tkeys = f.tkeys;
+    P.trep = f.trep;
+    P.tmask = (uint32_t)(f.tcap - 1);
+    P.max_width = (uint32_t)L.max_width;
+    P.out_allowed = L.out_allowed;
+    P.out_err = L.out_err;
+    P.err_detail = L.err_detail;
+    P.fb_list = f.fb_list;
+    P.fb_count = fb_count;
+    constexpr uint32_t BLOCK = 256;
+    hipLaunchKernelGGL(fr_init, dim3((uint32_t)((L.n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st.stream, P);
+    KETO_HIP(hipGetLastError());
+    // expansion: generations until one is empty; the goal counts are read back every CHUNK
+    const dim3 eg(cus * 8), eb(BLOCK);
+    constexpr uint32_t CHUNK = 12;
+    uint32_t gens = 0;
+    uint32_t *hc = f.host_ctrl;
+    for (uint32_t k = 0; gens == 0;) {
+        const uint32_t kend = std::min(k + CHUNK, MAX_GEN);
+        for (; k < kend; k++) {
+            P.gen = k;
+            if (lds_tables) hipLaunchKernelGGL(fr_expand<true>, eg, eb, lds, st.stream, P);
+            else hipLaunchKernelGGL(fr_expand<false>, eg, eb, 0, st.stream, P);
+            KETO_HIP(hipGetLastError());
+        }
+        KETO_HIP(hipMemcpyAsync(hc, f.ctrl, 2 * (MAX_GEN + 2) * 4, hipMemcpyDeviceToHost, st.stream));
+        KETO_HIP(hipStreamSynchronize(st.stream));
+        for (uint32_t g = 0; g <= k && g <= MAX_GEN; g++)
+            if (hc[(MAX_GEN + 2) + g] == 0) {
+                gens = g;
+                break;
+            }
+        if (gens == 0 && k >= MAX_GEN) gens = MAX_GEN;  // the last generation spawned nothing (routed)
+    }
+    // reduction, deepest generation first
+    for (int32_t g = (int32_t)gens - 1; g >= 0; g--) {
+        const uint32_t c = std::min<uint32_t>(hc[(MAX_GEN + 2) + g], (uint32_t)f.cap - std::min<uint32_t>(hc[g], (uint32_t)f.cap));
+        P.gen = (uint32_t)g;
+        const dim3 rg(std::max<uint32_t>(1, std::min<uint32_t>((c + BLOCK - 1) / BLOCK, cus * 16)));
+        hipLaunchKernelGGL(fr_reduce, rg, eb, 0, st.stream, P);
+        KETO_HIP(hipGetLastError());
+    }
+    const uint32_t top = std::min<uint32_t>(hc[gens], (uint32_t)f.cap);
+    KETO_HIP(hipMemsetAsync(f.tkeys, 0, f.tcap * 9, st.stream));
+    KETO_HIP(hipMemcpyAsync(hc, fb_count, 4, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipStreamSynchronize(st.stream));
+    f.last_gens = gens;
+    f.last_goals = top;
+    f.last_routed = hc[0];
+    f.stats.batches++;
+    f.stats.queries += L.n;
+    f.stats.routed += hc[0];
+    f.stats.goals += top;
+    f.stats.generations += gens;
+    f.stats.max_generations = std::max<uint64_t>(f.stats.max_generations, gens);
+    static const bool verbose = getenv("KETO_FR_VERBOSE") != nullptr;
+    if (verbose) {
+        fprintf(stderr, "[frontier] n %llu generations %u goals %u routed %u:", (unsigned long long)L.n, gens, top, hc[0]);
+        for (uint32_t g = 0; g < gens; g++) fprintf(stderr, " %u", f.host_ctrl[(MAX_GEN + 2) + g]);
+        fprintf(stderr, "\n");
+    }
+    return hc[0];
+}
+
+}  // namespace keto

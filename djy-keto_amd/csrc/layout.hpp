@@ -95,6 +95,7 @@ constexpr uint32_t WEIGHT_ROUNDS = 12;     // path-count relaxation rounds (> ty
 constexpr uint32_t WEIGHT_CAP = 1u << 20;
 constexpr uint32_t HEAVY_WEIGHT = 32;      // roots at or above this weight are scheduled first
 constexpr uint32_t START_HEAVY = 1u << 31;  // start record: subject row answered by the probe hash
+constexpr uint32_t START_R_HEAVY = 0xFFFFFFFEu;  // second start record of a heavy subject: {subject, this, -, -}
 constexpr uint32_t PROBE_K = 4;           // VGPR-resident reverse row capacity (<= 4: two windows)
 constexpr uint32_t LDS_TABLE_LIMIT = 48 * 1024;
 

@@ -90,6 +90,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
             R.z = len > 2 ? w8(v0, v1, o + 2) : NONE32;
             R.w = len > 3 ? w8(v0, v1, o + 3) : NONE32;
         }
+        // the second record is the whole subject test: its reverse row, or {subject, START_R_HEAVY}
+        if (heavy) R = make_uint4(sidx, START_R_HEAVY, NONE32, NONE32);
         // x root, y subject index, z depth | hash-probe flag, w query index
         r0 = make_uint4(root, sidx, d | (heavy ? START_HEAVY : 0u), i);
         heavy_cls = wgt >= HEAVY_WEIGHT;

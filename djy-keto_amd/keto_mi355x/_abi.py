@@ -52,6 +52,11 @@ class WorkCounters(ctypes.Structure):
                 ("wave_steps", ctypes.c_uint64 * 3), ("lane_steps", ctypes.c_uint64 * 3)]
 
 
+class FrontierStats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in ("batches", "queries", "routed", "goals", "generations",
+                                               "max_generations")]
+
+
 class DispatcherConfig(ctypes.Structure):
     _fields_ = [("limits", Limits), ("max_batch", ctypes.c_uint32), ("max_wait_us", ctypes.c_uint32),
                 ("inflight", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
@@ -96,6 +101,7 @@ SIGNATURES = {
     "keto_stream_sync": (ctypes.c_int, [_VP]),
     "keto_stream_counters": (ctypes.c_int, [_VP, ctypes.POINTER(WorkCounters), _I32]),
     "keto_stream_last_kernel_ms": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double)]),
+    "keto_stream_frontier_stats": (ctypes.c_int, [_VP, ctypes.POINTER(FrontierStats), _I32]),
     "keto_stream_kernel_time": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64), _I32]),
     "keto_check_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),
     "keto_expand_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _U64, _VP, _VP]),

@@ -147,6 +147,12 @@ class Stream:
         out["per_tier"] = per
         return out
 
+    def frontier_stats(self, reset: bool = False) -> dict:
+        """frontier-engine activity on this stream (keto_stream_frontier_stats)"""
+        c = _abi.FrontierStats()
+        check(lib().keto_stream_frontier_stats(self.handle, ctypes.byref(c), int(reset)))
+        return {k: int(getattr(c, k)) for k, _ in c._fields_}
+
     def kernel_time(self, reset: bool = False) -> tuple:
         """(summed main-kernel ms, launches) timed with HIP events on this stream"""
         ms, n = ctypes.c_double(), ctypes.c_uint64()

@@ -166,6 +166,14 @@ int keto_stream_counters(keto_stream *s, keto_work_counters *out, int32_t reset)
 /* average device time (ms) of the last batch's main check kernel, measured with
  * HIP events on the stream the kernel ran on */
 int keto_stream_last_kernel_ms(keto_stream *s, double *ms);
+/* Frontier-engine activity on the stream (check batches of rewrite snapshots): batches, the
+ * queries they held, the queries routed to the DFS interpreter (a repeated visited key with a
+ * decisive occurrence, the goal budget, the generation cap or the arena), goals spawned and
+ * generations run (sum and max).  reset != 0 zeroes them afterwards. */
+typedef struct keto_frontier_stats {
+    uint64_t batches, queries, routed, goals, generations, max_generations;
+} keto_frontier_stats;
+int keto_stream_frontier_stats(keto_stream *s, keto_frontier_stats *out, int32_t reset);
 /* Synchronises the stream, then reports the summed device time (ms) and count of the main
  * check kernel launches timed on it (HIP events around every batch's launch, async batches
  * included); reset != 0 zeroes the sums afterwards. */

@@ -861,6 +861,332 @@ int rs_check_ex(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, uint32
 }
 
 /* ------------------------------------------------------------------ */
+/* Frontier semantics: the spec of the product's frontier engine (csrc/frontier.hip)         */
+/*
+ * U = the recursion above evaluated WITHOUT visited pruning.  Each check is a goal; a goal
+ * spawns every sub-check of its group unless a result known when the goal is expanded
+ * already decides it (a shortcut IN hit, a found-lookahead hit, a direct tuple) or a known
+ * leaf result ends the group in add order.  Groups still reduce in add order (first Err /
+ * IsMember; AND: first non-IsMember), so U is a pure function of the snapshot.
+ *
+ * Claim: if every key that a visited scope of U's goal tree receives more than once has
+ * only non-decisive occurrences (U-value NotMember / Unknown), the eager DFS above
+ * (rs_check) returns U's result.  Its explored tree is a subtree of U's with the same
+ * scopes, and it only ever prunes an ES child whose key the scope already holds, i.e. an
+ * occurrence of a repeated key.  By induction from the leaves every check it evaluates has
+ * its U-value: a pruned child is non-decisive in U, and dropping a non-decisive child does
+ * not change a first-decisive reduction (pruning happens only in ES loops, which reduce that
+ * way).  Queries with a decisive occurrence of a repeated key, or with more than `budget`
+ * goals, are "routed": the product runs them on the DFS interpreter instead.  Goal counting
+ * and spawn rules here are the engine's exactly, so routing flags compare one to one.
+ */
+typedef struct {
+    uint64_t vk;
+    uint32_t scope, used; /* used: occurrences of (scope, key) */
+    uint32_t decisive;    /* some occurrence evaluated to IsMember / an error */
+    uint32_t pad;
+} upair;
+
+typedef struct {
+    qctx *c;
+    upair *set;
+    size_t cap, cnt;
+    uint32_t goals, budget, scopes, maxgen;
+    int routed;
+} uctx;
+
+#define U_NONE 0xFFFFFFFFu
+
+/* insert (scope, key) or count another occurrence; returns its slot */
+static size_t u_insert(uctx *u, uint32_t scope, uint64_t vk) {
+    if (2 * (u->cnt + 1) > u->cap) {
+        size_t nc = u->cap ? u->cap * 2 : 64;
+        upair *ns = calloc(nc, sizeof *ns);
+        for (size_t i = 0; i < u->cap; i++) {
+            if (!u->set[i].used) continue;
+            size_t h = mix64(u->set[i].vk ^ ((uint64_t)u->set[i].scope << 17)) & (nc - 1);
+            while (ns[h].used) h = (h + 1) & (nc - 1);
+            ns[h] = u->set[i];
+        }
+        free(u->set);
+        u->set = ns;
+        u->cap = nc;
+    }
+    size_t h = mix64(vk ^ ((uint64_t)scope << 17)) & (u->cap - 1);
+    while (u->set[h].used) {
+        if (u->set[h].vk == vk && u->set[h].scope == scope) {
+            u->set[h].used++;
+            return h;
+        }
+        h = (h + 1) & (u->cap - 1);
+    }
+    u->set[h].vk = vk;
+    u->set[h].scope = scope;
+    u->set[h].used = 1;
+    u->cnt++;
+    return h;
+}
+
+static size_t u_insert_find(uctx *u, uint32_t scope, uint64_t vk) {
+    size_t h = mix64(vk ^ ((uint64_t)scope << 17)) & (u->cap - 1);
+    while (!(u->set[h].vk == vk && u->set[h].scope == scope)) h = (h + 1) & (u->cap - 1);
+    return h;
+}
+
+/* one more goal for this query; 0 once the budget is exceeded (the query is routed) */
+static int u_spawn(uctx *u, uint32_t gen) {
+    if (u->routed) return 0;
+    if (++u->goals > u->budget) {
+        u->routed = 1;
+        return 0;
+    }
+    if (gen > u->maxgen) u->maxgen = gen;
+    return 1;
+}
+
+static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, uint32_t scope, uint32_t gen);
+static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen);
+
+/* a rewrite child (check_child): 1 = spawned as a goal (result in *out), 0 = a leaf result */
+static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, uint32_t scope, uint32_t gen,
+                   res *out);
+
+static res u_ttu(uctx *u, uint32_t ns, uint32_t obj, const rs_ast *a, int d, uint32_t scope, uint32_t gen) {
+    const rs_db *db = u->c->db;
+    size_t lo, hi;
+    node_rows(db, ns, obj, a->rel, &lo, &hi);
+    res out = R_NOT;
+    int have = 0;
+    if (d - 1 <= 0) return R_NOT; /* every parent check is Unknown (engine.go:215-220) */
+    for (size_t i = lo; i < hi; i++) {
+        const key7 *t = ROW(db, i);
+        if (t->kind != 1) continue;
+        if (!u_spawn(u, gen + 1)) return R_NOT;
+        res r = u_ia(u, t->sns, t->sid, a->computed, d - 1, 0, scope, gen + 1);
+        if (!have && decisive(r)) {
+            out = r;
+            have = 1;
+        }
+    }
+    return out;
+}
+
+static res u_inv(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen) {
+    const rs_ast *a = &u->c->db->ast[ai];
+    if (a->child_count != 1) {
+        res r = {RS_UNKNOWN, RS_ERR_NOT_IMPLEMENTED};
+        return r;
+    }
+    res r;
+    u_child(u, ns, obj, u->c->db->children[a->child_begin], d, 0, scope, gen, &r);
+    if (r.m == RS_IS_MEMBER) r.m = RS_NOT_MEMBER;
+    else if (r.m == RS_NOT_MEMBER) r.m = RS_IS_MEMBER;
+    return r;
+}
+
+static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, uint32_t scope, uint32_t gen,
+                   res *out) {
+    const rs_ast *ch = &u->c->db->ast[ci];
+    *out = R_UNK;
+    switch (ch->type) {
+    case RS_TTU:
+        if (d < 0 || !u_spawn(u, gen + 1)) return 0;
+        *out = u_ttu(u, ns, obj, ch, d, scope, gen + 1);
+        return 1;
+    case RS_CSS:
+        if (d <= 0 || !u_spawn(u, gen + 1)) return 0;
+        *out = u_ia(u, ns, obj, ch->rel, d, 0, scope, gen + 1);
+        return 1;
+    case RS_REWRITE:
+        if (d - cost <= 0 || !u_spawn(u, gen + 1)) return 0;
+        *out = u_rw(u, ns, obj, ci, d - cost, scope, gen + 1);
+        return 1;
+    case RS_INVERT:
+        if (d < 0 || !u_spawn(u, gen + 1)) return 0;
+        *out = u_inv(u, ns, obj, ci, d, scope, gen + 1);
+        return 1;
+    default:
+        out->err = RS_ERR_NOT_IMPLEMENTED;
+        return 0;
+    }
+}
+
+static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen) {
+    const rs_db *db = u->c->db;
+    const rs_ast *a = &db->ast[ai];
+    if (a->op != RS_OP_OR && a->op != RS_OP_AND) {
+        res r = {RS_UNKNOWN, RS_ERR_NOT_IMPLEMENTED};
+        return r;
+    }
+    const int is_or = a->op == RS_OP_OR;
+    res out = R_NOT;
+    int have = 0; /* the group's result is fixed (by a child in add order) */
+    if (is_or) {
+        int has_css = 0, found = 0;
+        for (int k = 0; k < a->child_count; k++) {
+            const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+            if (ch->type != RS_CSS) continue;
+            has_css = 1;
+            int err;
+            int ri = ast_relation_for(db, ns, ch->rel, &err);
+            if (db->strict && ri >= 0 && db->rels[ri].rewrite >= 0) continue;
+            if (!found && exists(u->c, ns, obj, ch->rel)) found = 1;
+        }
+        if (found) return R_IS;
+        if (has_css && d - 1 > 0)
+            for (int k = 0; k < a->child_count; k++) {
+                const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+                if (ch->type != RS_CSS) continue;
+                if (!u_spawn(u, gen + 1)) return R_NOT;
+                res r = u_ia(u, ns, obj, ch->rel, d - 1, 1, scope, gen + 1);
+                if (!have && decisive(r)) {
+                    out = r;
+                    have = 1;
+                }
+            }
+    }
+    for (int k = 0; k < a->child_count; k++) {
+        int ci = db->children[a->child_begin + k];
+        if (is_or && db->ast[ci].type == RS_CSS) continue;
+        res r;
+        const int spawned = u_child(u, ns, obj, ci, d, 1, scope, gen, &r);
+        if (u->routed) return R_NOT;
+        const int dec = is_or ? decisive(r) : (r.err || r.m != RS_IS_MEMBER);
+        if (!have && dec) {
+            out = r;
+            if (!is_or) out.m = RS_NOT_MEMBER;
+            have = 1;
+        }
+        if (!spawned && dec) break; /* a leaf decides the group: later children are never spawned */
+    }
+    if (!have) out = (!is_or && a->child_count > 0) ? R_IS : R_NOT;
+    return out;
+}
+
+static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen) {
+    const rs_db *db = u->c->db;
+    size_t lo, hi;
+    node_rows(db, ns, obj, rel, &lo, &hi);
+    size_t nres = 0;
+    for (size_t i = lo; i < hi; i++) {
+        const key7 *t = ROW(db, i);
+        if (t->kind != 1) continue;
+        nres++;
+        if (exists(u->c, t->sns, t->sid, t->srel)) return R_IS;
+    }
+    size_t keep = nres;
+    if ((long)nres > (long)db->max_width) keep = db->max_width > 0 ? (size_t)(db->max_width - 1) : 0;
+    if (scope == U_NONE) scope = u->scopes++;
+    res out = R_NOT;
+    int have = 0;
+    for (size_t i = lo; i < hi && keep; i++) {
+        const key7 *t = ROW(db, i);
+        if (t->kind != 1) continue;
+        keep--;
+        const uint64_t vk = vkey(db, t->sns, t->sid, t->srel);
+        u_insert(u, scope, vk);
+        if (!u_spawn(u, gen + 1)) return R_NOT;
+        res r = u_ia(u, t->sns, t->sid, t->srel, d, 1, scope, gen + 1);
+        if (decisive(r)) u->set[u_insert_find(u, scope, vk)].decisive = 1; /* the table may have grown */
+        if (!have && decisive(r)) {
+            out = r;
+            have = 1;
+        }
+    }
+    return out;
+}
+
+static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, uint32_t scope, uint32_t gen) {
+    if (d <= 0) return R_UNK;
+    const rs_db *db = u->c->db;
+    int err;
+    int ri = ast_relation_for(db, ns, rel, &err);
+    if (err) {
+        res r = {RS_UNKNOWN, err};
+        return r;
+    }
+    const int has_rewrite = ri >= 0 && db->rels[ri].rewrite >= 0;
+    const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
+    res rr = R_NOT, er = R_NOT;
+    if (has_rewrite && u_spawn(u, gen + 1)) rr = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
+    const int direct_is = (!db->strict || !has_rewrite) && !skip && d - 1 > 0 && exists(u->c, ns, obj, rel);
+    if (can_ss && !direct_is && d - 1 > 0 && u_spawn(u, gen + 1)) er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
+    if (decisive(rr)) return rr;
+    if (direct_is) return R_IS;
+    if (decisive(er)) return er;
+    return R_NOT;
+}
+
+int rs_check_u(rs_db *db, const rs_query *q, uint32_t budget, int32_t *err, uint32_t *routed, uint32_t *goals,
+               uint32_t *gens) {
+    rs_stats dummy = {0, 0, 0, 0};
+    qctx c = {db, q->kind, q->sid, q->kind == 1 ? q->sns : 0, q->kind == 1 ? q->srel : 0, &dummy, 0, SCHED_EAGER, 0};
+    uctx u;
+    memset(&u, 0, sizeof u);
+    u.c = &c;
+    u.budget = budget;
+    int d = q->depth;
+    if (d <= 0 || db->max_depth < d) d = db->max_depth; /* engine.go:82-84 */
+    res r = R_NOT;
+    if (u_spawn(&u, 0)) r = u_ia(&u, q->ns, q->obj, q->rel, d, 0, U_NONE, 0);
+    for (size_t i = 0; i < u.cap; i++)
+        if (u.set[i].used > 1 && u.set[i].decisive) u.routed = 1;
+    free(u.set);
+    if (err) *err = r.err;
+    if (routed) *routed = (uint32_t)u.routed;
+    if (goals) *goals = u.goals;
+    if (gens) *gens = u.maxgen + 1;
+    return r.m;
+}
+
+typedef struct {
+    rs_db *db;
+    const rs_query *q;
+    size_t n;
+    uint32_t budget;
+    uint8_t *decision;
+    int32_t *err;
+    uint32_t *routed, *goals, *gens;
+    atomic_size_t next;
+} ubatch_job;
+
+static void *ubatch_worker(void *arg) {
+    ubatch_job *j = arg;
+    for (;;) {
+        size_t i = atomic_fetch_add(&j->next, 64);
+        if (i >= j->n) break;
+        size_t e = i + 64 < j->n ? i + 64 : j->n;
+        for (; i < e; i++) {
+            int32_t er = 0;
+            int m = rs_check_u(j->db, &j->q[i], j->budget, &er, &j->routed[i], &j->goals[i], &j->gens[i]);
+            j->decision[i] = (er == 0 && m == RS_IS_MEMBER);
+            j->err[i] = er;
+        }
+    }
+    return NULL;
+}
+
+void rs_check_u_batch(rs_db *db, const rs_query *q, size_t n, int threads, uint32_t budget, uint8_t *decision,
+                      int32_t *err, uint32_t *routed, uint32_t *goals, uint32_t *gens) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    ubatch_job j;
+    j.db = db;
+    j.q = q;
+    j.n = n;
+    j.budget = budget;
+    j.decision = decision;
+    j.err = err;
+    j.routed = routed;
+    j.goals = goals;
+    j.gens = gens;
+    atomic_init(&j.next, 0);
+    pthread_t th[256];
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, ubatch_worker, &j);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+}
+
+/* ------------------------------------------------------------------ */
 /* batch (CPU baseline)                                                  */
 
 typedef struct {

@@ -128,6 +128,15 @@ int rs_check_ex(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, uint32
 void rs_check_batch_ex(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t *decision,
                        int32_t *err, uint32_t *flags, rs_stats *st);
 
+/* Frontier semantics (refsem.c "Frontier semantics"; the spec of csrc/frontier.hip): the
+ * query evaluated without visited pruning.  *routed = 1 when a visited scope would receive a
+ * key twice or the query spawns more than `budget` goals -- only then may the result differ
+ * from rs_check's.  *goals = goals spawned, *gens = goal-tree generations. */
+int rs_check_u(rs_db *db, const rs_query *q, uint32_t budget, int32_t *err, uint32_t *routed, uint32_t *goals,
+               uint32_t *gens);
+void rs_check_u_batch(rs_db *db, const rs_query *q, size_t n, int threads, uint32_t budget, uint8_t *decision,
+                      int32_t *err, uint32_t *routed, uint32_t *goals, uint32_t *gens);
+
 /* Rows of every object within `levels` subject-set hops of (ns[i], obj[i]) (the SQL-mode
  * baseline's store, oracle/refsql.py): pos = the row's rank in the index, which keeps every
  * (ns, obj, rel)'s shard order.  Returns the count; only the first cap are written. */

@@ -70,6 +70,9 @@ def lib():
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.rs_check_batch_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Stats)]
+        L.rs_check_u_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]
         L.rs_expand.restype = ctypes.c_long
         L.rs_expand.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
@@ -357,6 +360,19 @@ class Oracle:
         lib().rs_check_batch_ex(self.db, q.ctypes.data, len(q), threads, dec.ctypes.data, err.ctypes.data,
                                 flags.ctypes.data, ctypes.byref(st))
         return dec, err, flags, st
+
+    def check_u_batch(self, queries: np.ndarray, threads: int, budget: int = 1024):
+        """frontier semantics (refsem.h rs_check_u): decisions, errors, routed flags, goals and
+        goal-tree generations per query"""
+        q = np.ascontiguousarray(queries)
+        self._check_ids(q)
+        n = len(q)
+        dec = np.zeros(n, dtype=np.uint8)
+        err = np.zeros(n, dtype=np.int32)
+        routed, goals, gens = (np.zeros(n, dtype=np.uint32) for _ in range(3))
+        lib().rs_check_u_batch(self.db, q.ctypes.data, n, threads, budget, dec.ctypes.data, err.ctypes.data,
+                               routed.ctypes.data, goals.ctypes.data, gens.ctypes.data)
+        return dec, err, routed, goals, gens
 
     def expand(self, kind, sid, sns, srel, depth, cap=1 << 16):
         out = np.zeros(cap, dtype=TREE_DT)

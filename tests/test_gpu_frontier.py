@@ -1,0 +1,114 @@
+"""Frontier engine (csrc/frontier.hip) against the oracle.
+
+A check batch on a rewrite snapshot runs breadth-first: one goal per sub-check, evaluated
+without visited pruning (oracle/refsem.c "Frontier semantics", rs_check_u), and the queries
+whose result could depend on pruning are routed to the DFS interpreter.  The decisions must be
+the oracle's canonical ones (rs_check) for every query; the routed count and, where nothing is
+routed, the number of goals spawned must equal the oracle's restatement of the engine's rules
+(rs_check_u) -- so the spawn rules themselves are pinned, not only the answers."""
+import os
+
+import numpy as np
+import pytest
+
+import keto_mi355x as km
+import refsem
+from product_helpers import product_snapshot, queries_to_oracle, queries_to_product, world_from_workload
+from randworld import random_world
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def stream():
+    s = km.Stream(0)
+    yield s
+    s.close()
+
+
+@pytest.fixture
+def budget():
+    old = os.environ.get("KETO_FR_BUDGET")
+
+    def set_budget(b):
+        os.environ["KETO_FR_BUDGET"] = str(b)
+        return b
+
+    yield set_budget
+    if old is None:
+        os.environ.pop("KETO_FR_BUDGET", None)
+    else:
+        os.environ["KETO_FR_BUDGET"] = old
+
+
+def _frontier_batch(stream, eng, q):
+    stream.frontier_stats(reset=True)
+    allowed, err = eng.check_batch(q)
+    return allowed, err, stream.frontier_stats(reset=True)
+
+
+@pytest.mark.parametrize("b", [1024, 6])
+@pytest.mark.parametrize("seed", list(range(60)))
+def test_random_worlds_frontier_vs_oracle(stream, budget, seed, b):
+    budget(b)
+    w, t, q, _ = random_world(seed, rewrites=True)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(w.max_depth, w.max_width)
+    dec, err, _ = orc.check_batch(q, threads=4)
+    udec, uerr, routed, goals, _ = orc.check_u_batch(q, threads=4, budget=b)
+    # the restatement's claim: unrouted queries decide as the canonical DFS does
+    ok = routed == 0
+    np.testing.assert_array_equal(udec[ok], dec[ok])
+    np.testing.assert_array_equal(uerr[ok], err[ok])
+    snap = product_snapshot(w, t)
+    eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+    allowed, gerr, fs = _frontier_batch(stream, eng, queries_to_product(q))
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    if fs["batches"] == 0:  # a world without rewrites: the union kernel (check_union.hip) ran
+        return
+    assert fs["batches"] == 1 and fs["queries"] == len(q)
+    assert fs["routed"] == int(routed.sum())
+    if not routed.any():
+        assert fs["goals"] == int(goals.sum())
+
+
+def test_drive_small_frontier_vs_oracle(stream):
+    from keto_mi355x import synth
+    wl = synth.drive(depth=6, n_groups=3000, n_users=8000, seed=4)
+    q = synth.drive_queries(wl, 20_000, seed=3)
+    q["max_depth"][:500] = np.random.default_rng(1).integers(1, 6, 500)  # truncation sub-batch
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    w, t = world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    qo = queries_to_oracle(q)
+    dec, err, _ = orc.check_batch(qo, threads=8)
+    _, _, routed, goals, gens = orc.check_u_batch(qo, threads=8, budget=1024)
+    eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    allowed, gerr, fs = _frontier_batch(stream, eng, q)
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    assert fs["routed"] == int(routed.sum())
+    assert fs["max_generations"] == int(gens.max())
+    if not routed.any():
+        assert fs["goals"] == int(goals.sum())
+    assert fs["routed"] < 0.01 * len(q)
+
+
+def test_every_query_routed_matches_oracle(stream, budget):
+    """budget 1: every query with a sub-check goes to the DFS interpreter through the routed list"""
+    from keto_mi355x import synth
+    budget(1)
+    wl = synth.drive(depth=5, n_groups=500, n_users=2000, seed=8)
+    q = synth.drive_queries(wl, 4096, seed=5)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    w, t = world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    dec, err, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+    eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    allowed, gerr, fs = _frontier_batch(stream, eng, q)
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    assert fs["routed"] == len(q)

@@ -5,6 +5,8 @@ KETO_GUARD=1, every lane runs exactly one transition per load slot, so every pse
 transition crosses a step boundary -- the path a lane takes on the GPU when its 24-transition
 budget runs out.  The GPU parity suite (golden fixtures + random worlds) must still agree with
 the oracle.  Without the S_FSCAN rule in check.hip's transition loop 41 of those cases failed.
+The frontier engine's tests (test_gpu_frontier.py) run in the same emulation: one-lane waves
+and blocks, so its wave-level scans and block allocation take their degenerate paths.
 """
 import os
 import subprocess
@@ -24,7 +26,8 @@ def test_one_transition_per_step_matches_oracle(tmp_path):
                    check=True, timeout=600)
     env = dict(os.environ, KETO_MI355X_ALLOW_OVERRIDE="tools", KETO_MI355X_LIB_OVERRIDE=str(lib))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
-                        os.path.join(ROOT, "tests", "test_gpu_parity.py"), "-k", "golden or random_worlds or synthetic_small"],
+                        os.path.join(ROOT, "tests", "test_gpu_parity.py"), os.path.join(ROOT, "tests", "test_gpu_frontier.py"),
+                        "-k", "golden or random_worlds or synthetic_small or frontier or routed"],
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert " passed" in r.stdout

@@ -23,6 +23,10 @@ struct uint4 {
     uint32_t x, y, z, w;
 };
 inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
+struct uint2 {
+    uint32_t x, y;
+};
+inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
 struct dim3 {
     uint32_t x, y, z;
     dim3(uint32_t a = 1, uint32_t b = 1, uint32_t c = 1) : x(a), y(b), z(c) {}
@@ -30,7 +34,7 @@ struct dim3 {
 struct EmuIdx {
     uint32_t x = 0, y = 0, z = 0;
 };
-inline thread_local EmuIdx threadIdx, blockIdx, blockDim;
+inline thread_local EmuIdx threadIdx, blockIdx, blockDim, gridDim;
 
 
 typedef int hipError_t;
@@ -78,6 +82,7 @@ template <class T> inline T __shfl(T v, int) { return v; }
 template <class T> inline T __shfl_down(T, int) { return T(0); }
 template <class T> inline T __shfl_up(T, int) { return T(0); }
 inline int __ffsll(long long v) { return __builtin_ffsll(v); }
+inline int __clzll(long long v) { return v ? __builtin_clzll((unsigned long long)v) : 64; }
 inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 inline void __syncthreads() {}
@@ -109,6 +114,7 @@ inline unsigned long long atomicCAS(unsigned long long *p, unsigned long long c,
             blockIdx.x = emu_g;                                                               \
             threadIdx.x = 0;                                                                  \
             blockDim.x = 1;                                                                   \
+            gridDim.x = emu_n;                                                                \
             kernel(__VA_ARGS__);                                                              \
         }                                                                                     \
     } while (0)

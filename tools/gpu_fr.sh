@@ -1,0 +1,12 @@
+#!/bin/bash
+# frontier engine: GPU tests, then frontier vs DFS on the Drive profiling batch (+ kernel trace)
+set -o pipefail
+mkdir -p gpurun_out
+export KETO_FR_VERBOSE=1
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_frontier.py tests/test_gpu_parity.py > gpurun_out/fr_tests.log 2>&1 || { tail -30 gpurun_out/fr_tests.log; exit 1; }
+tail -2 gpurun_out/fr_tests.log
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+rm -rf gpurun_out/frprof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/frprof -o frprof -- python3 -u tools/prof_check.py --workload drive --batches 0 --compare > gpurun_out/fr_drive.log 2>&1 || { tail -30 gpurun_out/fr_drive.log; exit 1; }
+grep -E "KETO_FRONTIER|stats|identical" gpurun_out/fr_drive.log; grep "^\[frontier\]" gpurun_out/fr_drive.log | tail -1
+python3 tools/rocpd_summary.py $(find gpurun_out/frprof -name "*results.db" | head -1) 8

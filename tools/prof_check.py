@@ -17,6 +17,7 @@ ap.add_argument("--tuples", type=int, default=10_000_000)
 ap.add_argument("--workload", default="c2")
 ap.add_argument("--count", action="store_true", help="one counted batch first: per-tier work and step counters")
 ap.add_argument("--single", type=int, default=-1, help="time one query alone, x64 and x(full grid) copies")
+ap.add_argument("--compare", action="store_true", help="frontier vs DFS interpreter: decisions and times")
 a = ap.parse_args()
 if a.workload == "c2":
     wl = synth.nested_groups(a.tuples, seed=1)
@@ -58,3 +59,21 @@ for i in range(a.batches):
     eng.check_batch_device(dq, len(q), da, de, sync=True)
     print(f"batch {i}: {(time.perf_counter() - t0) * 1e3:.2f} ms, tier-0 kernel {st.last_kernel_ms():.2f} ms",
           flush=True)
+if a.compare:
+    res = {}
+    for mode in ("0", "1"):
+        os.environ["KETO_FRONTIER"] = mode
+        ms = []
+        for i in range(3):
+            t0 = time.perf_counter()
+            eng.check_batch_device(dq, len(q), da, de, sync=True)
+            ms.append((time.perf_counter() - t0) * 1e3)
+        res[mode] = (da.download(st, np.zeros(len(q), np.uint8)), de.download(st, np.zeros(len(q), np.int32)), min(ms),
+                     st.last_kernel_ms())
+        print(f"KETO_FRONTIER={mode}: batch {min(ms):.2f} ms, device path {res[mode][3]:.2f} ms", flush=True)
+    fs = st.frontier_stats(reset=True)
+    print("frontier stats", fs, flush=True)
+    same = (res["0"][0] == res["1"][0]).all() and (res["0"][1] == res["1"][1]).all()
+    print("decisions identical:", bool(same), "allowed", int(res["1"][0].sum()), flush=True)
+    if not same:
+        sys.exit(1)
