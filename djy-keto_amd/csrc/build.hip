@@ -306,6 +306,23 @@ __global__ __launch_bounds__(BLK) void k_weight(const uint32_t *set_off, const u
     nw[v] = r;
     if (r != w[v]) *changed = 1;
 }
+// global slots whose rows hold a subject set somewhere (relinfo RI_SETROWS)
+__global__ __launch_bounds__(BLK) void k_slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns,
+                                                      uint32_t *flag) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n_rows) return;
+    const uint4 r = set_row[i];
+    if (r.x == r.y) return;
+    uint32_t lo = 0, hi = n_ns;  // last namespace whose node_base <= i
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (ns[m].node_base <= i) lo = m;
+        else hi = m;
+    }
+    const uint32_t gs = ns[lo].slot_base + (uint32_t)((i - ns[lo].node_base) % ns[lo].n_slots);
+    if (!flag[gs]) atomicOr(&flag[gs], 1u);
+}
+
 __global__ __launch_bounds__(BLK) void k_fill32(uint32_t *a, uint64_t n, uint32_t x) {
     const uint64_t i = gid();
     if (i < n) a[i] = x;
@@ -493,6 +510,11 @@ void rows(const RowsIn &in, RowsOut &out) {
         KETO_HIP(hipGetLastError());
     }
     KETO_HIP(hipDeviceSynchronize());
+}
+
+void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag) {
+    hipLaunchKernelGGL(k_slot_setrows, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, ns, n_ns, flag);
+    KETO_HIP(hipGetLastError());
 }
 
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows) {

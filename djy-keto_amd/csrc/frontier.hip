@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "device_common.hpp"
 
@@ -48,8 +49,14 @@ constexpr uint32_t GF_SKIP = 1u << 15, GF_ESCHILD = 1u << 16, GF_ALIAS = 1u << 1
 enum ReduceOp : uint32_t { R_FIRST = 0, R_AND = 1, R_NOT = 2 };
 constexpr uint32_t NC_MAX = (1u << 24) - 1;
 constexpr uint32_t MAX_GEN = 192;
-// ctrl: gbase[MAX_GEN + 2] | gcount[MAX_GEN + 2] | fallback count (+3)
-constexpr size_t FR_CTRL_BYTES = (2 * (MAX_GEN + 2) + 4) * 4;
+// The arena is cut into FR_SHARDS slices of `scap` goals; a block spawns into slice
+// blockIdx % FR_SHARDS, so the allocation counters of a generation are FR_SHARDS addresses,
+// not one (a single counter serialises every block's atomic: ~60M/s).  A generation is the
+// union of one contiguous range per slice; slices stack their generations.
+constexpr uint32_t FR_SHARDS = 64;
+constexpr uint32_t GEN_STRIDE = MAX_GEN + 2;
+// ctrl: gbase[FR_SHARDS][GEN_STRIDE] | gcount[FR_SHARDS][GEN_STRIDE] | fallback count (+3)
+constexpr size_t FR_CTRL_BYTES = (2 * FR_SHARDS * GEN_STRIDE + 4) * 4;
 __device__ __forceinline__ uint32_t gword(uint32_t kind, uint32_t d, uint32_t op = 0, uint32_t flags = 0) {
     return (d & GD_MAX) | (kind << 12) | flags | (op << 16);
 }
@@ -61,8 +68,8 @@ struct FrontierParams {
     uint4 *g0;
     uint2 *gfn;
     uint32_t *gval;
-    uint32_t cap;                // arena goals
-    uint32_t *gbase, *gcount;    // [MAX_GEN + 1] per generation
+    uint32_t cap, scap;          // arena goals, goals per slice
+    uint32_t *gbase, *gcount;    // [FR_SHARDS][GEN_STRIDE]: slice-local base and count per generation
     uint32_t gen;
     uint32_t *qgoals, *qroute;   // [n] per query position
     uint32_t budget;
@@ -74,7 +81,20 @@ struct FrontierParams {
     int32_t *out_err;
     uint32_t err_detail;
     uint32_t *fb_list, *fb_count;  // routed positions, for the DFS interpreter
+    unsigned long long *prof;      // KETO_FR_PROF builds: wave-cycles per phase of fr_expand
 };
+
+// Profiling builds (-DKETO_FR_PROF, tools/ab_build.sh): shader clock between phase marks
+#ifdef KETO_FR_PROF
+#define FR_MARK(n)                                                     \
+    do {                                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+        pacc[n] += t_ - pt;                                            \
+        pt = t_;                                                       \
+    } while (0)
+#else
+#define FR_MARK(n) ((void)0)
+#endif
 
 // the query subject's membership test (checkDirect / the found-lookahead / the IN shortcut):
 // a short reverse row sits in the start record, a long one is answered by the probe hash
@@ -122,20 +142,41 @@ __device__ __forceinline__ unsigned long long tab_key(uint32_t scope, uint32_t v
     return (((unsigned long long)scope << 32) | vk) + 1ull;
 }
 
-// claim (scope, key) or find it; a second occurrence raises the slot's repeat flag
-__device__ __forceinline__ uint32_t tab_insert(const FrontierParams &P, uint32_t scope, uint32_t vk) {
+// A sub-check checkIsAllowed(c, dc, skip) shaped when its parent spawns it (oracle u_sub): a
+// relation with a rewrite is an IA goal; one without is decided on the spot (dc <= 0: Unknown;
+// an error; a direct tuple: IsMember) or is just its expand-subject, an ES(dc-1) goal -- or
+// NotMember when no row of the relation holds a subject set.  `esf` (an ES's children:
+// GF_ESCHILD [| GF_ALIAS]) makes an error a goal too, so every decisive occurrence of a scope
+// key is a goal, and goes into the word.  word != 0: spawn it; else `leaf` is the result.
+struct Sub {
+    uint32_t word, leaf;
+};
+__device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t c, uint32_t dc,
+                                         bool skip, uint32_t esf) {
+    if (dc == 0) return Sub{0, M_UNK};
+    const NodeInfo ni = t_node_info(T, c);
+    const bool err = ri_status(ni.ri) == REL_ERROR;
+    if (ri_rw(ni.ri) || (err && esf)) return Sub{gword(G_IA, dc, 0, (skip ? GF_SKIP : 0u) | esf), 0};
+    if (err) return Sub{0, mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16)};
+    if (!skip && dc > 1 && !(c & VIRT_BIT) && member(s, q, c)) return Sub{0, M_IS};
+    if (ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri)) return Sub{gword(G_ES, dc - 1, 0, esf), 0};
+    return Sub{0, M_NOT};
+}
+
+// count an occurrence of (scope, key) that is not a goal; false when the table is crowded
+__device__ __forceinline__ bool tab_mark(const FrontierParams &P, uint32_t scope, uint32_t vk) {
     const unsigned long long key = tab_key(scope, vk);
     uint32_t h = (uint32_t)mix64(key) & P.tmask;
     for (int probe = 0; probe < 64; probe++) {
         const unsigned long long old = atomicCAS(&P.tkeys[h], 0ull, key);
-        if (old == 0ull) return h;
+        if (old == 0ull) return true;
         if (old == key) {
             P.trep[h] = 1;
-            return h;
+            return true;
         }
         h = (h + 1) & P.tmask;
     }
-    return NONE32;  // crowded: the caller routes the query
+    return false;
 }
 
 // a routed query also saturates its goal count, so the budget atomic of any later spawn refuses
@@ -163,16 +204,46 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t &total) {
     return x - v;
 }
 
+// a generation's slices: exclusive prefix of their counts and their slice-local bases (LDS)
+struct GenMap {
+    uint32_t pre[FR_SHARDS + 1], base[FR_SHARDS];
+};
+__device__ __forceinline__ void load_gen(const FrontierParams &P, uint32_t k, GenMap &m) {
+    for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x) {
+        const uint32_t b = P.gbase[t * GEN_STRIDE + k];
+        m.base[t] = b;
+        m.pre[t + 1] = std::min(P.gcount[t * GEN_STRIDE + k], P.scap - std::min(b, P.scap));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m.pre[0] = 0;
+        for (uint32_t t = 0; t < FR_SHARDS; t++) m.pre[t + 1] += m.pre[t];
+    }
+    __syncthreads();
+}
+// the j-th goal of the generation (j < pre[FR_SHARDS]) -> arena index
+__device__ __forceinline__ uint32_t gen_goal(const FrontierParams &P, const GenMap &m, uint32_t j) {
+    uint32_t lo = 0, hi = FR_SHARDS;  // last slice with pre[t] <= j
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (m.pre[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    return lo * P.scap + m.base[lo] + (j - m.pre[lo]);
+}
+
+// generation 0: query position i in slice i / chunk
 __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {
-        P.gbase[0] = 0;
-        P.gcount[0] = P.n;
+    const uint32_t chunk = (P.n + FR_SHARDS - 1) / FR_SHARDS;
+    if (i < FR_SHARDS) {
+        P.gbase[i * GEN_STRIDE] = 0;
+        P.gcount[i * GEN_STRIDE] = std::min(chunk, P.n - std::min(P.n, i * chunk));
     }
     if (i >= P.n) return;
     const uint4 r0 = P.start[2 * (size_t)i];
     const uint32_t d = r0.z & 0xFFFFu;
-    spawn(P, i, r0.x, i, gword(G_IA, d), NONE32);
+    P.g0[(i / chunk) * P.scap + i % chunk] = make_uint4(r0.x, i, gword(G_IA, d), NONE32);
     P.qgoals[i] = d > GD_MAX ? QG_ROUTED : 1u;
     P.qroute[i] = d > GD_MAX ? 1u : 0u;
 }
@@ -182,27 +253,57 @@ template <bool LDS_TABLES>
 __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const DevSnapshot &s = P.s;
+    __shared__ GenMap gm;
     const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
     const uint32_t k = P.gen;
-    const uint32_t base = P.gbase[k];
-    const uint32_t cnt = std::min(P.gcount[k], P.cap - std::min(base, P.cap));
-    const uint32_t nbase = base + cnt;
-    if (blockIdx.x == 0 && threadIdx.x == 0) P.gbase[k + 1] = nbase;
+    load_gen(P, k, gm);
+    const uint32_t cnt = gm.pre[FR_SHARDS];
+    // the next generation in each slice starts where this one ends
+    if (blockIdx.x == 0)
+        for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x)
+            P.gbase[t * GEN_STRIDE + k + 1] = gm.base[t] + (gm.pre[t + 1] - gm.pre[t]);
+    // this wave's slice
+    const uint32_t so = (blockIdx.x * ((blockDim.x + 63) >> 6) + (threadIdx.x >> 6)) % FR_SHARDS;
+    const uint32_t nbase = so * P.scap + gm.base[so] + (gm.pre[so + 1] - gm.pre[so]), send = (so + 1) * P.scap;
     const bool last = k + 1 >= MAX_GEN;
     const uint32_t W = P.max_width;
+#ifdef KETO_FR_PROF
+    unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
         // goals of queries routed meanwhile still run (rare); they can no longer spawn
         const bool live = j < cnt;
-        const uint32_t i = base + j;
+        const uint32_t i = live ? gen_goal(P, gm, j) : 0u;
         const uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
         const uint32_t node = g.x, pos = g.y, w = g.z, scope = g.w;
         const uint32_t d = w & GD_MAX, kind = (w >> 12) & 7u, op = w >> 16;
+        const uint32_t qg = live ? P.qgoals[pos] : 0u;
+        // An ES child counts its key into the scope table (CheckAndAddVisited, engine.go:157-160):
+        // the CAS is issued here and its answer consumed after the goal's own work.
+        const bool ins = live && (kind == G_IA || kind == G_ES) && (w & GF_ESCHILD);
+        unsigned long long tkey = 0, told = 0;
+        uint32_t th = 0;
+        if (ins) {
+            tkey = tab_key(scope, (w & GF_ALIAS) ? s.vkey[node] : node);
+            th = (uint32_t)mix64(tkey) & P.tmask;
+            told = atomicCAS(&P.tkeys[th], 0ull, tkey);
+        }
+        // The loads the goal kinds start from, issued together: the row an ES / TTU reads, and
+        // the subject's membership record (IA direct check, ES lookahead, OR shortcut).
+        uint32_t rnode = NONE32;
+        if (live && kind == G_ES && !(node & VIRT_BIT)) rnode = node;
+        if (live && kind == G_TTU && d > 1) {
+            const uint32_t ts = t_sibling(T, node, t_node_info(T, node), T.ops[op].rel_computed & 0xFFFFu);
+            if (!(ts & VIRT_BIT)) rnode = ts;
+        }
+        const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
+        const Subject q = live ? load_subject(P, pos) : Subject{0, false, make_uint4(0, 0, 0, 0)};
+        FR_MARK(0);
         // ---- phase A: decide, or count the children -------------------------------------------
         uint32_t nc = 0, val = M_NOT;  // value if nc == 0, else the partial (tail) for fr_reduce
         uint32_t rop = kind == G_INV ? R_NOT : R_FIRST;
         uint32_t pat = 0;              // per kind: which children (phase B regenerates them)
-        uint4 row = make_uint4(0, 0, 0, 0);
         uint32_t sc = scope, xrel = 0;
         if (live) {
             switch (kind) {
@@ -219,8 +320,9 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
                 const bool rw = ri_rw(ni.ri);
                 bool direct = false;
                 if ((!s.strict || !rw) && !(w & GF_SKIP) && d > 1 && !(node & VIRT_BIT))  // :239-243
-                    direct = member(s, load_subject(P, pos), node);
-                const bool es = ri_ss(ni.ri) && d > 1 && !direct;  // :244-246
+                    direct = member(s, q, node);
+                // expand-subject(d-1) (:244-246), unless no row of the relation holds a subject set
+                const bool es = ri_ss(ni.ri) && d > 1 && !direct && ri_setrows(ni.ri);
                 pat = (rw ? 1u : 0u) | (es ? 2u : 0u);
                 xrel = ri_op(ni.ri);
                 nc = (rw ? 1u : 0u) + (es ? 1u : 0u);
@@ -228,22 +330,25 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
                 break;
             }
             case G_ES: {  // checkExpandSubject (engine.go:102-164)
-                if (node & VIRT_BIT) break;
-                row = s.set_row[node];
-                if (row.x == row.y) break;
-                const Subject q = load_subject(P, pos);
-                Edges it(s, row);
-                bool found = false;  // found-lookahead over every row (traverser.go:73-80, 109-111)
-                while (it.cur < it.end && !found) found = member(s, q, it.next() & ~EDGE_ALIAS);
-                if (found) {
-                    val = M_IS;
-                    break;
-                }
+                if (row.x == row.y) break;  // (virtual nodes have no row)
                 uint32_t keep = row.y - row.x;
                 if (keep > W) keep = W > 0 ? W - 1 : 0;  // results[:maxWidth-1] (engine.go:141-150)
-                if (scope == NONE32) sc = i;              // graph.InitVisited (graph_utils.go:38-43)
-                nc = keep;
-                val = keep ? NONE32 : M_NOT;
+                Edges it(s, row);
+                bool found = false;  // found-lookahead over every row (traverser.go:73-80, 109-111)
+                for (uint32_t e = 0; it.cur < it.end && !found; e++) {
+                    const uint32_t c = it.next() & ~EDGE_ALIAS;
+                    found = member(s, q, c);
+                    if (e < keep && sub_check(s, T, q, c, d, true, GF_ESCHILD).word) nc++;  // the children that are goals
+                }
+                if (found) {
+                    val = M_IS;
+                    nc = 0;
+                    break;
+                }
+                if (scope == NONE32) sc = i;  // graph.InitVisited (graph_utils.go:38-43)
+                pat = keep;
+                val = nc ? NONE32 : M_NOT;  // (leaf children are NotMember: they only mark their key)
+                xrel = (!nc && keep) ? 1u : 0u;  // phase B still marks the leaf children's keys
                 break;
             }
             case G_RW: {  // checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73)
@@ -260,14 +365,12 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
                 const bool is_or = okind == OPK_OR;
                 if (!is_or) rop = R_AND;
                 const NodeInfo ni = t_node_info(T, node);
-                uint32_t ncss = 0;
+                uint32_t tail = NONE32, cand_end = 0, kend = o.child_count;
                 if (is_or && ((o.type_kind >> 16) & 1u)) {  // the IN shortcut (rewrites.go:62-92)
-                    const Subject q = load_subject(P, pos);
                     bool found = false;
                     for (uint32_t c = 0; c < o.child_count && !found; c++) {
                         const Op ch = T.ops[T.op_children[o.child_begin + c]];
                         if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
-                        ncss++;
                         const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
                         if (t & VIRT_BIT) continue;
                         if (s.strict) {  // traverser.go:137-139
@@ -280,37 +383,69 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
                         val = M_IS;
                         break;
                     }
-                    if (d <= 1) ncss = 0;  // candidates checkIsAllowed(c, d-1 <= 0) are Unknown
+                    // no direct member: candidates checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
+                    if (d > 1) {
+                        cand_end = o.child_count;
+                        for (uint32_t c = 0; c < o.child_count; c++) {
+                            const Op ch = T.ops[T.op_children[o.child_begin + c]];
+                            if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
+                            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d - 1, true, 0);
+                            if (sb.word) nc++;
+                            else if (decisive(sb.leaf)) {  // an error decides the OR: nothing after it runs
+                                tail = sb.leaf;
+                                cand_end = c;
+                                kend = 0;
+                                break;
+                            }
+                        }
+                    }
                 }
                 // the other children in AST order, up to a leaf that decides the group
-                uint32_t kend = o.child_count, tail = NONE32, ns = 0;
-                for (uint32_t c = 0; c < o.child_count; c++) {
-                    const uint32_t ct = T.ops[T.op_children[o.child_begin + c]].type_kind & 0xFFu;
+                for (uint32_t c = 0; c < kend; c++) {
+                    const Op ch = T.ops[T.op_children[o.child_begin + c]];
+                    const uint32_t ct = ch.type_kind & 0xFFu;
                     if (is_or && ct == OP_CSS) continue;
-                    if (ct == OP_REWRITE && d <= 1) {  // nested rewrite at d-1 <= 0: Unknown (:39-42)
-                        if (is_or) continue;
-                        tail = M_NOT;  // AND: the first non-member decides (binop.go:52-54)
+                    uint32_t leaf = NONE32;
+                    if (ct == OP_REWRITE && d <= 1) leaf = M_UNK;  // nested rewrite at d-1 <= 0 (:39-42)
+                    else if (ct == OP_CSS) {  // AND: checkComputedSubjectSet (rewrites.go:208-230)
+                        const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
+                        if (!sb.word) leaf = sb.leaf;
+                    }
+                    if (leaf == NONE32) {
+                        nc++;
+                        continue;
+                    }
+                    const bool decides = is_or ? decisive(leaf) : ((leaf >> 8) != 0 || (leaf & 3u) != M_IS);
+                    if (decides) {  // binop.go:23-26 / 52-54
+                        tail = is_or ? leaf : ((leaf & ~3u) | M_NOT);
                         kend = c;
                         break;
                     }
-                    ns++;
                 }
-                nc = ncss + ns;
                 pat = kend;
-                xrel = ncss;
+                xrel = cand_end;
                 if (nc == 0) val = tail != NONE32 ? tail : ((!is_or && o.child_count > 0) ? M_IS : M_NOT);
                 else val = tail;
                 break;
             }
             case G_TTU: {  // checkTupleToSubjectSet (rewrites.go:242-293)
-                const Op o = T.ops[op];
-                const NodeInfo ni = t_node_info(T, node);
-                const uint32_t ts = t_sibling(T, node, ni, o.rel_computed & 0xFFFFu);
-                if ((ts & VIRT_BIT) || d <= 1) break;  // no rows, or every parent check is Unknown
-                row = s.set_row[ts];
-                nc = row.y - row.x;
-                xrel = o.rel_computed >> 16;
-                val = nc ? NONE32 : M_NOT;
+                // row: the tupleset relation's row (none when virtual, or when d <= 1 makes every
+                // parent check Unknown); each parent: checkIsAllowed(S#computed, d-1) (:279-288)
+                xrel = T.ops[op].rel_computed >> 16;
+                Edges it(s, row);
+                uint32_t tail = NONE32, e = 0;
+                for (; it.cur < it.end; e++) {
+                    const uint32_t pn = it.next() & ~EDGE_ALIAS;
+                    const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), xrel), d - 1, false, 0);
+                    if (sb.word) nc++;
+                    else if (decisive(sb.leaf)) {
+                        tail = sb.leaf;
+                        e++;
+                        break;
+                    }
+                }
+                pat = e;  // parents phase B walks
+                val = nc ? tail : (tail != NONE32 ? tail : M_NOT);
                 break;
             }
             case G_INV: {  // checkInverted (rewrites.go:136-200)
@@ -319,9 +454,17 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
                     val = mk_err(KETO_QERR_NOT_IMPLEMENTED);
                     break;
                 }
-                const uint32_t ct = T.ops[T.op_children[o.child_begin]].type_kind & 0xFFu;
-                if ((ct == OP_CSS || ct == OP_REWRITE) && d == 0) {  // the child is Unknown: NOT keeps it
-                    val = M_UNK;
+                const Op ch = T.ops[T.op_children[o.child_begin]];
+                const uint32_t ct = ch.type_kind & 0xFFu;
+                uint32_t leaf = NONE32;
+                if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
+                else if (ct == OP_CSS) {
+                    const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
+                    if (!sb.word) leaf = sb.leaf;
+                }
+                if (leaf != NONE32) {  // NOT of a result known now: IsMember <-> NotMember, Unknown / errors kept
+                    const uint32_t m = leaf & 3u;
+                    val = m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
                     break;
                 }
                 nc = 1;
@@ -336,9 +479,15 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
             route(P, pos);
             nc = 0;
         }
-        // ---- budget and generation cap: one atomic per run of lanes holding goals of one query
-        // (a parent's children are contiguous, so siblings share a run) -----------------------------
+        FR_MARK(1);
+        // ---- budget and generation cap.  The goal count read when the goal started is the
+        // check (fr_reduce re-checks the final count); the count is raised without waiting, one
+        // atomic per run of lanes holding goals of one query (siblings are contiguous) --------------
         const uint32_t lane = __lane_id();
+        if (nc && (qg > P.budget || last)) {
+            route(P, pos);
+            nc = 0;
+        }
         {
             const uint32_t key = live ? pos : NONE32;
             const uint32_t prev = __shfl_up(key, 1);
@@ -352,34 +501,18 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
             }
             const unsigned long long after = lane == 63 ? 0ull : (heads >> (lane + 1));
             const uint32_t tl = after ? lane + (uint32_t)__ffsll((long long)after) - 1u : wl;
-            uint32_t over = 0;
-            if (lane == tl && x) {
-                over = (atomicAdd(&P.qgoals[pos], x) + x > P.budget || last) ? 1u : 0u;
-                if (over) route(P, pos);
-            }
-            if (__shfl(over, tl)) nc = 0;
+            if (lane == tl && x) atomicAdd(&P.qgoals[pos], x);
         }
-        // ---- allocation: one atomic per block iteration -------------------------------------------
-        __shared__ uint32_t s_woff[2][4], s_base[2];
-        const uint32_t par = (j0 / (gridDim.x * blockDim.x)) & 1u, wid = threadIdx.x >> 6;
+        FR_MARK(2);
+        // ---- allocation: one atomic per wave, on the wave's slice counter -------------------------
         uint32_t wtot = 0;
         const uint32_t off = wave_excl(nc, wtot);
-        if (lane == 0) s_woff[par][wid] = wtot;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t sum = 0;
-            for (uint32_t q = 0; q < (blockDim.x + 63) / 64; q++) {
-                const uint32_t t = s_woff[par][q];
-                s_woff[par][q] = sum;
-                sum += t;
-            }
-            s_base[par] = sum ? atomicAdd(&P.gcount[k + 1], sum) : 0u;
-        }
-        __syncthreads();
-        const uint32_t cb = nbase + s_base[par] + s_woff[par][wid] + off;
-        if (nc && (uint64_t)cb + nc > P.cap) {  // arena full: route; fill the allocated slots that exist
+        uint32_t wbase = 0;
+        if (lane == 0 && wtot) wbase = atomicAdd(&P.gcount[so * GEN_STRIDE + k + 1], wtot);
+        const uint32_t cb = nbase + __shfl(wbase, 0) + off;
+        if (nc && (uint64_t)cb + nc > send) {  // slice full: route; fill the allocated slots that exist
             route(P, pos);
-            for (uint32_t c = cb; c < P.cap && c < cb + nc; c++) spawn(P, c, 0, pos, gword(G_DEAD, 0), NONE32);
+            for (uint32_t c = cb; c < send && c < cb + nc; c++) spawn(P, c, 0, pos, gword(G_DEAD, 0), NONE32);
             nc = 0;
             val = M_NOT;
         }
@@ -387,21 +520,36 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
             P.gfn[i] = make_uint2(cb, nc | (rop << 24));
             P.gval[i] = val;
         }
-        if (!nc) continue;
-        // ---- phase B: write the children ---------------------------------------------------------
-        switch (kind) {
+        if (ins && told != 0ull) {  // the key was there (a repeat), or another key is: probe on
+            for (int probe = 1; told != tkey; probe++) {
+                if (probe == 64) {  // crowded: the DFS interpreter takes the query
+                    route(P, pos);
+                    break;
+                }
+                th = (th + 1) & P.tmask;
+                told = atomicCAS(&P.tkeys[th], 0ull, tkey);
+                if (told == 0ull) break;
+            }
+            if (told == tkey) P.trep[th] = 1;
+        }
+        FR_MARK(3);
+        // ---- phase B: write the children (the same walk as phase A) -------------------------------
+        if (nc || (kind == G_ES && xrel)) switch (kind) {
         case G_IA:
             if (pat & 1u) spawn(P, cb, node, pos, gword(G_RW, d, xrel), scope);
             if (pat & 2u) spawn(P, cb + ((pat & 1u) ? 1 : 0), node, pos, gword(G_ES, d - 1), scope);
             break;
         case G_ES: {
             Edges it(s, row);
-            for (uint32_t c = 0; c < nc; c++) {
+            uint32_t c = cb;
+            for (uint32_t e = 0; e < pat; e++) {
                 const uint32_t raw = it.next(), cn = raw & ~EDGE_ALIAS;
-                const bool alias = (raw & EDGE_ALIAS) != 0;
-                // CheckAndAddVisited (engine.go:157-160); then checkIsAllowed(c, d, skipDirect) (:161)
-                if (tab_insert(P, sc, alias ? s.vkey[cn] : cn) == NONE32) route(P, pos);
-                spawn(P, cb + c, cn, pos, gword(G_IA, d, 0, GF_SKIP | GF_ESCHILD | (alias ? GF_ALIAS : 0u)), sc);
+                const uint32_t esf = GF_ESCHILD | ((raw & EDGE_ALIAS) ? GF_ALIAS : 0u);
+                // checkIsAllowed(c, d, skipDirect) (:161); a goal marks its key itself, a leaf
+                // child's key is marked here (CheckAndAddVisited, :157-160)
+                const Sub sb = sub_check(s, T, q, cn, d, true, esf);
+                if (sb.word) spawn(P, c++, cn, pos, sb.word, sc);
+                else if (!tab_mark(P, sc, (raw & EDGE_ALIAS) ? s.vkey[cn] : cn)) route(P, pos);
             }
             break;
         }
@@ -410,12 +558,13 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
             const NodeInfo ni = t_node_info(T, node);
             const bool is_or = ((o.type_kind >> 8) & 0xFFu) == OPK_OR;
             uint32_t c = cb;
-            if (xrel)  // shortcut candidates checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
-                for (uint32_t k2 = 0; k2 < o.child_count; k2++) {
-                    const Op ch = T.ops[T.op_children[o.child_begin + k2]];
-                    if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
-                    spawn(P, c++, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), pos, gword(G_IA, d - 1, 0, GF_SKIP), scope);
-                }
+            for (uint32_t k2 = 0; k2 < xrel; k2++) {  // shortcut candidates (rewrites.go:88-90)
+                const Op ch = T.ops[T.op_children[o.child_begin + k2]];
+                if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
+                const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
+                const Sub sb = sub_check(s, T, q, t, d - 1, true, 0);
+                if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
+            }
             for (uint32_t k2 = 0; k2 < pat; k2++) {  // rewrites.go:95-129
                 const uint32_t ci = T.op_children[o.child_begin + k2];
                 const Op ch = T.ops[ci];
@@ -423,19 +572,23 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
                 if (is_or && ct == OP_CSS) continue;
                 if (ct == OP_REWRITE && d <= 1) continue;  // (OR only: an AND stopped at kend)
                 if (ct == OP_TTU) spawn(P, c++, node, pos, gword(G_TTU, d, ci), scope);
-                else if (ct == OP_CSS)
-                    spawn(P, c++, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), pos, gword(G_IA, d), scope);
-                else if (ct == OP_REWRITE) spawn(P, c++, node, pos, gword(G_RW, d - 1, ci), scope);  // :118
+                else if (ct == OP_CSS) {
+                    const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
+                    const Sub sb = sub_check(s, T, q, t, d, false, 0);
+                    if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
+                } else if (ct == OP_REWRITE) spawn(P, c++, node, pos, gword(G_RW, d - 1, ci), scope);  // :118
                 else spawn(P, c++, node, pos, gword(G_INV, d, ci), scope);
             }
             break;
         }
         case G_TTU: {
             Edges it(s, row);
-            for (uint32_t c = 0; c < nc; c++) {  // each parent: checkIsAllowed(S#computed, d-1) (:279-288)
+            uint32_t c = cb;
+            for (uint32_t e = 0; e < pat; e++) {
                 const uint32_t pn = it.next() & ~EDGE_ALIAS;
-                const NodeInfo pi = t_node_info(T, pn);
-                spawn(P, cb + c, t_sibling(T, pn, pi, xrel), pos, gword(G_IA, d - 1), scope);
+                const uint32_t t = t_sibling(T, pn, t_node_info(T, pn), xrel);
+                const Sub sb = sub_check(s, T, q, t, d - 1, false, 0);
+                if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
             }
             break;
         }
@@ -446,8 +599,8 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
             const uint32_t ct = ch.type_kind & 0xFFu;
             if (ct == OP_TTU) spawn(P, cb, node, pos, gword(G_TTU, d, ci), scope);
             else if (ct == OP_CSS) {
-                const NodeInfo ni = t_node_info(T, node);
-                spawn(P, cb, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), pos, gword(G_IA, d), scope);
+                const uint32_t t = t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu);
+                spawn(P, cb, t, pos, sub_check(s, T, q, t, d, false, 0).word, scope);
             } else if (ct == OP_REWRITE) spawn(P, cb, node, pos, gword(G_RW, d, ci), scope);  // keeps depth (:171)
             else spawn(P, cb, node, pos, gword(G_INV, d, ci), scope);
             break;
@@ -455,7 +608,12 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
         default:
             break;
         }
+        FR_MARK(4);
     }
+#ifdef KETO_FR_PROF
+    if (__lane_id() == 0)
+        for (int n = 0; n < 7; n++) atomicAdd(&P.prof[n], pacc[n]);
+#endif
 }
 
 // One generation, bottom-up: each goal reduces its children in add order (checkgroup H0,
@@ -465,10 +623,11 @@ __global__ __launch_bounds__(256) void fr_expand(FrontierParams P) {
 __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
     const DevSnapshot &s = P.s;
     const uint32_t k = P.gen;
-    const uint32_t base = P.gbase[k];
-    const uint32_t cnt = std::min(P.gcount[k], P.cap - std::min(base, P.cap));
+    __shared__ GenMap gm;
+    load_gen(P, k, gm);
+    const uint32_t cnt = gm.pre[FR_SHARDS];
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
-        const uint32_t i = base + j;
+        const uint32_t i = gen_goal(P, gm, j);
         const uint2 fn = P.gfn[i];
         uint32_t val = P.gval[i];
         const uint32_t nc = fn.y & NC_MAX, rop = fn.y >> 24;
@@ -497,7 +656,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         }
         if (k > 0 && decisive(val)) {  // an ES child: was its key repeated in the scope?
             const uint4 g = P.g0[i];
-            if (((g.z >> 12) & 7u) == G_IA && (g.z & GF_ESCHILD)) {  // (other kinds hold an op there)
+            if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD)) {  // (RW / TTU / INV hold an op there)
                 const unsigned long long key = tab_key(g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x);
                 uint32_t h = (uint32_t)mix64(key) & P.tmask;
                 for (int probe = 0; probe < 64; probe++) {
@@ -511,12 +670,13 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
                 }
             }
         }
-        if (k == 0) {  // generation 0 holds query position j
-            if (P.qroute[j]) {
-                P.fb_list[atomicAdd(P.fb_count, 1u)] = j;
+        if (k == 0) {  // generation 0: one goal per query position
+            const uint32_t pos = P.g0[i].y;
+            if (P.qroute[pos] || P.qgoals[pos] > P.budget) {
+                P.fb_list[atomicAdd(P.fb_count, 1u)] = pos;
                 continue;
             }
-            const uint32_t q = P.start[2 * (size_t)j].w;
+            const uint32_t q = P.start[2 * (size_t)pos].w;
             const uint32_t err = val >> 8;
             P.out_allowed[q] = (err == 0 && (val & 3u) == M_IS) ? 1 : 0;
             P.out_err[q] = (int32_t)(P.err_detail ? err : err & 0xFFu);
@@ -536,7 +696,8 @@ static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 #endif
 
 void ensure_frontier(FrontierScratch &f, uint64_t n) {
-    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n * KETO_FR_GOALS_PER_QUERY, 1u << 20), 1ull << 29);
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n * KETO_FR_GOALS_PER_QUERY, 1u << 20), 1ull << 29) / FR_SHARDS *
+                          FR_SHARDS;
     if (f.mem && f.cap >= want && f.ncap >= n) return;
     if (f.mem) KETO_HIP(hipFree(f.mem));
     f.mem = nullptr;
@@ -549,7 +710,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     KETO_HIP(hipMalloc(&f.mem, bytes));
     char *p = static_cast<char *>(f.mem);
     f.ctrl = reinterpret_cast<uint32_t *>(p);
-    f.fb_count = f.ctrl + 2 * (MAX_GEN + 2);
+    f.fb_count = f.ctrl + 2 * FR_SHARDS * GEN_STRIDE;
     p += ctrl;
     f.qgoals = reinterpret_cast<uint32_t *>(p);
     f.qroute = f.qgoals + ncap;
@@ -569,7 +730,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     f.cap = cap;
     f.ncap = ncap;
     f.tcap = tcap;
-    if (!f.host_ctrl) KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&f.host_ctrl), 2 * (MAX_GEN + 2) * 4 + 16, 0));
+    if (!f.host_ctrl) KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&f.host_ctrl), FR_CTRL_BYTES, 0));
 }
 
 uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
@@ -578,7 +739,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     const uint32_t cus = (uint32_t)num_cus(s.device);
     const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
     const size_t lds = lds_tables ? s.dev.lds_bytes : 0;
-    uint32_t *gbase = f.ctrl, *gcount = f.ctrl + (MAX_GEN + 2), *fb_count = f.fb_count;
+    uint32_t *gbase = f.ctrl, *gcount = f.ctrl + FR_SHARDS * GEN_STRIDE, *fb_count = f.fb_count;
     KETO_HIP(hipMemsetAsync(f.ctrl, 0, FR_CTRL_BYTES, st.stream));
     FrontierParams P{};
     P.s = s.dev;
@@ -588,6 +749,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.gfn = f.gfn;
     P.gval = f.gval;
     P.cap = (uint32_t)f.cap;
+    P.scap = (uint32_t)(f.cap / FR_SHARDS);
     P.gbase = gbase;
     P.gcount = gcount;
     P.qgoals = f.qgoals;
@@ -603,14 +765,17 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.err_detail = L.err_detail;
     P.fb_list = f.fb_list;
     P.fb_count = fb_count;
+    P.prof = st.counters;
     constexpr uint32_t BLOCK = 256;
     hipLaunchKernelGGL(fr_init, dim3((uint32_t)((L.n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st.stream, P);
     KETO_HIP(hipGetLastError());
-    // expansion: generations until one is empty; the goal counts are read back every CHUNK
+    // expansion: generations until one is empty; the slice counts are read back every CHUNK
     const dim3 eg(cus * 8), eb(BLOCK);
     constexpr uint32_t CHUNK = 12;
     uint32_t gens = 0;
     uint32_t *hc = f.host_ctrl;
+    std::vector<uint64_t> tot(MAX_GEN + 1, 0);  // goals per generation
+    const uint64_t scap = f.cap / FR_SHARDS;
     for (uint32_t k = 0; gens == 0;) {
         const uint32_t kend = std::min(k + CHUNK, MAX_GEN);
         for (; k < kend; k++) {
@@ -619,29 +784,36 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
             else hipLaunchKernelGGL(fr_expand<false>, eg, eb, 0, st.stream, P);
             KETO_HIP(hipGetLastError());
         }
-        KETO_HIP(hipMemcpyAsync(hc, f.ctrl, 2 * (MAX_GEN + 2) * 4, hipMemcpyDeviceToHost, st.stream));
+        KETO_HIP(hipMemcpyAsync(hc, f.ctrl, 2 * FR_SHARDS * GEN_STRIDE * 4, hipMemcpyDeviceToHost, st.stream));
         KETO_HIP(hipStreamSynchronize(st.stream));
-        for (uint32_t g = 0; g <= k && g <= MAX_GEN; g++)
-            if (hc[(MAX_GEN + 2) + g] == 0) {
+        for (uint32_t g = 0; g <= k && g <= MAX_GEN; g++) {
+            uint64_t t = 0;  // as fr_expand counts it: clamped to each slice
+            for (uint32_t sh = 0; sh < FR_SHARDS; sh++) {
+                const uint64_t b = hc[sh * GEN_STRIDE + g], c = hc[FR_SHARDS * GEN_STRIDE + sh * GEN_STRIDE + g];
+                t += std::min<uint64_t>(c, scap - std::min<uint64_t>(b, scap));
+            }
+            tot[g] = t;
+            if (t == 0) {
                 gens = g;
                 break;
             }
+        }
         if (gens == 0 && k >= MAX_GEN) gens = MAX_GEN;  // the last generation spawned nothing (routed)
     }
     // reduction, deepest generation first
+    uint64_t top = 0;
     for (int32_t g = (int32_t)gens - 1; g >= 0; g--) {
-        const uint32_t c = std::min<uint32_t>(hc[(MAX_GEN + 2) + g], (uint32_t)f.cap - std::min<uint32_t>(hc[g], (uint32_t)f.cap));
+        top += tot[g];
         P.gen = (uint32_t)g;
-        const dim3 rg(std::max<uint32_t>(1, std::min<uint32_t>((c + BLOCK - 1) / BLOCK, cus * 16)));
+        const dim3 rg((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tot[g] + BLOCK - 1) / BLOCK, cus * 16)));
         hipLaunchKernelGGL(fr_reduce, rg, eb, 0, st.stream, P);
         KETO_HIP(hipGetLastError());
     }
-    const uint32_t top = std::min<uint32_t>(hc[gens], (uint32_t)f.cap);
     KETO_HIP(hipMemsetAsync(f.tkeys, 0, f.tcap * 9, st.stream));
     KETO_HIP(hipMemcpyAsync(hc, fb_count, 4, hipMemcpyDeviceToHost, st.stream));
     KETO_HIP(hipStreamSynchronize(st.stream));
     f.last_gens = gens;
-    f.last_goals = top;
+    f.last_goals = (uint32_t)top;
     f.last_routed = hc[0];
     f.stats.batches++;
     f.stats.queries += L.n;
@@ -651,8 +823,9 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     f.stats.max_generations = std::max<uint64_t>(f.stats.max_generations, gens);
     static const bool verbose = getenv("KETO_FR_VERBOSE") != nullptr;
     if (verbose) {
-        fprintf(stderr, "[frontier] n %llu generations %u goals %u routed %u:", (unsigned long long)L.n, gens, top, hc[0]);
-        for (uint32_t g = 0; g < gens; g++) fprintf(stderr, " %u", f.host_ctrl[(MAX_GEN + 2) + g]);
+        fprintf(stderr, "[frontier] n %llu generations %u goals %llu routed %u:", (unsigned long long)L.n, gens,
+                (unsigned long long)top, hc[0]);
+        for (uint32_t g = 0; g < gens; g++) fprintf(stderr, " %llu", (unsigned long long)tot[g]);
         fprintf(stderr, "\n");
     }
     return hc[0];

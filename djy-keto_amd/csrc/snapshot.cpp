@@ -430,6 +430,16 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
             D.vkey = dv;
         }
     }
+    // slots whose rows can hold subject sets: an expand-subject of any other slot finds none
+    if (total_slots) {
+        DevBuf flag(4ull * total_slots);
+        KETO_HIP(hipMemset(flag.p, 0, 4ull * total_slots));
+        build::slot_setrows(ro.set_row, N, D.ns, s.n_ns, flag.u32());
+        std::vector<uint32_t> hf(total_slots);
+        KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
+        for (uint32_t gs = 0; gs < total_slots; gs++)
+            if (hf[gs]) s.relinfo[gs] |= RI_SETROWS;
+    }
     auto upload_small = [&](const auto &v) {
         using T = typename std::decay_t<decltype(v)>::value_type;
         T *p = static_cast<T *>(dalloc(std::max<size_t>(1, v.size()) * sizeof(T)));

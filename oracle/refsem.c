@@ -48,6 +48,7 @@ struct rs_db {
     rs_ast *ast;
     int32_t *children;
     uint32_t *vclass;
+    uint8_t *ssrel;    /* [n_ns * n_relnames]: some tuple of (ns, rel) has a subject set */
     uint32_t n_ns, n_relnames, empty_rel, n_rels, n_ast, n_children;
     int32_t strict, max_depth, max_width;
 };
@@ -316,6 +317,11 @@ rs_db *rs_build(const rs_tuple *tuples, size_t n, const rs_config *cfg) {
     db->strict = cfg->strict;
     db->max_depth = cfg->max_depth;
     db->max_width = cfg->max_width;
+    db->ssrel = calloc((size_t)db->n_ns * db->n_relnames + 1, 1);
+    for (size_t i = 0; i < n; i++) {
+        const key7 *t = &db->rt[i];
+        if (t->kind == 1 && t->ns < db->n_ns && t->rel < db->n_relnames) db->ssrel[(size_t)t->ns * db->n_relnames + t->rel] = 1;
+    }
     return db;
 }
 
@@ -330,6 +336,7 @@ void rs_free(rs_db *db) {
     free(db->ast);
     free(db->children);
     free(db->vclass);
+    free(db->ssrel);
     free(db);
 }
 
@@ -946,6 +953,49 @@ static int u_spawn(uctx *u, uint32_t gen) {
 
 static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, uint32_t scope, uint32_t gen);
 static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen);
+static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen);
+
+/* a relation whose rows can hold subject sets: some tuple of (ns, rel) has one (per snapshot) */
+static int has_set_rows(const rs_db *db, uint32_t ns, uint32_t rel) {
+    return ns < db->n_ns && rel < db->n_relnames && db->ssrel[(size_t)ns * db->n_relnames + rel];
+}
+
+/* A sub-check checkIsAllowed(ns:obj#rel, d, skip) shaped when its parent spawns it: a relation
+ * with a rewrite is an IA goal; one without is decided on the spot (d <= 0: Unknown; an error;
+ * a direct tuple: IsMember) or is just its expand-subject, an ES(d-1) goal -- or NotMember when
+ * that could find no subject set.  An ES's children (es_child) are goals also for an error, so
+ * every decisive occurrence of a scope key is a goal.  Returns 1 when spawned, 0 for a leaf;
+ * *out = the result either way. */
+static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, int es_child, uint32_t scope,
+                 uint32_t gen, res *out) {
+    const rs_db *db = u->c->db;
+    *out = R_UNK;
+    if (d <= 0) return 0; /* engine.go:215-220 */
+    int err;
+    const int ri = ast_relation_for(db, ns, rel, &err);
+    const int has_rewrite = !err && ri >= 0 && db->rels[ri].rewrite >= 0;
+    if (has_rewrite || (err && es_child)) {
+        if (!u_spawn(u, gen + 1)) return 0;
+        *out = u_ia(u, ns, obj, rel, d, skip, scope, gen + 1);
+        return 1;
+    }
+    if (err) {
+        out->err = err;
+        return 0;
+    }
+    const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
+    if (!skip && d - 1 > 0 && exists(u->c, ns, obj, rel)) {
+        *out = R_IS;
+        return 0;
+    }
+    if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel)) {
+        if (!u_spawn(u, gen + 1)) return 0;
+        *out = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
+        return 1;
+    }
+    *out = R_NOT;
+    return 0;
+}
 
 /* a rewrite child (check_child): 1 = spawned as a goal (result in *out), 0 = a leaf result */
 static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, uint32_t scope, uint32_t gen,
@@ -961,12 +1011,14 @@ static res u_ttu(uctx *u, uint32_t ns, uint32_t obj, const rs_ast *a, int d, uin
     for (size_t i = lo; i < hi; i++) {
         const key7 *t = ROW(db, i);
         if (t->kind != 1) continue;
-        if (!u_spawn(u, gen + 1)) return R_NOT;
-        res r = u_ia(u, t->sns, t->sid, a->computed, d - 1, 0, scope, gen + 1);
+        res r;
+        const int spawned = u_sub(u, t->sns, t->sid, a->computed, d - 1, 0, 0, scope, gen, &r);
+        if (u->routed) return R_NOT;
         if (!have && decisive(r)) {
             out = r;
             have = 1;
         }
+        if (!spawned && decisive(r)) break; /* later parents are never spawned */
     }
     return out;
 }
@@ -994,9 +1046,8 @@ static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, 
         *out = u_ttu(u, ns, obj, ch, d, scope, gen + 1);
         return 1;
     case RS_CSS:
-        if (d <= 0 || !u_spawn(u, gen + 1)) return 0;
-        *out = u_ia(u, ns, obj, ch->rel, d, 0, scope, gen + 1);
-        return 1;
+        if (d < 0) return 0;
+        return u_sub(u, ns, obj, ch->rel, d, 0, 0, scope, gen, out);
     case RS_REWRITE:
         if (d - cost <= 0 || !u_spawn(u, gen + 1)) return 0;
         *out = u_rw(u, ns, obj, ci, d - cost, scope, gen + 1);
@@ -1021,6 +1072,7 @@ static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scop
     const int is_or = a->op == RS_OP_OR;
     res out = R_NOT;
     int have = 0; /* the group's result is fixed (by a child in add order) */
+    int stop = 0; /* a leaf decided it: later children are never spawned */
     if (is_or) {
         int has_css = 0, found = 0;
         for (int k = 0; k < a->child_count; k++) {
@@ -1034,18 +1086,20 @@ static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scop
         }
         if (found) return R_IS;
         if (has_css && d - 1 > 0)
-            for (int k = 0; k < a->child_count; k++) {
+            for (int k = 0; k < a->child_count && !stop; k++) {
                 const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
                 if (ch->type != RS_CSS) continue;
-                if (!u_spawn(u, gen + 1)) return R_NOT;
-                res r = u_ia(u, ns, obj, ch->rel, d - 1, 1, scope, gen + 1);
+                res r;
+                const int spawned = u_sub(u, ns, obj, ch->rel, d - 1, 1, 0, scope, gen, &r);
+                if (u->routed) return R_NOT;
                 if (!have && decisive(r)) {
                     out = r;
                     have = 1;
                 }
+                if (!spawned && decisive(r)) stop = 1;
             }
     }
-    for (int k = 0; k < a->child_count; k++) {
+    for (int k = 0; k < a->child_count && !stop; k++) {
         int ci = db->children[a->child_begin + k];
         if (is_or && db->ast[ci].type == RS_CSS) continue;
         res r;
@@ -1057,7 +1111,7 @@ static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scop
             if (!is_or) out.m = RS_NOT_MEMBER;
             have = 1;
         }
-        if (!spawned && dec) break; /* a leaf decides the group: later children are never spawned */
+        if (!spawned && dec) stop = 1;
     }
     if (!have) out = (!is_or && a->child_count > 0) ? R_IS : R_NOT;
     return out;
@@ -1085,9 +1139,11 @@ static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_
         keep--;
         const uint64_t vk = vkey(db, t->sns, t->sid, t->srel);
         u_insert(u, scope, vk);
-        if (!u_spawn(u, gen + 1)) return R_NOT;
-        res r = u_ia(u, t->sns, t->sid, t->srel, d, 1, scope, gen + 1);
-        if (decisive(r)) u->set[u_insert_find(u, scope, vk)].decisive = 1; /* the table may have grown */
+        res r;
+        /* checkIsAllowed(c, d, skipDirect) (engine.go:161); its leaves are never decisive */
+        const int spawned = u_sub(u, t->sns, t->sid, t->srel, d, 1, 1, scope, gen, &r);
+        if (u->routed) return R_NOT;
+        if (spawned && decisive(r)) u->set[u_insert_find(u, scope, vk)].decisive = 1; /* the table may have grown */
         if (!have && decisive(r)) {
             out = r;
             have = 1;
@@ -1110,7 +1166,8 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
     res rr = R_NOT, er = R_NOT;
     if (has_rewrite && u_spawn(u, gen + 1)) rr = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
     const int direct_is = (!db->strict || !has_rewrite) && !skip && d - 1 > 0 && exists(u->c, ns, obj, rel);
-    if (can_ss && !direct_is && d - 1 > 0 && u_spawn(u, gen + 1)) er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
+    if (can_ss && !direct_is && d - 1 > 0 && has_set_rows(db, ns, rel) && u_spawn(u, gen + 1))
+        er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
     if (decisive(rr)) return rr;
     if (direct_is) return R_IS;
     if (decisive(er)) return er;

@@ -89,6 +89,7 @@ inline void __syncthreads() {}
 inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
 inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) { auto o = *p; *p += v; return o; }
 inline unsigned long long atomicOr(unsigned long long *p, unsigned long long v) { auto o = *p; *p |= v; return o; }
+inline uint32_t atomicOr(uint32_t *p, uint32_t v) { uint32_t o = *p; *p |= v; return o; }
 inline unsigned long long atomicMin(unsigned long long *p, unsigned long long v) { auto o = *p; *p = std::min(o, v); return o; }
 inline uint32_t atomicCAS(uint32_t *p, uint32_t c, uint32_t v) {
     uint32_t o = *p;
@@ -99,6 +100,7 @@ constexpr int warpSize = 1;
 #define __builtin_amdgcn_readfirstlane(x) (x)
 #define __builtin_amdgcn_readlane(x, l) (x)
 #define __builtin_amdgcn_fence(...) ((void)0)
+#define __builtin_amdgcn_s_memtime() 0ull
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 inline unsigned long long atomicCAS(unsigned long long *p, unsigned long long c, unsigned long long v) {
     auto o = *p;
