@@ -86,12 +86,25 @@ def schedule_report(orc, q, gpu_allowed, n: int, cores: int):
                          "pruned occurrences at different rest depths plus depth truncation (oracle/refsem.c)"}
 
 
-def _sql_worker(args):
+SQL_MAX_ROWS = 2_000_000  # per worker: the rows become Python tuples before they reach SQLite
+
+
+_SQL_CTX = None  # (oracle, workload, max_depth, max_width): inherited by the forked workers, never pickled
+
+
+def _sql_worker(q):
     """one host core of the SQL-mode baseline: load the rows its queries can read into an
-    in-memory SQLite store (untimed), then run the restated engine (oracle/refsql.py)"""
-    orc, wl, q, max_depth, max_width = args
+    in-memory SQLite store (untimed), then run the restated engine (oracle/refsql.py).  On a
+    graph where the sample's closure exceeds SQL_MAX_ROWS the share is halved until it fits."""
+    orc, wl, max_depth, max_width = _SQL_CTX
     import refsql
-    rows = refsql.closure_rows(orc, q["ns"], q["obj"], max_depth + 1)
+    while True:
+        rows = refsql.closure_rows(orc, q["ns"], q["obj"], max_depth + 1, max_rows=SQL_MAX_ROWS)
+        if rows is not None or len(q) <= 1:
+            break
+        q = q[: len(q) // 2]
+    if rows is None:
+        return np.zeros(0, np.uint8), 0.0, 0, 0
     eng = refsql.SqlEngine(rows, wl.namespaces, wl.ns_names, wl.rel_names, max_depth=max_depth, max_width=max_width,
                            strict=wl.strict)
     dec = np.zeros(len(q), np.uint8)
@@ -110,18 +123,32 @@ def sql_baseline(orc, wl, q, max_depth, max_width, cores, per_core=512):
     host cores, one process per core, each over the rows its share of the sample can read
     (per_core queries each: a few seconds in all, store loading included)"""
     import multiprocessing as mp
+    global _SQL_CTX
     n = min(len(q), per_core * cores)
-    parts = [q[i:n:cores] for i in range(cores)]
-    with mp.get_context("fork").Pool(cores) as pool:
-        res = pool.map(_sql_worker, [(orc, wl, p, max_depth, max_width) for p in parts])
+    parts = [np.ascontiguousarray(q[i:n:cores]) for i in range(cores)]
+    _SQL_CTX = (orc, wl, max_depth, max_width)  # the workers fork with it: only the query shares travel
+    try:
+        with mp.get_context("fork").Pool(cores) as pool:
+            res = pool.map(_sql_worker, parts)
+    finally:
+        _SQL_CTX = None
     dt = max(r[1] for r in res)
-    dec = np.zeros(n, np.uint8)
-    for i in range(cores):
-        dec[i:n:cores] = res[i][0]
+    done = sum(len(r[0]) for r in res)
+    if done < n:  # some shares were cut to fit SQL_MAX_ROWS: the first len(share) of each
+        n = done
+        dec = np.concatenate([r[0] for r in res])
+        parity_idx = np.concatenate([np.arange(i, i + cores * len(r[0]), cores)[:len(r[0])] for i, r in enumerate(res)])
+    else:
+        dec = np.zeros(n, np.uint8)
+        for i in range(cores):
+            dec[i:n:cores] = res[i][0]
+        parity_idx = np.arange(n)
     stmts = sum(r[2] for r in res)
+    sql_baseline.parity_idx = parity_idx
     return {"value": n / dt, "unit": "checks/s", "cores": cores, "kind": "port",
             "label": "restated reference (SQL mode)",
-            "sample": f"first {n} of the {len(q)}-query batch, oracle/refsql.py: the engine recursion issuing the "
+            "sample": f"{n} queries of the {len(q)}-query batch (a strided sample; each process's share cut to "
+                      f"closures of <= {SQL_MAX_ROWS} rows), oracle/refsql.py: the engine recursion issuing the "
                       f"reference's 4 SQL statements per hop against in-memory SQLite (python sqlite3 "
                       f"{__import__('sqlite3').sqlite_version}), {cores} processes, slowest {dt:.2f} s; "
                       f"{stmts / n:.1f} statements/check; store = the {sum(r[3] for r in res)} rows the sample can "
@@ -165,8 +192,9 @@ def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0, gpu_allowed=N
     try:
         t0 = time.perf_counter()
         sql, sdec = sql_baseline(orc, wl, q, max_depth, max_width, cores)
-        ns = len(sdec)
-        sql["parity_vs_port"] = {"n": ns, "mismatches": int((sdec != dec[:ns]).sum()) if ns <= len(dec) else None}
+        idx = sql_baseline.parity_idx
+        ok = idx < len(dec)
+        sql["parity_vs_port"] = {"n": int(ok.sum()), "mismatches": int((sdec[ok] != dec[idx[ok]]).sum())}
         log(f"sql-mode baseline: {sql['value']:.0f} checks/s ({time.perf_counter() - t0:.1f}s)")
     except Exception as e:  # reported, never fatal to the bench line
         sql = {"error": repr(e)}
@@ -429,6 +457,7 @@ def main():
     torch.cuda.synchronize()
     stream.sync()
     stream.kernel_time(reset=True)
+    stream.frontier_stats(reset=True)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         eng.check_batch_device(dq, len(q), da, de, sync=True)
@@ -439,11 +468,13 @@ def main():
     elapsed_local = time.perf_counter() - t_start
     value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps,
                                      f"cuda:{device}" if dist_on else "cpu")
-    # average tier-0 kernel duration over the timed region: HIP event pairs recorded on the
-    # kernel's own stream around every launch, summed natively
+    # average device time of a batch's check path over the timed region: HIP event pairs recorded
+    # on the engine's own stream around every batch (rewrite snapshots: the frontier engine's
+    # generations plus the DFS interpreter on the routed queries; C2: the union kernel's tier 0)
     k_sum, k_n = stream.kernel_time(reset=True)
     assert k_n == args.steps, f"timed {k_n} kernel launches, expected {args.steps}"
     kernel_ms = k_sum / k_n
+    fr = stream.frontier_stats(reset=True)
 
     log(f"[rank {rank}] timed: {elapsed_local / args.steps * 1e3:.2f} ms/step, kernel {kernel_ms:.2f} ms "
         f"({time.perf_counter() - t_setup:.1f}s since start)")
@@ -472,7 +503,7 @@ def main():
     log(f"[rank {rank}] expand + serving probes done ({time.perf_counter() - t_setup:.1f}s since start)")
 
     achieved = bytes_t0 / (kernel_ms * 1e-3) / 1e9
-    kname = "check_union_kernel" if union_only else "check_kernel"
+    kname = "check_union_kernel" if union_only else "frontier"
     traffic, traffic_src = committed_traffic(args.workload, kname)
     if args.workload == "c2":
         data, cfgno = "nested-group graph", 2
@@ -507,7 +538,9 @@ def main():
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": kname + " (tier 0)", "kernel_ms": kernel_ms,
+                     "kernel": ("check_union_kernel (tier 0)" if union_only else
+                                "check path: frontier generations (fr_init, fr_expand, fr_reduce) + DFS on routed"),
+                     "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": int(bytes_t0),
                      "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (BASELINE.md)",
                      "work": {"rows": pt["rows"][0], "edges": pt["edges"][0], "probes": pt["probes"][0],
@@ -515,6 +548,9 @@ def main():
                               "queries_tier2": pt["queries"][2]}},
         "cpu_baseline": None,
     }
+    if fr["batches"]:
+        out["frontier"] = {"goals_per_batch": fr["goals"] / fr["batches"], "generations_max": fr["max_generations"],
+                           "routed_fraction": fr["routed"] / max(1, fr["queries"]), "budget": 1024}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sched, cb, dec = cpu_baseline(wl, q, wl.max_depth, wl.max_width, args.cpu_budget, gpu_allowed=allowed)
         out["cpu_baseline"] = cb

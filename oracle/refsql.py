@@ -50,8 +50,9 @@ ERR_NO_RELATION, ERR_INTERNAL, ERR_NOT_IMPLEMENTED = 1, 2, 3
 MAX_RECURSION = 4096  # refsem.c's guard: a zero-cost rewrite cycle never returns in the reference
 
 
-def closure_rows(orc, ns, obj, levels: int) -> np.ndarray:
-    """rows an oracle (refsem.Oracle) holds for every object within `levels` hops"""
+def closure_rows(orc, ns, obj, levels: int, max_rows: int = 0):
+    """rows an oracle (refsem.Oracle) holds for every object within `levels` hops (None when
+    there are more than max_rows > 0 of them)"""
     import refsem
     L = refsem.lib()
     L.rs_closure.restype = ctypes.c_size_t
@@ -60,6 +61,8 @@ def closure_rows(orc, ns, obj, levels: int) -> np.ndarray:
     ns = np.ascontiguousarray(ns, np.uint32)
     obj = np.ascontiguousarray(obj, np.uint32)
     need = L.rs_closure(orc.db, ns.ctypes.data, obj.ctypes.data, len(ns), levels, None, 0)
+    if max_rows and need > max_rows:
+        return None
     out = np.zeros(max(1, need), ROW_DT)
     L.rs_closure(orc.db, ns.ctypes.data, obj.ctypes.data, len(ns), levels, out.ctypes.data, need)
     return out[:need]

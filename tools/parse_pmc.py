@@ -19,6 +19,13 @@ def per_launch(counter, sub):
             if r["Counter_Name"] != counter:
                 continue
             vals[(r["Dispatch_Id"], r["Kernel_Name"], int(r["Grid_Size"]))] += float(r["Counter_Value"])
+    if any("fr_expand" in k[1] for k in vals):
+        # the frontier path: every kernel a batch's timed region launches (fr_init, the generations'
+        # fr_expand / fr_reduce, the DFS interpreter on routed queries), per batch (fr_init count)
+        batches = sum(1 for k in vals if "fr_init" in k[1])
+        tot = sum(v for k, v in vals.items() if any(x in k[1] for x in ("fr_init", "fr_expand", "fr_reduce"))
+                  or ("check_kernel<false" in k[1]))
+        return "frontier check path (fr_init + fr_expand + fr_reduce + DFS on routed)", batches, [tot / max(1, batches)]
     # dominant kernel: the uncounted interpreter (<false, ...>) at its largest grid (tier 0)
     cands = [(k, v) for k, v in vals.items() if "check" in k[1] and "<false" in k[1]]
     gmax = max(k[2] for k, _ in cands)
