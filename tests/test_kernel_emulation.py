@@ -31,3 +31,26 @@ def test_one_transition_per_step_matches_oracle(tmp_path):
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert " passed" in r.stdout
+
+
+@pytest.mark.slow
+def test_one_transition_per_step_is_address_clean(tmp_path):
+    """The same worst-case schedule under AddressSanitizer, with the DFS interpreter answering
+    every batch (KETO_FRONTIER=0): no out-of-range access from any interpreter state at a step
+    boundary.  (the round-1 waterfall-dispatch fault.)"""
+    asan = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()
+    if not asan or not os.path.isabs(asan):
+        pytest.skip("no libasan")
+    lib = tmp_path / "libketo_emu_asan.so"
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(ROOT, "tools", "cpuemu"),
+                    f"OBJDIR={tmp_path / 'obj'}", f"LIB={lib}",
+                    "OPT=-O1 -fsanitize=address -fno-omit-frame-pointer -DKETO_GUARD=1"],
+                   check=True, timeout=900)
+    env = dict(os.environ, KETO_MI355X_ALLOW_OVERRIDE="tools", KETO_MI355X_LIB_OVERRIDE=str(lib), KETO_FRONTIER="0",
+               LD_PRELOAD=asan, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_gpu_parity.py"), "-k", "golden or random_worlds or synthetic_small"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=1200)
+    assert "AddressSanitizer" not in r.stdout + r.stderr, (r.stdout + r.stderr)[-3000:]
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
