@@ -47,6 +47,8 @@ struct Tables {
     const uint32_t *nsrel;
     const Op *ops;
     const uint32_t *op_children;
+    const uint32_t *op_items;
+    const uint2 *or_items;
     uint32_t n_ns, n_rel;
 };
 
@@ -115,12 +117,13 @@ __device__ __forceinline__ Tables stage_tables(const DevSnapshot &s, char *lds) 
     Tables T;
     T.n_ns = s.n_ns;
     T.n_rel = s.n_rel;
-    const uint4 *src[5] = {reinterpret_cast<const uint4 *>(s.ns), reinterpret_cast<const uint4 *>(s.relinfo),
+    const uint4 *src[7] = {reinterpret_cast<const uint4 *>(s.ns), reinterpret_cast<const uint4 *>(s.relinfo),
                            reinterpret_cast<const uint4 *>(s.nsrel), reinterpret_cast<const uint4 *>(s.ops),
-                           reinterpret_cast<const uint4 *>(s.op_children)};
+                           reinterpret_cast<const uint4 *>(s.op_children), reinterpret_cast<const uint4 *>(s.op_items),
+                           reinterpret_cast<const uint4 *>(s.or_items)};
     uint32_t off = 0;
-    char *dst[5];
-    for (int i = 0; i < 5; i++) {
+    char *dst[7];
+    for (int i = 0; i < 7; i++) {
         dst[i] = lds + off;
         const uint32_t n16 = s.tab_bytes[i] / 16;
         for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) reinterpret_cast<uint4 *>(dst[i])[k] = src[i][k];
@@ -132,11 +135,13 @@ __device__ __forceinline__ Tables stage_tables(const DevSnapshot &s, char *lds) 
     T.nsrel = reinterpret_cast<const uint32_t *>(dst[2]);
     T.ops = reinterpret_cast<const Op *>(dst[3]);
     T.op_children = reinterpret_cast<const uint32_t *>(dst[4]);
+    T.op_items = reinterpret_cast<const uint32_t *>(dst[5]);
+    T.or_items = reinterpret_cast<const uint2 *>(dst[6]);
     return T;
 }
 
 __device__ __forceinline__ Tables global_tables(const DevSnapshot &s) {
-    return Tables{s.ns, s.relinfo, s.nsrel, s.ops, s.op_children, s.n_ns, s.n_rel};
+    return Tables{s.ns, s.relinfo, s.nsrel, s.ops, s.op_children, s.op_items, s.or_items, s.n_ns, s.n_rel};
 }
 
 }  // namespace keto

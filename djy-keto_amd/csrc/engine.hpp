@@ -37,6 +37,8 @@ struct Snapshot {
     std::vector<uint32_t> relinfo, nsrel;
     std::vector<Op> ops;
     std::vector<uint32_t> op_children;
+    std::vector<uint32_t> op_items;  // flattened OR rewrites (layout.hpp IT_*)
+    std::vector<uint2> or_items;
     DevSnapshot dev{};
     std::vector<void *> allocs;
     keto_snapshot_info info{};

@@ -368,67 +368,79 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                     break;
                 }
                 const bool is_or = okind == OPK_OR;
-                if (!is_or) rop = R_AND;
                 const NodeInfo ni = t_node_info(T, node);
-                uint32_t tail = NONE32, cand_end = 0, kend = o.child_count;
-                if (is_or && ((o.type_kind >> 16) & 1u)) {  // the IN shortcut (rewrites.go:62-92)
-                    bool found = false;
-                    for (uint32_t c = 0; c < o.child_count && !found; c++) {
-                        const Op ch = T.ops[T.op_children[o.child_begin + c]];
-                        if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
-                        const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
-                        if (t & VIRT_BIT) continue;
-                        if (s.strict) {  // traverser.go:137-139
-                            const NodeInfo ti = t_node_info(T, t);
-                            if (ri_status(ti.ri) == REL_DECLARED && ri_rw(ti.ri)) continue;
+                uint32_t tail = NONE32;
+                if (is_or) {  // the flattened items (layout.hpp IT_*), nested ORs spliced in
+                    const uint32_t oi = T.op_items[op], end = (oi & 0xFFFFu) + (oi >> 16);
+                    uint32_t it = oi & 0xFFFFu;
+                    while (it < end) {
+                        const uint2 item = T.or_items[it];
+                        const uint32_t ik = it_kind(item.x), kk = it_k(item.x);
+                        if (ik == IT_NEST) {  // a nested OR at rest depth d - k <= 0 is Unknown (:39-42)
+                            it = d <= kk ? it_end(item.x) : it + 1;
+                            continue;
                         }
-                        found = member(s, q, t);
-                    }
-                    if (found) {
-                        val = M_IS;
-                        break;
-                    }
-                    // no direct member: candidates checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
-                    if (d > 1) {
-                        cand_end = o.child_count;
-                        for (uint32_t c = 0; c < o.child_count; c++) {
-                            const Op ch = T.ops[T.op_children[o.child_begin + c]];
-                            if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
-                            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d - 1, true, 0);
-                            if (sb.word) nc++;
-                            else if (decisive(sb.leaf)) {  // an error decides the OR: nothing after it runs
-                                tail = sb.leaf;
-                                cand_end = c;
-                                kend = 0;
-                                break;
+                        const uint32_t dk = d - kk;
+                        uint32_t leaf = NONE32;
+                        if (ik == IT_SHORT) {  // the IN shortcut (rewrites.go:62-92, traverser.go:123-191)
+                            const Op x = T.ops[item.y];
+                            for (uint32_t c = 0; c < x.child_count; c++) {
+                                const Op ch = T.ops[T.op_children[x.child_begin + c]];
+                                if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
+                                const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
+                                if (t & VIRT_BIT) continue;
+                                if (s.strict) {  // traverser.go:137-139
+                                    const NodeInfo ti = t_node_info(T, t);
+                                    if (ri_status(ti.ri) == REL_DECLARED && ri_rw(ti.ri)) continue;
+                                }
+                                if (member(s, q, t)) {
+                                    leaf = M_IS;
+                                    break;
+                                }
                             }
+                        } else if (ik == IT_CAND) {  // checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
+                            if (dk > 1) {
+                                const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0);
+                                if (sb.word) nc++;
+                                else leaf = sb.leaf;
+                            }
+                        } else if (ik == IT_RW) {
+                            if (dk > 1) nc++;  // nested AND: its own goal at d-1 (:118)
+                        } else {
+                            nc++;  // TTU, NOT
+                        }
+                        if (leaf != NONE32 && decisive(leaf)) {  // binop.go:23-26: nothing after it runs
+                            tail = leaf;
+                            break;
+                        }
+                        it++;
+                    }
+                    pat = it;  // fr_expand's second walk stops here
+                } else {
+                    rop = R_AND;
+                    // the children in AST order, up to a leaf that decides the group
+                    uint32_t kend = o.child_count;
+                    for (uint32_t c = 0; c < o.child_count; c++) {
+                        const Op ch = T.ops[T.op_children[o.child_begin + c]];
+                        const uint32_t ct = ch.type_kind & 0xFFu;
+                        uint32_t leaf = NONE32;
+                        if (ct == OP_REWRITE && d <= 1) leaf = M_UNK;  // nested rewrite at d-1 <= 0 (:39-42)
+                        else if (ct == OP_CSS) {  // checkComputedSubjectSet (rewrites.go:208-230)
+                            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
+                            if (!sb.word) leaf = sb.leaf;
+                        }
+                        if (leaf == NONE32) {
+                            nc++;
+                            continue;
+                        }
+                        if ((leaf >> 8) != 0 || (leaf & 3u) != M_IS) {  // binop.go:52-54
+                            tail = (leaf & ~3u) | M_NOT;
+                            kend = c;
+                            break;
                         }
                     }
+                    pat = kend;
                 }
-                // the other children in AST order, up to a leaf that decides the group
-                for (uint32_t c = 0; c < kend; c++) {
-                    const Op ch = T.ops[T.op_children[o.child_begin + c]];
-                    const uint32_t ct = ch.type_kind & 0xFFu;
-                    if (is_or && ct == OP_CSS) continue;
-                    uint32_t leaf = NONE32;
-                    if (ct == OP_REWRITE && d <= 1) leaf = M_UNK;  // nested rewrite at d-1 <= 0 (:39-42)
-                    else if (ct == OP_CSS) {  // AND: checkComputedSubjectSet (rewrites.go:208-230)
-                        const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
-                        if (!sb.word) leaf = sb.leaf;
-                    }
-                    if (leaf == NONE32) {
-                        nc++;
-                        continue;
-                    }
-                    const bool decides = is_or ? decisive(leaf) : ((leaf >> 8) != 0 || (leaf & 3u) != M_IS);
-                    if (decides) {  // binop.go:23-26 / 52-54
-                        tail = is_or ? leaf : ((leaf & ~3u) | M_NOT);
-                        kend = c;
-                        break;
-                    }
-                }
-                pat = kend;
-                xrel = cand_end;
                 if (nc == 0) val = tail != NONE32 ? tail : ((!is_or && o.child_count > 0) ? M_IS : M_NOT);
                 else val = tail;
                 break;
@@ -561,21 +573,34 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
         case G_RW: {
             const Op o = T.ops[op];
             const NodeInfo ni = t_node_info(T, node);
-            const bool is_or = ((o.type_kind >> 8) & 0xFFu) == OPK_OR;
             uint32_t c = cb;
-            for (uint32_t k2 = 0; k2 < xrel; k2++) {  // shortcut candidates (rewrites.go:88-90)
-                const Op ch = T.ops[T.op_children[o.child_begin + k2]];
-                if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
-                const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
-                const Sub sb = sub_check(s, T, q, t, d - 1, true, 0);
-                if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
+            if (((o.type_kind >> 8) & 0xFFu) == OPK_OR) {
+                uint32_t it = T.op_items[op] & 0xFFFFu;
+                while (it < pat) {
+                    const uint2 item = T.or_items[it];
+                    const uint32_t ik = it_kind(item.x), kk = it_k(item.x);
+                    if (ik == IT_NEST) {
+                        it = d <= kk ? it_end(item.x) : it + 1;
+                        continue;
+                    }
+                    const uint32_t dk = d - kk;
+                    if (ik == IT_CAND) {
+                        if (dk > 1) {
+                            const uint32_t t = t_sibling(T, node, ni, item.y);
+                            const Sub sb = sub_check(s, T, q, t, dk - 1, true, 0);
+                            if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
+                        }
+                    } else if (ik == IT_TTU) spawn(P, c++, node, pos, gword(G_TTU, dk, item.y), scope);
+                    else if (ik == IT_INV) spawn(P, c++, node, pos, gword(G_INV, dk, item.y), scope);
+                    else if (ik == IT_RW && dk > 1) spawn(P, c++, node, pos, gword(G_RW, dk - 1, item.y), scope);
+                    it++;
+                }
+                break;
             }
-            for (uint32_t k2 = 0; k2 < pat; k2++) {  // rewrites.go:95-129
+            for (uint32_t k2 = 0; k2 < pat; k2++) {  // AND: rewrites.go:95-129
                 const uint32_t ci = T.op_children[o.child_begin + k2];
                 const Op ch = T.ops[ci];
                 const uint32_t ct = ch.type_kind & 0xFFu;
-                if (is_or && ct == OP_CSS) continue;
-                if (ct == OP_REWRITE && d <= 1) continue;  // (OR only: an AND stopped at kend)
                 if (ct == OP_TTU) spawn(P, c++, node, pos, gword(G_TTU, d, ci), scope);
                 else if (ct == OP_CSS) {
                     const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);

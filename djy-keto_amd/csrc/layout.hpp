@@ -56,6 +56,15 @@ struct alignas(16) Op {
     uint32_t rel_computed; // CSS: rel | 0 ; TTU: tupleset rel | computed << 16
 };
 
+// OR rewrites flattened for the frontier engine (frontier.hip): an OR's items in add order --
+// its IN shortcut, the shortcut candidates, its other children -- with nested OR rewrites spliced
+// in (IT_NEST guards them: rest depth d - k <= 0 makes the nested OR Unknown; skip to `end`).
+// item {x = kind | k << 4 | end << 16, y = arg}; k = nesting depth (each nested rewrite costs 1)
+enum OrItemKind : uint32_t { IT_NEST = 0, IT_SHORT = 1, IT_CAND = 2, IT_TTU = 3, IT_INV = 4, IT_RW = 5 };
+__host__ __device__ inline uint32_t it_kind(uint32_t x) { return x & 0xFu; }
+__host__ __device__ inline uint32_t it_k(uint32_t x) { return (x >> 4) & 0xFFFu; }
+__host__ __device__ inline uint32_t it_end(uint32_t x) { return x >> 16; }
+
 struct alignas(16) NsDev {
     uint32_t ent_base, node_base, n_slots, slot_base;
 };
@@ -78,6 +87,8 @@ struct DevSnapshot {
     const uint32_t *nsrel;     // [n_ns * n_rel]
     const Op *ops;
     const uint32_t *op_children;
+    const uint32_t *op_items;  // [ops] OR ops: first item | item count << 16 (0: not an OR)
+    const uint2 *or_items;     // flattened OR items
     // (ns, obj) -> entity rank table: block b covers ids [64b, 64b+64) of ck = ns*ent_stride+obj,
     // {set bits lo, hi, entity of the block's first set bit, 0}; an unset bit = no entity
     const uint4 *ent_rank;
@@ -89,8 +100,9 @@ struct DevSnapshot {
     uint32_t probe_k;     // reverse rows up to this length are kept in VGPRs instead
     uint32_t n_ns, n_rel, n_nodes, n_uuids;
     int32_t strict;
-    // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children: staged in LDS
-    uint32_t tab_bytes[5];
+    // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children, op_items, or_items:
+    // staged in LDS
+    uint32_t tab_bytes[7];
     uint32_t lds_bytes;
 };
 

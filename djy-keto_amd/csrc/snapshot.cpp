@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <numeric>
 #include <thread>
 #include <unordered_map>
@@ -448,13 +449,54 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     };
     D.relinfo = upload_small(s.relinfo);
     D.nsrel = upload_small(s.nsrel);
+    // OR rewrites flattened for the frontier engine: nested ORs spliced into their parent's items
+    s.op_items.assign(s.ops.size(), 0u);
+    s.or_items.clear();
+    for (uint32_t op = 0; op < s.ops.size(); op++) {
+        const Op &o = s.ops[op];
+        if ((o.type_kind & 0xFFu) != OP_REWRITE || ((o.type_kind >> 8) & 0xFFu) != OPK_OR) continue;
+        const uint32_t beg = (uint32_t)s.or_items.size();
+        std::function<void(uint32_t, uint32_t)> flat = [&](uint32_t a, uint32_t k) {
+            const Op &x = s.ops[a];
+            auto item = [&](uint32_t kind, uint32_t arg) { s.or_items.push_back(make_uint2(kind | (k << 4), arg)); };
+            if ((x.type_kind >> 16) & 1u) {  // the IN shortcut, then its candidates (rewrites.go:62-92)
+                item(IT_SHORT, a);
+                for (uint32_t c = 0; c < x.child_count; c++) {
+                    const Op &ch = s.ops[s.op_children[x.child_begin + c]];
+                    if ((ch.type_kind & 0xFFu) == OP_CSS) item(IT_CAND, ch.rel_computed & 0xFFFFu);
+                }
+            }
+            for (uint32_t c = 0; c < x.child_count; c++) {  // the other children (rewrites.go:95-129)
+                const uint32_t ci = s.op_children[x.child_begin + c];
+                const Op &ch = s.ops[ci];
+                const uint32_t ct = ch.type_kind & 0xFFu;
+                if (ct == OP_CSS) continue;
+                if (ct == OP_TTU) item(IT_TTU, ci);
+                else if (ct == OP_INVERT) item(IT_INV, ci);
+                else if (((ch.type_kind >> 8) & 0xFFu) == OPK_OR && k + 1 < 0xFFFu) {  // a nested OR: spliced
+                    const size_t at = s.or_items.size();
+                    s.or_items.push_back(make_uint2(IT_NEST | ((k + 1) << 4), ci));
+                    flat(ci, k + 1);
+                    s.or_items[at].x |= (uint32_t)s.or_items.size() << 16;
+                } else item(IT_RW, ci);  // AND (or a bad operator): its own goal
+            }
+        };
+        flat(op, 0);
+        const uint32_t cnt = (uint32_t)s.or_items.size() - beg;
+        if (s.or_items.size() >= 0xFFFFu || cnt >= 0xFFFFu) throw Error(KETO_E_LIMIT, "flattened rewrite programs exceed 65535 items");
+        s.op_items[op] = beg | (cnt << 16);
+    }
     D.ops = upload_small(s.ops);
     D.op_children = upload_small(s.op_children);
+    D.op_items = upload_small(s.op_items);
+    D.or_items = upload_small(s.or_items);
     D.tab_bytes[0] = bytes16(s.ns);
     D.tab_bytes[1] = bytes16(s.relinfo);
     D.tab_bytes[2] = bytes16(s.nsrel);
     D.tab_bytes[3] = bytes16(s.ops);
     D.tab_bytes[4] = bytes16(s.op_children);
+    D.tab_bytes[5] = bytes16(s.op_items);
+    D.tab_bytes[6] = bytes16(s.or_items);
     D.lds_bytes = 0;
     for (uint32_t b : D.tab_bytes) D.lds_bytes += b;
     D.n_ns = s.n_ns;

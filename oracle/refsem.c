@@ -1062,6 +1062,65 @@ static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, 
     }
 }
 
+/* fold one item of a group into its first-decisive result; a deciding leaf stops the group */
+static void u_fold(res r, int spawned, int is_or, res *out, int *have, int *stop) {
+    const int dec = is_or ? decisive(r) : (r.err || r.m != RS_IS_MEMBER);
+    if (!*have && dec) {
+        *out = r;
+        if (!is_or) out->m = RS_NOT_MEMBER;
+        *have = 1;
+    }
+    if (!spawned && dec) *stop = 1;
+}
+
+/* The items of an OR rewrite in add order -- its IN shortcut, the shortcut candidates, its other
+ * children (rewrites.go:62-129) -- with nested OR rewrites spliced in: a nested OR's result is
+ * the first decisive of its own items (NotMember if none), so the concatenation decides the same
+ * group; it only contributes when its rest depth d-1 > 0 (rewrites.go:39-42).  No goal is
+ * spawned for the nested OR itself. */
+static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen, res *out,
+                       int *have, int *stop) {
+    const rs_db *db = u->c->db;
+    const rs_ast *a = &db->ast[ai];
+    int has_css = 0, found = 0;
+    for (int k = 0; k < a->child_count; k++) {
+        const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+        if (ch->type != RS_CSS) continue;
+        has_css = 1;
+        int err;
+        int ri = ast_relation_for(db, ns, ch->rel, &err);
+        if (db->strict && ri >= 0 && db->rels[ri].rewrite >= 0) continue;
+        if (!found && exists(u->c, ns, obj, ch->rel)) found = 1;
+    }
+    if (found) {
+        u_fold(R_IS, 0, 1, out, have, stop);
+        return;
+    }
+    if (has_css && d - 1 > 0)
+        for (int k = 0; k < a->child_count && !*stop; k++) {
+            const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+            if (ch->type != RS_CSS) continue;
+            res r;
+            const int spawned = u_sub(u, ns, obj, ch->rel, d - 1, 1, 0, scope, gen, &r);
+            if (u->routed) return;
+            u_fold(r, spawned, 1, out, have, stop);
+        }
+    for (int k = 0; k < a->child_count && !*stop; k++) {
+        int ci = db->children[a->child_begin + k];
+        const rs_ast *ch = &db->ast[ci];
+        if (ch->type == RS_CSS) continue;
+        if (ch->type == RS_REWRITE && ch->op == RS_OP_OR) { /* restDepth-1 (:118) */
+            if (d - 1 > 0) u_or_items(u, ns, obj, ci, d - 1, scope, gen, out, have, stop);
+            if (u->routed) return;
+            continue;
+        }
+        res r;
+        const int spawned = u_child(u, ns, obj, ci, d, 1, scope, gen, &r);
+        if (u->routed) return;
+        u_fold(r, spawned, 1, out, have, stop);
+    }
+}
+
 static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen) {
     const rs_db *db = u->c->db;
     const rs_ast *a = &db->ast[ai];
@@ -1069,51 +1128,22 @@ static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scop
         res r = {RS_UNKNOWN, RS_ERR_NOT_IMPLEMENTED};
         return r;
     }
-    const int is_or = a->op == RS_OP_OR;
     res out = R_NOT;
     int have = 0; /* the group's result is fixed (by a child in add order) */
     int stop = 0; /* a leaf decided it: later children are never spawned */
-    if (is_or) {
-        int has_css = 0, found = 0;
-        for (int k = 0; k < a->child_count; k++) {
-            const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
-            if (ch->type != RS_CSS) continue;
-            has_css = 1;
-            int err;
-            int ri = ast_relation_for(db, ns, ch->rel, &err);
-            if (db->strict && ri >= 0 && db->rels[ri].rewrite >= 0) continue;
-            if (!found && exists(u->c, ns, obj, ch->rel)) found = 1;
-        }
-        if (found) return R_IS;
-        if (has_css && d - 1 > 0)
-            for (int k = 0; k < a->child_count && !stop; k++) {
-                const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
-                if (ch->type != RS_CSS) continue;
-                res r;
-                const int spawned = u_sub(u, ns, obj, ch->rel, d - 1, 1, 0, scope, gen, &r);
-                if (u->routed) return R_NOT;
-                if (!have && decisive(r)) {
-                    out = r;
-                    have = 1;
-                }
-                if (!spawned && decisive(r)) stop = 1;
-            }
+    if (a->op == RS_OP_OR) {
+        u_or_items(u, ns, obj, ai, d, scope, gen, &out, &have, &stop);
+        if (u->routed) return R_NOT;
+        return have ? out : R_NOT;
     }
     for (int k = 0; k < a->child_count && !stop; k++) {
         int ci = db->children[a->child_begin + k];
-        if (is_or && db->ast[ci].type == RS_CSS) continue;
         res r;
         const int spawned = u_child(u, ns, obj, ci, d, 1, scope, gen, &r);
         if (u->routed) return R_NOT;
-        const int dec = is_or ? decisive(r) : (r.err || r.m != RS_IS_MEMBER);
-        if (!have && dec) {
-            out = r;
-            if (!is_or) out.m = RS_NOT_MEMBER;
-            have = 1;
-        }
-        if (!spawned && dec) stop = 1;
+        u_fold(r, spawned, 0, &out, &have, &stop);
     }
-    if (!have) out = (!is_or && a->child_count > 0) ? R_IS : R_NOT;
+    if (!have) out = a->child_count > 0 ? R_IS : R_NOT;
     return out;
 }
 
