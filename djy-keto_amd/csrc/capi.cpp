@@ -240,6 +240,14 @@ int keto_stream_last_kernel_ms(keto_stream *hs, double *ms) {
     return KETO_OK;
 }
 
+// rewrite-free snapshots run the union interpreter unless KETO_UNION_FRONTIER=1 sends them
+// through the frontier engine (+ DFS on routed queries) like rewrite snapshots
+static void (*check_engine(const keto::Snapshot &snap))(const keto::Snapshot &, keto::Stream &, const keto::CheckLaunch &) {
+    static const char *e = getenv("KETO_UNION_FRONTIER");
+    if (snap.ops.empty() && !(e && e[0] == '1')) return keto::run_check_union;
+    return keto::run_check;
+}
+
 int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *queries, uint64_t n,
                      const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags) {
     keto::Snapshot *snap = SN(hsnap);
@@ -262,7 +270,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
             L.queries = queries;
             L.out_allowed = out_allowed;
             L.out_err = out_err;
-            (snap->ops.empty() ? keto::run_check_union : keto::run_check)(*snap, *s, L);
+            check_engine(*snap)(*snap, *s, L);
             if (!(flags & KETO_F_ASYNC)) {
                 KETO_HIP(hipStreamSynchronize(s->stream));
                 s->harvest();
@@ -279,7 +287,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         L.queries = static_cast<const keto_query *>(s->qbuf);
         L.out_allowed = d_allowed;
         L.out_err = d_err;
-        (snap->ops.empty() ? keto::run_check_union : keto::run_check)(*snap, *s, L);
+        check_engine(*snap)(*snap, *s, L);
         KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipStreamSynchronize(s->stream));
