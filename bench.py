@@ -433,7 +433,6 @@ def main():
         q = synth.nested_groups_queries(wl, args.batch, seed=shard_seed(7, rank))
     else:
         q = synth.drive_queries(wl, args.batch, seed=shard_seed(11, rank))
-    union_only = not any("rewrite" in r for rels in wl.namespaces.values() for r in rels)
     dq = km.DeviceBuffer(device, q.nbytes)
     da = km.DeviceBuffer(device, len(q))
     de = km.DeviceBuffer(device, 4 * len(q))
@@ -503,7 +502,7 @@ def main():
     log(f"[rank {rank}] expand + serving probes done ({time.perf_counter() - t_setup:.1f}s since start)")
 
     achieved = bytes_t0 / (kernel_ms * 1e-3) / 1e9
-    kname = "check_union_kernel" if union_only else "frontier"
+    kname = "frontier"
     traffic, traffic_src = committed_traffic(args.workload, kname)
     if args.workload == "c2":
         data, cfgno = "nested-group graph", 2
@@ -538,8 +537,7 @@ def main():
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": ("check_union_kernel (tier 0)" if union_only else
-                                "check path: frontier generations (fr_init, fr_expand, fr_reduce) + DFS on routed"),
+                     "kernel": "check path: frontier generations (fr_init, fr_expand, fr_reduce) + DFS on routed",
                      "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": int(bytes_t0),
                      "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (BASELINE.md)",

@@ -323,6 +323,17 @@ __global__ __launch_bounds__(BLK) void k_slot_setrows(const uint4 *set_row, uint
     if (!flag[gs]) atomicOr(&flag[gs], 1u);
 }
 
+// slots holding a subject-id tuple: a direct check of any other slot against a subject id fails
+__global__ __launch_bounds__(BLK) void k_slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of,
+                                                     uint32_t n_rel, const NsDev *ns, uint32_t *flag) {
+    const uint64_t i = gid();
+    if (i >= n || t[i].subj_kind != 0) return;
+    const uint32_t k = slot_of[(size_t)t[i].ns * n_rel + t[i].rel];
+    if (k == NO_SLOT) return;
+    const uint32_t gs = ns[t[i].ns].slot_base + k;
+    if (!flag[gs]) atomicOr(&flag[gs], 1u);
+}
+
 __global__ __launch_bounds__(BLK) void k_fill32(uint32_t *a, uint64_t n, uint32_t x) {
     const uint64_t i = gid();
     if (i < n) a[i] = x;
@@ -478,7 +489,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         DevBuf w2(4 * (N + 1)), changed(4);
         hipLaunchKernelGGL(k_fill32, grid_for(N), dim3(BLK), 0, 0, out.weight, N, 1u);
         uint32_t *w = out.weight, *nw = w2.u32();
-        for (uint32_t round = 0; round < WEIGHT_ROUNDS; round++) {
+        for (uint32_t round = 0; in.weights && round < WEIGHT_ROUNDS; round++) {
             KETO_HIP(hipMemset(changed.p, 0, 4));
             hipLaunchKernelGGL(k_weight, grid_for(N), dim3(BLK), 0, 0, set_cnt.u32(), out.set_dst.u32(), N, w, nw,
                                changed.u32());
@@ -514,6 +525,11 @@ void rows(const RowsIn &in, RowsOut &out) {
 
 void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag) {
     hipLaunchKernelGGL(k_slot_setrows, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, ns, n_ns, flag);
+    KETO_HIP(hipGetLastError());
+}
+
+void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag) {
+    if (n) hipLaunchKernelGGL(k_slot_idrows, grid_for(n), dim3(BLK), 0, 0, t, n, slot_of, n_rel, ns, flag);
     KETO_HIP(hipGetLastError());
 }
 

@@ -190,6 +190,10 @@ __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
             c_lsteps += st != S_IDLE ? 1 : 0;
         }
         if (st == S_IDLE) continue;
+#ifdef KETO_EMU_SKIP  // CPU-emulation builds only: the round-1 waterfall variant's unserved lanes
+        // (a lane sits out the step after its operands were loaded; they are gone next step)
+        if (mix64(((uint64_t)gl << 32) ^ (c_wsteps++ * 0x9E3779B97F4A7C15ull)) % KETO_EMU_SKIP == 0) continue;
+#endif
 #ifdef KETO_EMU_TRACE
         keto_emu_trace_step(st == S_START ? pos : NONE32);
 #endif

@@ -48,7 +48,8 @@ struct Snapshot {
     uint32_t ns_of(uint32_t node) const;
 };
 
-Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples);
+Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
+                         bool sched_weights = true);
 
 // build.hip: device-side snapshot construction (one-thread-per-item kernels)
 namespace build {
@@ -84,6 +85,7 @@ struct RowsIn {
     const uint32_t *slot_of;
     uint64_t stride;
     uint32_t n_rel, n_uuids;
+    bool weights = true;            // scheduling weights (false: all 1, e.g. per-batch closure snapshots)
 };
 struct RowsOut {
     uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *weight;  // caller-allocated
@@ -95,6 +97,7 @@ void rows(const RowsIn &in, RowsOut &out);
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows);
 // flag[global slot] |= 1 where a row of the slot holds a subject set (flag zeroed by the caller)
 void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag);
+void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag);
 }  // namespace build
 
 // scratch tier: per-lane visited capacity (slots, pow2) and stack frames

@@ -107,6 +107,13 @@ __device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_
     const uint4 b = P.start[2 * (size_t)pos + 1];  // one load: resolve.hip packs a heavy subject here too
     return Subject{b.x, b.y == START_R_HEAVY, b};
 }
+// can node c's rows hold the query subject at all: a subject id needs a slot with subject-id
+// tuples, a subject set one with subject-set tuples (RI_IDROWS / RI_SETROWS, per snapshot).
+// Only a heavy subject's probe is worth skipping (a light one's entries are registers, and its
+// record holds them in place of the subject index).
+__device__ __forceinline__ bool may_hold(const DevSnapshot &s, const Subject &q, uint32_t ri) {
+    return !q.heavy || (q.sidx < s.n_uuids ? ri_idrows(ri) : ri_setrows(ri));
+}
 __device__ __forceinline__ bool member(const DevSnapshot &s, const Subject &q, uint32_t c) {
     if (!q.heavy) return c == q.R.x || c == q.R.y || c == q.R.z || c == q.R.w;
     const uint64_t key = (((uint64_t)q.sidx << 32) | c) + 1;
@@ -156,9 +163,16 @@ __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, 
     if (dc == 0) return Sub{0, M_UNK};
     const NodeInfo ni = t_node_info(T, c);
     const bool err = ri_status(ni.ri) == REL_ERROR;
+    if (ri_rw(ni.ri) && !esf) {
+        // with neither a direct check (engine.go:239-243) nor an expand-subject (:244-246) to
+        // run, checkIsAllowed is its rewrite's result (an OR / AND never yields a bare Unknown):
+        // the RW goal is spawned in the IA's place, one generation earlier (oracle u_sub)
+        const bool direct = !s.strict && !skip && dc > 1 && !(c & VIRT_BIT) && may_hold(s, q, ni.ri) && member(s, q, c);
+        if (!direct && !(ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri))) return Sub{gword(G_RW, dc, ri_op(ni.ri)), 0};
+    }
     if (ri_rw(ni.ri) || (err && esf)) return Sub{gword(G_IA, dc, 0, (skip ? GF_SKIP : 0u) | esf), 0};
     if (err) return Sub{0, mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16)};
-    if (!skip && dc > 1 && !(c & VIRT_BIT) && member(s, q, c)) return Sub{0, M_IS};
+    if (!skip && dc > 1 && !(c & VIRT_BIT) && may_hold(s, q, ni.ri) && member(s, q, c)) return Sub{0, M_IS};
     if (ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri)) return Sub{gword(G_ES, dc - 1, 0, esf), 0};
     return Sub{0, M_NOT};
 }
@@ -324,7 +338,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 }
                 const bool rw = ri_rw(ni.ri);
                 bool direct = false;
-                if ((!s.strict || !rw) && !(w & GF_SKIP) && d > 1 && !(node & VIRT_BIT))  // :239-243
+                if ((!s.strict || !rw) && !(w & GF_SKIP) && d > 1 && !(node & VIRT_BIT) && may_hold(s, q, ni.ri))  // :239-243
                     direct = member(s, q, node);
                 // expand-subject(d-1) (:244-246), unless no row of the relation holds a subject set
                 const bool es = ri_ss(ni.ri) && d > 1 && !direct && ri_setrows(ni.ri);
@@ -370,6 +384,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 const bool is_or = okind == OPK_OR;
                 const NodeInfo ni = t_node_info(T, node);
                 uint32_t tail = NONE32;
+                xrel = NONE32;  // OR: parents of the stopping TTU item phase B spawns (NONE32: all)
                 if (is_or) {  // the flattened items (layout.hpp IT_*), nested ORs spliced in
                     const uint32_t oi = T.op_items[op], end = (oi & 0xFFFFu) + (oi >> 16);
                     uint32_t it = oi & 0xFFFFu;
@@ -406,8 +421,29 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                             }
                         } else if (ik == IT_RW) {
                             if (dk > 1) nc++;  // nested AND: its own goal at d-1 (:118)
+                        } else if (ik == IT_TTU) {
+                            // spliced: a tuple-to-userset is the first decisive of its parents'
+                            // checks in row order, so they are this OR's own items (rewrites.go:
+                            // 242-293; oracle u_or_items); d - 1 <= 0 makes each one Unknown
+                            if (dk > 1) {
+                                const uint32_t rc = T.ops[item.y].rel_computed;
+                                const uint32_t ts = t_sibling(T, node, ni, rc & 0xFFFFu);
+                                if (!(ts & VIRT_BIT)) {
+                                    Edges et(s, s.set_row[ts]);
+                                    for (uint32_t e = 0; et.cur < et.end; e++) {
+                                        const uint32_t pn = et.next() & ~EDGE_ALIAS;
+                                        const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), rc >> 16), dk - 1, false, 0);
+                                        if (sb.word) nc++;
+                                        else if (decisive(sb.leaf)) {
+                                            leaf = sb.leaf;
+                                            xrel = e;
+                                            break;
+                                        }
+                                    }
+                                }
+                            }
                         } else {
-                            nc++;  // TTU, NOT
+                            nc++;  // NOT
                         }
                         if (leaf != NONE32 && decisive(leaf)) {  // binop.go:23-26: nothing after it runs
                             tail = leaf;
@@ -576,7 +612,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             uint32_t c = cb;
             if (((o.type_kind >> 8) & 0xFFu) == OPK_OR) {
                 uint32_t it = T.op_items[op] & 0xFFFFu;
-                while (it < pat) {
+                while (it < pat || (it == pat && xrel != NONE32)) {  // (+ the stopping TTU item's parents)
                     const uint2 item = T.or_items[it];
                     const uint32_t ik = it_kind(item.x), kk = it_k(item.x);
                     if (ik == IT_NEST) {
@@ -590,8 +626,22 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                             const Sub sb = sub_check(s, T, q, t, dk - 1, true, 0);
                             if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
                         }
-                    } else if (ik == IT_TTU) spawn(P, c++, node, pos, gword(G_TTU, dk, item.y), scope);
-                    else if (ik == IT_INV) spawn(P, c++, node, pos, gword(G_INV, dk, item.y), scope);
+                    } else if (ik == IT_TTU) {
+                        if (dk > 1) {
+                            const uint32_t rc = T.ops[item.y].rel_computed;
+                            const uint32_t ts = t_sibling(T, node, ni, rc & 0xFFFFu);
+                            if (!(ts & VIRT_BIT)) {
+                                Edges et(s, s.set_row[ts]);
+                                const uint32_t lim = it == pat ? xrel : NONE32;
+                                for (uint32_t e = 0; et.cur < et.end && e < lim; e++) {
+                                    const uint32_t pn = et.next() & ~EDGE_ALIAS;
+                                    const uint32_t t = t_sibling(T, pn, t_node_info(T, pn), rc >> 16);
+                                    const Sub sb = sub_check(s, T, q, t, dk - 1, false, 0);
+                                    if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
+                                }
+                            }
+                        }
+                    } else if (ik == IT_INV) spawn(P, c++, node, pos, gword(G_INV, dk, item.y), scope);
                     else if (ik == IT_RW && dk > 1) spawn(P, c++, node, pos, gword(G_RW, dk - 1, item.y), scope);
                     it++;
                 }

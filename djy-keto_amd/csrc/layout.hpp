@@ -31,7 +31,8 @@ enum RelStatus : uint32_t { REL_NIL = 0, REL_DECLARED = 1, REL_ERROR = 2 };
 // relinfo word (per (ns, slot)):  bits 0-15 rewrite op (NO_OP = none)
 //   bit 16 has_rewrite, bit 17 can_have_subject_sets (engine.go:233-235), bits 18-19 status
 //   bit 20 shared visited class (vkey array must be consulted), bit 21 some row of the slot holds
-//   a subject set (set by the snapshot builder; virtual nodes never)
+//   a subject set, bit 22 some row of the slot holds a subject id (both set by the snapshot
+//   builder; virtual nodes never)
 __host__ __device__ inline uint32_t ri_op(uint32_t ri) { return ri & 0xFFFFu; }
 __host__ __device__ inline bool ri_rw(uint32_t ri) { return (ri >> 16) & 1u; }
 __host__ __device__ inline bool ri_ss(uint32_t ri) { return (ri >> 17) & 1u; }
@@ -39,6 +40,8 @@ __host__ __device__ inline uint32_t ri_status(uint32_t ri) { return (ri >> 18) &
 __host__ __device__ inline bool ri_shared(uint32_t ri) { return (ri >> 20) & 1u; }
 constexpr uint32_t RI_SETROWS = 1u << 21;
 __host__ __device__ inline bool ri_setrows(uint32_t ri) { return (ri >> 21) & 1u; }
+constexpr uint32_t RI_IDROWS = 1u << 22;
+__host__ __device__ inline bool ri_idrows(uint32_t ri) { return (ri >> 22) & 1u; }
 __host__ __device__ inline uint32_t make_ri(uint32_t op, bool rw, bool ss, uint32_t status, bool shared) {
     return (op & 0xFFFFu) | (uint32_t(rw) << 16) | (uint32_t(ss) << 17) | (status << 18) | (uint32_t(shared) << 20);
 }

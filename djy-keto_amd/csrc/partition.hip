@@ -155,11 +155,33 @@ struct Lookup {
     const keto_tuple *tuples;
     const uint64_t *req;          // requested keys, grouped by source rank
     const uint64_t *req_off;      // [world+1] request offsets per source
-    const uint32_t *subj;         // sorted subject lists of every source, concatenated
-    const uint64_t *subj_off;     // [world+1]
+    const unsigned long long *subj_set;  // (source, subject id) hash set (k_subj_fill)
+    uint64_t subj_mask;
     uint32_t world;
     int filter;
 };
+__device__ __forceinline__ unsigned long long subj_key(uint32_t src, uint32_t sid) {
+    return (((unsigned long long)src << 32) | sid) + 1ull;  // 0 = empty slot
+}
+// the subject lists every source sent (concatenated, soff[world+1]) into one hash set
+__global__ __launch_bounds__(BLK) void k_subj_fill(const uint32_t *subj, const uint64_t *soff, uint32_t world,
+                                                    uint64_t n, unsigned long long *set, uint64_t mask) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        uint32_t lo = 0, hi = world;  // last source whose offset <= i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (soff[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        const unsigned long long k = subj_key(lo, subj[i]);
+        uint64_t h = mix64(k) & mask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&set[h], 0ull, k);
+            if (prev == 0ull || prev == k) break;
+            h = (h + 1) & mask;
+        }
+    }
+}
 __device__ __forceinline__ bool run_of(const Lookup &L, uint64_t key, uint64_t &b, uint64_t &e) {
     uint64_t h = mix64(key + 1) & L.index_mask;
     for (;;) {  // one 16-byte probe per step; the table is at most half full
@@ -184,13 +206,14 @@ __device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
 }
 __device__ __forceinline__ bool keep(const Lookup &L, const keto_tuple &t, uint32_t src) {
     if (!L.filter || t.subj_kind == 1) return true;
-    uint64_t lo = L.subj_off[src], hi = L.subj_off[src + 1];
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (L.subj[mid] < t.s_obj) lo = mid + 1;
-        else hi = mid;
+    const unsigned long long k = subj_key(src, t.s_obj);
+    uint64_t h = mix64(k) & L.subj_mask;
+    for (;;) {  // at most half full: every probe sequence ends at an empty slot
+        const unsigned long long v = L.subj_set[h];
+        if (v == k) return true;
+        if (v == 0ull) return false;
+        h = (h + 1) & L.subj_mask;
     }
-    return lo < L.subj_off[src + 1] && L.subj[lo] == t.s_obj;
 }
 __global__ __launch_bounds__(BLK) void k_lookup_count(Lookup L, uint64_t n, uint64_t *cnt) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
@@ -217,6 +240,62 @@ __global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, u
                                                unsigned long long *n_cand) {
     for (uint64_t i = gid(); i < n; i += gstride())
         if (t[i].subj_kind == 1) cand[atomicAdd(n_cand, 1ull)] = okey(t[i].s_ns, t[i].s_obj);
+}
+
+// Compact id space of a closure (remap_ids): the uuid ids its tuples and the batch's queries /
+// roots name, ranked in global order.  The builder sizes its entity table and reverse offsets
+// by the id space, so a closure snapshot over local ids costs its tuples, not the whole graph's
+// uuid range.  Decisions and trees do not depend on the ids' values, only on equality.
+__global__ __launch_bounds__(BLK) void k_ids_tuples(const keto_tuple *t, uint64_t n, uint32_t *ids, uint32_t *pos) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        ids[2 * i] = t[i].obj;
+        ids[2 * i + 1] = t[i].s_obj;
+        pos[2 * i] = (uint32_t)(2 * i);
+        pos[2 * i + 1] = (uint32_t)(2 * i + 1);
+    }
+}
+__global__ __launch_bounds__(BLK) void k_ids_queries(const keto_query *q, uint64_t n, uint64_t base, uint32_t *ids,
+                                                      uint32_t *pos) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        ids[base + 2 * i] = q[i].obj;
+        ids[base + 2 * i + 1] = q[i].s_obj;
+        pos[base + 2 * i] = (uint32_t)(base + 2 * i);
+        pos[base + 2 * i + 1] = (uint32_t)(base + 2 * i + 1);
+    }
+}
+__global__ __launch_bounds__(BLK) void k_ids_roots(const keto_subject_set *r, uint64_t n, uint64_t base, uint32_t *ids,
+                                                    uint32_t *pos) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        ids[base + i] = r[i].obj;
+        pos[base + i] = (uint32_t)(base + i);
+    }
+}
+__global__ __launch_bounds__(BLK) void k_flags32(const uint32_t *k, uint64_t n, uint32_t *flag) {
+    for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+}
+// sorted entry i: local id = (inclusive count of distinct ids up to i) - 1
+__global__ __launch_bounds__(BLK) void k_ids_assign(const uint32_t *sk, const uint32_t *spos, const uint32_t *flag,
+                                                     const uint32_t *incl, uint64_t n, uint32_t *lid, uint32_t *uniq) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        const uint32_t l = incl[i] - 1;
+        lid[spos[i]] = l;
+        if (flag[i]) uniq[l] = sk[i];
+    }
+}
+__global__ __launch_bounds__(BLK) void k_apply_tuples(keto_tuple *t, uint64_t n, const uint32_t *lid) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        t[i].obj = lid[2 * i];
+        t[i].s_obj = lid[2 * i + 1];
+    }
+}
+__global__ __launch_bounds__(BLK) void k_apply_queries(keto_query *q, uint64_t n, uint64_t base, const uint32_t *lid) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        q[i].obj = lid[base + 2 * i];
+        q[i].s_obj = lid[base + 2 * i + 1];
+    }
+}
+__global__ __launch_bounds__(BLK) void k_apply_roots(keto_subject_set *r, uint64_t n, uint64_t base, const uint32_t *lid) {
+    for (uint64_t i = gid(); i < n; i += gstride()) r[i].obj = lid[base + i];
 }
 
 // ------------------------------------------------------------------ host side
@@ -246,7 +325,11 @@ struct Partition {
     hipStream_t hs = nullptr;
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
-    DevBuf table, seen, cand, fresh, routed, req, req_off, subj, subj_off, cnt, pos, out, got, scratch, ctr, closure;
+    DevBuf table, seen, cand, fresh, routed, req, req_off, subj, subj_off, subj_set, cnt, pos, out, got, scratch, ctr, closure;
+    uint64_t subj_mask = 0;
+    // compact id space of the last closure (remap_ids): local id -> global uuid id
+    DevBuf rm_ids, rm_pos, rm_ids2, rm_pos2, rm_flag, rm_rank, rm_lid, uniq, bout;
+    uint64_t n_local = 0;
     DevBuf bq, braw, bsorted, bkeys, bsubj, bsubj_src, bhist;  // per-batch inputs, reused
     bool verbose = false;
     uint64_t table_mask = 0, n_seen = 0;
@@ -364,6 +447,15 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
     for (uint32_t r = 0; r < W; r++) soff[r + 1] = soff[r] + subj_from[r];
     ensure(P.subj_off, (W + 1) * 8);
     KETO_HIP(hipMemcpyAsync(P.subj_off.p, soff.data(), (W + 1) * 8, hipMemcpyHostToDevice, P.hs));
+    // (source, subject) hash set: an owner's filter is one probe per subject-id tuple
+    uint64_t scap = 1u << 10;
+    while (scap < 2 * std::max<uint64_t>(1, soff[W])) scap *= 2;
+    ensure(P.subj_set, scap * 8);
+    P.subj_mask = scap - 1;
+    KETO_HIP(hipMemsetAsync(P.subj_set.p, 0, scap * 8, P.hs));
+    if (filter && soff[W])
+        hipLaunchKernelGGL(k_subj_fill, grid_for(soff[W]), dim3(BLK), 0, P.hs, dptr<uint32_t>(P.subj),
+                           dptr<uint64_t>(P.subj_off), W, soff[W], dptr<unsigned long long>(P.subj_set), P.subj_mask);
 
     // seen set: fresh per batch
     P.n_seen = 0;
@@ -435,7 +527,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         KETO_HIP(hipMemcpyAsync(P.req_off.p, roff.data(), (W + 1) * 8, hipMemcpyHostToDevice, P.hs));
         Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
                  dptr<keto_tuple>(P.tuples),
-                 dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<uint32_t>(P.subj), dptr<uint64_t>(P.subj_off),
+                 dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<unsigned long long>(P.subj_set), P.subj_mask,
                  W, filter ? 1 : 0};
         ensure(P.cnt, (n_req + 1) * 8);
         ensure(P.pos, (n_req + 1) * 8);
@@ -607,8 +699,43 @@ uint64_t batch_keys(Partition &P, const keto_query *q, uint64_t n, DevBuf &keys,
     return d2h_u64(P, nu);
 }
 
+// The closure's tuples plus the batch's queries (q, device) or Expand roots (r, device) over the
+// compact id space: rewritten in place, P.uniq[local] = global, P.n_local ids.
+void remap_ids(Partition &P, uint64_t nt, keto_query *q, keto_subject_set *r, uint64_t n) {
+    const uint64_t E = 2 * nt + (q ? 2 * n : n);
+    if (E >= (1ull << 31)) throw Error(KETO_E_LIMIT, "closure too large for the compact id pass (2^31 ids)");
+    for (DevBuf *b : {&P.rm_ids, &P.rm_pos, &P.rm_ids2, &P.rm_pos2, &P.rm_flag, &P.rm_rank, &P.rm_lid, &P.uniq})
+        ensure(*b, std::max<uint64_t>(1, E) * 4);
+    uint32_t *ids = dptr<uint32_t>(P.rm_ids), *pos = dptr<uint32_t>(P.rm_pos), *sk = dptr<uint32_t>(P.rm_ids2),
+             *sp = dptr<uint32_t>(P.rm_pos2), *fl = dptr<uint32_t>(P.rm_flag), *rk = dptr<uint32_t>(P.rm_rank),
+             *lid = dptr<uint32_t>(P.rm_lid);
+    keto_tuple *t = dptr<keto_tuple>(P.closure);
+    if (nt) hipLaunchKernelGGL(k_ids_tuples, grid_for(nt), dim3(BLK), 0, P.hs, t, nt, ids, pos);
+    if (n && q) hipLaunchKernelGGL(k_ids_queries, grid_for(n), dim3(BLK), 0, P.hs, q, n, 2 * nt, ids, pos);
+    if (n && r) hipLaunchKernelGGL(k_ids_roots, grid_for(n), dim3(BLK), 0, P.hs, r, n, 2 * nt, ids, pos);
+    P.n_local = 0;
+    if (E) {
+        const int ne = (int)E;
+        cub_call(P, [&](void *tmp, size_t &b) {
+            return hipcub::DeviceRadixSort::SortPairs(tmp, b, ids, sk, pos, sp, ne, 0, 32, P.hs);
+        });
+        hipLaunchKernelGGL(k_flags32, grid_for(E), dim3(BLK), 0, P.hs, sk, E, fl);
+        cub_call(P, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::InclusiveSum(tmp, b, fl, rk, ne, P.hs); });
+        hipLaunchKernelGGL(k_ids_assign, grid_for(E), dim3(BLK), 0, P.hs, sk, sp, fl, rk, E, lid, dptr<uint32_t>(P.uniq));
+        uint32_t m = 0;
+        KETO_HIP(hipMemcpyAsync(&m, rk + E - 1, 4, hipMemcpyDeviceToHost, P.hs));
+        if (nt) hipLaunchKernelGGL(k_apply_tuples, grid_for(nt), dim3(BLK), 0, P.hs, t, nt, lid);
+        if (n && q) hipLaunchKernelGGL(k_apply_queries, grid_for(n), dim3(BLK), 0, P.hs, q, n, 2 * nt, lid);
+        if (n && r) hipLaunchKernelGGL(k_apply_roots, grid_for(n), dim3(BLK), 0, P.hs, r, n, 2 * nt, lid);
+        sync(P);
+        P.n_local = m;
+    }
+}
+
 Snapshot *closure_snapshot(Partition &P, uint64_t n_tuples) {
-    return build_snapshot(&P.cfg, dptr<keto_tuple>(P.closure), n_tuples, true);
+    keto_snapshot_config cfg = P.cfg;
+    cfg.n_uuids = (uint32_t)std::max<uint64_t>(1, P.n_local);
+    return build_snapshot(&cfg, dptr<keto_tuple>(P.closure), n_tuples, true, false);  // (one batch: no weights)
 }
 }  // namespace
 
@@ -624,15 +751,25 @@ void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8
     const uint64_t nt = closure(P, dptr<uint64_t>(keys), n, dptr<uint32_t>(subj), n_subj, true, st);
     st.closure_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
+    keto_query *dq = dptr<keto_query>(P.bq);  // the batch, uploaded by batch_keys
+    remap_ids(P, nt, dq, nullptr, n);
     std::unique_ptr<Snapshot> snap(closure_snapshot(P, nt));
     st.build_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
-    const int rc = keto_check_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, q, n, &P.limits, allowed, err,
-                                    flags & (KETO_F_COUNT_WORK | KETO_F_ERR_DETAIL));
+    ensure(P.bout, std::max<uint64_t>(1, n) * 8 + 256);
+    uint8_t *d_allowed = dptr<uint8_t>(P.bout);
+    int32_t *d_err = reinterpret_cast<int32_t *>(dptr<uint8_t>(P.bout) + (n + 255) / 256 * 256);
+    const int rc = keto_check_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, dq, n, &P.limits, d_allowed,
+                                    d_err, KETO_F_DEVICE_PTRS | (flags & (KETO_F_COUNT_WORK | KETO_F_ERR_DETAIL)));
     if (rc != KETO_OK) {
         char buf[512];
         keto_last_error(buf, sizeof buf);
         throw Error(rc, buf);
+    }
+    if (n) {
+        KETO_HIP(hipMemcpyAsync(allowed, d_allowed, n, hipMemcpyDeviceToHost, P.hs));
+        KETO_HIP(hipMemcpyAsync(err, d_err, n * 4, hipMemcpyDeviceToHost, P.hs));
+        sync(P);
     }
     st.run_s = secs(t0);
     P.last = st;
@@ -650,6 +787,11 @@ uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, ui
     const uint64_t nt = closure(P, dptr<uint64_t>(keys), n, nullptr, 0, false, st);
     st.closure_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
+    remap_ids(P, nt, nullptr, dptr<keto_subject_set>(dr), n);
+    std::vector<keto_subject_set> lroots(n);
+    if (n) KETO_HIP(hipMemcpy(lroots.data(), dr.p, n * sizeof(keto_subject_set), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> uniq(P.n_local);
+    if (P.n_local) KETO_HIP(hipMemcpy(uniq.data(), P.uniq.p, P.n_local * 4, hipMemcpyDeviceToHost));
     std::unique_ptr<Snapshot> snap(closure_snapshot(P, nt));
     st.build_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
@@ -657,7 +799,7 @@ uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, ui
     P.xerr.assign(std::max<uint64_t>(1, n), 0);
     if (P.xnodes.empty()) P.xnodes.resize(1u << 16);
     for (;;) {
-        const int rc = keto_expand_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, roots, n, &P.limits,
+        const int rc = keto_expand_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, lroots.data(), n, &P.limits,
                                          P.xnodes.data(), P.xnodes.size(), P.xoffs.data(), P.xerr.data());
         if (rc == KETO_E_CAPACITY) {
             P.xnodes.resize(P.xoffs[n]);
@@ -670,6 +812,8 @@ uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, ui
         }
         break;
     }
+    for (uint64_t i = 0; i < P.xoffs[n]; i++)  // the trees' subject ids back to the global id space
+        if (P.xnodes[i].s_obj < P.n_local) P.xnodes[i].s_obj = uniq[P.xnodes[i].s_obj];
     st.run_s = secs(t0);
     P.last = st;
     return P.xoffs[n];

@@ -120,7 +120,8 @@ uint32_t Snapshot::ns_of(uint32_t node) const {
     return lo;
 }
 
-Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples) {
+Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
+                         bool sched_weights) {
     auto t0 = std::chrono::steady_clock::now();
     if (!cfg) throw Error(KETO_E_INVALID, "null config");
     if (n && !tuples) throw Error(KETO_E_INVALID, "null tuples");
@@ -342,8 +343,6 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         D.ent_rank = table;
         D.ent_stride = stride;
         D.ent_obj = d_eo;
-        s.ent_obj.resize(ent_total);
-        KETO_HIP(hipMemcpy(s.ent_obj.data(), d_eo, 4 * ent_total, hipMemcpyDeviceToHost));
         uint32_t *d_sr = static_cast<uint32_t *>(dalloc(4 * std::max<size_t>(1, s.slot_rel.size())));
         if (!s.slot_rel.empty())
             KETO_HIP(hipMemcpy(d_sr, s.slot_rel.data(), 4 * s.slot_rel.size(), hipMemcpyHostToDevice));
@@ -362,12 +361,20 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     ro.rev_nodes = static_cast<uint32_t *>(dalloc(4 * n));
     ro.set_row = static_cast<uint4 *>(dalloc(16 * (uint64_t)N));
     ro.weight = static_cast<uint32_t *>(dalloc(4 * (uint64_t)N));
+    std::vector<uint32_t> idrows(total_slots, 0);  // slots holding a subject-id tuple (RI_IDROWS)
     {
         DevBuf d_slot(4 * NR);
         KETO_HIP(hipMemcpy(d_slot.p, slot_of.data(), 4 * NR, hipMemcpyHostToDevice));
         build::RowsIn ri{dt, device_tuples ? nullptr : tuples, n, N, n_subj_idx, static_cast<const unsigned long long *>(d_bits.p), d_rank.u32(),
                          D.ns, d_slot.u32(), stride, s.n_rel, s.n_uuids};
+        ri.weights = sched_weights;
         build::rows(ri, ro);
+        if (total_slots) {
+            DevBuf flag(4ull * total_slots);
+            KETO_HIP(hipMemset(flag.p, 0, 4ull * total_slots));
+            build::slot_idrows(dt, n, d_slot.u32(), s.n_rel, D.ns, flag.u32());
+            KETO_HIP(hipMemcpy(idrows.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
+        }
     }
     d_t.reset();
     d_bits.reset();
@@ -397,6 +404,8 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         for (auto &kv : cls)
             if (kv.second.size() > 1) any_shared = true;
         if (any_shared) {
+            s.ent_obj.resize(ent_total);  // (host copy only for this rare case: 4 B per entity over PCIe)
+            KETO_HIP(hipMemcpy(s.ent_obj.data(), D.ent_obj, 4 * ent_total, hipMemcpyDeviceToHost));
             std::vector<uint32_t> vkey(N);
             std::iota(vkey.begin(), vkey.end(), 0u);
             std::vector<uint32_t> slot_ns(total_slots);
@@ -438,8 +447,10 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         build::slot_setrows(ro.set_row, N, D.ns, s.n_ns, flag.u32());
         std::vector<uint32_t> hf(total_slots);
         KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
-        for (uint32_t gs = 0; gs < total_slots; gs++)
+        for (uint32_t gs = 0; gs < total_slots; gs++) {
             if (hf[gs]) s.relinfo[gs] |= RI_SETROWS;
+            if (idrows[gs]) s.relinfo[gs] |= RI_IDROWS;
+        }
     }
     auto upload_small = [&](const auto &v) {
         using T = typename std::decay_t<decltype(v)>::value_type;

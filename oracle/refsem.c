@@ -974,6 +974,19 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
     int err;
     const int ri = ast_relation_for(db, ns, rel, &err);
     const int has_rewrite = !err && ri >= 0 && db->rels[ri].rewrite >= 0;
+    if (has_rewrite && !es_child) {
+        /* u_ia below with neither a direct check nor an expand-subject to run is its rewrite's
+         * result: an OR / AND rewrite never yields a bare Unknown (u_rw), so the group's
+         * Unknown -> NotMember changes nothing.  Its RW goal is spawned in the IA's place. */
+        const int can_ss_rw = !db->strict || db->rels[ri].has_ss_type;
+        const int direct = !db->strict && !skip && d - 1 > 0 && exists(u->c, ns, obj, rel);
+        const int es = can_ss_rw && d - 1 > 0 && has_set_rows(db, ns, rel);
+        if (!direct && !es) {
+            if (!u_spawn(u, gen + 1)) return 0;
+            *out = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
+            return 1;
+        }
+    }
     if (has_rewrite || (err && es_child)) {
         if (!u_spawn(u, gen + 1)) return 0;
         *out = u_ia(u, ns, obj, rel, d, skip, scope, gen + 1);
@@ -1112,6 +1125,23 @@ static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32
         if (ch->type == RS_REWRITE && ch->op == RS_OP_OR) { /* restDepth-1 (:118) */
             if (d - 1 > 0) u_or_items(u, ns, obj, ci, d - 1, scope, gen, out, have, stop);
             if (u->routed) return;
+            continue;
+        }
+        if (ch->type == RS_TTU) {
+            /* spliced like a nested OR: a tuple-to-userset's result is the first decisive of
+             * its parents' checks in row order (u_ttu), so the parents are this OR's own items;
+             * with d - 1 <= 0 every parent check is Unknown and contributes nothing */
+            if (d - 1 <= 0) continue;
+            size_t lo, hi;
+            node_rows(db, ns, obj, ch->rel, &lo, &hi);
+            for (size_t i = lo; i < hi && !*stop; i++) {
+                const key7 *t = ROW(db, i);
+                if (t->kind != 1) continue;
+                res r;
+                const int spawned = u_sub(u, t->sns, t->sid, ch->computed, d - 1, 0, 0, scope, gen, &r);
+                if (u->routed) return;
+                u_fold(r, spawned, 1, out, have, stop);
+            }
             continue;
         }
         res r;

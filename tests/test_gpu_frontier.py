@@ -47,11 +47,12 @@ def _frontier_batch(stream, eng, q):
     return allowed, err, stream.frontier_stats(reset=True)
 
 
+@pytest.mark.parametrize("rewrites", [True, False])
 @pytest.mark.parametrize("b", [1024, 6])
 @pytest.mark.parametrize("seed", list(range(60)))
-def test_random_worlds_frontier_vs_oracle(stream, budget, seed, b):
+def test_random_worlds_frontier_vs_oracle(stream, budget, seed, b, rewrites):
     budget(b)
-    w, t, q, _ = random_world(seed, rewrites=True)
+    w, t, q, _ = random_world(seed, rewrites=rewrites)
     orc = refsem.Oracle(w, t)
     orc.set_limits(w.max_depth, w.max_width)
     dec, err, _ = orc.check_batch(q, threads=4)
@@ -65,8 +66,6 @@ def test_random_worlds_frontier_vs_oracle(stream, budget, seed, b):
     allowed, gerr, fs = _frontier_batch(stream, eng, queries_to_product(q))
     np.testing.assert_array_equal(gerr, err)
     np.testing.assert_array_equal(allowed, dec)
-    if fs["batches"] == 0:  # a world without rewrites: the union kernel (check_union.hip) ran
-        return
     assert fs["batches"] == 1 and fs["queries"] == len(q)
     assert fs["routed"] == int(routed.sum())
     if not routed.any():
@@ -94,6 +93,53 @@ def test_drive_small_frontier_vs_oracle(stream):
     if not routed.any():
         assert fs["goals"] == int(goals.sum())
     assert fs["routed"] < 0.01 * len(q)
+
+
+def test_nested_groups_small_frontier_vs_oracle(stream):
+    """a rewrite-free snapshot (BASELINE config 2's shape) on the frontier engine, the default for
+    every snapshot: decisions, routed count and goals pinned to the restatement"""
+    from keto_mi355x import synth
+    wl = synth.nested_groups(200_000, seed=5)
+    q = synth.nested_groups_queries(wl, 20_000, seed=9, trunc_frac=0.05)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    w, t = world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    qo = queries_to_oracle(q)
+    dec, err, _ = orc.check_batch(qo, threads=8)
+    _, _, routed, goals, gens = orc.check_u_batch(qo, threads=8, budget=1024)
+    eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    allowed, gerr, fs = _frontier_batch(stream, eng, q)
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    assert fs["batches"] == 1 and fs["routed"] == int(routed.sum())
+    assert fs["max_generations"] == int(gens.max())
+    if not routed.any():
+        assert fs["goals"] == int(goals.sum())
+    assert 0.05 < allowed.mean() < 0.95
+
+
+@pytest.mark.parametrize("seed", list(range(0, 60, 3)))
+def test_union_interpreter_opt_out_vs_oracle(stream, seed):
+    """KETO_UNION_FRONTIER=0 keeps rewrite-free snapshots on the lane interpreter (check_union.hip)"""
+    w, t, q, _ = random_world(seed, rewrites=False)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(w.max_depth, w.max_width)
+    dec, err, _ = orc.check_batch(q, threads=4)
+    snap = product_snapshot(w, t)
+    eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+    old = os.environ.get("KETO_UNION_FRONTIER")
+    os.environ["KETO_UNION_FRONTIER"] = "0"
+    try:
+        allowed, gerr, fs = _frontier_batch(stream, eng, queries_to_product(q))
+    finally:
+        if old is None:
+            os.environ.pop("KETO_UNION_FRONTIER")
+        else:
+            os.environ["KETO_UNION_FRONTIER"] = old
+    np.testing.assert_array_equal(gerr, err)
+    np.testing.assert_array_equal(allowed, dec)
+    assert fs["batches"] == 0  # the frontier engine did not run
 
 
 def test_every_query_routed_matches_oracle(stream, budget):
