@@ -177,6 +177,26 @@ __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, 
     return Sub{0, M_NOT};
 }
 
+// A NOT decided where it is spawned (a malformed NOT, a computed userset that is a leaf, a
+// rewrite at rest depth 0) is folded into its parent: its result, or NONE32 when it must be an
+// INV goal (oracle u_inv_folds; the G_INV case of fr_expand evaluates the same way)
+__device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
+                                             uint32_t op, uint32_t d) {
+    const Op o = T.ops[op];
+    if (o.child_count != 1) return mk_err(KETO_QERR_NOT_IMPLEMENTED);
+    const Op ch = T.ops[T.op_children[o.child_begin]];
+    const uint32_t ct = ch.type_kind & 0xFFu;
+    uint32_t leaf = NONE32;
+    if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
+    else if (ct == OP_CSS) {
+        const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
+        if (!sb.word) leaf = sb.leaf;
+    }
+    if (leaf == NONE32) return NONE32;
+    const uint32_t m = leaf & 3u;  // NOT: IsMember <-> NotMember, Unknown / errors kept (rewrites.go:183-199)
+    return m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
+}
+
 // count an occurrence of (scope, key) that is not a goal; false when the table is crowded
 __device__ __forceinline__ bool tab_mark(const FrontierParams &P, uint32_t scope, uint32_t vk) {
     const unsigned long long key = tab_key(scope, vk);
@@ -442,8 +462,9 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                                     }
                                 }
                             }
-                        } else {
-                            nc++;  // NOT
+                        } else {  // NOT: a leaf when decided here, else its own goal
+                            leaf = inv_leaf(s, T, q, node, item.y, dk);
+                            if (leaf == NONE32) nc++;
                         }
                         if (leaf != NONE32 && decisive(leaf)) {  // binop.go:23-26: nothing after it runs
                             tail = leaf;
@@ -464,7 +485,8 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                         else if (ct == OP_CSS) {  // checkComputedSubjectSet (rewrites.go:208-230)
                             const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
                             if (!sb.word) leaf = sb.leaf;
-                        }
+                        } else if (ct == OP_INVERT)
+                            leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin + c], d);
                         if (leaf == NONE32) {
                             nc++;
                             continue;
@@ -514,7 +536,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 else if (ct == OP_CSS) {
                     const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
                     if (!sb.word) leaf = sb.leaf;
-                }
+                } else if (ct == OP_INVERT) leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin], d);  // folded inner NOT
                 if (leaf != NONE32) {  // NOT of a result known now: IsMember <-> NotMember, Unknown / errors kept
                     const uint32_t m = leaf & 3u;
                     val = m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
@@ -641,7 +663,9 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                                 }
                             }
                         }
-                    } else if (ik == IT_INV) spawn(P, c++, node, pos, gword(G_INV, dk, item.y), scope);
+                    } else if (ik == IT_INV) {
+                        if (inv_leaf(s, T, q, node, item.y, dk) == NONE32) spawn(P, c++, node, pos, gword(G_INV, dk, item.y), scope);
+                    }
                     else if (ik == IT_RW && dk > 1) spawn(P, c++, node, pos, gword(G_RW, dk - 1, item.y), scope);
                     it++;
                 }
@@ -657,7 +681,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                     const Sub sb = sub_check(s, T, q, t, d, false, 0);
                     if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
                 } else if (ct == OP_REWRITE) spawn(P, c++, node, pos, gword(G_RW, d - 1, ci), scope);  // :118
-                else spawn(P, c++, node, pos, gword(G_INV, d, ci), scope);
+                else if (inv_leaf(s, T, q, node, ci, d) == NONE32) spawn(P, c++, node, pos, gword(G_INV, d, ci), scope);
             }
             break;
         }

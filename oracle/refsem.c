@@ -1010,6 +1010,33 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
     return 0;
 }
 
+/* u_sub's shaping decision without evaluating anything: 1 when it would spawn a goal */
+static int u_sub_spawns(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, int es_child) {
+    const rs_db *db = u->c->db;
+    if (d <= 0) return 0;
+    int err;
+    const int ri = ast_relation_for(db, ns, rel, &err);
+    const int has_rewrite = !err && ri >= 0 && db->rels[ri].rewrite >= 0;
+    if (has_rewrite || (err && es_child)) return 1;
+    if (err) return 0;
+    const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
+    if (!skip && d - 1 > 0 && exists(u->c, ns, obj, rel)) return 0;
+    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel);
+}
+
+/* A NOT whose operand is decided where it is spawned -- a malformed NOT, a computed userset
+ * that is a leaf, a rewrite at rest depth 0 -- is folded into its parent: u_inv evaluates it
+ * there and no goal is spawned for it or below it. */
+static int u_inv_folds(uctx *u, uint32_t ns, uint32_t obj, int ai, int d) {
+    const rs_db *db = u->c->db;
+    const rs_ast *a = &db->ast[ai];
+    if (a->child_count != 1) return 1;
+    const rs_ast *ch = &db->ast[db->children[a->child_begin]];
+    if (ch->type == RS_CSS) return !u_sub_spawns(u, ns, obj, ch->rel, d, 0, 0);
+    if (ch->type == RS_REWRITE) return d <= 0;
+    return 0;
+}
+
 /* a rewrite child (check_child): 1 = spawned as a goal (result in *out), 0 = a leaf result */
 static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, uint32_t scope, uint32_t gen,
                    res *out);
@@ -1066,7 +1093,12 @@ static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, 
         *out = u_rw(u, ns, obj, ci, d - cost, scope, gen + 1);
         return 1;
     case RS_INVERT:
-        if (d < 0 || !u_spawn(u, gen + 1)) return 0;
+        if (d < 0) return 0;
+        if (u_inv_folds(u, ns, obj, ci, d)) {
+            *out = u_inv(u, ns, obj, ci, d, scope, gen);
+            return 0;
+        }
+        if (!u_spawn(u, gen + 1)) return 0;
         *out = u_inv(u, ns, obj, ci, d, scope, gen + 1);
         return 1;
     default:

@@ -54,3 +54,28 @@ def test_one_transition_per_step_is_address_clean(tmp_path):
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=1200)
     assert "AddressSanitizer" not in r.stdout + r.stderr, (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+@pytest.mark.slow
+def test_unserved_lanes_lose_operands_but_stay_in_range(tmp_path):
+    """The round-1 waterfall variant's failure mode: lanes that sit out a step
+    after their operands were loaded (-DKETO_EMU_SKIP=3: every third lane-step on average) run
+    their next transition on cleared operands.  That gives wrong decisions -- the invariant the
+    shipped kernel keeps -- but never an out-of-range access under AddressSanitizer."""
+    asan = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()
+    if not asan or not os.path.isabs(asan):
+        pytest.skip("no libasan")
+    lib = tmp_path / "libketo_emu_skip.so"
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(ROOT, "tools", "cpuemu"),
+                    f"OBJDIR={tmp_path / 'obj'}", f"LIB={lib}",
+                    "OPT=-O1 -fsanitize=address -fno-omit-frame-pointer -DKETO_EMU_SKIP=3"],
+                   check=True, timeout=900)
+    env = dict(os.environ, KETO_MI355X_ALLOW_OVERRIDE="tools", KETO_MI355X_LIB_OVERRIDE=str(lib), KETO_FRONTIER="0",
+               LD_PRELOAD=asan, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_gpu_parity.py"), "-k", "golden or random_worlds"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=1200)
+    out = r.stdout + r.stderr
+    assert "AddressSanitizer" not in out, out[-3000:]
+    assert " failed" in r.stdout, "lost operands should change decisions (else the knob did nothing)"

@@ -19,7 +19,8 @@ eng.check_batch(q)
 c = st.counters(reset=True)["per_tier"]
 vals = [c["rows"][0], c["edges"][0], c["probes"][0], c["out_nodes"][0], c["queries"][0], c["wave_steps"][0],
         c["lane_steps"][0]]
-names = ["g0+qg loads", "phase A", "budget", "allocation (2 barriers)", "stores+CAS+phase B", "copy barrier", "copy"]
+names = ["loads (g0, qgoals, row, subject, CAS issue)", "phase A (decide / count)", "budget + qgoals atomics",
+         "allocation + gfn/gval stores + CAS result", "phase B (spawn children)", "-", "-"]
 tot = sum(vals)
 for n, v in zip(names, vals):
     print(f"{n:28s} {v:16d} {100 * v / max(1, tot):6.1f}%")
