@@ -13,6 +13,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -419,6 +422,15 @@ void entity_ids(const unsigned long long *bits, uint32_t *rank, uint64_t nblk, u
 
 void rows(const RowsIn &in, RowsOut &out) {
     const uint64_t n = in.n, N = in.n_nodes, M = in.n_subj;
+    static const bool verbose = getenv("KETO_BUILD_VERBOSE") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto step = [&](const char *what) {
+        if (!verbose) return;
+        KETO_HIP(hipDeviceSynchronize());
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[keto build]   rows/%-12s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
     NodeMap map{in.bits, in.rank, in.ns, in.slot_of, in.stride, in.n_rel, in.n_uuids};
     DevBuf src(4 * n), dst(4 * n), skey(8 * n);
     KETO_HIP(hipMemset(out.all_off, 0, 4 * (N + 1)));
@@ -428,6 +440,7 @@ void rows(const RowsIn &in, RowsOut &out) {
     KETO_HIP(hipGetLastError());
     scan_excl(out.all_off, N);
     scan_excl(out.rev_off, M);
+    step("count+scan");
     // tuples of each row node, in shard order
     DevBuf row_idx(4 * n);
     {
@@ -436,6 +449,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         hipLaunchKernelGGL(k_scatter_rows, grid_for(n), dim3(BLK), 0, 0, src.u32(), n, cur.u32(), row_idx.u32());
         KETO_HIP(hipGetLastError());
     }
+    step("scatter");
     {
         DevBuf longs(4 * (n / ROW_SORT_MAX + 2)), n_long(4);
         KETO_HIP(hipMemset(n_long.p, 0, 4));
@@ -473,6 +487,7 @@ void rows(const RowsIn &in, RowsOut &out) {
             }
         }
     }
+    step("shard sort");
     {
         DevBuf set_cnt(4 * (N + 1));
         hipLaunchKernelGGL(k_row_fill, grid_for(N), dim3(BLK), 0, 0, out.all_off, N, row_idx.u32(), dst.u32(), out.all_subj,
@@ -500,6 +515,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         if (w != out.weight) KETO_HIP(hipMemcpy(out.weight, w, 4 * N, hipMemcpyDeviceToDevice));
     }
     row_idx.reset();
+    step("rows+weights");
     // reverse rows (subject -> nodes holding it directly, unordered) + the heavy-subject probe hash
     {
         DevBuf heavy(8);
@@ -521,6 +537,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         KETO_HIP(hipGetLastError());
     }
     KETO_HIP(hipDeviceSynchronize());
+    step("reverse+probe");
 }
 
 void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag) {

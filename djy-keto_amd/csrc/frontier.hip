@@ -885,8 +885,10 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     uint32_t *hc = f.host_ctrl;
     std::vector<uint64_t> tot(MAX_GEN + 1, 0);  // goals per generation
     const uint64_t scap = f.cap / FR_SHARDS;
+    // the first read-back comes after as many generations as the stream's previous batch had (+1,
+    // the empty one that ends it): a steady workload pays one host round trip per batch
     for (uint32_t k = 0; gens == 0;) {
-        const uint32_t kend = std::min(k + CHUNK, MAX_GEN);
+        const uint32_t kend = std::min(k + (k == 0 ? std::max(CHUNK, f.last_gens + 1) : CHUNK), MAX_GEN);
         for (; k < kend; k++) {
             P.gen = k;
             if (lds_tables) hipLaunchKernelGGL(fr_expand<true>, eg, eb, lds, st.stream, P);

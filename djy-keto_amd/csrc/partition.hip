@@ -66,6 +66,25 @@ __host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t wor
 
 // ------------------------------------------------------------------ kernels
 
+// append v (where `has`) to out[] with one atomic per wave instead of one per lane (a single
+// counter takes every append: per-lane atomics serialise at its L2 channel).  Every lane of the
+// wave calls it.
+template <class T>
+__device__ __forceinline__ void wave_append(bool has, T v, T *out, unsigned long long *n_out) {
+    const unsigned long long m = __ballot(has);
+    if (!m) return;
+    const uint32_t lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    unsigned long long base = 0;
+    if ((int)lane == leader) base = atomicAdd(n_out, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (has) out[base + __popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+// grid-stride loop whose trip count is uniform per block (wave-level collectives inside)
+#define FOR_UNIFORM(i, n)                                                                                  \
+    for (uint64_t i##0 = (uint64_t)blockIdx.x * blockDim.x, i = i##0 + threadIdx.x; i##0 < (n);           \
+         i##0 += gstride(), i = i##0 + threadIdx.x)
+
 __global__ __launch_bounds__(BLK) void k_tuple_keys(const keto_tuple *t, uint64_t n, uint64_t *keys, uint32_t *idx) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
         keys[i] = okey(t[i].ns, t[i].obj);
@@ -91,9 +110,10 @@ __global__ __launch_bounds__(BLK) void k_run_starts(const uint64_t *k, const uin
 }
 __global__ __launch_bounds__(BLK) void k_query_keys(const keto_query *q, uint64_t n, uint64_t *keys, uint32_t *subj,
                                                      unsigned long long *n_subj) {
-    for (uint64_t i = gid(); i < n; i += gstride()) {
-        keys[i] = okey(q[i].ns, q[i].obj);
-        if (q[i].subj_kind == 0) subj[atomicAdd(n_subj, 1ull)] = q[i].s_obj;
+    FOR_UNIFORM(i, n) {
+        const bool in = i < n;
+        if (in) keys[i] = okey(q[i].ns, q[i].obj);
+        wave_append<uint32_t>(in && q[i].subj_kind == 0, in ? q[i].s_obj : 0u, subj, n_subj);
     }
 }
 __global__ __launch_bounds__(BLK) void k_root_keys(const keto_subject_set *r, uint64_t n, uint64_t *keys) {
@@ -102,18 +122,25 @@ __global__ __launch_bounds__(BLK) void k_root_keys(const keto_subject_set *r, ui
 // seen-set insert: keys never asked for before go to `out` (each once)
 __global__ __launch_bounds__(BLK) void k_insert(const uint64_t *cand, uint64_t n, unsigned long long *table,
                                                  uint64_t mask, uint64_t *out, unsigned long long *n_out) {
-    for (uint64_t i = gid(); i < n; i += gstride()) {
-        const unsigned long long k = cand[i] + 1;  // 0 = empty slot
-        uint64_t h = mix64(k) & mask;
-        for (;;) {
-            const unsigned long long prev = atomicCAS(&table[h], 0ull, k);
-            if (prev == 0ull) {
-                out[atomicAdd(n_out, 1ull)] = k - 1;
-                break;
+    FOR_UNIFORM(i, n) {
+        bool fresh = false;
+        const unsigned long long k = i < n ? cand[i] + 1 : 0ull;  // 0 = empty slot
+        if (i < n) {
+            uint64_t h = mix64(k) & mask;
+            for (;;) {
+                // most candidates were seen before (popular groups, shared ancestors): a plain load
+                // answers them, the atomic is only for an empty slot
+                unsigned long long prev = __atomic_load_n(&table[h], __ATOMIC_RELAXED);
+                if (prev == 0ull) prev = atomicCAS(&table[h], 0ull, k);
+                if (prev == 0ull) {
+                    fresh = true;
+                    break;
+                }
+                if (prev == k) break;
+                h = (h + 1) & mask;
             }
-            if (prev == k) break;
-            h = (h + 1) & mask;
         }
+        wave_append<uint64_t>(fresh, k - 1, out, n_out);
     }
 }
 __global__ __launch_bounds__(BLK) void k_rehash(const uint64_t *keys, uint64_t n, unsigned long long *table,
@@ -235,11 +262,46 @@ __global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const
             if (keep(L, L.tuples[j], src)) out[o++] = L.tuples[j];
     }
 }
+// One pass for a rank gathering for itself (no grouping by source needed): each request counts
+// its kept tuples, takes its range with one atomic per wave, and copies them (the run is re-read
+// from L2).  The closure's order is free: the builder sorts every row by shard_id.  A range past
+// `cap` sets *overflow and writes nothing; the host then reruns the level with the two passes.
+__global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, keto_tuple *out, uint64_t cap,
+                                                        unsigned long long *total, unsigned long long *overflow) {
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += gstride()) {
+        const uint64_t i = i0 + threadIdx.x;
+        uint64_t b = 0, e = 0, c = 0;
+        if (i < n && run_of(L, L.req[i], b, e))
+            for (uint64_t j = b; j < e; j++) c += keep(L, L.tuples[j], 0) ? 1 : 0;
+        // wave-aggregated allocation
+        uint64_t x = c;
+        const uint32_t lane = __lane_id();
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint64_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        const uint64_t wsum = __shfl(x, 63);
+        unsigned long long base = 0;
+        if (lane == 63 && wsum) base = atomicAdd(total, (unsigned long long)wsum);
+        base = __shfl(base, 63);
+        uint64_t o = base + x - c;
+        if (!c) continue;
+        if (o + c > cap) {
+            atomicOr(overflow, 1ull);
+            continue;
+        }
+        for (uint64_t j = b; j < e; j++)
+            if (keep(L, L.tuples[j], 0)) out[o++] = L.tuples[j];
+    }
+}
+
 // next frontier: the subject-set objects of the tuples received
 __global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, uint64_t *cand,
                                                unsigned long long *n_cand) {
-    for (uint64_t i = gid(); i < n; i += gstride())
-        if (t[i].subj_kind == 1) cand[atomicAdd(n_cand, 1ull)] = okey(t[i].s_ns, t[i].s_obj);
+    FOR_UNIFORM(i, n) {
+        const bool set = i < n && t[i].subj_kind == 1;
+        wave_append<uint64_t>(set, set ? okey(t[i].s_ns, t[i].s_obj) : 0ull, cand, n_cand);
+    }
 }
 
 // Compact id space of a closure (remap_ids): the uuid ids its tuples and the batch's queries /
@@ -467,6 +529,15 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
     uint64_t n_cand = n_keys, total = 0;
     const int levels = P.limits.max_read_depth + 1;
     auto tl = std::chrono::steady_clock::now();
+    double step_ms[6] = {0, 0, 0, 0, 0, 0};  // verbose: insert, route+exchange, count+scan, fill, next, (spare)
+    auto ts = std::chrono::steady_clock::now();
+    auto mark = [&](int k) {
+        if (!P.verbose) return;
+        sync(P);
+        const auto now = std::chrono::steady_clock::now();
+        step_ms[k] += std::chrono::duration<double, std::milli>(now - ts).count();
+        ts = now;
+    };
     for (int level = 0; level < levels; level++) {
         if (P.verbose) {
             sync(P);
@@ -484,6 +555,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             hipLaunchKernelGGL(k_insert, grid_for(n_cand), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.cand), n_cand,
                                dptr<unsigned long long>(P.table), P.table_mask, dptr<uint64_t>(P.fresh), c);
         const uint64_t n_new = d2h_u64(P, c);
+        mark(0);
         if (allreduce_max(P, n_new) == 0) break;
         st.levels++;
         st.objects += n_new;
@@ -519,6 +591,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                                    W, dptr<unsigned long long>(hist), dptr<uint64_t>(P.routed));
         }
         std::vector<uint64_t> from = exchange(P, P.routed.p, send, 8, P.req, st.bytes_sent);
+        mark(1);
         std::vector<uint64_t> roff(W + 1, 0);
         for (uint32_t r = 0; r < W; r++) roff[r + 1] = roff[r] + from[r];
         const uint64_t n_req = roff[W];
@@ -529,6 +602,31 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                  dptr<keto_tuple>(P.tuples),
                  dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<unsigned long long>(P.subj_set), P.subj_mask,
                  W, filter ? 1 : 0};
+        if (W == 1 && P.closure.p) {  // one rank: a single gathering pass into the closure (k_lookup_gather)
+            const uint64_t cap = P.closure.bytes / sizeof(keto_tuple) - total;
+            unsigned long long *g = dptr<unsigned long long>(P.ctr) + 2;  // [2] total, [3] overflow
+            KETO_HIP(hipMemsetAsync(g, 0, 16, P.hs));
+            if (n_req)
+                hipLaunchKernelGGL(k_lookup_gather, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req,
+                                   dptr<keto_tuple>(P.closure) + total, cap, g, g + 1);
+            unsigned long long gv[2] = {0, 0};
+            KETO_HIP(hipMemcpyAsync(gv, g, 16, hipMemcpyDeviceToHost, P.hs));
+            sync(P);
+            mark(3);
+            if (!gv[1]) {
+                const uint64_t n_got = gv[0];
+                ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
+                KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
+                if (n_got)
+                    hipLaunchKernelGGL(k_next, grid_for(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total,
+                                       n_got, dptr<uint64_t>(P.cand), c);
+                n_cand = d2h_u64(P, c);
+                mark(4);
+                total += n_got;
+                continue;
+            }
+            // overflow: the level again with the two passes (the closure grows to fit)
+        }
         ensure(P.cnt, (n_req + 1) * 8);
         ensure(P.pos, (n_req + 1) * 8);
         KETO_HIP(hipMemsetAsync(P.cnt.p, 0, (n_req + 1) * 8, P.hs));
@@ -543,6 +641,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         for (uint32_t r = 0; r <= W; r++)
             KETO_HIP(hipMemcpyAsync(&pb[r], posp + roff[r], 8, hipMemcpyDeviceToHost, P.hs));
         sync(P);
+        mark(2);
         const uint64_t n_out = pb[W];
         uint64_t n_got = 0;
         if (W == 1) {  // one rank: the owner's gather lands in the closure directly
@@ -565,6 +664,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                 KETO_HIP(hipMemcpyAsync(dptr<keto_tuple>(P.closure) + total, P.got.p, n_got * sizeof(keto_tuple),
                                         hipMemcpyDeviceToDevice, P.hs));
         }
+        mark(3);
         // next frontier: the subject sets of the tuples received
         ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
         KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
@@ -572,9 +672,13 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             hipLaunchKernelGGL(k_next, grid_for(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total, n_got,
                                dptr<uint64_t>(P.cand), c);
         n_cand = d2h_u64(P, c);
+        mark(4);
         total += n_got;
     }
     sync(P);
+    if (P.verbose)
+        fprintf(stderr, "[keto partition] steps (ms): insert %.2f, route+exchange %.2f, count+scan %.2f, fill %.2f, next %.2f\n",
+                step_ms[0], step_ms[1], step_ms[2], step_ms[3], step_ms[4]);
     st.tuples = total;
     return total;
 }
