@@ -130,6 +130,7 @@ struct FrontierScratch {
     uint8_t *trep = nullptr;
     uint32_t *host_ctrl = nullptr;  // pinned
     uint32_t last_gens = 0, last_goals = 0, last_routed = 0;
+    uint32_t epoch = 1;  // scope-table epoch of the next batch (frontier.hip TAB_EPOCHS)
     keto_frontier_stats stats{};
 };
 

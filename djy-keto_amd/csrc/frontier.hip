@@ -74,8 +74,8 @@ struct FrontierParams {
     uint32_t *qgoals, *qroute;   // [n] per query position
     uint32_t budget;
     unsigned long long *tkeys;   // (scope, visited key) table
-    uint8_t *trep;               // slot received its key more than once
-    uint32_t tmask;
+    uint8_t *trep;               // == epoch: the slot received its key more than once
+    uint32_t tmask, epoch;
     uint32_t max_width;
     uint8_t *out_allowed;
     int32_t *out_err;
@@ -116,6 +116,8 @@ __device__ __forceinline__ bool may_hold(const DevSnapshot &s, const Subject &q,
 }
 __device__ __forceinline__ bool member(const DevSnapshot &s, const Subject &q, uint32_t c) {
     if (!q.heavy) return c == q.R.x || c == q.R.y || c == q.R.z || c == q.R.w;
+    const uint64_t fb = subj_filter_bits(c), f = (uint64_t)q.R.z | ((uint64_t)q.R.w << 32);
+    if ((f & fb) != fb) return false;  // not in the subject's reverse row: no probe load
     const uint64_t key = (((uint64_t)q.sidx << 32) | c) + 1;
     uint32_t b = (uint32_t)mix64(key) & s.probe_mask;
     for (;;) {  // the table keeps empty slots: every probe sequence ends
@@ -145,8 +147,39 @@ struct Edges {
     }
 };
 
-__device__ __forceinline__ unsigned long long tab_key(uint32_t scope, uint32_t vk) {
-    return (((unsigned long long)scope << 32) | vk) + 1ull;
+// Scope-table keys carry the batch's epoch (1..TAB_EPOCHS) in bits 61-63 (scope < 2^29: a goal
+// index), so the table is cleared once every TAB_EPOCHS batches instead of after each one: a
+// slot holding 0 or another epoch's key is free.  Within a batch a slot only ever goes from free
+// to a key of the batch, so a lookup may stop at the first free slot.  trep[h] == epoch marks a
+// key received more than once.
+constexpr uint32_t TAB_EPOCHS = 7;
+__device__ __forceinline__ unsigned long long tab_key(uint32_t ep, uint32_t scope, uint32_t vk) {
+    return ((unsigned long long)ep << 61) | ((unsigned long long)scope << 32) | vk;
+}
+__device__ __forceinline__ bool tab_free(unsigned long long k, uint32_t ep) { return (uint32_t)(k >> 61) != ep; }
+// insert `key` starting at slot h whose current content is `old` (the caller's first CAS of 0 ->
+// key returned it); the slot where the key lives, -1 when the table is crowded.  *rep: the key
+// was already there.
+__device__ __forceinline__ int64_t tab_insert(unsigned long long *tk, uint32_t mask, uint32_t ep, unsigned long long key,
+                                              uint32_t h, unsigned long long old, bool *rep) {
+    *rep = false;
+    for (int probe = 0; probe < 64;) {
+        if (old == 0ull) return h;  // the CAS of 0 -> key that produced `old` inserted it
+        if (old == key) {
+            *rep = true;
+            return h;
+        }
+        if (tab_free(old, ep)) {  // a stale key: replace it
+            const unsigned long long r = atomicCAS(&tk[h], old, key);
+            if (r == old) return h;
+            old = r;  // another lane wrote a key of this batch here: look at it again
+            continue;
+        }
+        h = (h + 1) & mask;
+        probe++;
+        old = atomicCAS(&tk[h], 0ull, key);
+    }
+    return -1;
 }
 
 // A sub-check checkIsAllowed(c, dc, skip) shaped when its parent spawns it (oracle u_sub): a
@@ -158,6 +191,9 @@ __device__ __forceinline__ unsigned long long tab_key(uint32_t scope, uint32_t v
 struct Sub {
     uint32_t word, leaf;
 };
+__device__ __forceinline__ uint2 rw_splice(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
+                                           uint32_t op, uint32_t d);
+template <bool SPLICE = true>
 __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t c, uint32_t dc,
                                          bool skip, uint32_t esf) {
     if (dc == 0) return Sub{0, M_UNK};
@@ -168,7 +204,11 @@ __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, 
         // run, checkIsAllowed is its rewrite's result (an OR / AND never yields a bare Unknown):
         // the RW goal is spawned in the IA's place, one generation earlier (oracle u_sub)
         const bool direct = !s.strict && !skip && dc > 1 && !(c & VIRT_BIT) && may_hold(s, q, ni.ri) && member(s, q, c);
-        if (!direct && !(ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri))) return Sub{gword(G_RW, dc, ri_op(ni.ri)), 0};
+        if (!direct && !(ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri))) {
+            if (!SPLICE) return Sub{gword(G_RW, dc, ri_op(ni.ri)), 0};
+            const uint2 sp = rw_splice(s, T, q, c, ri_op(ni.ri), dc);
+            return Sub{gword(G_RW, sp.y, sp.x), 0};
+        }
     }
     if (ri_rw(ni.ri) || (err && esf)) return Sub{gword(G_IA, dc, 0, (skip ? GF_SKIP : 0u) | esf), 0};
     if (err) return Sub{0, mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16)};
@@ -189,7 +229,7 @@ __device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables 
     uint32_t leaf = NONE32;
     if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
     else if (ct == OP_CSS) {
-        const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
+        const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
         if (!sb.word) leaf = sb.leaf;
     }
     if (leaf == NONE32) return NONE32;
@@ -197,20 +237,62 @@ __device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables 
     return m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
 }
 
+// An AND rewrite at rest depth d > 1 whose only goal child is a nested rewrite (an RW goal at
+// d-1, rewrites.go:118) and whose other children are leaves known at spawn to be IsMember without
+// an error is spawned as that nested rewrite: AND(x, IsMember...) is x for IsMember / NotMember,
+// no RW / IA goal yields a bare Unknown, and an error stays an error (oracle u_and_splice).  One
+// goal and one generation less per level of `(a | b | parents.traverse(...)) & !banned`.
+// Returns {op, d} of the goal to spawn.
+__device__ __forceinline__ uint2 rw_splice(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
+                                           uint32_t op, uint32_t d) {
+    const NodeInfo ni = t_node_info(T, node);
+    for (;;) {
+#ifdef KETO_FR_NOSPLICE  // measurement builds only (tools/ab)
+        break;
+#endif
+        if (d <= 1) break;
+        const Op o = T.ops[op];
+        if ((o.type_kind & 0xFFu) != OP_REWRITE || ((o.type_kind >> 8) & 0xFFu) != OPK_AND) break;
+        uint32_t only = NONE32;
+        bool ok = true;
+        for (uint32_t c = 0; c < o.child_count && ok; c++) {
+            const uint32_t ci = T.op_children[o.child_begin + c];
+            const Op ch = T.ops[ci];
+            const uint32_t ct = ch.type_kind & 0xFFu;
+            if (ct == OP_REWRITE) {
+                ok = only == NONE32;
+                only = ci;
+            } else if (ct == OP_CSS) {
+                const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
+                ok = !sb.word && sb.leaf == M_IS;
+            } else if (ct == OP_INVERT) {
+                ok = inv_leaf(s, T, q, node, ci, d) == M_IS;
+            } else {
+                ok = false;  // a tuple-to-userset is always a goal
+            }
+        }
+        if (!ok || only == NONE32) break;
+        op = only;
+        d -= 1;
+    }
+    return make_uint2(op, d);
+}
+
+__device__ __forceinline__ uint32_t tab_hash(unsigned long long key, uint32_t mask) {
+    return (uint32_t)mix64(key & ((1ull << 61) - 1ull)) & mask;  // the epoch does not move a key
+}
 // count an occurrence of (scope, key) that is not a goal; false when the table is crowded
 __device__ __forceinline__ bool tab_mark(const FrontierParams &P, uint32_t scope, uint32_t vk) {
-    const unsigned long long key = tab_key(scope, vk);
-    uint32_t h = (uint32_t)mix64(key) & P.tmask;
-    for (int probe = 0; probe < 64; probe++) {
-        const unsigned long long old = atomicCAS(&P.tkeys[h], 0ull, key);
-        if (old == 0ull) return true;
-        if (old == key) {
-            P.trep[h] = 1;
-            return true;
-        }
-        h = (h + 1) & P.tmask;
-    }
-    return false;
+#ifdef KETO_FR_NOTAB
+    return true;
+#endif
+    const unsigned long long key = tab_key(P.epoch, scope, vk);
+    const uint32_t h = tab_hash(key, P.tmask);
+    bool rep = false;
+    const int64_t at = tab_insert(P.tkeys, P.tmask, P.epoch, key, h, atomicCAS(&P.tkeys[h], 0ull, key), &rep);
+    if (at < 0) return false;
+    if (rep) P.trep[at] = (uint8_t)P.epoch;
+    return true;
 }
 
 // a routed query also saturates its goal count, so the budget atomic of any later spawn refuses
@@ -320,12 +402,16 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
         const uint32_t qg = live ? P.qgoals[pos] : 0u;
         // An ES child counts its key into the scope table (CheckAndAddVisited, engine.go:157-160):
         // the CAS is issued here and its answer consumed after the goal's own work.
+#ifdef KETO_FR_NOTAB  // measurement builds only (tools/ab): the scope table's cost, routing disabled
+        const bool ins = false;
+#else
         const bool ins = live && (kind == G_IA || kind == G_ES) && (w & GF_ESCHILD);
+#endif
         unsigned long long tkey = 0, told = 0;
         uint32_t th = 0;
         if (ins) {
-            tkey = tab_key(scope, (w & GF_ALIAS) ? s.vkey[node] : node);
-            th = (uint32_t)mix64(tkey) & P.tmask;
+            tkey = tab_key(P.epoch, scope, (w & GF_ALIAS) ? s.vkey[node] : node);
+            th = tab_hash(tkey, P.tmask);
             told = atomicCAS(&P.tkeys[th], 0ull, tkey);
         }
         // The loads the goal kinds start from, issued together: the row an ES / TTU reads, and
@@ -377,7 +463,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 for (uint32_t e = 0; it.cur < it.end && !found; e++) {
                     const uint32_t c = it.next() & ~EDGE_ALIAS;
                     found = member(s, q, c);
-                    if (e < keep && sub_check(s, T, q, c, d, true, GF_ESCHILD).word) nc++;  // the children that are goals
+                    if (e < keep && sub_check<false>(s, T, q, c, d, true, GF_ESCHILD).word) nc++;  // the children that are goals
                 }
                 if (found) {
                     val = M_IS;
@@ -435,7 +521,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                             }
                         } else if (ik == IT_CAND) {  // checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
                             if (dk > 1) {
-                                const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0);
+                                const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0);
                                 if (sb.word) nc++;
                                 else leaf = sb.leaf;
                             }
@@ -452,7 +538,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                                     Edges et(s, s.set_row[ts]);
                                     for (uint32_t e = 0; et.cur < et.end; e++) {
                                         const uint32_t pn = et.next() & ~EDGE_ALIAS;
-                                        const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), rc >> 16), dk - 1, false, 0);
+                                        const Sub sb = sub_check<false>(s, T, q, t_sibling(T, pn, t_node_info(T, pn), rc >> 16), dk - 1, false, 0);
                                         if (sb.word) nc++;
                                         else if (decisive(sb.leaf)) {
                                             leaf = sb.leaf;
@@ -483,7 +569,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                         uint32_t leaf = NONE32;
                         if (ct == OP_REWRITE && d <= 1) leaf = M_UNK;  // nested rewrite at d-1 <= 0 (:39-42)
                         else if (ct == OP_CSS) {  // checkComputedSubjectSet (rewrites.go:208-230)
-                            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
+                            const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
                             if (!sb.word) leaf = sb.leaf;
                         } else if (ct == OP_INVERT)
                             leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin + c], d);
@@ -511,7 +597,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 uint32_t tail = NONE32, e = 0;
                 for (; it.cur < it.end; e++) {
                     const uint32_t pn = it.next() & ~EDGE_ALIAS;
-                    const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), xrel), d - 1, false, 0);
+                    const Sub sb = sub_check<false>(s, T, q, t_sibling(T, pn, t_node_info(T, pn), xrel), d - 1, false, 0);
                     if (sb.word) nc++;
                     else if (decisive(sb.leaf)) {
                         tail = sb.leaf;
@@ -534,7 +620,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 uint32_t leaf = NONE32;
                 if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
                 else if (ct == OP_CSS) {
-                    const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
+                    const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
                     if (!sb.word) leaf = sb.leaf;
                 } else if (ct == OP_INVERT) leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin], d);  // folded inner NOT
                 if (leaf != NONE32) {  // NOT of a result known now: IsMember <-> NotMember, Unknown / errors kept
@@ -595,23 +681,20 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             P.gfn[i] = make_uint2(cb, nc | (rop << 24));
             P.gval[i] = val;
         }
-        if (ins && told != 0ull) {  // the key was there (a repeat), or another key is: probe on
-            for (int probe = 1; told != tkey; probe++) {
-                if (probe == 64) {  // crowded: the DFS interpreter takes the query
-                    route(P, pos);
-                    break;
-                }
-                th = (th + 1) & P.tmask;
-                told = atomicCAS(&P.tkeys[th], 0ull, tkey);
-                if (told == 0ull) break;
-            }
-            if (told == tkey) P.trep[th] = 1;
+        if (ins && told != 0ull) {  // the key was there (a repeat), a stale key or another key is
+            bool rep = false;
+            const int64_t at = tab_insert(P.tkeys, P.tmask, P.epoch, tkey, th, told, &rep);
+            if (at < 0) route(P, pos);  // crowded: the DFS interpreter takes the query
+            else if (rep) P.trep[at] = (uint8_t)P.epoch;
         }
         FR_MARK(3);
         // ---- phase B: write the children (the same walk as phase A) -------------------------------
         if (nc || (kind == G_ES && xrel)) switch (kind) {
         case G_IA:
-            if (pat & 1u) spawn(P, cb, node, pos, gword(G_RW, d, xrel), scope);
+            if (pat & 1u) {
+                const uint2 sp = rw_splice(s, T, q, node, xrel, d);
+                spawn(P, cb, node, pos, gword(G_RW, sp.y, sp.x), scope);
+            }
             if (pat & 2u) spawn(P, cb + ((pat & 1u) ? 1 : 0), node, pos, gword(G_ES, d - 1), scope);
             break;
         case G_ES: {
@@ -758,18 +841,22 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
             val = res;
             P.gval[i] = val;
         }
+#ifdef KETO_FR_NOTAB
+        if (false) {
+#else
         if (k > 0 && decisive(val)) {  // an ES child: was its key repeated in the scope?
+#endif
             const uint4 g = P.g0[i];
             if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD)) {  // (RW / TTU / INV hold an op there)
-                const unsigned long long key = tab_key(g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x);
-                uint32_t h = (uint32_t)mix64(key) & P.tmask;
+                const unsigned long long key = tab_key(P.epoch, g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x);
+                uint32_t h = tab_hash(key, P.tmask);
                 for (int probe = 0; probe < 64; probe++) {
                     const unsigned long long kk = P.tkeys[h];
                     if (kk == key) {
-                        if (P.trep[h]) route(P, g.y);
+                        if (P.trep[h] == P.epoch) route(P, g.y);
                         break;
                     }
-                    if (kk == 0ull) break;  // not inserted (crowded): the query was routed then
+                    if (tab_free(kk, P.epoch)) break;  // not inserted (crowded): the query was routed then
                     h = (h + 1) & P.tmask;
                 }
             }
@@ -808,7 +895,11 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     const uint64_t cap = std::max<uint64_t>(want, f.cap);
     const uint64_t ncap = std::max<uint64_t>(n, f.ncap);
     uint64_t tcap = 1;
+#ifdef KETO_FR_TAB_LOG2  // measurement builds (tools/ab): a fixed scope-table size
+    tcap = 1ull << KETO_FR_TAB_LOG2;
+#else
     while (tcap < cap / 2) tcap <<= 1;
+#endif
     const size_t ctrl = al256(FR_CTRL_BYTES);
     const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 4) + al256(tcap * 9);
     KETO_HIP(hipMalloc(&f.mem, bytes));
@@ -828,8 +919,9 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     p += al256(cap * 4);
     f.tkeys = reinterpret_cast<unsigned long long *>(p);
     f.trep = reinterpret_cast<uint8_t *>(f.tkeys + tcap);
-    // the table starts empty and is emptied after every batch
+    // the table starts empty; batches tag their keys with an epoch (TAB_EPOCHS)
     KETO_HIP(hipMemset(f.tkeys, 0, tcap * 9));
+    f.epoch = 1;
     KETO_HIP(hipDeviceSynchronize());
     f.cap = cap;
     f.ncap = ncap;
@@ -863,6 +955,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.tkeys = f.tkeys;
     P.trep = f.trep;
     P.tmask = (uint32_t)(f.tcap - 1);
+    P.epoch = f.epoch;
     P.max_width = (uint32_t)L.max_width;
     P.out_allowed = L.out_allowed;
     P.out_err = L.out_err;
@@ -920,7 +1013,10 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         hipLaunchKernelGGL(fr_reduce, rg, eb, 0, st.stream, P);
         KETO_HIP(hipGetLastError());
     }
-    KETO_HIP(hipMemsetAsync(f.tkeys, 0, f.tcap * 9, st.stream));
+    if (++f.epoch > TAB_EPOCHS) {  // every TAB_EPOCHS batches: clear the table
+        KETO_HIP(hipMemsetAsync(f.tkeys, 0, f.tcap * 9, st.stream));
+        f.epoch = 1;
+    }
     KETO_HIP(hipMemcpyAsync(hc, fb_count, 4, hipMemcpyDeviceToHost, st.stream));
     KETO_HIP(hipStreamSynchronize(st.stream));
     f.last_gens = gens;

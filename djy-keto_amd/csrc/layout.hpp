@@ -113,7 +113,15 @@ constexpr uint32_t WEIGHT_ROUNDS = 12;     // path-count relaxation rounds (> ty
 constexpr uint32_t WEIGHT_CAP = 1u << 20;
 constexpr uint32_t HEAVY_WEIGHT = 32;      // roots at or above this weight are scheduled first
 constexpr uint32_t START_HEAVY = 1u << 31;  // start record: subject row answered by the probe hash
-constexpr uint32_t START_R_HEAVY = 0xFFFFFFFEu;  // second start record of a heavy subject: {subject, this, -, -}
+constexpr uint32_t START_R_HEAVY = 0xFFFFFFFEu;  // second start record of a heavy subject: {subject, this, filter lo, hi}
+// A heavy subject's start record carries a 64-bit filter of its reverse row (two bits per node,
+// subj_filter_bits): a membership test whose bits are not all set is answered NotMember without
+// the probe-hash load.  Rows longer than FILTER_MAX_LEN get an all-ones filter (no filtering).
+constexpr uint32_t FILTER_MAX_LEN = 96;
+__host__ __device__ __forceinline__ uint64_t subj_filter_bits(uint32_t node) {
+    const uint32_t h = node * 0x9E3779B1u;
+    return (1ull << (h >> 26)) | (1ull << ((h >> 20) & 63u));
+}
 constexpr uint32_t PROBE_K = 4;           // VGPR-resident reverse row capacity (<= 4: two windows)
 constexpr uint32_t LDS_TABLE_LIMIT = 48 * 1024;
 

@@ -90,8 +90,16 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
             R.z = len > 2 ? w8(v0, v1, o + 2) : NONE32;
             R.w = len > 3 ? w8(v0, v1, o + 3) : NONE32;
         }
-        // the second record is the whole subject test: its reverse row, or {subject, START_R_HEAVY}
-        if (heavy) R = make_uint4(sidx, START_R_HEAVY, NONE32, NONE32);
+        // the second record is the whole subject test: its reverse row, or {subject, START_R_HEAVY,
+        // filter of the row} (layout.hpp subj_filter_bits)
+        if (heavy) {
+            uint64_t f = ~0ull;
+            if (len <= FILTER_MAX_LEN) {
+                f = 0;
+                for (uint32_t j = rb; j < re; j++) f |= subj_filter_bits(s.rev_nodes[j]);
+            }
+            R = make_uint4(sidx, START_R_HEAVY, (uint32_t)f, (uint32_t)(f >> 32));
+        }
         // x root, y subject index, z depth | hash-probe flag, w query index
         r0 = make_uint4(root, sidx, d | (heavy ? START_HEAVY : 0u), i);
         heavy_cls = wgt >= HEAVY_WEIGHT;
