@@ -120,14 +120,15 @@ struct Scratch {
 // per-stream arena of the frontier engine (frontier.hip)
 struct FrontierScratch {
     void *mem = nullptr;
-    uint64_t cap = 0, ncap = 0, tcap = 0;  // goals, queries, scope-key table slots
+    uint64_t cap = 0, ncap = 0, dcap = 0, ocap = 0;  // goals, queries, decisive-key slots, occurrences per slice
     uint32_t *ctrl = nullptr;              // [gbase | gcount | fallback count]
     uint32_t *qgoals = nullptr, *qroute = nullptr, *fb_list = nullptr, *fb_count = nullptr;
     uint4 *g0 = nullptr;
     uint2 *gfn = nullptr;
     uint32_t *gval = nullptr;
-    unsigned long long *tkeys = nullptr;
-    uint8_t *trep = nullptr;
+    unsigned long long *dkeys = nullptr;
+    uint32_t *dcnt = nullptr, *occ_count = nullptr;
+    uint2 *occ = nullptr;
     uint32_t *host_ctrl = nullptr;  // pinned
     uint32_t last_gens = 0, last_goals = 0, last_routed = 0;
     uint32_t epoch = 1;  // scope-table epoch of the next batch (frontier.hip TAB_EPOCHS)

@@ -14,10 +14,14 @@
 // Every goal is one lane: no per-query state machine, no divergence across interpreter
 // states, no frame stack.  A goal reads what its hop needs (its row, the subject's probe),
 // decides what it can on the spot (a direct tuple, the OR shortcut's IN query, the
-// found-lookahead), and writes its children contiguously into the next generation.  ES
-// children are counted per (scope, visited key) in a device hash table; a decisive
-// occurrence of a repeated key routes the query to the DFS interpreter, as do queries that
-// spawn more than `budget` goals, run past MAX_GEN generations or overflow the arena.
+// found-lookahead), and writes its children contiguously into the next generation.  A query
+// whose answer could depend on visited pruning -- some (scope, visited key) of an ES child
+// occurs more than once in the scope and one occurrence is decisive -- is routed to the DFS
+// interpreter, as are queries that spawn more than `budget` goals, run past MAX_GEN
+// generations or overflow the arena.  Repeats are found without hashing every occurrence:
+// fr_expand appends each ES child's (scope, key) to an occurrence list (sequential writes),
+// fr_reduce enters only the decisive ones into a small table, and fr_repeat counts the list's
+// occurrences of those keys.
 //
 // Goal records (HBM, one arena per stream, structure of arrays; 28 bytes per goal):
 //   g0[i]   = {node, query position, word, scope}   16 B, written by the parent at spawn
@@ -55,8 +59,9 @@ constexpr uint32_t MAX_GEN = 192;
 // union of one contiguous range per slice; slices stack their generations.
 constexpr uint32_t FR_SHARDS = 64;
 constexpr uint32_t GEN_STRIDE = MAX_GEN + 2;
-// ctrl: gbase[FR_SHARDS][GEN_STRIDE] | gcount[FR_SHARDS][GEN_STRIDE] | fallback count (+3)
-constexpr size_t FR_CTRL_BYTES = (2 * FR_SHARDS * GEN_STRIDE + 4) * 4;
+// ctrl: gbase[FR_SHARDS][GEN_STRIDE] | gcount[FR_SHARDS][GEN_STRIDE] | fallback count (+3) |
+// occurrence counts[FR_SHARDS]
+constexpr size_t FR_CTRL_BYTES = (2 * FR_SHARDS * GEN_STRIDE + 4 + FR_SHARDS) * 4;
 __device__ __forceinline__ uint32_t gword(uint32_t kind, uint32_t d, uint32_t op = 0, uint32_t flags = 0) {
     return (d & GD_MAX) | (kind << 12) | flags | (op << 16);
 }
@@ -73,9 +78,12 @@ struct FrontierParams {
     uint32_t gen;
     uint32_t *qgoals, *qroute;   // [n] per query position
     uint32_t budget;
-    unsigned long long *tkeys;   // (scope, visited key) table
-    uint8_t *trep;               // == epoch: the slot received its key more than once
-    uint32_t tmask, epoch;
+    unsigned long long *dkeys;   // decisive (scope, visited key) pairs of the batch (epoch-tagged)
+    uint32_t *dcnt;              // their occurrences, counted by fr_repeat
+    uint32_t dmask, epoch;
+    uint2 *occ;                  // every ES child's {scope, visited key}: FR_SHARDS slices of ocap
+    uint32_t *occ_count;         // [FR_SHARDS] entries per slice
+    uint32_t ocap;
     uint32_t max_width;
     uint8_t *out_allowed;
     int32_t *out_err;
@@ -147,12 +155,12 @@ struct Edges {
     }
 };
 
-// Scope-table keys carry the batch's epoch (1..TAB_EPOCHS) in bits 61-63 (scope < 2^29: a goal
-// index), so the table is cleared once every TAB_EPOCHS batches instead of after each one: a
-// slot holding 0 or another epoch's key is free.  Within a batch a slot only ever goes from free
-// to a key of the batch, so a lookup may stop at the first free slot.  trep[h] == epoch marks a
-// key received more than once.
+// Decisive-key table: keys carry the batch's epoch (1..TAB_EPOCHS) in bits 61-63 (scope < 2^29:
+// a goal index), so the table is cleared once every TAB_EPOCHS batches instead of after each one:
+// a slot holding 0 or another epoch's key is free.  Within a batch a slot only ever goes from
+// free to a key of the batch, so a lookup may stop at the first free slot.
 constexpr uint32_t TAB_EPOCHS = 7;
+constexpr int TAB_PROBES = 256;  // a longer walk than this routes the query (crowded)
 __device__ __forceinline__ unsigned long long tab_key(uint32_t ep, uint32_t scope, uint32_t vk) {
     return ((unsigned long long)ep << 61) | ((unsigned long long)scope << 32) | vk;
 }
@@ -163,7 +171,7 @@ __device__ __forceinline__ bool tab_free(unsigned long long k, uint32_t ep) { re
 __device__ __forceinline__ int64_t tab_insert(unsigned long long *tk, uint32_t mask, uint32_t ep, unsigned long long key,
                                               uint32_t h, unsigned long long old, bool *rep) {
     *rep = false;
-    for (int probe = 0; probe < 64;) {
+    for (int probe = 0; probe < TAB_PROBES;) {
         if (old == 0ull) return h;  // the CAS of 0 -> key that produced `old` inserted it
         if (old == key) {
             *rep = true;
@@ -191,9 +199,6 @@ __device__ __forceinline__ int64_t tab_insert(unsigned long long *tk, uint32_t m
 struct Sub {
     uint32_t word, leaf;
 };
-__device__ __forceinline__ uint2 rw_splice(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
-                                           uint32_t op, uint32_t d);
-template <bool SPLICE = true>
 __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t c, uint32_t dc,
                                          bool skip, uint32_t esf) {
     if (dc == 0) return Sub{0, M_UNK};
@@ -204,11 +209,7 @@ __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, 
         // run, checkIsAllowed is its rewrite's result (an OR / AND never yields a bare Unknown):
         // the RW goal is spawned in the IA's place, one generation earlier (oracle u_sub)
         const bool direct = !s.strict && !skip && dc > 1 && !(c & VIRT_BIT) && may_hold(s, q, ni.ri) && member(s, q, c);
-        if (!direct && !(ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri))) {
-            if (!SPLICE) return Sub{gword(G_RW, dc, ri_op(ni.ri)), 0};
-            const uint2 sp = rw_splice(s, T, q, c, ri_op(ni.ri), dc);
-            return Sub{gword(G_RW, sp.y, sp.x), 0};
-        }
+        if (!direct && !(ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri))) return Sub{gword(G_RW, dc, ri_op(ni.ri)), 0};
     }
     if (ri_rw(ni.ri) || (err && esf)) return Sub{gword(G_IA, dc, 0, (skip ? GF_SKIP : 0u) | esf), 0};
     if (err) return Sub{0, mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16)};
@@ -229,7 +230,7 @@ __device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables 
     uint32_t leaf = NONE32;
     if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
     else if (ct == OP_CSS) {
-        const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
+        const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
         if (!sb.word) leaf = sb.leaf;
     }
     if (leaf == NONE32) return NONE32;
@@ -237,62 +238,9 @@ __device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables 
     return m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
 }
 
-// An AND rewrite at rest depth d > 1 whose only goal child is a nested rewrite (an RW goal at
-// d-1, rewrites.go:118) and whose other children are leaves known at spawn to be IsMember without
-// an error is spawned as that nested rewrite: AND(x, IsMember...) is x for IsMember / NotMember,
-// no RW / IA goal yields a bare Unknown, and an error stays an error (oracle u_and_splice).  One
-// goal and one generation less per level of `(a | b | parents.traverse(...)) & !banned`.
-// Returns {op, d} of the goal to spawn.
-__device__ __forceinline__ uint2 rw_splice(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
-                                           uint32_t op, uint32_t d) {
-    const NodeInfo ni = t_node_info(T, node);
-    for (;;) {
-#ifdef KETO_FR_NOSPLICE  // measurement builds only (tools/ab)
-        break;
-#endif
-        if (d <= 1) break;
-        const Op o = T.ops[op];
-        if ((o.type_kind & 0xFFu) != OP_REWRITE || ((o.type_kind >> 8) & 0xFFu) != OPK_AND) break;
-        uint32_t only = NONE32;
-        bool ok = true;
-        for (uint32_t c = 0; c < o.child_count && ok; c++) {
-            const uint32_t ci = T.op_children[o.child_begin + c];
-            const Op ch = T.ops[ci];
-            const uint32_t ct = ch.type_kind & 0xFFu;
-            if (ct == OP_REWRITE) {
-                ok = only == NONE32;
-                only = ci;
-            } else if (ct == OP_CSS) {
-                const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
-                ok = !sb.word && sb.leaf == M_IS;
-            } else if (ct == OP_INVERT) {
-                ok = inv_leaf(s, T, q, node, ci, d) == M_IS;
-            } else {
-                ok = false;  // a tuple-to-userset is always a goal
-            }
-        }
-        if (!ok || only == NONE32) break;
-        op = only;
-        d -= 1;
-    }
-    return make_uint2(op, d);
-}
 
 __device__ __forceinline__ uint32_t tab_hash(unsigned long long key, uint32_t mask) {
     return (uint32_t)mix64(key & ((1ull << 61) - 1ull)) & mask;  // the epoch does not move a key
-}
-// count an occurrence of (scope, key) that is not a goal; false when the table is crowded
-__device__ __forceinline__ bool tab_mark(const FrontierParams &P, uint32_t scope, uint32_t vk) {
-#ifdef KETO_FR_NOTAB
-    return true;
-#endif
-    const unsigned long long key = tab_key(P.epoch, scope, vk);
-    const uint32_t h = tab_hash(key, P.tmask);
-    bool rep = false;
-    const int64_t at = tab_insert(P.tkeys, P.tmask, P.epoch, key, h, atomicCAS(&P.tkeys[h], 0ull, key), &rep);
-    if (at < 0) return false;
-    if (rep) P.trep[at] = (uint8_t)P.epoch;
-    return true;
 }
 
 // a routed query also saturates its goal count, so the budget atomic of any later spawn refuses
@@ -400,20 +348,6 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
         const uint32_t node = g.x, pos = g.y, w = g.z, scope = g.w;
         const uint32_t d = w & GD_MAX, kind = (w >> 12) & 7u, op = w >> 16;
         const uint32_t qg = live ? P.qgoals[pos] : 0u;
-        // An ES child counts its key into the scope table (CheckAndAddVisited, engine.go:157-160):
-        // the CAS is issued here and its answer consumed after the goal's own work.
-#ifdef KETO_FR_NOTAB  // measurement builds only (tools/ab): the scope table's cost, routing disabled
-        const bool ins = false;
-#else
-        const bool ins = live && (kind == G_IA || kind == G_ES) && (w & GF_ESCHILD);
-#endif
-        unsigned long long tkey = 0, told = 0;
-        uint32_t th = 0;
-        if (ins) {
-            tkey = tab_key(P.epoch, scope, (w & GF_ALIAS) ? s.vkey[node] : node);
-            th = tab_hash(tkey, P.tmask);
-            told = atomicCAS(&P.tkeys[th], 0ull, tkey);
-        }
         // The loads the goal kinds start from, issued together: the row an ES / TTU reads, and
         // the subject's membership record (IA direct check, ES lookahead, OR shortcut).
         uint32_t rnode = NONE32;
@@ -463,7 +397,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 for (uint32_t e = 0; it.cur < it.end && !found; e++) {
                     const uint32_t c = it.next() & ~EDGE_ALIAS;
                     found = member(s, q, c);
-                    if (e < keep && sub_check<false>(s, T, q, c, d, true, GF_ESCHILD).word) nc++;  // the children that are goals
+                    if (e < keep && sub_check(s, T, q, c, d, true, GF_ESCHILD).word) nc++;  // the children that are goals
                 }
                 if (found) {
                     val = M_IS;
@@ -521,7 +455,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                             }
                         } else if (ik == IT_CAND) {  // checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
                             if (dk > 1) {
-                                const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0);
+                                const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0);
                                 if (sb.word) nc++;
                                 else leaf = sb.leaf;
                             }
@@ -538,7 +472,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                                     Edges et(s, s.set_row[ts]);
                                     for (uint32_t e = 0; et.cur < et.end; e++) {
                                         const uint32_t pn = et.next() & ~EDGE_ALIAS;
-                                        const Sub sb = sub_check<false>(s, T, q, t_sibling(T, pn, t_node_info(T, pn), rc >> 16), dk - 1, false, 0);
+                                        const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), rc >> 16), dk - 1, false, 0);
                                         if (sb.word) nc++;
                                         else if (decisive(sb.leaf)) {
                                             leaf = sb.leaf;
@@ -569,7 +503,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                         uint32_t leaf = NONE32;
                         if (ct == OP_REWRITE && d <= 1) leaf = M_UNK;  // nested rewrite at d-1 <= 0 (:39-42)
                         else if (ct == OP_CSS) {  // checkComputedSubjectSet (rewrites.go:208-230)
-                            const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
+                            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
                             if (!sb.word) leaf = sb.leaf;
                         } else if (ct == OP_INVERT)
                             leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin + c], d);
@@ -597,7 +531,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 uint32_t tail = NONE32, e = 0;
                 for (; it.cur < it.end; e++) {
                     const uint32_t pn = it.next() & ~EDGE_ALIAS;
-                    const Sub sb = sub_check<false>(s, T, q, t_sibling(T, pn, t_node_info(T, pn), xrel), d - 1, false, 0);
+                    const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), xrel), d - 1, false, 0);
                     if (sb.word) nc++;
                     else if (decisive(sb.leaf)) {
                         tail = sb.leaf;
@@ -620,7 +554,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 uint32_t leaf = NONE32;
                 if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
                 else if (ct == OP_CSS) {
-                    const Sub sb = sub_check<false>(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
+                    const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
                     if (!sb.word) leaf = sb.leaf;
                 } else if (ct == OP_INVERT) leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin], d);  // folded inner NOT
                 if (leaf != NONE32) {  // NOT of a result known now: IsMember <-> NotMember, Unknown / errors kept
@@ -681,20 +615,22 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             P.gfn[i] = make_uint2(cb, nc | (rop << 24));
             P.gval[i] = val;
         }
-        if (ins && told != 0ull) {  // the key was there (a repeat), a stale key or another key is
-            bool rep = false;
-            const int64_t at = tab_insert(P.tkeys, P.tmask, P.epoch, tkey, th, told, &rep);
-            if (at < 0) route(P, pos);  // crowded: the DFS interpreter takes the query
-            else if (rep) P.trep[at] = (uint8_t)P.epoch;
-        }
+        // ---- occurrences: an ES goal's kept children, goals and leaves alike, are the keys it
+        // adds to its scope (CheckAndAddVisited, engine.go:157-160): one run of its wave's slice
+        const uint32_t nocc = (live && kind == G_ES && (nc || xrel)) ? pat : 0u;
+        uint32_t otot = 0;
+        const uint32_t ooff = wave_excl(nocc, otot);
+        uint32_t obase = 0;
+        if (lane == 0 && otot) obase = atomicAdd(&P.occ_count[so], otot);
+        uint32_t oc = __shfl(obase, 0) + ooff;
+        const bool occ_ok = (uint64_t)oc + nocc <= P.ocap;
+        if (nocc && !occ_ok) route(P, pos);  // list full: the DFS interpreter takes the query
+        oc += so * P.ocap;
         FR_MARK(3);
         // ---- phase B: write the children (the same walk as phase A) -------------------------------
         if (nc || (kind == G_ES && xrel)) switch (kind) {
         case G_IA:
-            if (pat & 1u) {
-                const uint2 sp = rw_splice(s, T, q, node, xrel, d);
-                spawn(P, cb, node, pos, gword(G_RW, sp.y, sp.x), scope);
-            }
+            if (pat & 1u) spawn(P, cb, node, pos, gword(G_RW, d, xrel), scope);
             if (pat & 2u) spawn(P, cb + ((pat & 1u) ? 1 : 0), node, pos, gword(G_ES, d - 1), scope);
             break;
         case G_ES: {
@@ -703,11 +639,10 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             for (uint32_t e = 0; e < pat; e++) {
                 const uint32_t raw = it.next(), cn = raw & ~EDGE_ALIAS;
                 const uint32_t esf = GF_ESCHILD | ((raw & EDGE_ALIAS) ? GF_ALIAS : 0u);
-                // checkIsAllowed(c, d, skipDirect) (:161); a goal marks its key itself, a leaf
-                // child's key is marked here (CheckAndAddVisited, :157-160)
+                // checkIsAllowed(c, d, skipDirect) (:161); every child's key is an occurrence
                 const Sub sb = sub_check(s, T, q, cn, d, true, esf);
                 if (sb.word) spawn(P, c++, cn, pos, sb.word, sc);
-                else if (!tab_mark(P, sc, (raw & EDGE_ALIAS) ? s.vkey[cn] : cn)) route(P, pos);
+                if (occ_ok) P.occ[oc + e] = make_uint2(sc, (raw & EDGE_ALIAS) ? s.vkey[cn] : cn);
             }
             break;
         }
@@ -841,24 +776,15 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
             val = res;
             P.gval[i] = val;
         }
-#ifdef KETO_FR_NOTAB
-        if (false) {
-#else
-        if (k > 0 && decisive(val)) {  // an ES child: was its key repeated in the scope?
-#endif
+        if (k > 0 && decisive(val)) {  // a decisive ES child: its key goes into the decisive table
             const uint4 g = P.g0[i];
             if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD)) {  // (RW / TTU / INV hold an op there)
                 const unsigned long long key = tab_key(P.epoch, g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x);
-                uint32_t h = tab_hash(key, P.tmask);
-                for (int probe = 0; probe < 64; probe++) {
-                    const unsigned long long kk = P.tkeys[h];
-                    if (kk == key) {
-                        if (P.trep[h] == P.epoch) route(P, g.y);
-                        break;
-                    }
-                    if (tab_free(kk, P.epoch)) break;  // not inserted (crowded): the query was routed then
-                    h = (h + 1) & P.tmask;
-                }
+                const uint32_t h = tab_hash(key, P.dmask);
+                bool rep = false;
+                const int64_t at = tab_insert(P.dkeys, P.dmask, P.epoch, key, h, atomicCAS(&P.dkeys[h], 0ull, key), &rep);
+                if (at < 0) route(P, g.y);  // crowded: the DFS interpreter takes the query
+                else if (!rep) P.dcnt[at] = 0;
             }
         }
         if (k == 0) {  // generation 0: one goal per query position
@@ -871,6 +797,40 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
             const uint32_t err = val >> 8;
             P.out_allowed[q] = (err == 0 && (val & 3u) == M_IS) ? 1 : 0;
             P.out_err[q] = (int32_t)(P.err_detail ? err : err & 0xFFu);
+        }
+    }
+}
+
+// After every generation above 0 is reduced: each occurrence of a decisive key counts itself;
+// a second occurrence routes the query (the scope's first goal holds its position).
+__global__ __launch_bounds__(256) void fr_repeat(FrontierParams P) {
+    __shared__ uint32_t pre[FR_SHARDS + 1];
+    for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x) pre[t + 1] = std::min(P.occ_count[t], P.ocap);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        pre[0] = 0;
+        for (uint32_t t = 0; t < FR_SHARDS; t++) pre[t + 1] += pre[t];
+    }
+    __syncthreads();
+    const uint32_t total = pre[FR_SHARDS];
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = FR_SHARDS;  // last slice with pre[t] <= j
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        const uint2 o = P.occ[(size_t)lo * P.ocap + (j - pre[lo])];
+        const unsigned long long key = tab_key(P.epoch, o.x, o.y);
+        uint32_t h = tab_hash(key, P.dmask);
+        for (int probe = 0; probe < TAB_PROBES; probe++) {
+            const unsigned long long kk = P.dkeys[h];
+            if (kk == key) {
+                if (atomicAdd(&P.dcnt[h], 1u) >= 1u) route(P, P.g0[o.x].y);
+                break;
+            }
+            if (tab_free(kk, P.epoch)) break;  // not a decisive key
+            h = (h + 1) & P.dmask;
         }
     }
 }
@@ -894,18 +854,19 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     f.mem = nullptr;
     const uint64_t cap = std::max<uint64_t>(want, f.cap);
     const uint64_t ncap = std::max<uint64_t>(n, f.ncap);
-    uint64_t tcap = 1;
-#ifdef KETO_FR_TAB_LOG2  // measurement builds (tools/ab): a fixed scope-table size
-    tcap = 1ull << KETO_FR_TAB_LOG2;
-#else
-    while (tcap < cap / 2) tcap <<= 1;
-#endif
+    // decisive-key table: a few decisive ES children per query at most in practice; a crowded
+    // table routes (never seen); the occurrence list: half the arena's goal count
+    uint64_t dcap = 1u << 16;
+    while (dcap < 4 * ncap) dcap <<= 1;
+    const uint64_t ocap = cap / 2 / FR_SHARDS;  // per slice
     const size_t ctrl = al256(FR_CTRL_BYTES);
-    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 4) + al256(tcap * 9);
+    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 4) + al256(dcap * 12) +
+                         al256(ocap * FR_SHARDS * 8);
     KETO_HIP(hipMalloc(&f.mem, bytes));
     char *p = static_cast<char *>(f.mem);
     f.ctrl = reinterpret_cast<uint32_t *>(p);
     f.fb_count = f.ctrl + 2 * FR_SHARDS * GEN_STRIDE;
+    f.occ_count = f.fb_count + 4;
     p += ctrl;
     f.qgoals = reinterpret_cast<uint32_t *>(p);
     f.qroute = f.qgoals + ncap;
@@ -917,15 +878,18 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     p += al256(cap * 8);
     f.gval = reinterpret_cast<uint32_t *>(p);
     p += al256(cap * 4);
-    f.tkeys = reinterpret_cast<unsigned long long *>(p);
-    f.trep = reinterpret_cast<uint8_t *>(f.tkeys + tcap);
+    f.dkeys = reinterpret_cast<unsigned long long *>(p);
+    f.dcnt = reinterpret_cast<uint32_t *>(f.dkeys + dcap);
+    p += al256(dcap * 12);
+    f.occ = reinterpret_cast<uint2 *>(p);
     // the table starts empty; batches tag their keys with an epoch (TAB_EPOCHS)
-    KETO_HIP(hipMemset(f.tkeys, 0, tcap * 9));
+    KETO_HIP(hipMemset(f.dkeys, 0, dcap * 12));
     f.epoch = 1;
     KETO_HIP(hipDeviceSynchronize());
     f.cap = cap;
     f.ncap = ncap;
-    f.tcap = tcap;
+    f.dcap = dcap;
+    f.ocap = ocap;
     if (!f.host_ctrl) KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&f.host_ctrl), FR_CTRL_BYTES, 0));
 }
 
@@ -952,9 +916,12 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.qroute = f.qroute;
     const char *be = getenv("KETO_FR_BUDGET");
     P.budget = be ? (uint32_t)std::max(1, atoi(be)) : 1024u;
-    P.tkeys = f.tkeys;
-    P.trep = f.trep;
-    P.tmask = (uint32_t)(f.tcap - 1);
+    P.dkeys = f.dkeys;
+    P.dcnt = f.dcnt;
+    P.dmask = (uint32_t)(f.dcap - 1);
+    P.occ = f.occ;
+    P.occ_count = f.occ_count;
+    P.ocap = (uint32_t)f.ocap;
     P.epoch = f.epoch;
     P.max_width = (uint32_t)L.max_width;
     P.out_allowed = L.out_allowed;
@@ -1009,12 +976,16 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     for (int32_t g = (int32_t)gens - 1; g >= 0; g--) {
         top += tot[g];
         P.gen = (uint32_t)g;
+        if (g == 0) {  // every decisive ES child is in the table: count the repeats of those keys
+            hipLaunchKernelGGL(fr_repeat, dim3(cus * 8), eb, 0, st.stream, P);
+            KETO_HIP(hipGetLastError());
+        }
         const dim3 rg((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tot[g] + BLOCK - 1) / BLOCK, cus * 16)));
         hipLaunchKernelGGL(fr_reduce, rg, eb, 0, st.stream, P);
         KETO_HIP(hipGetLastError());
     }
     if (++f.epoch > TAB_EPOCHS) {  // every TAB_EPOCHS batches: clear the table
-        KETO_HIP(hipMemsetAsync(f.tkeys, 0, f.tcap * 9, st.stream));
+        KETO_HIP(hipMemsetAsync(f.dkeys, 0, f.dcap * 12, st.stream));
         f.epoch = 1;
     }
     KETO_HIP(hipMemcpyAsync(hc, fb_count, 4, hipMemcpyDeviceToHost, st.stream));

@@ -954,7 +954,6 @@ static int u_spawn(uctx *u, uint32_t gen) {
 static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, uint32_t scope, uint32_t gen);
 static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen);
 static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen);
-static void u_and_splice(uctx *u, uint32_t ns, uint32_t obj, int *ai, int *d);
 
 /* a relation whose rows can hold subject sets: some tuple of (ns, rel) has one (per snapshot) */
 static int has_set_rows(const rs_db *db, uint32_t ns, uint32_t rel) {
@@ -984,9 +983,7 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
         const int es = can_ss_rw && d - 1 > 0 && has_set_rows(db, ns, rel);
         if (!direct && !es) {
             if (!u_spawn(u, gen + 1)) return 0;
-            int ai = db->rels[ri].rewrite, dd = d;
-            u_and_splice(u, ns, obj, &ai, &dd);
-            *out = u_rw(u, ns, obj, ai, dd, scope, gen + 1);
+            *out = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
             return 1;
         }
     }
@@ -1043,52 +1040,6 @@ static int u_inv_folds(uctx *u, uint32_t ns, uint32_t obj, int ai, int d) {
 /* a rewrite child (check_child): 1 = spawned as a goal (result in *out), 0 = a leaf result */
 static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, uint32_t scope, uint32_t gen,
                    res *out);
-static res u_inv(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen);
-
-/* An AND rewrite at rest depth d > 1 whose only goal child is a nested rewrite (an RW goal at
- * d-1, rewrites.go:118) and whose other children are leaves known at spawn to be IsMember
- * without an error (a computed userset decided on the spot, a folded NOT) is that nested
- * rewrite: AND(x, IsMember...) is x whenever x is IsMember or NotMember, and an OR / AND / IA
- * goal never yields a bare Unknown (u_rw, u_ia); with an error x keeps it (the membership bits
- * beside an error decide nothing).  No goal is spawned for the AND -- one goal and one
- * generation less per level of an `(a | b | parents.traverse(...)) & !banned` permission.
- * Applied while the result is again such an AND.  (csrc/frontier.hip rw_splice) */
-static void u_and_splice(uctx *u, uint32_t ns, uint32_t obj, int *ai, int *d) {
-    const rs_db *db = u->c->db;
-    for (;;) {
-        const rs_ast *a = &db->ast[*ai];
-        if (a->type != RS_REWRITE || a->op != RS_OP_AND || *d <= 1) return;
-        int only = -1;
-        for (int k = 0; k < a->child_count; k++) {
-            const int ci = db->children[a->child_begin + k];
-            const rs_ast *ch = &db->ast[ci];
-            res r = R_UNK;
-            if (ch->type == RS_REWRITE) {
-                if (only >= 0) return;
-                only = ci;
-                continue;
-            }
-            if (ch->type == RS_CSS) {
-                if (u_sub_spawns(u, ns, obj, ch->rel, *d, 0, 0)) return;
-                int err;
-                const int ri = ast_relation_for(db, ns, ch->rel, &err);
-                (void)ri;
-                if (err || !(*d - 1 > 0 && exists(u->c, ns, obj, ch->rel))) return;
-                continue; /* a direct tuple: IsMember */
-            }
-            if (ch->type == RS_INVERT) {
-                if (!u_inv_folds(u, ns, obj, ci, *d)) return;
-                r = u_inv(u, ns, obj, ci, *d, U_NONE, 0);
-                if (r.err || r.m != RS_IS_MEMBER) return;
-                continue;
-            }
-            return; /* a tuple-to-userset is always a goal; anything else an error leaf */
-        }
-        if (only < 0) return;
-        *ai = only;
-        *d -= 1;
-    }
-}
 
 static res u_ttu(uctx *u, uint32_t ns, uint32_t obj, const rs_ast *a, int d, uint32_t scope, uint32_t gen) {
     const rs_db *db = u->c->db;
@@ -1305,11 +1256,7 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
     const int has_rewrite = ri >= 0 && db->rels[ri].rewrite >= 0;
     const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
     res rr = R_NOT, er = R_NOT;
-    if (has_rewrite && u_spawn(u, gen + 1)) {
-        int ai = db->rels[ri].rewrite, dd = d;
-        u_and_splice(u, ns, obj, &ai, &dd);
-        rr = u_rw(u, ns, obj, ai, dd, scope, gen + 1);
-    }
+    if (has_rewrite && u_spawn(u, gen + 1)) rr = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
     const int direct_is = (!db->strict || !has_rewrite) && !skip && d - 1 > 0 && exists(u->c, ns, obj, rel);
     if (can_ss && !direct_is && d - 1 > 0 && has_set_rows(db, ns, rel) && u_spawn(u, gen + 1))
         er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
