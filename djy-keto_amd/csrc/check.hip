@@ -513,19 +513,20 @@ static void run_dfs(const Snapshot &s, Stream &st, const CheckLaunch &L, const u
 
 // Check over a resolved batch: the frontier engine (frontier.hip) answers every query whose
 // result cannot depend on visited pruning and routes the rest here; KETO_FRONTIER=0 (A/B) and
-// work-counting launches run the DFS interpreter on the whole batch.  The timed region is the
-// whole device path of the batch after the resolve pass.
+// work-counting launches run the DFS interpreter on the whole batch.  The frontier engine's timed
+// region is the whole device path of the batch, request resolution (A1) included.
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     if (L.n == 0) return;
     if (L.n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
-    run_resolve(s, st, L.queries, L.n, L.max_depth);
     const char *fe = getenv("KETO_FRONTIER");
     const bool frontier = !L.count && !(fe && fe[0] == '0');
     if (!frontier) {
+        run_resolve(s, st, L.queries, L.n, L.max_depth);
         run_dfs(s, st, L, nullptr, nullptr, L.n, true);
         return;
     }
     st.mark_begin();
+    run_resolve(s, st, L.queries, L.n, L.max_depth, false);
     const uint32_t routed = run_frontier(s, st, L);
     if (routed) run_dfs(s, st, L, st.frontier.fb_list, st.frontier.fb_count, routed, false);
     st.mark_end();

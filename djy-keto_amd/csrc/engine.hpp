@@ -127,7 +127,7 @@ struct FrontierScratch {
     uint2 *gfn = nullptr;
     uint32_t *gval = nullptr;
     unsigned long long *dkeys = nullptr;
-    uint32_t *dcnt = nullptr, *occ_count = nullptr;
+    uint32_t *dcnt = nullptr, *occ_count = nullptr, *dbits = nullptr;
     uint2 *occ = nullptr;
     uint32_t *host_ctrl = nullptr;  // pinned
     uint32_t last_gens = 0, last_goals = 0, last_routed = 0;
@@ -179,7 +179,9 @@ struct CheckLaunch {
     bool err_detail;  // KETO_F_ERR_DETAIL: out_err carries the failing relation name id << 8
 };
 // resolve.hip: per-query start records, longest-first, into st.resolved
-void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth);
+// ordered: heavy-first work order for the DFS interpreters (two atomics per wave); else batch order
+void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth,
+                 bool ordered = true);
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
 void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // rewrite-free snapshots
 // frontier.hip: the batch (already resolved) breadth-first; returns the number of queries routed

@@ -80,6 +80,7 @@ struct FrontierParams {
     uint32_t budget;
     unsigned long long *dkeys;   // decisive (scope, visited key) pairs of the batch (epoch-tagged)
     uint32_t *dcnt;              // their occurrences, counted by fr_repeat
+    uint32_t *dbits;             // 2^DBITS_LOG2-bit filter of the decisive keys (L2-resident)
     uint32_t dmask, epoch;
     uint2 *occ;                  // every ES child's {scope, visited key}: FR_SHARDS slices of ocap
     uint32_t *occ_count;         // [FR_SHARDS] entries per slice
@@ -241,6 +242,14 @@ __device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables 
 
 __device__ __forceinline__ uint32_t tab_hash(unsigned long long key, uint32_t mask) {
     return (uint32_t)mix64(key & ((1ull << 61) - 1ull)) & mask;  // the epoch does not move a key
+}
+// The decisive keys' bit filter: fr_repeat looks up the table only for occurrences whose bit is
+// set.  64 KB: every fr_repeat block holds it in LDS.  Decisive ES children are rare (Drive: ~3
+// per 1000 queries), so nearly every occurrence is dismissed without a global access.
+constexpr uint32_t DBITS_LOG2 = 19;
+constexpr uint32_t REPEAT_BLOCK = 1024;
+__device__ __forceinline__ uint32_t dbit(unsigned long long key) {
+    return (uint32_t)(mix64(key & ((1ull << 61) - 1ull)) >> 40) & ((1u << DBITS_LOG2) - 1u);
 }
 
 // a routed query also saturates its goal count, so the budget atomic of any later spawn refuses
@@ -785,6 +794,8 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
                 const int64_t at = tab_insert(P.dkeys, P.dmask, P.epoch, key, h, atomicCAS(&P.dkeys[h], 0ull, key), &rep);
                 if (at < 0) route(P, g.y);  // crowded: the DFS interpreter takes the query
                 else if (!rep) P.dcnt[at] = 0;
+                const uint32_t b = dbit(key);
+                atomicOr(&P.dbits[b >> 5], 1u << (b & 31u));
             }
         }
         if (k == 0) {  // generation 0: one goal per query position
@@ -803,8 +814,10 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
 
 // After every generation above 0 is reduced: each occurrence of a decisive key counts itself;
 // a second occurrence routes the query (the scope's first goal holds its position).
-__global__ __launch_bounds__(256) void fr_repeat(FrontierParams P) {
+__global__ __launch_bounds__(REPEAT_BLOCK) void fr_repeat(FrontierParams P) {
     __shared__ uint32_t pre[FR_SHARDS + 1];
+    __shared__ uint4 bits[(1u << DBITS_LOG2) / 128];
+    for (uint32_t t = threadIdx.x; t < (1u << DBITS_LOG2) / 128; t += blockDim.x) bits[t] = reinterpret_cast<const uint4 *>(P.dbits)[t];
     for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x) pre[t + 1] = std::min(P.occ_count[t], P.ocap);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -813,24 +826,40 @@ __global__ __launch_bounds__(256) void fr_repeat(FrontierParams P) {
     }
     __syncthreads();
     const uint32_t total = pre[FR_SHARDS];
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
-        uint32_t lo = 0, hi = FR_SHARDS;  // last slice with pre[t] <= j
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pre[mid] <= j) lo = mid;
-            else hi = mid;
-        }
-        const uint2 o = P.occ[(size_t)lo * P.ocap + (j - pre[lo])];
-        const unsigned long long key = tab_key(P.epoch, o.x, o.y);
-        uint32_t h = tab_hash(key, P.dmask);
-        for (int probe = 0; probe < TAB_PROBES; probe++) {
-            const unsigned long long kk = P.dkeys[h];
-            if (kk == key) {
-                if (atomicAdd(&P.dcnt[h], 1u) >= 1u) route(P, P.g0[o.x].y);
-                break;
+    constexpr uint32_t U = 4;  // occurrences in flight per lane (the loop is latency-bound)
+    const uint32_t G = gridDim.x * blockDim.x;
+    for (uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x; j0 < total; j0 += U * G) {
+        uint2 o[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t j = j0 + u * G;
+            o[u] = make_uint2(NONE32, 0);
+            if (j < total) {
+                uint32_t lo = 0, hi = FR_SHARDS;  // last slice with pre[t] <= j
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pre[mid] <= j) lo = mid;
+                    else hi = mid;
+                }
+                o[u] = P.occ[(size_t)lo * P.ocap + (j - pre[lo])];
             }
-            if (tab_free(kk, P.epoch)) break;  // not a decisive key
-            h = (h + 1) & P.dmask;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            if (o[u].x == NONE32) continue;
+            const unsigned long long key = tab_key(P.epoch, o[u].x, o[u].y);
+            const uint32_t b = dbit(key);
+            if (!((reinterpret_cast<const uint32_t *>(bits)[b >> 5] >> (b & 31u)) & 1u)) continue;  // not a decisive key
+            uint32_t h = tab_hash(key, P.dmask);
+            for (int probe = 0; probe < TAB_PROBES; probe++) {
+                const unsigned long long kk = P.dkeys[h];
+                if (kk == key) {
+                    if (atomicAdd(&P.dcnt[h], 1u) >= 1u) route(P, P.g0[o[u].x].y);
+                    break;
+                }
+                if (tab_free(kk, P.epoch)) break;
+                h = (h + 1) & P.dmask;
+            }
         }
     }
 }
@@ -861,7 +890,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     const uint64_t ocap = cap / 2 / FR_SHARDS;  // per slice
     const size_t ctrl = al256(FR_CTRL_BYTES);
     const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 4) + al256(dcap * 12) +
-                         al256(ocap * FR_SHARDS * 8);
+                         al256(ocap * FR_SHARDS * 8) + (1u << DBITS_LOG2) / 8;
     KETO_HIP(hipMalloc(&f.mem, bytes));
     char *p = static_cast<char *>(f.mem);
     f.ctrl = reinterpret_cast<uint32_t *>(p);
@@ -882,6 +911,8 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     f.dcnt = reinterpret_cast<uint32_t *>(f.dkeys + dcap);
     p += al256(dcap * 12);
     f.occ = reinterpret_cast<uint2 *>(p);
+    p += al256(ocap * FR_SHARDS * 8);
+    f.dbits = reinterpret_cast<uint32_t *>(p);
     // the table starts empty; batches tag their keys with an epoch (TAB_EPOCHS)
     KETO_HIP(hipMemset(f.dkeys, 0, dcap * 12));
     f.epoch = 1;
@@ -901,6 +932,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     const size_t lds = lds_tables ? s.dev.lds_bytes : 0;
     uint32_t *gbase = f.ctrl, *gcount = f.ctrl + FR_SHARDS * GEN_STRIDE, *fb_count = f.fb_count;
     KETO_HIP(hipMemsetAsync(f.ctrl, 0, FR_CTRL_BYTES, st.stream));
+    KETO_HIP(hipMemsetAsync(f.dbits, 0, (1u << DBITS_LOG2) / 8, st.stream));
     FrontierParams P{};
     P.s = s.dev;
     P.start = st.resolved;
@@ -918,6 +950,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.budget = be ? (uint32_t)std::max(1, atoi(be)) : 1024u;
     P.dkeys = f.dkeys;
     P.dcnt = f.dcnt;
+    P.dbits = f.dbits;
     P.dmask = (uint32_t)(f.dcap - 1);
     P.occ = f.occ;
     P.occ_count = f.occ_count;
@@ -977,7 +1010,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         top += tot[g];
         P.gen = (uint32_t)g;
         if (g == 0) {  // every decisive ES child is in the table: count the repeats of those keys
-            hipLaunchKernelGGL(fr_repeat, dim3(cus * 8), eb, 0, st.stream, P);
+            hipLaunchKernelGGL(fr_repeat, dim3(cus * 2), dim3(REPEAT_BLOCK), 0, st.stream, P);
             KETO_HIP(hipGetLastError());
         }
         const dim3 rg((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tot[g] + BLOCK - 1) / BLOCK, cus * 16)));

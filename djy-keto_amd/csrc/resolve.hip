@@ -30,7 +30,7 @@ struct ResolveParams {
     uint32_t n;
     int32_t max_depth;
     uint4 *resolved;  // [2n], in work order: heavy from the front, light from the back
-    uint32_t *ctrl;   // [0] heavy count, [1] light count
+    uint32_t *ctrl;   // [0] heavy count, [1] light count; null: batch order (the frontier engine)
 };
 
 __device__ __forceinline__ uint32_t w8(const uint4 &v0, const uint4 &v1, uint32_t j) {
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
             rb = s.rev_off[sidx];
             re = s.rev_off[sidx + 1];
         }
-        if (!(root & VIRT_BIT)) wgt = s.weight[root];
+        if (P.ctrl && !(root & VIRT_BIT)) wgt = s.weight[root];  // (the work order's cost class)
         const uint32_t len = re - rb;
         const bool heavy = len > PROBE_K;
         if (!heavy && len > 0) {
@@ -94,15 +94,30 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
         // filter of the row} (layout.hpp subj_filter_bits)
         if (heavy) {
             uint64_t f = ~0ull;
-            if (len <= FILTER_MAX_LEN) {
+            if (len <= FILTER_MAX_LEN) {  // 16-byte windows of the row, two loads in flight
                 f = 0;
-                for (uint32_t j = rb; j < re; j++) f |= subj_filter_bits(s.rev_nodes[j]);
+                const uint32_t w0 = rb & ~3u;
+                for (uint32_t j = w0; j < re; j += 8) {
+                    const uint4 a = *reinterpret_cast<const uint4 *>(s.rev_nodes + j);
+                    const uint4 b = j + 4 < re ? *reinterpret_cast<const uint4 *>(s.rev_nodes + j + 4) : make_uint4(0, 0, 0, 0);
+                    for (uint32_t k = 0; k < 8; k++) {
+                        const uint32_t e = j + k;
+                        if (e >= rb && e < re) f |= subj_filter_bits(k < 4 ? wword(a, k) : wword(b, k - 4));
+                    }
+                }
             }
             R = make_uint4(sidx, START_R_HEAVY, (uint32_t)f, (uint32_t)(f >> 32));
         }
         // x root, y subject index, z depth | hash-probe flag, w query index
         r0 = make_uint4(root, sidx, d | (heavy ? START_HEAVY : 0u), i);
         heavy_cls = wgt >= HEAVY_WEIGHT;
+    }
+    if (!P.ctrl) {  // the frontier engine needs no work order: position = query index, no atomics
+        if (valid) {
+            P.resolved[2 * (size_t)i] = r0;
+            P.resolved[2 * (size_t)i + 1] = R;
+        }
+        return;
     }
     // order: one atomic per class per wavefront
     const unsigned long long mh = __ballot(valid && heavy_cls), ml = __ballot(valid && !heavy_cls);
@@ -126,16 +141,16 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
 
 }  // namespace
 
-void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth) {
+void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth, bool ordered) {
     ensure_lists(st, n);
-    KETO_HIP(hipMemsetAsync(st.order_ctrl, 0, 8, st.stream));
+    if (ordered) KETO_HIP(hipMemsetAsync(st.order_ctrl, 0, 8, st.stream));
     ResolveParams P{};
     P.s = s.dev;
     P.queries = queries;
     P.n = (uint32_t)n;
     P.max_depth = max_depth;
     P.resolved = st.resolved;
-    P.ctrl = st.order_ctrl;
+    P.ctrl = ordered ? st.order_ctrl : nullptr;
     constexpr uint32_t BLOCK = 256;
     hipLaunchKernelGGL(resolve_kernel, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st.stream, P);
     KETO_HIP(hipGetLastError());
