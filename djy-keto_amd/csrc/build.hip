@@ -346,6 +346,13 @@ __global__ __launch_bounds__(BLK) void k_alias_mark(uint32_t *set_dst, uint64_t 
     if (i < n && vkey[set_dst[i]] != set_dst[i]) set_dst[i] |= EDGE_ALIAS;
 }
 
+__global__ __launch_bounds__(BLK) void k_leaf_mark(uint32_t *set_dst, uint64_t n, const uint4 *set_row) {
+    const uint64_t i = gid();
+    if (i >= n) return;
+    const uint32_t c = set_dst[i] & ~(EDGE_ALIAS | EDGE_LEAF);
+    const uint4 r = set_row[c];
+    if (r.x == r.y) set_dst[i] |= EDGE_LEAF;
+}
 }  // namespace
 
 // ---------------------------------------------------------------- host side
@@ -547,6 +554,12 @@ void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32
 
 void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag) {
     if (n) hipLaunchKernelGGL(k_slot_idrows, grid_for(n), dim3(BLK), 0, 0, t, n, slot_of, n_rel, ns, flag);
+    KETO_HIP(hipGetLastError());
+}
+
+void leaf_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows) {
+    if (n) hipLaunchKernelGGL(k_leaf_mark, grid_for(n), dim3(BLK), 0, 0, set_dst, n, set_row);
+    hipLaunchKernelGGL(k_row_inline, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, set_dst);  // inline copies too
     KETO_HIP(hipGetLastError());
 }
 

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 if (!heavy) {
                     bool found = false;
                     while (cur < end && cur < ew_hi) {
-                        const uint32_t c = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
+                        const uint32_t c = wword(ew, cur - ew_lo) & s.edge_mask;
                         cur++;
                         if (COUNT) {
                             q_edges++;
@@ -278,12 +278,12 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                         break;
                     }
                 } else if (cur < end) {  // two probes per step, in edge order
-                    const uint32_t c0 = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
+                    const uint32_t c0 = wword(ew, cur - ew_lo) & s.edge_mask;
                     aux = (uint32_t)mix64((((uint64_t)sidx << 32) | c0) + 1) & s.probe_mask;
                     la0 = s.probe + aux;
                     ln = 1;
                     if (cur + 1 < end && cur + 1 < ew_hi) {
-                        const uint32_t c1 = wword(ew, cur + 1 - ew_lo) & ~EDGE_ALIAS;
+                        const uint32_t c1 = wword(ew, cur + 1 - ew_lo) & s.edge_mask;
                         aux2 = (uint32_t)mix64((((uint64_t)sidx << 32) | c1) + 1) & s.probe_mask;
                         la1 = s.probe + aux2;
                         ln = 2;
@@ -304,13 +304,13 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 break;
             }
             case U_SPROBE: {
-                const uint32_t c0 = wword(ew, cur - ew_lo) & ~EDGE_ALIAS;
+                const uint32_t c0 = wword(ew, cur - ew_lo) & s.edge_mask;
                 uint32_t r0 = probe_check(v0, (((uint64_t)sidx << 32) | c0) + 1);
                 uint32_t r1 = 0;
                 const bool two = cur + 1 < end && cur + 1 < ew_hi;
                 uint32_t c1 = 0;
                 if (two) {
-                    c1 = wword(ew, cur + 1 - ew_lo) & ~EDGE_ALIAS;
+                    c1 = wword(ew, cur + 1 - ew_lo) & s.edge_mask;
                     r1 = probe_check(v1, (((uint64_t)sidx << 32) | c1) + 1);
                 }
                 if (r0 == 2 || r1 == 2) {  // full buckets: continue those probes (rare)
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void check_union_kernel(UParams P) {
                 }
                 const uint32_t raw = wword(ew, cur - ew_lo);
                 cur++;
-                aux2 = raw & ~EDGE_ALIAS;  // child node
+                aux2 = raw & s.edge_mask;  // child node
                 if (raw & EDGE_ALIAS) {
                     la0 = win(s.vkey, aux2);
                     ln = 1;

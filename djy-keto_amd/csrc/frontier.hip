@@ -197,11 +197,15 @@ __device__ __forceinline__ int64_t tab_insert(unsigned long long *tk, uint32_t m
 // NotMember when no row of the relation holds a subject set.  `esf` (an ES's children:
 // GF_ESCHILD [| GF_ALIAS]) makes an error a goal too, so every decisive occurrence of a scope
 // key is a goal, and goes into the word.  word != 0: spawn it; else `leaf` is the result.
+// `row`: what is known of c's own subject-set row -- ROW_ANY (nothing: its relation's flag
+// decides), ROW_EMPTY (an ES child's edge says so, EDGE_LEAF), ROW_LOAD (load it): an
+// expand-subject of an empty row is NotMember, decided here (oracle u_sub `node_check`).
+enum RowHint : uint32_t { ROW_ANY = 0, ROW_EMPTY = 1, ROW_LOAD = 2 };
 struct Sub {
     uint32_t word, leaf;
 };
 __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t c, uint32_t dc,
-                                         bool skip, uint32_t esf) {
+                                         bool skip, uint32_t esf, uint32_t row = ROW_ANY) {
     if (dc == 0) return Sub{0, M_UNK};
     const NodeInfo ni = t_node_info(T, c);
     const bool err = ri_status(ni.ri) == REL_ERROR;
@@ -215,8 +219,15 @@ __device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, 
     if (ri_rw(ni.ri) || (err && esf)) return Sub{gword(G_IA, dc, 0, (skip ? GF_SKIP : 0u) | esf), 0};
     if (err) return Sub{0, mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16)};
     if (!skip && dc > 1 && !(c & VIRT_BIT) && may_hold(s, q, ni.ri) && member(s, q, c)) return Sub{0, M_IS};
-    if (ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri)) return Sub{gword(G_ES, dc - 1, 0, esf), 0};
+    if (ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri)) {
+        if (row == ROW_EMPTY || (row == ROW_LOAD && ((c & VIRT_BIT) || s.set_row[c].x == s.set_row[c].y))) return Sub{0, M_NOT};
+        return Sub{gword(G_ES, dc - 1, 0, esf), 0};
+    }
     return Sub{0, M_NOT};
+}
+// the row hint of an ES child from its edge
+__device__ __forceinline__ uint32_t edge_row(const DevSnapshot &s, uint32_t raw) {
+    return (s.edge_leaf && (raw & EDGE_LEAF)) ? ROW_EMPTY : ROW_ANY;
 }
 
 // A NOT decided where it is spawned (a malformed NOT, a computed userset that is a leaf, a
@@ -404,9 +415,9 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 Edges it(s, row);
                 bool found = false;  // found-lookahead over every row (traverser.go:73-80, 109-111)
                 for (uint32_t e = 0; it.cur < it.end && !found; e++) {
-                    const uint32_t c = it.next() & ~EDGE_ALIAS;
+                    const uint32_t raw = it.next(), c = raw & s.edge_mask;
                     found = member(s, q, c);
-                    if (e < keep && sub_check(s, T, q, c, d, true, GF_ESCHILD).word) nc++;  // the children that are goals
+                    if (e < keep && sub_check(s, T, q, c, d, true, GF_ESCHILD, edge_row(s, raw)).word) nc++;  // the children that are goals
                 }
                 if (found) {
                     val = M_IS;
@@ -464,7 +475,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                             }
                         } else if (ik == IT_CAND) {  // checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
                             if (dk > 1) {
-                                const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0);
+                                const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0, ROW_LOAD);
                                 if (sb.word) nc++;
                                 else leaf = sb.leaf;
                             }
@@ -480,7 +491,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                                 if (!(ts & VIRT_BIT)) {
                                     Edges et(s, s.set_row[ts]);
                                     for (uint32_t e = 0; et.cur < et.end; e++) {
-                                        const uint32_t pn = et.next() & ~EDGE_ALIAS;
+                                        const uint32_t pn = et.next() & s.edge_mask;
                                         const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), rc >> 16), dk - 1, false, 0);
                                         if (sb.word) nc++;
                                         else if (decisive(sb.leaf)) {
@@ -539,7 +550,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 Edges it(s, row);
                 uint32_t tail = NONE32, e = 0;
                 for (; it.cur < it.end; e++) {
-                    const uint32_t pn = it.next() & ~EDGE_ALIAS;
+                    const uint32_t pn = it.next() & s.edge_mask;
                     const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), xrel), d - 1, false, 0);
                     if (sb.word) nc++;
                     else if (decisive(sb.leaf)) {
@@ -646,10 +657,10 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             Edges it(s, row);
             uint32_t c = cb;
             for (uint32_t e = 0; e < pat; e++) {
-                const uint32_t raw = it.next(), cn = raw & ~EDGE_ALIAS;
+                const uint32_t raw = it.next(), cn = raw & s.edge_mask;
                 const uint32_t esf = GF_ESCHILD | ((raw & EDGE_ALIAS) ? GF_ALIAS : 0u);
                 // checkIsAllowed(c, d, skipDirect) (:161); every child's key is an occurrence
-                const Sub sb = sub_check(s, T, q, cn, d, true, esf);
+                const Sub sb = sub_check(s, T, q, cn, d, true, esf, edge_row(s, raw));
                 if (sb.word) spawn(P, c++, cn, pos, sb.word, sc);
                 if (occ_ok) P.occ[oc + e] = make_uint2(sc, (raw & EDGE_ALIAS) ? s.vkey[cn] : cn);
             }
@@ -672,7 +683,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                     if (ik == IT_CAND) {
                         if (dk > 1) {
                             const uint32_t t = t_sibling(T, node, ni, item.y);
-                            const Sub sb = sub_check(s, T, q, t, dk - 1, true, 0);
+                            const Sub sb = sub_check(s, T, q, t, dk - 1, true, 0, ROW_LOAD);
                             if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
                         }
                     } else if (ik == IT_TTU) {
@@ -683,7 +694,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                                 Edges et(s, s.set_row[ts]);
                                 const uint32_t lim = it == pat ? xrel : NONE32;
                                 for (uint32_t e = 0; et.cur < et.end && e < lim; e++) {
-                                    const uint32_t pn = et.next() & ~EDGE_ALIAS;
+                                    const uint32_t pn = et.next() & s.edge_mask;
                                     const uint32_t t = t_sibling(T, pn, t_node_info(T, pn), rc >> 16);
                                     const Sub sb = sub_check(s, T, q, t, dk - 1, false, 0);
                                     if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
@@ -716,7 +727,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             Edges it(s, row);
             uint32_t c = cb;
             for (uint32_t e = 0; e < pat; e++) {
-                const uint32_t pn = it.next() & ~EDGE_ALIAS;
+                const uint32_t pn = it.next() & s.edge_mask;
                 const uint32_t t = t_sibling(T, pn, t_node_info(T, pn), xrel);
                 const Sub sb = sub_check(s, T, q, t, d - 1, false, 0);
                 if (sb.word) spawn(P, c++, t, pos, sb.word, scope);

@@ -19,6 +19,10 @@ namespace keto {
 
 constexpr uint32_t VIRT_BIT = 0x80000000u;  // frame node id: virtual node
 constexpr uint32_t EDGE_ALIAS = 0x80000000u; // set_dst entry: visited key != node id
+// set_dst entry (snapshots of < 2^30 nodes, DevSnapshot::edge_leaf): the child node holds no
+// subject-set tuple, so its expand-subject finds nothing -- an ES child the frontier engine
+// decides at spawn instead of spawning a goal that reads an empty row
+constexpr uint32_t EDGE_LEAF = 0x40000000u;
 constexpr uint32_t SKEY_SET = 0x80000000u;   // all-row entry: subject set (else subject id)
 constexpr uint32_t NO_SLOT = 0xFFFFu;
 constexpr uint32_t NO_OP = 0xFFFFu;
@@ -76,7 +80,9 @@ struct alignas(16) NsDev {
 struct DevSnapshot {
     const uint4 *set_row;      // [n_nodes] {begin, end, edge 0, edge 1} of each subject-set row (ES + TTU):
                                // one 16 B load; rows of <= 2 edges need no set_dst load
-    const uint32_t *set_dst;   // node | EDGE_ALIAS, shard order within a row
+    const uint32_t *set_dst;   // node | EDGE_ALIAS | EDGE_LEAF, shard order within a row
+    uint32_t edge_mask;        // node bits of a set_dst entry (and of set_row's inline edges)
+    uint32_t edge_leaf;        // set_dst entries carry EDGE_LEAF
     const uint32_t *weight;    // [n_nodes] capped path count below a node (longest-first scheduling)
     const uint32_t *ent_obj;   // [n_entities] entity -> uuid id (NONE32 for phantoms): Expand output
     const uint32_t *slot_rel;  // [total slots] global slot -> relation name id: Expand output

@@ -440,6 +440,15 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
             D.vkey = dv;
         }
     }
+    // ES children without subject-set rows flagged on their edges (EDGE_LEAF); node ids then keep
+    // 30 bits, so only snapshots of fewer than 2^30 nodes carry the flag
+    D.edge_mask = ~EDGE_ALIAS;
+    D.edge_leaf = 0;
+    if (N < (1ull << 30) && ro.n_set) {
+        build::leaf_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, ro.set_row, N);
+        D.edge_mask = ~(EDGE_ALIAS | EDGE_LEAF);
+        D.edge_leaf = 1;
+    }
     // slots whose rows can hold subject sets: an expand-subject of any other slot finds none
     if (total_slots) {
         DevBuf flag(4ull * total_slots);

@@ -960,14 +960,25 @@ static int has_set_rows(const rs_db *db, uint32_t ns, uint32_t rel) {
     return ns < db->n_ns && rel < db->n_relnames && db->ssrel[(size_t)ns * db->n_relnames + rel];
 }
 
+/* a node with at least one subject-set tuple (what an expand-subject of it reads) */
+static int node_has_set_rows(const rs_db *db, uint32_t ns, uint32_t obj, uint32_t rel) {
+    size_t lo, hi;
+    node_rows(db, ns, obj, rel, &lo, &hi);
+    for (size_t i = lo; i < hi; i++)
+        if (ROW(db, i)->kind == 1) return 1;
+    return 0;
+}
+
 /* A sub-check checkIsAllowed(ns:obj#rel, d, skip) shaped when its parent spawns it: a relation
  * with a rewrite is an IA goal; one without is decided on the spot (d <= 0: Unknown; an error;
  * a direct tuple: IsMember) or is just its expand-subject, an ES(d-1) goal -- or NotMember when
- * that could find no subject set.  An ES's children (es_child) are goals also for an error, so
- * every decisive occurrence of a scope key is a goal.  Returns 1 when spawned, 0 for a leaf;
- * *out = the result either way. */
+ * that could find no subject set: no row of the relation holds one, or, with node_check (an
+ * ES's children and an OR's shortcut candidates, whose rows the engine knows at spawn), the
+ * node's own row holds none.  An ES's children (es_child) are goals also for an error, so every
+ * decisive occurrence of a scope key is a goal.  Returns 1 when spawned, 0 for a leaf; *out =
+ * the result either way. */
 static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, int es_child, uint32_t scope,
-                 uint32_t gen, res *out) {
+                 uint32_t gen, res *out, int node_check) {
     const rs_db *db = u->c->db;
     *out = R_UNK;
     if (d <= 0) return 0; /* engine.go:215-220 */
@@ -1001,7 +1012,7 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
         *out = R_IS;
         return 0;
     }
-    if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel)) {
+    if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && (!node_check || node_has_set_rows(db, ns, obj, rel))) {
         if (!u_spawn(u, gen + 1)) return 0;
         *out = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
         return 1;
@@ -1052,7 +1063,7 @@ static res u_ttu(uctx *u, uint32_t ns, uint32_t obj, const rs_ast *a, int d, uin
         const key7 *t = ROW(db, i);
         if (t->kind != 1) continue;
         res r;
-        const int spawned = u_sub(u, t->sns, t->sid, a->computed, d - 1, 0, 0, scope, gen, &r);
+        const int spawned = u_sub(u, t->sns, t->sid, a->computed, d - 1, 0, 0, scope, gen, &r, 0);
         if (u->routed) return R_NOT;
         if (!have && decisive(r)) {
             out = r;
@@ -1087,7 +1098,7 @@ static int u_child(uctx *u, uint32_t ns, uint32_t obj, int ci, int d, int cost, 
         return 1;
     case RS_CSS:
         if (d < 0) return 0;
-        return u_sub(u, ns, obj, ch->rel, d, 0, 0, scope, gen, out);
+        return u_sub(u, ns, obj, ch->rel, d, 0, 0, scope, gen, out, 0);
     case RS_REWRITE:
         if (d - cost <= 0 || !u_spawn(u, gen + 1)) return 0;
         *out = u_rw(u, ns, obj, ci, d - cost, scope, gen + 1);
@@ -1146,7 +1157,7 @@ static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32
             const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
             if (ch->type != RS_CSS) continue;
             res r;
-            const int spawned = u_sub(u, ns, obj, ch->rel, d - 1, 1, 0, scope, gen, &r);
+            const int spawned = u_sub(u, ns, obj, ch->rel, d - 1, 1, 0, scope, gen, &r, 1);
             if (u->routed) return;
             u_fold(r, spawned, 1, out, have, stop);
         }
@@ -1170,7 +1181,7 @@ static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32
                 const key7 *t = ROW(db, i);
                 if (t->kind != 1) continue;
                 res r;
-                const int spawned = u_sub(u, t->sns, t->sid, ch->computed, d - 1, 0, 0, scope, gen, &r);
+                const int spawned = u_sub(u, t->sns, t->sid, ch->computed, d - 1, 0, 0, scope, gen, &r, 0);
                 if (u->routed) return;
                 u_fold(r, spawned, 1, out, have, stop);
             }
@@ -1233,7 +1244,7 @@ static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_
         u_insert(u, scope, vk);
         res r;
         /* checkIsAllowed(c, d, skipDirect) (engine.go:161); its leaves are never decisive */
-        const int spawned = u_sub(u, t->sns, t->sid, t->srel, d, 1, 1, scope, gen, &r);
+        const int spawned = u_sub(u, t->sns, t->sid, t->srel, d, 1, 1, scope, gen, &r, 1);
         if (u->routed) return R_NOT;
         if (spawned && decisive(r)) u->set[u_insert_find(u, scope, vk)].decisive = 1; /* the table may have grown */
         if (!have && decisive(r)) {
