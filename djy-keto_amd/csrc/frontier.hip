@@ -52,6 +52,7 @@ constexpr uint32_t GF_SKIP = 1u << 15, GF_ESCHILD = 1u << 16, GF_ALIAS = 1u << 1
 // gfn.y: children (< 2^24) | reduce op << 24
 enum ReduceOp : uint32_t { R_FIRST = 0, R_AND = 1, R_NOT = 2 };
 constexpr uint32_t NC_MAX = (1u << 24) - 1;
+constexpr uint32_t GFN_CHAIN = 1u << 28;  // gfn.y: an ES goal that ran its one child's expand-subject
 constexpr uint32_t MAX_GEN = 192;
 // The arena is cut into FR_SHARDS slices of `scap` goals; a block spawns into slice
 // blockIdx % FR_SHARDS, so the allocation counters of a generation are FR_SHARDS addresses,
@@ -384,6 +385,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
         uint32_t rop = kind == G_INV ? R_NOT : R_FIRST;
         uint32_t pat = 0;              // per kind: which children (phase B regenerates them)
         uint32_t sc = scope, xrel = 0;
+        bool chain = false;            // G_ES: the one child's expand-subject runs in this goal
         if (live) {
             switch (kind) {
             case G_IA: {  // checkIsAllowed (engine.go:214-249)
@@ -414,10 +416,14 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 if (keep > W) keep = W > 0 ? W - 1 : 0;  // results[:maxWidth-1] (engine.go:141-150)
                 Edges it(s, row);
                 bool found = false;  // found-lookahead over every row (traverser.go:73-80, 109-111)
+                uint32_t cw = 0;
                 for (uint32_t e = 0; it.cur < it.end && !found; e++) {
                     const uint32_t raw = it.next(), c = raw & s.edge_mask;
                     found = member(s, q, c);
-                    if (e < keep && sub_check(s, T, q, c, d, true, GF_ESCHILD, edge_row(s, raw)).word) nc++;  // the children that are goals
+                    if (e < keep) {
+                        cw = sub_check(s, T, q, c, d, true, GF_ESCHILD, edge_row(s, raw)).word;
+                        if (cw) nc++;  // the children that are goals
+                    }
                 }
                 if (found) {
                     val = M_IS;
@@ -425,6 +431,31 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                     break;
                 }
                 if (scope == NONE32) sc = i;  // graph.InitVisited (graph_utils.go:38-43)
+                if (row.y - row.x == 1 && keep == 1 && cw && ((cw >> 12) & 7u) == G_ES) {
+                    // chain (oracle u_es): the one child is an expand-subject goal; run its
+                    // expand-subject here instead -- its key stays an occurrence of the scope,
+                    // its children are this goal's, and this goal's result is the child's
+                    const uint4 rc = s.set_row[row.z & s.edge_mask];
+                    uint32_t kc = rc.y - rc.x;
+                    if (kc > W) kc = W > 0 ? W - 1 : 0;
+                    Edges ic(s, rc);
+                    bool fc = false;
+                    nc = 0;
+                    for (uint32_t e = 0; ic.cur < ic.end && !fc; e++) {
+                        const uint32_t raw = ic.next(), g = raw & s.edge_mask;
+                        fc = member(s, q, g);
+                        if (e < kc && sub_check(s, T, q, g, d - 1, true, GF_ESCHILD, edge_row(s, raw)).word) nc++;
+                    }
+                    if (fc) {  // the child's found-lookahead: IsMember, only the child's key is an occurrence
+                        nc = 0;
+                        kc = 0;
+                    }
+                    chain = true;
+                    pat = kc;
+                    val = fc ? M_IS : (nc ? NONE32 : M_NOT);
+                    xrel = 1;  // phase B writes the occurrences
+                    break;
+                }
                 pat = keep;
                 val = nc ? NONE32 : M_NOT;  // (leaf children are NotMember: they only mark their key)
                 xrel = (!nc && keep) ? 1u : 0u;  // phase B still marks the leaf children's keys
@@ -632,12 +663,12 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             val = M_NOT;
         }
         if (live) {
-            P.gfn[i] = make_uint2(cb, nc | (rop << 24));
+            P.gfn[i] = make_uint2(cb, nc | (rop << 24) | (chain ? GFN_CHAIN : 0u));
             P.gval[i] = val;
         }
         // ---- occurrences: an ES goal's kept children, goals and leaves alike, are the keys it
         // adds to its scope (CheckAndAddVisited, engine.go:157-160): one run of its wave's slice
-        const uint32_t nocc = (live && kind == G_ES && (nc || xrel)) ? pat : 0u;
+        const uint32_t nocc = (live && kind == G_ES && (nc || xrel)) ? pat + (chain ? 1u : 0u) : 0u;
         uint32_t otot = 0;
         const uint32_t ooff = wave_excl(nocc, otot);
         uint32_t obase = 0;
@@ -654,15 +685,24 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             if (pat & 2u) spawn(P, cb + ((pat & 1u) ? 1 : 0), node, pos, gword(G_ES, d - 1), scope);
             break;
         case G_ES: {
-            Edges it(s, row);
+            uint4 r = row;
+            uint32_t o0 = oc, dd = d;
+            if (chain) {  // the one child: its key, then its row's children one level down
+                const uint32_t rawc = row.z, cc = rawc & s.edge_mask;
+                if (occ_ok) P.occ[oc] = make_uint2(sc, (rawc & EDGE_ALIAS) ? s.vkey[cc] : cc);
+                r = s.set_row[cc];
+                o0 = oc + 1;
+                dd = d - 1;
+            }
+            Edges it(s, r);
             uint32_t c = cb;
             for (uint32_t e = 0; e < pat; e++) {
                 const uint32_t raw = it.next(), cn = raw & s.edge_mask;
                 const uint32_t esf = GF_ESCHILD | ((raw & EDGE_ALIAS) ? GF_ALIAS : 0u);
                 // checkIsAllowed(c, d, skipDirect) (:161); every child's key is an occurrence
-                const Sub sb = sub_check(s, T, q, cn, d, true, esf, edge_row(s, raw));
-                if (sb.word) spawn(P, c++, cn, pos, sb.word, sc);
-                if (occ_ok) P.occ[oc + e] = make_uint2(sc, (raw & EDGE_ALIAS) ? s.vkey[cn] : cn);
+                const Sub sb = sub_check(s, T, q, cn, dd, true, esf, edge_row(s, raw));
+                if (sb.word && nc) spawn(P, c++, cn, pos, sb.word, sc);
+                if (occ_ok) P.occ[o0 + e] = make_uint2(sc, (raw & EDGE_ALIAS) ? s.vkey[cn] : cn);
             }
             break;
         }
@@ -758,6 +798,18 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
 #endif
 }
 
+// a decisive occurrence of (scope, key): into the decisive table and its bit filter
+__device__ __forceinline__ void dec_insert(const FrontierParams &P, uint32_t scope, uint32_t vk, uint32_t pos) {
+    const unsigned long long key = tab_key(P.epoch, scope, vk);
+    const uint32_t h = tab_hash(key, P.dmask);
+    bool rep = false;
+    const int64_t at = tab_insert(P.dkeys, P.dmask, P.epoch, key, h, atomicCAS(&P.dkeys[h], 0ull, key), &rep);
+    if (at < 0) route(P, pos);  // crowded: the DFS interpreter takes the query
+    else if (!rep) P.dcnt[at] = 0;
+    const uint32_t b = dbit(key);
+    atomicOr(&P.dbits[b >> 5], 1u << (b & 31u));
+}
+
 // One generation, bottom-up: each goal reduces its children in add order (checkgroup H0,
 // binop.go, rewrites.go:183-199); a decisive occurrence of a repeated scope key routes the
 // query; generation 0 writes the decisions.  Every goal of the generation was expanded in
@@ -772,7 +824,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         const uint32_t i = gen_goal(P, gm, j);
         const uint2 fn = P.gfn[i];
         uint32_t val = P.gval[i];
-        const uint32_t nc = fn.y & NC_MAX, rop = fn.y >> 24;
+        const uint32_t nc = fn.y & NC_MAX, rop = (fn.y >> 24) & 3u;
         if (nc) {
             uint32_t res = NONE32;
             for (uint32_t c = fn.x; c < fn.x + nc; c++) {
@@ -798,15 +850,11 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         }
         if (k > 0 && decisive(val)) {  // a decisive ES child: its key goes into the decisive table
             const uint4 g = P.g0[i];
-            if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD)) {  // (RW / TTU / INV hold an op there)
-                const unsigned long long key = tab_key(P.epoch, g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x);
-                const uint32_t h = tab_hash(key, P.dmask);
-                bool rep = false;
-                const int64_t at = tab_insert(P.dkeys, P.dmask, P.epoch, key, h, atomicCAS(&P.dkeys[h], 0ull, key), &rep);
-                if (at < 0) route(P, g.y);  // crowded: the DFS interpreter takes the query
-                else if (!rep) P.dcnt[at] = 0;
-                const uint32_t b = dbit(key);
-                atomicOr(&P.dbits[b >> 5], 1u << (b & 31u));
+            if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD))  // (RW / TTU / INV hold an op there)
+                dec_insert(P, g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x, g.y);
+            if (fn.y & GFN_CHAIN) {  // the child whose expand-subject it ran is decisive too
+                const uint32_t rawc = s.set_row[g.x].z, cc = rawc & s.edge_mask;
+                dec_insert(P, g.w == NONE32 ? i : g.w, (rawc & EDGE_ALIAS) ? s.vkey[cc] : cc, g.y);
             }
         }
         if (k == 0) {  // generation 0: one goal per query position

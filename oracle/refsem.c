@@ -953,7 +953,7 @@ static int u_spawn(uctx *u, uint32_t gen) {
 
 static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip, uint32_t scope, uint32_t gen);
 static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen);
-static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen);
+static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen, int chain);
 
 /* a relation whose rows can hold subject sets: some tuple of (ns, rel) has one (per snapshot) */
 static int has_set_rows(const rs_db *db, uint32_t ns, uint32_t rel) {
@@ -1014,7 +1014,7 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
     }
     if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && (!node_check || node_has_set_rows(db, ns, obj, rel))) {
         if (!u_spawn(u, gen + 1)) return 0;
-        *out = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
+        *out = u_es(u, ns, obj, rel, d - 1, scope, gen + 1, 1);
         return 1;
     }
     *out = R_NOT;
@@ -1220,20 +1220,48 @@ static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scop
     return out;
 }
 
-static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen) {
+/* would u_sub(ns:obj#rel, d, skipDirect, es_child, node_check) spawn an ES goal (not an IA
+ * goal, not a leaf)? */
+static int u_es_child_is_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d) {
+    const rs_db *db = u->c->db;
+    if (d <= 0) return 0;
+    int err;
+    const int ri = ast_relation_for(db, ns, rel, &err);
+    if (err || (ri >= 0 && db->rels[ri].rewrite >= 0)) return 0; /* an IA goal */
+    const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
+    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && node_has_set_rows(db, ns, obj, rel);
+}
+
+/* chain: an expand-subject whose row holds exactly one subject set, kept, that would be an ES
+ * goal runs that child's expand-subject itself (one step; the child's own children are goals
+ * as usual): the child's key is still an occurrence of the scope, its children are this goal's,
+ * one generation earlier, and no goal is spawned for it.  Its result is the child's: the first
+ * decisive of a one-child group is that child's result when decisive, else NotMember.
+ * (csrc/frontier.hip G_ES "chain") */
+static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen, int chain) {
     const rs_db *db = u->c->db;
     size_t lo, hi;
     node_rows(db, ns, obj, rel, &lo, &hi);
     size_t nres = 0;
+    const key7 *only = NULL;
     for (size_t i = lo; i < hi; i++) {
         const key7 *t = ROW(db, i);
         if (t->kind != 1) continue;
         nres++;
+        only = t;
         if (exists(u->c, t->sns, t->sid, t->srel)) return R_IS;
     }
     size_t keep = nres;
     if ((long)nres > (long)db->max_width) keep = db->max_width > 0 ? (size_t)(db->max_width - 1) : 0;
     if (scope == U_NONE) scope = u->scopes++;
+    if (chain && nres == 1 && keep == 1 && u_es_child_is_es(u, only->sns, only->sid, only->srel, d)) {
+        const uint64_t vk = vkey(db, only->sns, only->sid, only->srel);
+        u_insert(u, scope, vk);
+        const res r = u_es(u, only->sns, only->sid, only->srel, d - 1, scope, gen, 0);
+        if (u->routed) return R_NOT;
+        if (decisive(r)) u->set[u_insert_find(u, scope, vk)].decisive = 1;
+        return decisive(r) ? r : R_NOT;
+    }
     res out = R_NOT;
     int have = 0;
     for (size_t i = lo; i < hi && keep; i++) {
@@ -1270,7 +1298,7 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
     if (has_rewrite && u_spawn(u, gen + 1)) rr = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
     const int direct_is = (!db->strict || !has_rewrite) && !skip && d - 1 > 0 && exists(u->c, ns, obj, rel);
     if (can_ss && !direct_is && d - 1 > 0 && has_set_rows(db, ns, rel) && u_spawn(u, gen + 1))
-        er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1);
+        er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1, 1);
     if (decisive(rr)) return rr;
     if (direct_is) return R_IS;
     if (decisive(er)) return er;
