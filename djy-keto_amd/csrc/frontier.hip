@@ -28,7 +28,7 @@
 //   gfn[i]  = {first child, children | reduce op}    8 B, written by fr_expand
 //   gval[i] = value (or the partial fr_reduce folds)  4 B, fr_expand, then fr_reduce
 // word: bits 0-11 rest depth, 12-14 kind, 15 skip_direct, 16-31 rewrite op (RW / TTU / INV);
-// an IA goal an ES spawned keeps bit 16 (its key went into the scope table) and bit 17 (the
+// an IA goal an ES spawned keeps bit 16 (its key is an occurrence of the scope) and bit 17 (the
 // key is the node's visited alias).
 #include <hip/hip_runtime.h>
 
@@ -360,12 +360,54 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
 #ifdef KETO_FR_PROF
     unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef KETO_FR_RG_BUCKETS
+#define KETO_FR_RG_BUCKETS 4
+#endif
+#ifndef KETO_FR_NOREGROUP
+    constexpr uint32_t NB = KETO_FR_RG_BUCKETS;  // goal classes; dead lanes are one more
+    __shared__ uint4 rg_g[256];
+    __shared__ uint32_t rg_i[256], rg_n[4][NB + 1];
+#endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
         // goals of queries routed meanwhile still run (rare); they can no longer spawn
-        const bool live = j < cnt;
-        const uint32_t i = live ? gen_goal(P, gm, j) : 0u;
-        const uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
+        bool live = j < cnt;
+        uint32_t i = live ? gen_goal(P, gm, j) : 0u;
+        uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
+#ifndef KETO_FR_NOREGROUP
+        {   // Block regroup: the block's goals ordered by class -- expand-subjects, ORs, ANDs, the
+            // rest, then dead lanes; batch order within a class -- so that a wave runs one class's
+            // code instead of several under divergence.
+            const uint32_t wv = threadIdx.x >> 6, ln = __lane_id(), nw = (blockDim.x + 63) >> 6;
+            uint32_t cls = NB;
+            if (live) {
+                const uint32_t kd = (g.z >> 12) & 7u;
+                if (kd == G_ES) cls = 0;
+                else if (NB > 2 && kd == G_RW) cls = ((T.ops[g.z >> 16].type_kind >> 8) & 0xFFu) == OPK_OR ? 1u : 2u;
+                else cls = NB - 1;
+            }
+            uint32_t rank = 0;
+            for (uint32_t c = 0; c <= NB; c++) {
+                const unsigned long long b = __ballot(cls == c);
+                if (c == cls) rank = (uint32_t)__popcll(b & ((1ull << ln) - 1ull));
+                if (ln == 0) rg_n[wv][c] = (uint32_t)__popcll(b);
+            }
+            __syncthreads();
+            uint32_t slot = rank, n_live = 0;
+            for (uint32_t c = 0; c <= NB; c++)
+                for (uint32_t t = 0; t < nw; t++) {
+                    const uint32_t m = rg_n[t][c];
+                    if (c < cls || (c == cls && t < wv)) slot += m;
+                    if (c < NB) n_live += m;
+                }
+            rg_g[slot] = g;
+            rg_i[slot] = i;
+            __syncthreads();
+            g = rg_g[threadIdx.x];
+            i = rg_i[threadIdx.x];
+            live = threadIdx.x < n_live;
+        }
+#endif
         const uint32_t node = g.x, pos = g.y, w = g.z, scope = g.w;
         const uint32_t d = w & GD_MAX, kind = (w >> 12) & 7u, op = w >> 16;
         const uint32_t qg = live ? P.qgoals[pos] : 0u;
