@@ -50,7 +50,7 @@ enum GoalKind : uint32_t { G_IA = 0, G_ES = 1, G_RW = 2, G_TTU = 3, G_INV = 4, G
 constexpr uint32_t GD_MAX = 0xFFFu;
 constexpr uint32_t GF_SKIP = 1u << 15, GF_ESCHILD = 1u << 16, GF_ALIAS = 1u << 17;
 // gfn.y: children (< 2^24) | reduce op << 24
-enum ReduceOp : uint32_t { R_FIRST = 0, R_AND = 1, R_NOT = 2 };
+enum ReduceOp : uint32_t { R_FIRST = 0, R_AND = 1, R_NOT = 2, R_FIRST_AND = 3 };  // (R_FIRST_AND: and_merge)
 constexpr uint32_t NC_MAX = (1u << 24) - 1;
 constexpr uint32_t GFN_CHAIN = 1u << 28;  // gfn.y: an ES goal that ran its one child's expand-subject
 constexpr uint32_t MAX_GEN = 192;
@@ -231,6 +231,9 @@ __device__ __forceinline__ uint32_t edge_row(const DevSnapshot &s, uint32_t raw)
     return (s.edge_leaf && (raw & EDGE_LEAF)) ? ROW_EMPTY : ROW_ANY;
 }
 
+// AND maps a non-member (an error kept) to NotMember (binop.go:52-54)
+__device__ __forceinline__ uint32_t and_map(uint32_t x) { return ((x >> 8) != 0 || (x & 3u) != M_IS) ? ((x & ~3u) | M_NOT) : x; }
+
 // A NOT decided where it is spawned (a malformed NOT, a computed userset that is a leaf, a
 // rewrite at rest depth 0) is folded into its parent: its result, or NONE32 when it must be an
 // INV goal (oracle u_inv_folds; the G_INV case of fr_expand evaluates the same way)
@@ -249,6 +252,38 @@ __device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables 
     if (leaf == NONE32) return NONE32;
     const uint32_t m = leaf & 3u;  // NOT: IsMember <-> NotMember, Unknown / errors kept (rewrites.go:183-199)
     return m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
+}
+
+// An AND at rest depth d > 1 whose children are one nested OR (a goal at d-1, rewrites.go:118)
+// and leaves that are all IsMember without an error is that OR mapped through AND (and_map; the
+// OR never yields a bare Unknown): the AND's goal runs the OR's items itself, reduced by
+// R_FIRST_AND, and no goal is spawned for the OR (oracle u_and_merge).  Returns the OR's op,
+// NONE32 when the AND is not of that form.  One goal and one generation less per level of
+// `(a | b | parents.traverse(...)) & !banned`.
+__device__ __forceinline__ uint32_t and_merge(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
+                                              const NodeInfo &ni, const Op &o, uint32_t d) {
+#ifdef KETO_FR_NOMERGE  // measurement builds only (tools/ab)
+    return NONE32;
+#endif
+    if (d <= 1) return NONE32;
+    uint32_t orop = NONE32;
+    for (uint32_t c = 0; c < o.child_count; c++) {
+        const uint32_t ci = T.op_children[o.child_begin + c];
+        const Op ch = T.ops[ci];
+        const uint32_t ct = ch.type_kind & 0xFFu;
+        if (ct == OP_REWRITE) {
+            if (orop != NONE32 || ((ch.type_kind >> 8) & 0xFFu) != OPK_OR) return NONE32;
+            orop = ci;
+        } else if (ct == OP_CSS) {
+            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
+            if (sb.word || sb.leaf != M_IS) return NONE32;
+        } else if (ct == OP_INVERT) {
+            if (inv_leaf(s, T, q, node, ci, d) != M_IS) return NONE32;
+        } else {
+            return NONE32;  // a tuple-to-userset is always a goal
+        }
+    }
+    return orop;
 }
 
 
@@ -361,7 +396,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
     unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
 #endif
 #ifndef KETO_FR_RG_BUCKETS
-#define KETO_FR_RG_BUCKETS 4
+#define KETO_FR_RG_BUCKETS 3
 #endif
 #ifndef KETO_FR_NOREGROUP
     constexpr uint32_t NB = KETO_FR_RG_BUCKETS;  // goal classes; dead lanes are one more
@@ -375,7 +410,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
         uint32_t i = live ? gen_goal(P, gm, j) : 0u;
         uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
 #ifndef KETO_FR_NOREGROUP
-        {   // Block regroup: the block's goals ordered by class -- expand-subjects, ORs, ANDs, the
+        {   // Block regroup: the block's goals ordered by class -- expand-subjects, rewrites, the
             // rest, then dead lanes; batch order within a class -- so that a wave runs one class's
             // code instead of several under divergence.
             const uint32_t wv = threadIdx.x >> 6, ln = __lane_id(), nw = (blockDim.x + 63) >> 6;
@@ -383,7 +418,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             if (live) {
                 const uint32_t kd = (g.z >> 12) & 7u;
                 if (kd == G_ES) cls = 0;
-                else if (NB > 2 && kd == G_RW) cls = ((T.ops[g.z >> 16].type_kind >> 8) & 0xFFu) == OPK_OR ? 1u : 2u;
+                else if (NB > 2 && kd == G_RW) cls = 1;  // (an AND over one OR runs the OR's code: and_merge)
                 else cls = NB - 1;
             }
             uint32_t rank = 0;
@@ -518,17 +553,24 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                 const NodeInfo ni = t_node_info(T, node);
                 uint32_t tail = NONE32;
                 xrel = NONE32;  // OR: parents of the stopping TTU item phase B spawns (NONE32: all)
-                if (is_or) {  // the flattened items (layout.hpp IT_*), nested ORs spliced in
-                    const uint32_t oi = T.op_items[op], end = (oi & 0xFFFFu) + (oi >> 16);
+                uint32_t xop = op, xd = d;  // the OR whose items run here (an and_merge: the AND's OR)
+                const uint32_t mo = is_or ? NONE32 : and_merge(s, T, q, node, ni, o, d);
+                if (mo != NONE32) {
+                    xop = mo;
+                    xd = d - 1;
+                    rop = R_FIRST_AND;
+                }
+                if (is_or || mo != NONE32) {  // the flattened items (layout.hpp IT_*), nested ORs spliced in
+                    const uint32_t oi = T.op_items[xop], end = (oi & 0xFFFFu) + (oi >> 16);
                     uint32_t it = oi & 0xFFFFu;
                     while (it < end) {
                         const uint2 item = T.or_items[it];
                         const uint32_t ik = it_kind(item.x), kk = it_k(item.x);
                         if (ik == IT_NEST) {  // a nested OR at rest depth d - k <= 0 is Unknown (:39-42)
-                            it = d <= kk ? it_end(item.x) : it + 1;
+                            it = xd <= kk ? it_end(item.x) : it + 1;
                             continue;
                         }
-                        const uint32_t dk = d - kk;
+                        const uint32_t dk = xd - kk;
                         uint32_t leaf = NONE32;
                         if (ik == IT_SHORT) {  // the IN shortcut (rewrites.go:62-92, traverser.go:123-191)
                             const Op x = T.ops[item.y];
@@ -612,8 +654,9 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
                     }
                     pat = kend;
                 }
-                if (nc == 0) val = tail != NONE32 ? tail : ((!is_or && o.child_count > 0) ? M_IS : M_NOT);
+                if (nc == 0) val = tail != NONE32 ? tail : ((!is_or && mo == NONE32 && o.child_count > 0) ? M_IS : M_NOT);
                 else val = tail;
+                if (mo != NONE32 && nc == 0) val = and_map(val);
                 break;
             }
             case G_TTU: {  // checkTupleToSubjectSet (rewrites.go:242-293)
@@ -752,16 +795,19 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             const Op o = T.ops[op];
             const NodeInfo ni = t_node_info(T, node);
             uint32_t c = cb;
-            if (((o.type_kind >> 8) & 0xFFu) == OPK_OR) {
-                uint32_t it = T.op_items[op] & 0xFFFFu;
+            const bool is_or = ((o.type_kind >> 8) & 0xFFu) == OPK_OR;
+            const uint32_t mo = (is_or || rop != R_FIRST_AND) ? NONE32 : and_merge(s, T, q, node, ni, o, d);
+            if (is_or || mo != NONE32) {
+                const uint32_t xop = is_or ? op : mo, xd = is_or ? d : d - 1;
+                uint32_t it = T.op_items[xop] & 0xFFFFu;
                 while (it < pat || (it == pat && xrel != NONE32)) {  // (+ the stopping TTU item's parents)
                     const uint2 item = T.or_items[it];
                     const uint32_t ik = it_kind(item.x), kk = it_k(item.x);
                     if (ik == IT_NEST) {
-                        it = d <= kk ? it_end(item.x) : it + 1;
+                        it = xd <= kk ? it_end(item.x) : it + 1;
                         continue;
                     }
-                    const uint32_t dk = d - kk;
+                    const uint32_t dk = xd - kk;
                     if (ik == IT_CAND) {
                         if (dk > 1) {
                             const uint32_t t = t_sibling(T, node, ni, item.y);
@@ -871,7 +917,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
             uint32_t res = NONE32;
             for (uint32_t c = fn.x; c < fn.x + nc; c++) {
                 const uint32_t cv = P.gval[c];
-                if (rop == R_FIRST) {  // first Err / IsMember
+                if (rop == R_FIRST || rop == R_FIRST_AND) {  // first Err / IsMember
                     if (decisive(cv)) {
                         res = cv;
                         break;
@@ -887,6 +933,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
                 }
             }
             if (res == NONE32) res = val != NONE32 ? val : (rop == R_AND ? M_IS : M_NOT);
+            if (rop == R_FIRST_AND) res = and_map(res);  // an AND over its merged OR
             val = res;
             P.gval[i] = val;
         }

@@ -1194,6 +1194,37 @@ static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32
     }
 }
 
+/* An AND at rest depth d > 1 whose children are one nested OR (a goal at d-1, rewrites.go:118)
+ * and leaves that are all IsMember without an error: the OR's index, else -1.  Such an AND is
+ * its OR mapped through AND -- a non-member (errors kept) becomes NotMember -- so its goal runs
+ * the OR's items itself and no goal is spawned for the OR (csrc/frontier.hip and_merge). */
+static int u_and_merge(uctx *u, uint32_t ns, uint32_t obj, int ai, int d) {
+    const rs_db *db = u->c->db;
+    const rs_ast *a = &db->ast[ai];
+    if (a->op != RS_OP_AND || d <= 1) return -1;
+    int orc = -1;
+    for (int k = 0; k < a->child_count; k++) {
+        const int ci = db->children[a->child_begin + k];
+        const rs_ast *ch = &db->ast[ci];
+        if (ch->type == RS_REWRITE) {
+            if (orc >= 0 || ch->op != RS_OP_OR) return -1;
+            orc = ci;
+        } else if (ch->type == RS_CSS) {
+            if (u_sub_spawns(u, ns, obj, ch->rel, d, 0, 0)) return -1;
+            int err;
+            (void)ast_relation_for(db, ns, ch->rel, &err);
+            if (err || !(d - 1 > 0 && exists(u->c, ns, obj, ch->rel))) return -1; /* not a direct IsMember */
+        } else if (ch->type == RS_INVERT) {
+            if (!u_inv_folds(u, ns, obj, ci, d)) return -1;
+            const res r = u_inv(u, ns, obj, ci, d, U_NONE, 0);
+            if (r.err || r.m != RS_IS_MEMBER) return -1;
+        } else {
+            return -1; /* a tuple-to-userset is always a goal */
+        }
+    }
+    return orc;
+}
+
 static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen) {
     const rs_db *db = u->c->db;
     const rs_ast *a = &db->ast[ai];
@@ -1204,6 +1235,14 @@ static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scop
     res out = R_NOT;
     int have = 0; /* the group's result is fixed (by a child in add order) */
     int stop = 0; /* a leaf decided it: later children are never spawned */
+    const int orc = u_and_merge(u, ns, obj, ai, d);
+    if (orc >= 0) {
+        u_or_items(u, ns, obj, orc, d - 1, scope, gen, &out, &have, &stop);
+        if (u->routed) return R_NOT;
+        res x = have ? out : R_NOT;
+        if (x.err || x.m != RS_IS_MEMBER) x.m = RS_NOT_MEMBER;
+        return x;
+    }
     if (a->op == RS_OP_OR) {
         u_or_items(u, ns, obj, ai, d, scope, gen, &out, &have, &stop);
         if (u->routed) return R_NOT;

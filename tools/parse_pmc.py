@@ -23,9 +23,14 @@ def per_launch(counter, sub):
         # the frontier path: every kernel a batch's timed region launches (fr_init, the generations'
         # fr_expand / fr_reduce, the DFS interpreter on routed queries), per batch (fr_init count)
         batches = sum(1 for k in vals if "fr_init" in k[1])
-        tot = sum(v for k, v in vals.items() if any(x in k[1] for x in ("fr_init", "fr_expand", "fr_reduce"))
+        tot = sum(v for k, v in vals.items() if any(x in k[1] for x in ("fr_init", "fr_expand", "fr_reduce", "fr_repeat"))
                   or ("check_kernel<false" in k[1]))
-        return "frontier check path (fr_init + fr_expand + fr_reduce + DFS on routed)", batches, [tot / max(1, batches)]
+        # request resolution is in the timed region too; the counted (DFS) batch adds one more launch
+        res = [v for k, v in vals.items() if "resolve_kernel" in k[1]]
+        if res:
+            tot += batches * sum(res) / len(res)
+        return ("frontier check path (resolve_kernel + fr_init + fr_expand + fr_reduce + fr_repeat + DFS on routed)",
+                batches, [tot / max(1, batches)])
     # dominant kernel: the uncounted interpreter (<false, ...>) at its largest grid (tier 0)
     cands = [(k, v) for k, v in vals.items() if "check" in k[1] and "<false" in k[1]]
     gmax = max(k[2] for k, _ in cands)
