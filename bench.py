@@ -537,7 +537,8 @@ def main():
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "check path: frontier generations (fr_init, fr_expand, fr_reduce) + DFS on routed",
+                     "kernel": "check path: resolve_kernel, frontier generations (fr_init, fr_expand, fr_reduce, fr_repeat) "
+                               "+ DFS on routed",
                      "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": int(bytes_t0),
                      "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (BASELINE.md)",

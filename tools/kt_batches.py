@@ -2,12 +2,13 @@
 .db or kernel_trace.csv), to set beside bench.py's roofline.kernel_ms (HIP events around the
 check path of every timed batch).
 
-A batch of the frontier path is fr_init, then one fr_expand per generation, one fr_reduce per
-generation (deepest first) and the DFS interpreter on any routed queries.  Batches are split at
-each fr_init whose grid covers `--n` queries (bench.py's 2^20: the latency probe's smaller
-batches are left out).  Reported per batch: the summed kernel durations ("busy") and the span
-from fr_init's start to the last kernel's end before the next batch ("span", what the HIP events
-see).   usage: kt_batches.py <db-or-csv> [--n 1048576] [--out summary.csv]"""
+A batch of the frontier path is the request resolution pass, fr_init, one fr_expand per
+generation, one fr_reduce per generation (deepest first) with fr_repeat before generation 0, and
+the DFS interpreter on any routed queries.  Batches are split at each resolve pass whose grid
+covers `--n` queries and that an fr_init follows (bench.py's 2^20: the latency probe's smaller
+batches and the counted DFS batch are left out).  Reported per batch: the summed kernel
+durations ("busy") and the span from the resolve pass's start to the last kernel's end before
+the next batch ("span", what the HIP events see).   usage: kt_batches.py <db-or-csv> [--n 1048576] [--out summary.csv]"""
 import argparse
 import csv
 import sqlite3
@@ -29,7 +30,7 @@ else:
         g = int(r["Grid_Size_X"] if "Grid_Size_X" in r else r["Grid_Size"])
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], g))
 rows.sort()
-PATH = ("fr_init", "fr_expand", "fr_reduce", "check_kernel<false")
+PATH = ("fr_init", "fr_expand", "fr_reduce", "fr_repeat", "check_kernel<false")
 
 
 def short(n):
@@ -38,19 +39,26 @@ def short(n):
 
 batches = []  # list of lists of rows
 cur = None
+pending = None  # a full-size resolve pass, until the kernel after it shows which path it starts
 for r in rows:
     nm = r[2]
+    if "resolve_kernel" in nm:  # the next batch's resolve pass: this batch is over
+        cur = None
+        pending = r if r[3] >= a.n else None
+        continue
     if "fr_init" in nm:
-        cur = [r] if r[3] >= a.n else None
+        cur = ([pending, r] if pending else [r]) if r[3] >= a.n else None
+        pending = None
         if cur is not None:
             batches.append(cur)
         continue
+    if "__amd_rocclr" in nm:  # (the frontier's control memsets between resolve and fr_init)
+        continue
+    pending = None
     if cur is None:
         continue
     if any(p in nm for p in PATH):
         cur.append(r)
-    elif "resolve_kernel" in nm:  # the next batch's resolve pass: this batch is over
-        cur = None
 
 per_kernel = defaultdict(list)
 busy, span, gens = [], [], []
