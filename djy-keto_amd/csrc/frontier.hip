@@ -74,6 +74,7 @@ struct FrontierParams {
     uint4 *g0;
     uint2 *gfn;
     uint32_t *gval;
+    uint32_t *gsub;              // goals below each goal (fr_reduce): the root's is the query's count
     uint32_t cap, scap;          // arena goals, goals per slice
     uint32_t *gbase, *gcount;    // [FR_SHARDS][GEN_STRIDE]: slice-local base and count per generation
     uint32_t gen;
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
     const uint4 r0 = P.start[2 * (size_t)i];
     const uint32_t d = r0.z & 0xFFFFu;
     P.g0[(i / chunk) * P.scap + i % chunk] = make_uint4(r0.x, i, gword(G_IA, d), NONE32);
-    P.qgoals[i] = d > GD_MAX ? QG_ROUTED : 1u;
+    P.qgoals[i] = d > GD_MAX ? QG_ROUTED : 0u;
     P.qroute[i] = d > GD_MAX ? 1u : 0u;
 }
 
@@ -711,28 +712,15 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
             nc = 0;
         }
         FR_MARK(1);
-        // ---- budget and generation cap.  The goal count read when the goal started is the
-        // check (fr_reduce re-checks the final count); the count is raised without waiting, one
-        // atomic per run of lanes holding goals of one query (siblings are contiguous) --------------
+        // ---- budget and generation cap.  A query's goal count is its root's subtree count, summed
+        // bottom-up by fr_reduce (gsub) without atomics, and compared with the budget at
+        // generation 0; here a routed query (qgoals saturated by route) stops spawning, as does
+        // a goal with more children than the budget or at the last generation.  A query past its
+        // budget spawns on meanwhile (bounded by MAX_GEN and its arena slice) -----------------------
         const uint32_t lane = __lane_id();
-        if (nc && (qg > P.budget || last)) {
+        if (nc && (qg > P.budget || nc > P.budget || last)) {
             route(P, pos);
             nc = 0;
-        }
-        {
-            const uint32_t key = live ? pos : NONE32;
-            const uint32_t prev = __shfl_up(key, 1);
-            const unsigned long long heads = __ballot(lane == 0 || prev != key);
-            const uint32_t wl = (uint32_t)warpSize - 1u;  // last lane of the wave
-            const uint32_t hl = 63u - (uint32_t)__clzll((long long)(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
-            uint32_t x = nc;  // segmented inclusive sum within the run
-            for (uint32_t o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o);
-                if (lane >= o && lane - o >= hl) x += y;
-            }
-            const unsigned long long after = lane == 63 ? 0ull : (heads >> (lane + 1));
-            const uint32_t tl = after ? lane + (uint32_t)__ffsll((long long)after) - 1u : wl;
-            if (lane == tl && x) atomicAdd(&P.qgoals[pos], x);
         }
         FR_MARK(2);
         // ---- allocation: one atomic per wave, on the wave's slice counter -------------------------
@@ -913,7 +901,9 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         const uint2 fn = P.gfn[i];
         uint32_t val = P.gval[i];
         const uint32_t nc = fn.y & NC_MAX, rop = (fn.y >> 24) & 3u;
+        uint32_t sub = nc;  // goals below this one (the budget's count)
         if (nc) {
+            for (uint32_t c = fn.x; c < fn.x + nc; c++) sub += P.gsub[c];
             uint32_t res = NONE32;
             for (uint32_t c = fn.x; c < fn.x + nc; c++) {
                 const uint32_t cv = P.gval[c];
@@ -937,6 +927,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
             val = res;
             P.gval[i] = val;
         }
+        if (k > 0) P.gsub[i] = sub;
         if (k > 0 && decisive(val)) {  // a decisive ES child: its key goes into the decisive table
             const uint4 g = P.g0[i];
             if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD))  // (RW / TTU / INV hold an op there)
@@ -948,7 +939,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         }
         if (k == 0) {  // generation 0: one goal per query position
             const uint32_t pos = P.g0[i].y;
-            if (P.qroute[pos] || P.qgoals[pos] > P.budget) {
+            if (P.qroute[pos] || 1u + sub > P.budget) {
                 P.fb_list[atomicAdd(P.fb_count, 1u)] = pos;
                 continue;
             }
@@ -1037,7 +1028,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     while (dcap < 4 * ncap) dcap <<= 1;
     const uint64_t ocap = cap / 2 / FR_SHARDS;  // per slice
     const size_t ctrl = al256(FR_CTRL_BYTES);
-    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 4) + al256(dcap * 12) +
+    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + 2 * al256(cap * 4) + al256(dcap * 12) +
                          al256(ocap * FR_SHARDS * 8) + (1u << DBITS_LOG2) / 8;
     KETO_HIP(hipMalloc(&f.mem, bytes));
     char *p = static_cast<char *>(f.mem);
@@ -1054,6 +1045,8 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     f.gfn = reinterpret_cast<uint2 *>(p);
     p += al256(cap * 8);
     f.gval = reinterpret_cast<uint32_t *>(p);
+    p += al256(cap * 4);
+    f.gsub = reinterpret_cast<uint32_t *>(p);
     p += al256(cap * 4);
     f.dkeys = reinterpret_cast<unsigned long long *>(p);
     f.dcnt = reinterpret_cast<uint32_t *>(f.dkeys + dcap);
@@ -1088,6 +1081,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.g0 = f.g0;
     P.gfn = f.gfn;
     P.gval = f.gval;
+    P.gsub = f.gsub;
     P.cap = (uint32_t)f.cap;
     P.scap = (uint32_t)(f.cap / FR_SHARDS);
     P.gbase = gbase;
