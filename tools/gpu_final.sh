@@ -16,7 +16,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_final -o kt 
   -- python3 bench.py --no-cpu-baseline --serve-clients 0 --latency-iters 0 > gpurun_out/kt_final.log 2>&1 || { echo "kernel trace failed"; exit 1; }
 f=$(find gpurun_out/kt_final -name "*kernel_trace.csv" | head -1)
 python3 tools/kt_summary.py "$f" gpurun_out/${ROUND}_c4_kernel_grid_stats.csv > /dev/null
-python3 tools/kt_batches.py "$f" gpurun_out/${ROUND}_c4_batch_stats.csv 2>&1 | tail -3 || true
+python3 tools/kt_batches.py "$f" --out gpurun_out/${ROUND}_c4_batch_stats.csv | tail -6
 cp $(find gpurun_out/kt_final -name "*kernel_stats.csv" | head -1) gpurun_out/${ROUND}_c4_kernel_stats.csv
 bash tools/pmc_traffic.sh $ROUND c4 > gpurun_out/pmc.log 2>&1 || { echo "pmc failed"; tail -5 gpurun_out/pmc.log; exit 1; }
 tail -1 gpurun_out/pmc.log
