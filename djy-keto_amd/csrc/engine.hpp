@@ -126,7 +126,7 @@ struct FrontierScratch {
     uint32_t *qgoals = nullptr, *qroute = nullptr, *fb_list = nullptr, *fb_count = nullptr;
     uint4 *g0 = nullptr;
     uint2 *gfn = nullptr;
-    uint32_t *gval = nullptr, *gsub = nullptr;
+    uint2 *gvs = nullptr;  // {value, goals below} per goal
     unsigned long long *dkeys = nullptr;
     uint32_t *dcnt = nullptr, *occ_count = nullptr, *dbits = nullptr;
     uint2 *occ = nullptr;

@@ -26,7 +26,8 @@
 // Goal records (HBM, one arena per stream, structure of arrays; 28 bytes per goal):
 //   g0[i]   = {node, query position, word, scope}   16 B, written by the parent at spawn
 //   gfn[i]  = {first child, children | reduce op}    8 B, written by fr_expand
-//   gval[i] = value (or the partial fr_reduce folds)  4 B, fr_expand, then fr_reduce
+//   gvs[i]  = {value (or the partial fr_reduce folds), goals below it}  8 B, fr_expand (value),
+//             then fr_reduce (both)
 // word: bits 0-11 rest depth, 12-14 kind, 15 skip_direct, 16-31 rewrite op (RW / TTU / INV);
 // an IA goal an ES spawned keeps bit 16 (its key is an occurrence of the scope) and bit 17 (the
 // key is the node's visited alias).
@@ -73,8 +74,7 @@ struct FrontierParams {
     uint32_t n;
     uint4 *g0;
     uint2 *gfn;
-    uint32_t *gval;
-    uint32_t *gsub;              // goals below each goal (fr_reduce): the root's is the query's count
+    uint2 *gvs;                  // {value, goals below (fr_reduce): the root's is the query's count}
     uint32_t cap, scap;          // arena goals, goals per slice
     uint32_t *gbase, *gcount;    // [FR_SHARDS][GEN_STRIDE]: slice-local base and count per generation
     uint32_t gen;
@@ -713,7 +713,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
         }
         FR_MARK(1);
         // ---- budget and generation cap.  A query's goal count is its root's subtree count, summed
-        // bottom-up by fr_reduce (gsub) without atomics, and compared with the budget at
+        // bottom-up by fr_reduce (gvs.y) without atomics, and compared with the budget at
         // generation 0; here a routed query (qgoals saturated by route) stops spawning, as does
         // a goal with more children than the budget or at the last generation.  A query past its
         // budget spawns on meanwhile (bounded by MAX_GEN and its arena slice) -----------------------
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
         }
         if (live) {
             P.gfn[i] = make_uint2(cb, nc | (rop << 24) | (chain ? GFN_CHAIN : 0u));
-            P.gval[i] = val;
+            reinterpret_cast<uint32_t *>(P.gvs)[2 * (size_t)i] = val;
         }
         // ---- occurrences: an ES goal's kept children, goals and leaves alike, are the keys it
         // adds to its scope (CheckAndAddVisited, engine.go:157-160): one run of its wave's slice
@@ -899,24 +899,20 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
         const uint32_t i = gen_goal(P, gm, j);
         const uint2 fn = P.gfn[i];
-        uint32_t val = P.gval[i];
+        uint32_t val = reinterpret_cast<const uint32_t *>(P.gvs)[2 * (size_t)i];
         const uint32_t nc = fn.y & NC_MAX, rop = (fn.y >> 24) & 3u;
         uint32_t sub = nc;  // goals below this one (the budget's count)
         if (nc) {
-            for (uint32_t c = fn.x; c < fn.x + nc; c++) sub += P.gsub[c];
             uint32_t res = NONE32;
-            for (uint32_t c = fn.x; c < fn.x + nc; c++) {
-                const uint32_t cv = P.gval[c];
+            for (uint32_t c = fn.x; c < fn.x + nc; c++) {  // every child's count; the fold up to its result
+                const uint2 v = P.gvs[c];
+                sub += v.y;
+                if (res != NONE32) continue;
+                const uint32_t cv = v.x;
                 if (rop == R_FIRST || rop == R_FIRST_AND) {  // first Err / IsMember
-                    if (decisive(cv)) {
-                        res = cv;
-                        break;
-                    }
+                    if (decisive(cv)) res = cv;
                 } else if (rop == R_AND) {  // AND: the first non-member, keeping its error
-                    if ((cv >> 8) != 0 || (cv & 3u) != M_IS) {
-                        res = (cv & ~3u) | M_NOT;
-                        break;
-                    }
+                    if ((cv >> 8) != 0 || (cv & 3u) != M_IS) res = (cv & ~3u) | M_NOT;
                 } else {  // NOT swaps IsMember / NotMember, keeps Unknown and the error
                     const uint32_t m = cv & 3u;
                     res = m == M_IS ? ((cv & ~3u) | M_NOT) : (m == M_NOT ? ((cv & ~3u) | M_IS) : cv);
@@ -925,9 +921,8 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
             if (res == NONE32) res = val != NONE32 ? val : (rop == R_AND ? M_IS : M_NOT);
             if (rop == R_FIRST_AND) res = and_map(res);  // an AND over its merged OR
             val = res;
-            P.gval[i] = val;
         }
-        if (k > 0) P.gsub[i] = sub;
+        P.gvs[i] = make_uint2(val, sub);
         if (k > 0 && decisive(val)) {  // a decisive ES child: its key goes into the decisive table
             const uint4 g = P.g0[i];
             if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD))  // (RW / TTU / INV hold an op there)
@@ -1028,7 +1023,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     while (dcap < 4 * ncap) dcap <<= 1;
     const uint64_t ocap = cap / 2 / FR_SHARDS;  // per slice
     const size_t ctrl = al256(FR_CTRL_BYTES);
-    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + 2 * al256(cap * 4) + al256(dcap * 12) +
+    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 8) + al256(dcap * 12) +
                          al256(ocap * FR_SHARDS * 8) + (1u << DBITS_LOG2) / 8;
     KETO_HIP(hipMalloc(&f.mem, bytes));
     char *p = static_cast<char *>(f.mem);
@@ -1044,10 +1039,8 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     p += al256(cap * 16);
     f.gfn = reinterpret_cast<uint2 *>(p);
     p += al256(cap * 8);
-    f.gval = reinterpret_cast<uint32_t *>(p);
-    p += al256(cap * 4);
-    f.gsub = reinterpret_cast<uint32_t *>(p);
-    p += al256(cap * 4);
+    f.gvs = reinterpret_cast<uint2 *>(p);
+    p += al256(cap * 8);
     f.dkeys = reinterpret_cast<unsigned long long *>(p);
     f.dcnt = reinterpret_cast<uint32_t *>(f.dkeys + dcap);
     p += al256(dcap * 12);
@@ -1080,8 +1073,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.n = (uint32_t)L.n;
     P.g0 = f.g0;
     P.gfn = f.gfn;
-    P.gval = f.gval;
-    P.gsub = f.gsub;
+    P.gvs = f.gvs;
     P.cap = (uint32_t)f.cap;
     P.scap = (uint32_t)(f.cap / FR_SHARDS);
     P.gbase = gbase;
