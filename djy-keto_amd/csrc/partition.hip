@@ -184,15 +184,20 @@ struct Lookup {
     const uint64_t *req_off;      // [world+1] request offsets per source
     const unsigned long long *subj_set;  // (source, subject id) hash set (k_subj_fill)
     uint64_t subj_mask;
+    const uint32_t *subj_bits;    // 2^SUBJ_BITS-bit filter of the set: most subject-id tuples miss it
     uint32_t world;
     int filter;
 };
 __device__ __forceinline__ unsigned long long subj_key(uint32_t src, uint32_t sid) {
     return (((unsigned long long)src << 32) | sid) + 1ull;  // 0 = empty slot
 }
+constexpr uint32_t SUBJ_BITS = 24;  // 2 MB: the batch's subjects set a few percent of the bits
+__device__ __forceinline__ uint32_t subj_bit(unsigned long long k) {
+    return (uint32_t)(mix64(k) >> 40) & ((1u << SUBJ_BITS) - 1u);
+}
 // the subject lists every source sent (concatenated, soff[world+1]) into one hash set
 __global__ __launch_bounds__(BLK) void k_subj_fill(const uint32_t *subj, const uint64_t *soff, uint32_t world,
-                                                    uint64_t n, unsigned long long *set, uint64_t mask) {
+                                                    uint64_t n, unsigned long long *set, uint64_t mask, uint32_t *bits) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
         uint32_t lo = 0, hi = world;  // last source whose offset <= i
         while (hi - lo > 1) {
@@ -201,6 +206,8 @@ __global__ __launch_bounds__(BLK) void k_subj_fill(const uint32_t *subj, const u
             else hi = mid;
         }
         const unsigned long long k = subj_key(lo, subj[i]);
+        const uint32_t b = subj_bit(k);
+        atomicOr(&bits[b >> 5], 1u << (b & 31u));
         uint64_t h = mix64(k) & mask;
         for (;;) {
             const unsigned long long prev = atomicCAS(&set[h], 0ull, k);
@@ -234,6 +241,8 @@ __device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
 __device__ __forceinline__ bool keep(const Lookup &L, const keto_tuple &t, uint32_t src) {
     if (!L.filter || t.subj_kind == 1) return true;
     const unsigned long long k = subj_key(src, t.s_obj);
+    const uint32_t b = subj_bit(k);
+    if (!((L.subj_bits[b >> 5] >> (b & 31u)) & 1u)) return false;
     uint64_t h = mix64(k) & L.subj_mask;
     for (;;) {  // at most half full: every probe sequence ends at an empty slot
         const unsigned long long v = L.subj_set[h];
@@ -270,9 +279,13 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, ket
                                                         unsigned long long *total, unsigned long long *overflow) {
     for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += gstride()) {
         const uint64_t i = i0 + threadIdx.x;
-        uint64_t b = 0, e = 0, c = 0;
+        uint64_t b = 0, e = 0, c = 0, km = 0;  // km: which of a run's first 64 tuples are kept
         if (i < n && run_of(L, L.req[i], b, e))
-            for (uint64_t j = b; j < e; j++) c += keep(L, L.tuples[j], 0) ? 1 : 0;
+            for (uint64_t j = b; j < e; j++)
+                if (keep(L, L.tuples[j], 0)) {
+                    c++;
+                    if (j - b < 64) km |= 1ull << (j - b);
+                }
         // wave-aggregated allocation
         uint64_t x = c;
         const uint32_t lane = __lane_id();
@@ -290,8 +303,8 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, ket
             atomicOr(overflow, 1ull);
             continue;
         }
-        for (uint64_t j = b; j < e; j++)
-            if (keep(L, L.tuples[j], 0)) out[o++] = L.tuples[j];
+        for (uint64_t j = b; j < e; j++)  // (the first pass's answers: no second probe of the filter)
+            if (j - b < 64 ? ((km >> (j - b)) & 1ull) : keep(L, L.tuples[j], 0)) out[o++] = L.tuples[j];
     }
 }
 
@@ -387,7 +400,8 @@ struct Partition {
     hipStream_t hs = nullptr;
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
-    DevBuf table, seen, cand, fresh, routed, req, req_off, subj, subj_off, subj_set, cnt, pos, out, got, scratch, ctr, closure;
+    DevBuf table, seen, cand, fresh, routed, req, req_off, subj, subj_off, subj_set, subj_bits, cnt, pos, out, got, scratch, ctr,
+        closure;
     uint64_t subj_mask = 0;
     // compact id space of the last closure (remap_ids): local id -> global uuid id
     DevBuf rm_ids, rm_pos, rm_ids2, rm_pos2, rm_flag, rm_rank, rm_lid, uniq, bout;
@@ -515,9 +529,12 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
     ensure(P.subj_set, scap * 8);
     P.subj_mask = scap - 1;
     KETO_HIP(hipMemsetAsync(P.subj_set.p, 0, scap * 8, P.hs));
+    ensure(P.subj_bits, (1u << SUBJ_BITS) / 8);
+    KETO_HIP(hipMemsetAsync(P.subj_bits.p, 0, (1u << SUBJ_BITS) / 8, P.hs));
     if (filter && soff[W])
         hipLaunchKernelGGL(k_subj_fill, grid_for(soff[W]), dim3(BLK), 0, P.hs, dptr<uint32_t>(P.subj),
-                           dptr<uint64_t>(P.subj_off), W, soff[W], dptr<unsigned long long>(P.subj_set), P.subj_mask);
+                           dptr<uint64_t>(P.subj_off), W, soff[W], dptr<unsigned long long>(P.subj_set), P.subj_mask,
+                           dptr<uint32_t>(P.subj_bits));
 
     // seen set: fresh per batch
     P.n_seen = 0;
@@ -601,7 +618,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
                  dptr<keto_tuple>(P.tuples),
                  dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<unsigned long long>(P.subj_set), P.subj_mask,
-                 W, filter ? 1 : 0};
+                 dptr<uint32_t>(P.subj_bits), W, filter ? 1 : 0};
         if (W == 1 && P.closure.p) {  // one rank: a single gathering pass into the closure (k_lookup_gather)
             const uint64_t cap = P.closure.bytes / sizeof(keto_tuple) - total;
             unsigned long long *g = dptr<unsigned long long>(P.ctr) + 2;  // [2] total, [3] overflow
