@@ -375,8 +375,12 @@ __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
 #ifndef KETO_FR_WAVES
 #define KETO_FR_WAVES 6
 #endif
+#ifndef KETO_FR_BLOCK
+#define KETO_FR_BLOCK 256
+#endif
+constexpr uint32_t XBLOCK = KETO_FR_BLOCK;  // fr_expand's block: the regroup window
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P) {
+__global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParams P) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const DevSnapshot &s = P.s;
     __shared__ GenMap gm;
@@ -401,8 +405,8 @@ __global__ __launch_bounds__(256, KETO_FR_WAVES) void fr_expand(FrontierParams P
 #endif
 #ifndef KETO_FR_NOREGROUP
     constexpr uint32_t NB = KETO_FR_RG_BUCKETS;  // goal classes; dead lanes are one more
-    __shared__ uint4 rg_g[256];
-    __shared__ uint32_t rg_i[256], rg_n[4][NB + 1];
+    __shared__ uint4 rg_g[XBLOCK];
+    __shared__ uint32_t rg_i[XBLOCK], rg_n[XBLOCK / 64][NB + 1];
 #endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
@@ -1105,8 +1109,8 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     // run only after a resident one finished its whole share)
     int per_cu = 0;
     const void *kx = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true>) : reinterpret_cast<const void *>(&fr_expand<false>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kx, BLOCK, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
-    const dim3 eg(cus * (uint32_t)std::min(per_cu, 8)), eb(BLOCK);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kx, XBLOCK, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
+    const dim3 eg(cus * (uint32_t)std::min(per_cu, (int)(2048 / XBLOCK))), xb(XBLOCK), eb(BLOCK);
     constexpr uint32_t CHUNK = 12;
     uint32_t gens = 0;
     uint32_t *hc = f.host_ctrl;
@@ -1118,8 +1122,8 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         const uint32_t kend = std::min(k + (k == 0 ? std::max(CHUNK, f.last_gens + 1) : CHUNK), MAX_GEN);
         for (; k < kend; k++) {
             P.gen = k;
-            if (lds_tables) hipLaunchKernelGGL(fr_expand<true>, eg, eb, lds, st.stream, P);
-            else hipLaunchKernelGGL(fr_expand<false>, eg, eb, 0, st.stream, P);
+            if (lds_tables) hipLaunchKernelGGL(fr_expand<true>, eg, xb, lds, st.stream, P);
+            else hipLaunchKernelGGL(fr_expand<false>, eg, xb, 0, st.stream, P);
             KETO_HIP(hipGetLastError());
         }
         KETO_HIP(hipMemcpyAsync(hc, f.ctrl, 2 * FR_SHARDS * GEN_STRIDE * 4, hipMemcpyDeviceToHost, st.stream));
