@@ -445,7 +445,7 @@ def main():
     c = stream.counters(reset=True)
     pt = c["per_tier"]
     bytes_t0 = 8 * pt["rows"][0] + 4 * pt["edges"][0] + 8 * pt["probes"][0] + 17 * pt["queries"][0]
-    allowed = da.download(stream, np.zeros(len(q), np.uint8))
+    dfs_allowed = da.download(stream, np.zeros(len(q), np.uint8))  # (the counted batch runs the DFS interpreter)
     errs = de.download(stream, np.zeros(len(q), np.int32))
     assert (errs == 0).all(), "unexpected query errors"
 
@@ -474,6 +474,12 @@ def main():
     assert k_n == args.steps, f"timed {k_n} kernel launches, expected {args.steps}"
     kernel_ms = k_sum / k_n
     fr = stream.frontier_stats(reset=True)
+    # the timed batches' decisions (the measured path): the CPU parity sample checks these, and
+    # they must equal the counted batch's DFS decisions on the same queries
+    allowed = da.download(stream, np.zeros(len(q), np.uint8))
+    errs = de.download(stream, np.zeros(len(q), np.int32))
+    assert (errs == 0).all(), "unexpected query errors"
+    dfs_mismatches = int((allowed != dfs_allowed).sum())
 
     log(f"[rank {rank}] timed: {elapsed_local / args.steps * 1e3:.2f} ms/step, kernel {kernel_ms:.2f} ms "
         f"({time.perf_counter() - t_setup:.1f}s since start)")
@@ -531,6 +537,8 @@ def main():
         "p99_batch_latency_ms": p99_ms,
         "latency_batch": nl,
         "allowed_fraction": float(allowed.mean()),
+        "timed_vs_dfs": {"n": int(len(q)), "mismatches": dfs_mismatches,
+                         "note": "timed batches' decisions vs the counted batch's DFS interpreter, same queries"},
         "pcie_inclusive_checks_per_s": pcie_rate,
         "serving": serving,
         "expand": expand,
