@@ -52,3 +52,24 @@ def test_routing_is_rare_on_baseline_generators(wl_name):
     np.testing.assert_array_equal(udec[ok], dec[ok])
     np.testing.assert_array_equal(uerr[ok], err[ok])
     assert routed.mean() < 0.01
+
+
+def test_spawn_shaping_keeps_drive_goals_few():
+    """Regression guard for the frontier's spawn-time shaping (oracle/refsem.c u_sub node_check,
+    u_es chains, u_and_merge), which the product mirrors goal for goal: on a Drive world the
+    restatement spawns under 20 goals per query (46 without the round-2 rules) and most queries
+    finish within a handful of generations, with their decisions still the DFS's."""
+    from keto_mi355x import synth
+    wl = synth.drive(depth=8, n_groups=20_000, n_users=100_000, seed=3)
+    q = synth.drive_queries(wl, 20_000, seed=4)
+    w, _ = world_from_workload(wl, with_tuples=False)
+    orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    qo = queries_to_oracle(q)
+    dec, err, _ = orc.check_batch(qo, threads=8)
+    udec, uerr, routed, goals, gens = orc.check_u_batch(qo, threads=8, budget=1024)
+    ok = routed == 0
+    np.testing.assert_array_equal(udec[ok], dec[ok])
+    assert goals.mean() < 20.0
+    assert gens.mean() < 8.0
+
