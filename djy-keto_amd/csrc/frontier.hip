@@ -23,7 +23,7 @@
 // fr_reduce enters only the decisive ones into a small table, and fr_repeat counts the list's
 // occurrences of those keys.
 //
-// Goal records (HBM, one arena per stream, structure of arrays; 28 bytes per goal):
+// Goal records (HBM, one arena per stream, structure of arrays; 32 bytes per goal):
 //   g0[i]   = {node, query position, word, scope}   16 B, written by the parent at spawn
 //   gfn[i]  = {first child, children | reduce op}    8 B, written by fr_expand
 //   gvs[i]  = {value (or the partial fr_reduce folds), goals below it}  8 B, fr_expand (value),
