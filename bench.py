@@ -357,9 +357,11 @@ def run_c5(args, rank, world, device, dist_on):
         dist.barrier()
     elapsed_local = time.perf_counter() - t_start
     value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps, f"cuda:{device}" if dist_on else "cpu")
+    ranks_ms = per_rank_ms(elapsed_local / args.steps * 1e3, f"cuda:{device}" if dist_on else "cpu")
     out = {
         "metric": METRIC, "value": value, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "per_rank_ms_per_step": ranks_ms,
+        "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (seeded Drive-style folder forest, BASELINE config 5; generated per partition)",
         "config": {"workload": f"C5 Drive-style x{args.scale}: {wl.meta['n_tuples']} tuples partitioned by "
@@ -381,7 +383,106 @@ def run_c5(args, rank, world, device, dist_on):
         dist.destroy_process_group()
 
 
-def main():
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising HIP (torch.cuda.device_count()
+    does not on this image), so the launcher can still start fresh children afterwards"""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` (N > 1) without torchrun: N fresh child processes, one per GPU, each
+    one rank of an RCCL job (RANK / LOCAL_RANK / WORLD_SIZE, MASTER_ADDR 127.0.0.1).  Nothing in
+    this process touches the GPU; it waits for the children and exits with the worst status.
+    Fewer visible GPUs than N is an error, never a silent 1-GPU run."""
+    import signal
+    import socket
+    import subprocess
+
+    n = args.gpus
+    have = n if args.dry_run else visible_gpus()
+    if have < n:
+        log(f"bench.py --gpus {n}: only {have} GPU(s) visible -- refusing to report a {n}-GPU line")
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0):  # one rank failed: the others would wait forever
+                    for q in procs:
+                        if q.poll() is None:
+                            q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    worst = max((abs(rc) for rc in rcs), default=0)
+    if worst:
+        log(f"bench.py --gpus {n}: rank exit codes {rcs}")
+    return worst
+
+
+def per_rank_ms(ms_local: float, device: str):
+    """every rank's ms/step (all ranks' values, rank order); without a process group: [this rank's]"""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return [ms_local]
+    t = torch.zeros(dist.get_world_size(), dtype=torch.float64, device=device)
+    t[dist.get_rank()] = ms_local
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(x) for x in t.tolist()]
+
+
+def dry_run_rank(args, rank, world):
+    """--dry-run (CPU, tests): the launcher and the rank protocol without a GPU -- every rank
+    joins a gloo group, checks its own seeded shard of a small nested-group batch with the
+    oracle `steps` times, and rank 0 prints the line the GPU job prints (n_gpus, per-rank ms)"""
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refsem
+    from keto_mi355x import synth
+    from product_helpers import queries_to_oracle, world_from_workload
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    wl = synth.nested_groups(20_000, seed=1)
+    q = synth.nested_groups_queries(wl, 256, seed=shard_seed(7, rank))
+    w, t = world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    qo = queries_to_oracle(q)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dec, _, _ = orc.check_batch(qo, threads=1)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    value, elapsed, total = job_rate(el, len(q) * args.steps, "cpu")
+    ranks_ms = per_rank_ms(el / args.steps * 1e3, "cpu")
+    out = {"metric": METRIC, "value": value, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "per_rank_ms_per_step": ranks_ms,
+           "dry_run": True, "checks": total, "allowed_checksum": int(dec.sum())}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    orc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -397,18 +498,34 @@ def main():
     ap.add_argument("--serve-clients", type=int, default=128, help="0 skips the dispatcher probe")
     ap.add_argument("--serve-request", type=int, default=64)
     ap.add_argument("--serve-seconds", type=float, default=3.0)
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # CPU: launcher + rank protocol only
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = ap.parse_args(argv)
 
+    # --gpus N decides the job size: without torchrun's environment this process launches the N
+    # ranks itself (before anything initialises HIP); under torchrun the world must be N
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: refusing a line whose n_gpus would be wrong")
+        return 2
+    if args.dry_run:
+        return dry_run_rank(args, rank, world)
     import torch
     import torch.distributed as dist
 
     dist_on = world > 1
     # one process per GPU; KETO_BENCH_BACKEND=gloo rehearses the multi-rank path with several
     # ranks sharing one GPU (RCCL needs distinct devices)
-    device = local % max(1, torch.cuda.device_count())
+    shared = os.environ.get("KETO_BENCH_BACKEND", "nccl") == "gloo"
+    ndev = visible_gpus()
+    if ndev < 1 or (not shared and local >= ndev):
+        log(f"rank {rank}: LOCAL_RANK {local} needs GPU {local}, {ndev} visible")
+        return 2
+    device = local % ndev
     if dist_on:
         import datetime
 
@@ -467,6 +584,7 @@ def main():
     elapsed_local = time.perf_counter() - t_start
     value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps,
                                      f"cuda:{device}" if dist_on else "cpu")
+    ranks_ms = per_rank_ms(elapsed_local / args.steps * 1e3, f"cuda:{device}" if dist_on else "cpu")
     # average device time of a batch's check path over the timed region: HIP event pairs recorded
     # on the engine's own stream around every batch (rewrite snapshots: the frontier engine's
     # generations plus the DFS interpreter on the routed queries; C2: the union kernel's tier 0)
@@ -527,6 +645,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "per_rank_ms_per_step": ranks_ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -572,4 +691,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

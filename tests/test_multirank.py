@@ -58,3 +58,43 @@ def test_single_rank_job_rate_without_group():
     assert not dist.is_initialized()
     assert bench.job_rate(2.0, 10) == (5.0, 2.0, 10)
     assert np.isfinite(bench.job_rate(1e-3, 1)[0])
+
+
+def test_bench_gpus_2_launches_two_ranks_cpu_dry_run():
+    """`bench.py --gpus 2` without torchrun starts two rank processes itself (fresh children,
+    127.0.0.1 rendezvous); --dry-run swaps the GPU work for an oracle batch per rank, so the
+    launcher, the max-over-ranks timing and the per-rank ms are exercised on the CPU"""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "0",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and len(out["per_rank_ms_per_step"]) == 2
+    assert out["checks"] == 2 * 256 * 2  # both ranks' units
+    assert out["ms_per_step"] == pytest.approx(max(out["per_rank_ms_per_step"]), rel=1e-6)
+
+
+def test_bench_gpus_n_fails_loudly_without_gpus():
+    """no GPU here: `bench.py --gpus 2` must exit non-zero, never print a 1-GPU line"""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "{" not in r.stdout
+    assert "GPU(s) visible" in r.stderr
+
+
+def test_bench_world_must_match_gpus():
+    import subprocess
+
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr

@@ -2,7 +2,7 @@
 // gfx950 as a function of the footprint, the waves per CU, the independent loads per step
 // and lane-private vs shared regions -- the access pattern of the Check interpreters.
 //
-//   chase <footprint_MiB> <waves_per_simd> <loads_per_step 1|2> <steps> [private_bytes_per_lane]
+//   chase <footprint_MiB> <waves_per_simd> <loads_per_step 1..8> <steps> [private_bytes_per_lane] [width 1|2|4]
 //
 // Each lane walks `steps` dependent steps; step k loads 1 or 2 random 16-byte windows whose
 // addresses depend on the previous step's data (a hash of it), like the interpreters' load
@@ -31,20 +31,30 @@ __device__ __forceinline__ unsigned long long mix(unsigned long long x) {
 }
 
 __global__ __launch_bounds__(256) void chase(const uint4 *buf, unsigned long long n_win, int loads, int steps,
-                                             unsigned long long priv_win, unsigned int *out) {
+                                             unsigned long long priv_win, unsigned int *out, int width) {
     const unsigned long long gl = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
     unsigned long long h = mix(gl + 1);
     unsigned int acc = 0;
     const unsigned long long base = priv_win ? (gl * priv_win) % (n_win - priv_win + 1) : 0;
-    const unsigned long long span = priv_win ? priv_win : n_win;
+    const unsigned long long span = (priv_win ? priv_win : n_win) - (width - 1);
     for (int k = 0; k < steps; k++) {
-        const unsigned long long i0 = base + h % span;
-        const unsigned long long i1 = base + (h >> 21) % span;
-        uint4 v0 = buf[i0];
-        uint4 v1 = make_uint4(0, 0, 0, 0);
-        if (loads > 1) v1 = buf[i1];
-        h = mix(h ^ v0.x ^ v1.y ^ (unsigned long long)k);
-        acc += v0.z + v1.w;
+        // `loads` independent random windows per step (1..8), each `width` x 16 B contiguous
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            v[j] = make_uint4(0, 0, 0, 0);
+            if (j < loads) {
+                const unsigned long long i = base + mix(h + j) % span;
+                v[j] = buf[i];
+                if (width > 1) { const uint4 u = buf[i + 1]; v[j].x ^= u.y; }
+                if (width > 2) { const uint4 u = buf[i + 2], w = buf[i + 3]; v[j].y ^= u.z ^ w.w; }
+            }
+        }
+        unsigned long long x = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) x ^= v[j].x ^ ((unsigned long long)v[j].y << 17);
+        h = mix(h ^ x ^ (unsigned long long)k);
+        acc += (unsigned)x;
     }
     out[gl] = acc;
 }
@@ -63,6 +73,7 @@ int main(int argc, char **argv) {
     const unsigned long long bytes = strtoull(argv[1], 0, 10) << 20;
     const int wps = atoi(argv[2]), loads = atoi(argv[3]), steps = atoi(argv[4]);
     const unsigned long long priv = argc > 5 ? strtoull(argv[5], 0, 10) : 0;
+    const int width = argc > 6 ? atoi(argv[6]) : 1;  // 16-B windows per access: 1, 2 or 4 (64 B)
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const unsigned long long n_win = bytes / 16;
@@ -78,7 +89,7 @@ int main(int argc, char **argv) {
     float best = 1e30f;
     for (int rep = 0; rep < 3; rep++) {
         CK(hipEventRecord(a, 0));
-        hipLaunchKernelGGL(chase, dim3(lanes / 256), dim3(256), 0, 0, buf, n_win, loads, steps, priv / 16, out);
+        hipLaunchKernelGGL(chase, dim3(lanes / 256), dim3(256), 0, 0, buf, n_win, loads, steps, priv / 16, out, width);
         CK(hipEventRecord(b, 0));
         CK(hipEventSynchronize(b));
         float ms;
@@ -87,7 +98,9 @@ int main(int argc, char **argv) {
     }
     const double ns_step = best * 1e6 / steps;
     const double lines = (double)lanes * steps * loads;
-    printf("footprint %6llu MiB waves/SIMD %d loads %d private %6llu B: %8.1f ns/step, %.2f G loads/s, %.0f GB/s (16 B)\n",
-           bytes >> 20, wps, loads, priv, ns_step, lines / (best * 1e-3) / 1e9, lines * 16 / (best * 1e-3) / 1e9);
+    printf("footprint %6llu MiB waves/SIMD %d loads %d width %2d B private %6llu B: %8.1f ns/step, %.2f G accesses/s, "
+           "%.0f GB/s useful\n",
+           bytes >> 20, wps, loads, 16 * width, priv, ns_step, lines / (best * 1e-3) / 1e9,
+           lines * 16 * width / (best * 1e-3) / 1e9);
     return 0;
 }
