@@ -156,6 +156,7 @@ int keto_stream_create(int32_t device, keto_stream **out) {
         KETO_HIP(hipSetDevice(device));
         auto s = std::make_unique<keto::Stream>();
         s->device = device;
+        if (const char *be = getenv("KETO_FR_BUDGET")) s->fr_budget = (uint32_t)std::max(1, atoi(be));
         KETO_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         for (int i = 0; i < keto::Stream::TIMER_SLOTS; i++) {
             KETO_HIP(hipEventCreate(&s->ev_a[i]));
@@ -267,6 +268,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         L.max_width = lim.max_read_width;
         L.count = (flags & KETO_F_COUNT_WORK) != 0;
         L.err_detail = (flags & KETO_F_ERR_DETAIL) != 0;
+        L.budget = s->fr_budget;
         if (flags & KETO_F_DEVICE_PTRS) {
             L.queries = queries;
             L.out_allowed = out_allowed;

@@ -527,8 +527,12 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     }
     st.mark_begin();
     run_resolve(s, st, L.queries, L.n, L.max_depth, false);
-    const uint32_t routed = run_frontier(s, st, L);
-    if (routed) run_dfs(s, st, L, st.frontier.fb_list, st.frontier.fb_count, routed, false);
+    for (uint64_t off = 0; off < L.n; off += FR_MAX_BATCH) {
+        CheckLaunch Lp = L;
+        Lp.n = std::min<uint64_t>(FR_MAX_BATCH, L.n - off);
+        const uint32_t routed = run_frontier(s, st, Lp, off);
+        if (routed) run_dfs(s, st, L, st.frontier.fb_list, st.frontier.fb_count, routed, false);
+    }
     st.mark_end();
 }
 

@@ -310,14 +310,12 @@ void dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, k
             KETO_HIP(hipMalloc(&x->da, nb));
             KETO_HIP(hipMalloc(&x->de, nb * sizeof(int32_t)));
         }
-        // every slot's scratch is allocated now (one 1-query batch on its stream), not by its
-        // first live batch: the allocation synchronises the device, which would stall the
-        // other slots' batches in flight
+        // every slot's scratch is allocated now, for its largest batch (one max_batch batch of
+        // empty queries on its stream), not by its first live batches: an allocation synchronises
+        // the device, which would stall the other slots' batches in flight
         for (auto &x : d->slots) {
-            keto_query q0{};
-            uint8_t a0 = 0;
-            int32_t e0 = 0;
-            if (keto_check_batch(snap, x->stream, &q0, 1, &d->limits, &a0, &e0, 0) != KETO_OK)
+            std::memset(x->hq, 0, nb * sizeof(keto_query));
+            if (keto_check_batch(snap, x->stream, x->hq, nb, &d->limits, x->ha, x->he, 0) != KETO_OK)
                 throw Error(KETO_E_DEVICE, "dispatcher slot warm-up failed");
         }
         for (auto &x : d->slots) {

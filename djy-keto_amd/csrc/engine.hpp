@@ -161,6 +161,7 @@ struct Stream {
     unsigned long long *counters = nullptr;  // device [3 tiers][8]
     keto_work_counters host_counters{};
     double last_kernel_ms = 0;
+    uint32_t fr_budget = 1024;  // KETO_FR_BUDGET, read once when the stream is created (tests lower it)
     ~Stream();
 };
 
@@ -178,6 +179,7 @@ struct CheckLaunch {
     int32_t max_depth, max_width;
     bool count;
     bool err_detail;  // KETO_F_ERR_DETAIL: out_err carries the failing relation name id << 8
+    uint32_t budget;  // frontier goals per query before it is routed to the DFS interpreter (Stream::fr_budget)
 };
 // resolve.hip: per-query start records, longest-first, into st.resolved
 // ordered: heavy-first work order for the DFS interpreters (two atomics per wave); else batch order
@@ -185,9 +187,11 @@ void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint6
                  bool ordered = true);
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
 void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // rewrite-free snapshots
-// frontier.hip: the batch (already resolved) breadth-first; returns the number of queries routed
-// to the DFS interpreter (positions in st.frontier.fb_list)
-uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L);
+// frontier.hip: L.n resolved queries from batch position pos_base on, breadth-first; returns the
+// number of queries routed to the DFS interpreter (batch positions in st.frontier.fb_list).
+// Batches above FR_MAX_BATCH run as several passes: the arena's goal indices stay in range.
+constexpr uint64_t FR_MAX_BATCH = 1ull << 21;
+uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint64_t pos_base);
 
 struct ExpandLaunch {
     const keto_subject_set *roots;  // device

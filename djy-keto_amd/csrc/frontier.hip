@@ -91,7 +91,8 @@ struct FrontierParams {
     uint8_t *out_allowed;
     int32_t *out_err;
     uint32_t err_detail;
-    uint32_t *fb_list, *fb_count;  // routed positions, for the DFS interpreter
+    uint32_t *fb_list, *fb_count;  // routed positions (+ pos_base: batch positions), for the DFS interpreter
+    uint32_t pos_base;             // this pass's first batch position (batches of > FR_MAX_BATCH run in passes)
     unsigned long long *prof;      // KETO_FR_PROF builds: wave-cycles per phase of fr_expand
 };
 
@@ -752,7 +753,10 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         if (lane == 0 && otot) obase = atomicAdd(&P.occ_count[so], otot);
         uint32_t oc = __shfl(obase, 0) + ooff;
         const bool occ_ok = (uint64_t)oc + nocc <= P.ocap;
-        if (nocc && !occ_ok) route(P, pos);  // list full: the DFS interpreter takes the query
+        if (nocc && !occ_ok) {  // list full: the DFS interpreter takes the query; the allocated slots
+            route(P, pos);      // that exist are cleared, so fr_repeat never counts an older batch's pair
+            for (uint32_t e = oc; e < P.ocap && e < oc + nocc; e++) P.occ[(size_t)so * P.ocap + e] = make_uint2(NONE32, 0);
+        }
         oc += so * P.ocap;
         FR_MARK(3);
         // ---- phase B: write the children (the same walk as phase A) -------------------------------
@@ -939,7 +943,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         if (k == 0) {  // generation 0: one goal per query position
             const uint32_t pos = P.g0[i].y;
             if (P.qroute[pos] || 1u + sub > P.budget) {
-                P.fb_list[atomicAdd(P.fb_count, 1u)] = pos;
+                P.fb_list[atomicAdd(P.fb_count, 1u)] = P.pos_base + pos;
                 continue;
             }
             const uint32_t q = P.start[2 * (size_t)pos].w;
@@ -1014,6 +1018,11 @@ static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 #endif
 
 void ensure_frontier(FrontierScratch &f, uint64_t n) {
+    // sized for the next power of two of the batch: a growing stream of batches reallocates (and
+    // synchronises the device) O(log n) times, not at every new largest batch
+    uint64_t np = 1;
+    while (np < n) np <<= 1;
+    n = std::min(np, FR_MAX_BATCH);
     const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n * KETO_FR_GOALS_PER_QUERY, 1u << 20), 1ull << 29) / FR_SHARDS *
                           FR_SHARDS;
     if (f.mem && f.cap >= want && f.ncap >= n) return;
@@ -1062,8 +1071,9 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     if (!f.host_ctrl) KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&f.host_ctrl), FR_CTRL_BYTES, 0));
 }
 
-uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
+uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint64_t pos_base) {
     FrontierScratch &f = st.frontier;
+    if (L.n > FR_MAX_BATCH) throw Error(KETO_E_LIMIT, "frontier pass larger than FR_MAX_BATCH");
     ensure_frontier(f, L.n);
     const uint32_t cus = (uint32_t)num_cus(s.device);
     const bool lds_tables = s.dev.lds_bytes <= LDS_TABLE_LIMIT;
@@ -1073,7 +1083,8 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     KETO_HIP(hipMemsetAsync(f.dbits, 0, (1u << DBITS_LOG2) / 8, st.stream));
     FrontierParams P{};
     P.s = s.dev;
-    P.start = st.resolved;
+    P.start = st.resolved + 2 * pos_base;
+    P.pos_base = (uint32_t)pos_base;
     P.n = (uint32_t)L.n;
     P.g0 = f.g0;
     P.gfn = f.gfn;
@@ -1084,8 +1095,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     P.gcount = gcount;
     P.qgoals = f.qgoals;
     P.qroute = f.qroute;
-    const char *be = getenv("KETO_FR_BUDGET");
-    P.budget = be ? (uint32_t)std::max(1, atoi(be)) : 1024u;
+    P.budget = L.budget;
     P.dkeys = f.dkeys;
     P.dcnt = f.dcnt;
     P.dbits = f.dbits;

@@ -28,13 +28,19 @@ def stream():
 
 @pytest.fixture
 def budget():
+    """budget(b) -> a stream whose frontier routes queries past b goals (KETO_FR_BUDGET is read
+    once, when a stream is created)"""
     old = os.environ.get("KETO_FR_BUDGET")
+    made = []
 
     def set_budget(b):
         os.environ["KETO_FR_BUDGET"] = str(b)
-        return b
+        made.append(km.Stream(0))
+        return made[-1]
 
     yield set_budget
+    for s in made:
+        s.close()
     if old is None:
         os.environ.pop("KETO_FR_BUDGET", None)
     else:
@@ -50,8 +56,8 @@ def _frontier_batch(stream, eng, q):
 @pytest.mark.parametrize("rewrites", [True, False])
 @pytest.mark.parametrize("b", [1024, 6])
 @pytest.mark.parametrize("seed", list(range(60)))
-def test_random_worlds_frontier_vs_oracle(stream, budget, seed, b, rewrites):
-    budget(b)
+def test_random_worlds_frontier_vs_oracle(budget, seed, b, rewrites):
+    stream = budget(b)
     w, t, q, _ = random_world(seed, rewrites=rewrites)
     orc = refsem.Oracle(w, t)
     orc.set_limits(w.max_depth, w.max_width)
@@ -142,10 +148,10 @@ def test_union_interpreter_opt_out_vs_oracle(stream, seed):
     assert fs["batches"] == 0  # the frontier engine did not run
 
 
-def test_every_query_routed_matches_oracle(stream, budget):
+def test_every_query_routed_matches_oracle(budget):
     """budget 1: every query with a sub-check goes to the DFS interpreter through the routed list"""
     from keto_mi355x import synth
-    budget(1)
+    stream = budget(1)
     wl = synth.drive(depth=5, n_groups=500, n_users=2000, seed=8)
     q = synth.drive_queries(wl, 4096, seed=5)
     snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
