@@ -269,6 +269,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         L.count = (flags & KETO_F_COUNT_WORK) != 0;
         L.err_detail = (flags & KETO_F_ERR_DETAIL) != 0;
         L.budget = s->fr_budget;
+        L.async = (flags & KETO_F_ASYNC) != 0 && !L.count;
         if (flags & KETO_F_DEVICE_PTRS) {
             L.queries = queries;
             L.out_allowed = out_allowed;
@@ -293,6 +294,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         check_engine(*snap)(*snap, *s, L);
         KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+        if (flags & KETO_F_ASYNC) return;  // the caller synchronises the stream (keto_stream_sync)
         KETO_HIP(hipStreamSynchronize(s->stream));
         s->harvest();
     });
@@ -353,6 +355,16 @@ int keto_expand_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_
         KETO_HIP(hipStreamSynchronize(s->stream));
     });
     return g != KETO_OK ? g : rc;
+}
+
+int keto_host_alloc(uint64_t bytes, void **out) {
+    if (!out) return fail(KETO_E_INVALID, "null output pointer");
+    *out = nullptr;
+    return guarded([&] { KETO_HIP(hipHostMalloc(out, bytes ? bytes : 1, 0)); });
+}
+
+int keto_host_free(void *p) {
+    return guarded([&] { KETO_HIP(hipHostFree(p)); });
 }
 
 int keto_device_alloc(int32_t device, uint64_t bytes, void **out) {

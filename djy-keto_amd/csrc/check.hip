@@ -531,7 +531,10 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         CheckLaunch Lp = L;
         Lp.n = std::min<uint64_t>(FR_MAX_BATCH, L.n - off);
         const uint32_t routed = run_frontier(s, st, Lp, off);
-        if (routed) run_dfs(s, st, L, st.frontier.fb_list, st.frontier.fb_count, routed, false);
+        // asynchronous: the interpreter is sized for the whole pass and reads the routed count on
+        // the device (its lanes find an empty list and leave)
+        if (routed) run_dfs(s, st, L, st.frontier.fb_list, st.frontier.fb_count, routed == FR_ROUTED_ON_DEVICE ? Lp.n : routed,
+                            false);
     }
     st.mark_end();
 }

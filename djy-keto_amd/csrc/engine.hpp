@@ -180,6 +180,7 @@ struct CheckLaunch {
     bool count;
     bool err_detail;  // KETO_F_ERR_DETAIL: out_err carries the failing relation name id << 8
     uint32_t budget;  // frontier goals per query before it is routed to the DFS interpreter (Stream::fr_budget)
+    bool async;       // KETO_F_ASYNC: enqueue only, no host read-back inside the batch
 };
 // resolve.hip: per-query start records, longest-first, into st.resolved
 // ordered: heavy-first work order for the DFS interpreters (two atomics per wave); else batch order
@@ -191,6 +192,7 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // r
 // number of queries routed to the DFS interpreter (batch positions in st.frontier.fb_list).
 // Batches above FR_MAX_BATCH run as several passes: the arena's goal indices stay in range.
 constexpr uint64_t FR_MAX_BATCH = 1ull << 21;
+constexpr uint32_t FR_ROUTED_ON_DEVICE = 0xFFFFFFFFu;  // run_frontier, asynchronous: the count stays on the device
 uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint64_t pos_base);
 
 struct ExpandLaunch {

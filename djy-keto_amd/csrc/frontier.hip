@@ -78,6 +78,7 @@ struct FrontierParams {
     uint32_t cap, scap;          // arena goals, goals per slice
     uint32_t *gbase, *gcount;    // [FR_SHARDS][GEN_STRIDE]: slice-local base and count per generation
     uint32_t gen;
+    uint32_t gen_cap;            // generations this batch may run (MAX_GEN; asynchronous batches: the speculated count)
     uint32_t *qgoals, *qroute;   // [n] per query position
     uint32_t budget;
     unsigned long long *dkeys;   // decisive (scope, visited key) pairs of the batch (epoch-tagged)
@@ -385,7 +386,6 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const DevSnapshot &s = P.s;
     __shared__ GenMap gm;
-    const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
     const uint32_t k = P.gen;
     load_gen(P, k, gm);
     const uint32_t cnt = gm.pre[FR_SHARDS];
@@ -393,10 +393,14 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
     if (blockIdx.x == 0)
         for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x)
             P.gbase[t * GEN_STRIDE + k + 1] = gm.base[t] + (gm.pre[t + 1] - gm.pre[t]);
+    // blocks without a goal of this generation leave before staging the tables: small batches
+    // and the empty generations an asynchronous batch launches speculatively cost ~nothing
+    if (blockIdx.x * blockDim.x >= cnt) return;
+    const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
     // this wave's slice
     const uint32_t so = (blockIdx.x * ((blockDim.x + 63) >> 6) + (threadIdx.x >> 6)) % FR_SHARDS;
     const uint32_t nbase = so * P.scap + gm.base[so] + (gm.pre[so + 1] - gm.pre[so]), send = (so + 1) * P.scap;
-    const bool last = k + 1 >= MAX_GEN;
+    const bool last = k + 1 >= P.gen_cap;
     const uint32_t W = P.max_width;
 #ifdef KETO_FR_PROF
     unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
@@ -1111,6 +1115,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     P.fb_list = f.fb_list;
     P.fb_count = fb_count;
     P.prof = st.counters;
+    P.gen_cap = MAX_GEN;
     constexpr uint32_t BLOCK = 256;
     hipLaunchKernelGGL(fr_init, dim3((uint32_t)((L.n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st.stream, P);
     KETO_HIP(hipGetLastError());
@@ -1121,6 +1126,37 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     const void *kx = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true>) : reinterpret_cast<const void *>(&fr_expand<false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kx, XBLOCK, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
     const dim3 eg(cus * (uint32_t)std::min(per_cu, (int)(2048 / XBLOCK))), xb(XBLOCK), eb(BLOCK);
+    if (L.async) {
+        // KETO_F_ASYNC: nothing comes back to the host.  The stream's last synchronous batch says
+        // how deep a batch goes; G generations (a margin over it) are launched and each one whose
+        // predecessor spawned nothing returns at once (its blocks leave before staging the
+        // tables).  A query that would spawn past G is routed: the DFS interpreter, launched on
+        // the device-side count, answers it.  So the answers are the synchronous path's; only a
+        // deeper-than-speculated query costs the slower engine.
+        const uint32_t G = std::min<uint32_t>(MAX_GEN, std::max<uint32_t>(f.last_gens + 4, 24));
+        P.gen_cap = G;
+        for (uint32_t k = 0; k < G; k++) {
+            P.gen = k;
+            if (lds_tables) hipLaunchKernelGGL(fr_expand<true>, eg, xb, lds, st.stream, P);
+            else hipLaunchKernelGGL(fr_expand<false>, eg, xb, 0, st.stream, P);
+            KETO_HIP(hipGetLastError());
+        }
+        for (int32_t g = (int32_t)G - 1; g >= 0; g--) {
+            P.gen = (uint32_t)g;
+            if (g == 0) {
+                hipLaunchKernelGGL(fr_repeat, dim3(cus * 2), dim3(REPEAT_BLOCK), 0, st.stream, P);
+                KETO_HIP(hipGetLastError());
+            }
+            hipLaunchKernelGGL(fr_reduce, dim3(cus * 8), eb, 0, st.stream, P);
+            KETO_HIP(hipGetLastError());
+        }
+        if (++f.epoch > TAB_EPOCHS) {
+            KETO_HIP(hipMemsetAsync(f.dkeys, 0, f.dcap * 12, st.stream));
+            f.epoch = 1;
+        }
+        f.stats.async_batches++;
+        return FR_ROUTED_ON_DEVICE;
+    }
     constexpr uint32_t CHUNK = 12;
     uint32_t gens = 0;
     uint32_t *hc = f.host_ctrl;

@@ -91,9 +91,35 @@ __global__ __launch_bounds__(BLK) void k_tuple_keys(const keto_tuple *t, uint64_
         idx[i] = (uint32_t)i;
     }
 }
-__global__ __launch_bounds__(BLK) void k_gather_tuples(const keto_tuple *t, const uint32_t *idx, uint64_t n,
-                                                        keto_tuple *out) {
-    for (uint64_t i = gid(); i < n; i += gstride()) out[i] = t[idx[i]];
+// The partition's store, grouped by object: a run's (ns, obj) is its key, so a tuple keeps only
+// its subject and relations -- 24 bytes instead of keto_tuple's 48 (a config-5 partition is
+// billions of tuples): meta = {s_obj, rel | s_rel << 10 | s_ns << 20 | subj_kind << 31} and
+// the shard_id (16 B, it orders every row).  partition_create checks that the name tables fit.
+constexpr uint32_t ST_REL_BITS = 10, ST_NS_BITS = 11;
+__device__ __forceinline__ uint2 st_meta(const keto_tuple &t) {
+    return make_uint2(t.s_obj, t.rel | (t.s_rel << ST_REL_BITS) | (t.s_ns << (2 * ST_REL_BITS)) | (t.subj_kind << 31));
+}
+__device__ __forceinline__ keto_tuple st_tuple(uint64_t key, uint2 m, uint4 shard) {
+    keto_tuple t;
+    t.ns = (uint32_t)(key >> 32);
+    t.obj = (uint32_t)key;
+    t.rel = m.y & ((1u << ST_REL_BITS) - 1u);
+    t.subj_kind = m.y >> 31;
+    t.s_obj = m.x;
+    t.s_ns = (m.y >> (2 * ST_REL_BITS)) & ((1u << ST_NS_BITS) - 1u);
+    t.s_rel = (m.y >> ST_REL_BITS) & ((1u << ST_REL_BITS) - 1u);
+    t.reserved = 0;
+    *reinterpret_cast<uint4 *>(t.shard_id) = shard;
+    return t;
+}
+__global__ __launch_bounds__(BLK) void k_gather_store(const keto_tuple *t, const uint32_t *idx, uint64_t n, uint2 *meta,
+                                                      uint4 *shard, unsigned long long *bad) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        const keto_tuple &x = t[idx[i]];
+        if (x.rel >> ST_REL_BITS || x.s_rel >> ST_REL_BITS || x.s_ns >> ST_NS_BITS || x.subj_kind > 1) atomicOr(bad, 1ull);
+        meta[i] = st_meta(x);
+        shard[i] = *reinterpret_cast<const uint4 *>(x.shard_id);
+    }
 }
 // run starts of the sorted keys: flag[i] = key[i] != key[i-1]
 __global__ __launch_bounds__(BLK) void k_run_flags(const uint64_t *k, uint64_t n, uint32_t *flag) {
@@ -179,7 +205,8 @@ struct Lookup {
     uint64_t m;
     const uint4 *index;           // k_index_fill table
     uint64_t index_mask;
-    const keto_tuple *tuples;
+    const uint2 *meta;            // the store (k_gather_store): subject + relations, and shard ids
+    const uint4 *shard;
     const uint64_t *req;          // requested keys, grouped by source rank
     const uint64_t *req_off;      // [world+1] request offsets per source
     const unsigned long long *subj_set;  // (source, subject id) hash set (k_subj_fill)
@@ -238,9 +265,9 @@ __device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
     }
     return lo;
 }
-__device__ __forceinline__ bool keep(const Lookup &L, const keto_tuple &t, uint32_t src) {
-    if (!L.filter || t.subj_kind == 1) return true;
-    const unsigned long long k = subj_key(src, t.s_obj);
+__device__ __forceinline__ bool keep(const Lookup &L, uint2 m, uint32_t src) {
+    if (!L.filter || (m.y >> 31)) return true;
+    const unsigned long long k = subj_key(src, m.x);
     const uint32_t b = subj_bit(k);
     if (!((L.subj_bits[b >> 5] >> (b & 31u)) & 1u)) return false;
     uint64_t h = mix64(k) & L.subj_mask;
@@ -256,7 +283,7 @@ __global__ __launch_bounds__(BLK) void k_lookup_count(Lookup L, uint64_t n, uint
         uint64_t b, e, c = 0;
         if (run_of(L, L.req[i], b, e)) {
             const uint32_t src = source_of(L, i);
-            for (uint64_t j = b; j < e; j++) c += keep(L, L.tuples[j], src) ? 1 : 0;
+            for (uint64_t j = b; j < e; j++) c += keep(L, L.meta[j], src) ? 1 : 0;
         }
         cnt[i] = c;
     }
@@ -267,8 +294,10 @@ __global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const
         if (!run_of(L, L.req[i], b, e)) continue;
         const uint32_t src = source_of(L, i);
         uint64_t o = pos[i];
-        for (uint64_t j = b; j < e; j++)
-            if (keep(L, L.tuples[j], src)) out[o++] = L.tuples[j];
+        for (uint64_t j = b; j < e; j++) {
+            const uint2 m = L.meta[j];
+            if (keep(L, m, src)) out[o++] = st_tuple(L.req[i], m, L.shard[j]);
+        }
     }
 }
 // One pass for a rank gathering for itself (no grouping by source needed): each request counts
@@ -282,7 +311,7 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, ket
         uint64_t b = 0, e = 0, c = 0, km = 0;  // km: which of a run's first 64 tuples are kept
         if (i < n && run_of(L, L.req[i], b, e))
             for (uint64_t j = b; j < e; j++)
-                if (keep(L, L.tuples[j], 0)) {
+                if (keep(L, L.meta[j], 0)) {
                     c++;
                     if (j - b < 64) km |= 1ull << (j - b);
                 }
@@ -303,8 +332,10 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, ket
             atomicOr(overflow, 1ull);
             continue;
         }
-        for (uint64_t j = b; j < e; j++)  // (the first pass's answers: no second probe of the filter)
-            if (j - b < 64 ? ((km >> (j - b)) & 1ull) : keep(L, L.tuples[j], 0)) out[o++] = L.tuples[j];
+        for (uint64_t j = b; j < e; j++) {  // (the first pass's answers: no second probe of the filter)
+            const uint2 m = L.meta[j];
+            if (j - b < 64 ? ((km >> (j - b)) & 1ull) : keep(L, m, 0)) out[o++] = st_tuple(L.req[i], m, L.shard[j]);
+        }
     }
 }
 
@@ -394,8 +425,9 @@ struct Partition {
     std::vector<const char *> ns_ptr, rel_ptr;
     std::string json;
     keto_snapshot_config cfg{};
-    // this rank's partition, sorted by object key: tuples[n], run keys ukeys[m], beg[m+1]
-    DevBuf tuples, ukeys, beg, index;
+    // this rank's partition, sorted by object key: store meta[n] + shard[n] (k_gather_store), run
+    // keys ukeys[m], beg[m+1]
+    DevBuf meta, shard, ukeys, beg, index;
     uint64_t n = 0, m = 0, index_mask = 0;
     hipStream_t hs = nullptr;
     keto_stream *kstream = nullptr;
@@ -616,7 +648,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         ensure(P.req_off, (W + 1) * 8);
         KETO_HIP(hipMemcpyAsync(P.req_off.p, roff.data(), (W + 1) * 8, hipMemcpyHostToDevice, P.hs));
         Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
-                 dptr<keto_tuple>(P.tuples),
+                 dptr<uint2>(P.meta), dptr<uint4>(P.shard),
                  dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<unsigned long long>(P.subj_set), P.subj_mask,
                  dptr<uint32_t>(P.subj_bits), W, filter ? 1 : 0};
         if (W == 1 && P.closure.p) {  // one rank: a single gathering pass into the closure (k_lookup_gather)
@@ -713,6 +745,8 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     if (!cfg) throw Error(KETO_E_INVALID, "null config");
     if (n && !tuples) throw Error(KETO_E_INVALID, "null tuples");
     if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "a partition holds at most 2^31 - 1 tuples");
+    if (cfg->n_relations > (1u << ST_REL_BITS) || cfg->n_namespaces > (1u << ST_NS_BITS))
+        throw Error(KETO_E_LIMIT, "a partitioned snapshot holds at most 1024 relation names and 2048 namespaces");
     auto P = std::make_unique<PartitionHandle>();
     P->device = cfg->device;
     KETO_HIP(hipSetDevice(P->device));
@@ -763,10 +797,18 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
         cub_call(Q, [&](void *tmp, size_t &b) {
             return hipcub::DeviceRadixSort::SortPairs(tmp, b, kin, kout, vin, vout, ni, 0, 64, Q.hs);
         });
-    Q.tuples = DevBuf(std::max<uint64_t>(1, n) * sizeof(keto_tuple));
-    if (n) hipLaunchKernelGGL(k_gather_tuples, grid_for(n), dim3(BLK), 0, Q.hs, src, vout, n, dptr<keto_tuple>(Q.tuples));
-    sync(Q);
+    Q.meta = DevBuf(std::max<uint64_t>(1, n) * sizeof(uint2));
+    Q.shard = DevBuf(std::max<uint64_t>(1, n) * sizeof(uint4));
+    ensure(Q.ctr, 64);
+    KETO_HIP(hipMemsetAsync(Q.ctr.p, 0, 8, Q.hs));
+    if (n)
+        hipLaunchKernelGGL(k_gather_store, grid_for(n), dim3(BLK), 0, Q.hs, src, vout, n, dptr<uint2>(Q.meta),
+                           dptr<uint4>(Q.shard), dptr<unsigned long long>(Q.ctr));
+    if (d2h_u64(Q, Q.ctr.p)) throw Error(KETO_E_INVALID, "partition tuple with a relation / namespace id past the store's fields");
     raw.reset();
+    k0 = DevBuf();  // (kout = k1 stays: the run boundaries below)
+    i0 = DevBuf();
+    i1 = DevBuf();
     // runs: one entry per object key
     DevBuf flag(std::max<uint64_t>(1, n + 1) * 4), fpos(std::max<uint64_t>(1, n + 1) * 8);
     KETO_HIP(hipMemsetAsync(flag.p, 0, (n + 1) * 4, Q.hs));

@@ -162,29 +162,42 @@ int ks_drive_tuples(const ks_drive_params *pp, keto_tuple *out, uint64_t n, int 
     return 0;
 }
 
-// The tuples whose object belongs to partition `part` of `nparts` (keto_object_owner), in
-// generation order: what one rank of a partitioned (config 5) job loads.  out == NULL only
-// counts.  Two passes over the index space (count per chunk, then fill at exact offsets), so
-// no partition ever needs the whole graph in host memory.
+// The tuples whose object belongs to partition `part` of `nparts` (keto_object_owner): what one
+// rank of a partitioned (config 5) job loads.  out == NULL only counts.  The walk is over
+// objects -- a node's parents + ACL tuples, a group's member tuples -- so the owner test runs
+// once per object and only the partition's own tuples are generated (every rank of an 8-way
+// job scans the object space, not the 4.2B-tuple index space); two passes (count per chunk,
+// then fill at exact offsets), so no partition ever needs the whole graph in host memory.
 int ks_drive_tuples_part(const ks_drive_params *pp, uint32_t nparts, uint32_t part, keto_tuple *out, uint64_t cap,
                          int threads, uint64_t *count) {
     ks_drive_layout L;
     if (ks_drive_layout_get(pp, &L) != 0 || nparts == 0 || part >= nparts || !count) return -1;
     const ks_drive_params p = *pp;
     const int T = std::max(1, std::min(threads, 64));
-    const uint64_t n = L.n_tuples;
+    const uint64_t n_obj = L.n_nodes + p.n_groups;  // objects: nodes, then groups
     std::vector<uint64_t> cnt(T + 1, 0);
     auto run = [&](bool fill) {
         std::vector<std::thread> th;
         for (int t = 0; t < T; t++)
             th.emplace_back([&, t] {
-                const uint64_t b = n * t / T, e = n * (t + 1) / T;
+                const uint64_t b = n_obj * t / T, e = n_obj * (t + 1) / T;
                 uint64_t c = 0, o = fill ? cnt[t] : 0;
-                for (uint64_t i = b; i < e; i++) {
-                    const keto_tuple x = drive_tuple(p, L, i);
-                    if (keto_object_owner(x.ns, x.obj, nparts) != part) continue;
-                    if (fill) out[o++] = x;
+                auto emit = [&](uint64_t i) {
+                    if (fill) out[o++] = drive_tuple(p, L, i);
                     c++;
+                };
+                for (uint64_t x = b; x < e; x++) {
+                    if (x < L.n_nodes) {
+                        if (keto_object_owner(node_ns(L, x), (uint32_t)x, nparts) != part) continue;
+                        const uint64_t r = x / L.nodes_per_root, cc = x % L.nodes_per_root;
+                        if (cc) emit(r * (L.nodes_per_root - 1) + cc - 1);
+                        for (uint64_t a = 0; a < p.acl_per_node; a++) emit(L.n_parent_tuples + x * p.acl_per_node + a);
+                    } else {
+                        const uint64_t g = x - L.n_nodes;
+                        if (keto_object_owner(NS_GROUP, (uint32_t)(L.gbase + g), nparts) != part) continue;
+                        for (uint64_t m = 0; m < p.members_per_group; m++)
+                            emit(L.n_parent_tuples + L.n_acl_tuples + g * p.members_per_group + m);
+                    }
                 }
                 if (!fill) cnt[t + 1] = c;
             });
@@ -197,6 +210,37 @@ int ks_drive_tuples_part(const ks_drive_params *pp, uint32_t nparts, uint32_t pa
     if (cap < cnt[T]) return -2;
     run(true);
     return 0;
+}
+
+// Every tuple of the given objects (keys = ns << 32 | obj), straight from the generator's index
+// space -- a node's parents tuple and its ACL tuples, a group's member tuples; users own none --
+// so a test can collect the closure of a batch on a multi-billion-tuple graph without holding
+// it.  out == NULL only counts; objects are emitted in key order, tuples in generation order.
+int ks_drive_object_tuples(const ks_drive_params *pp, const uint64_t *keys, uint64_t n, keto_tuple *out, uint64_t cap,
+                           uint64_t *count) {
+    ks_drive_layout L;
+    if (ks_drive_layout_get(pp, &L) != 0 || !count || (n && !keys)) return -1;
+    const ks_drive_params p = *pp;
+    uint64_t c = 0;
+    auto emit = [&](uint64_t i) {
+        if (out && c < cap) out[c] = drive_tuple(p, L, i);
+        c++;
+    };
+    for (uint64_t k = 0; k < n; k++) {
+        const uint32_t ns = (uint32_t)(keys[k] >> 32);
+        const uint64_t obj = (uint32_t)keys[k];
+        if ((ns == NS_FOLDER || ns == NS_FILE) && obj < L.n_nodes && node_ns(L, obj) == ns) {
+            const uint64_t r = obj / L.nodes_per_root, cc = obj % L.nodes_per_root;
+            if (cc) emit(r * (L.nodes_per_root - 1) + cc - 1);
+            for (uint64_t a = 0; a < p.acl_per_node; a++) emit(L.n_parent_tuples + obj * p.acl_per_node + a);
+        } else if (ns == NS_GROUP && obj >= L.gbase && obj < L.gbase + p.n_groups) {
+            const uint64_t g = obj - L.gbase;
+            for (uint64_t m = 0; m < p.members_per_group; m++)
+                emit(L.n_parent_tuples + L.n_acl_tuples + g * p.members_per_group + m);
+        }
+    }
+    *count = c;
+    return out && c > cap ? -2 : 0;
 }
 
 // view (80%) / edit checks: half name a user taken from a random user ACL tuple of the queried

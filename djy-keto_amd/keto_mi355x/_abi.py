@@ -54,7 +54,7 @@ class WorkCounters(ctypes.Structure):
 
 class FrontierStats(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint64) for k in ("batches", "queries", "routed", "goals", "generations",
-                                               "max_generations")]
+                                               "max_generations", "async_batches")]
 
 
 class DispatcherConfig(ctypes.Structure):
@@ -102,6 +102,8 @@ SIGNATURES = {
     "keto_stream_counters": (ctypes.c_int, [_VP, ctypes.POINTER(WorkCounters), _I32]),
     "keto_stream_last_kernel_ms": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double)]),
     "keto_stream_frontier_stats": (ctypes.c_int, [_VP, ctypes.POINTER(FrontierStats), _I32]),
+    "keto_host_alloc": (ctypes.c_int, [_U64, ctypes.POINTER(ctypes.c_void_p)]),
+    "keto_host_free": (ctypes.c_int, [_VP]),
     "keto_stream_kernel_time": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64), _I32]),
     "keto_check_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),
     "keto_expand_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _U64, _VP, _VP]),

@@ -199,6 +199,29 @@ class DeviceBuffer:
         self.free()
 
 
+class PinnedArray:
+    """numpy array over pinned host memory (keto_host_alloc): the buffers of KETO_F_ASYNC batches,
+    whose copies then run asynchronously on the stream."""
+
+    def __init__(self, n: int, dtype):
+        dtype = np.dtype(dtype)
+        self.nbytes = max(1, n * dtype.itemsize)
+        p = ctypes.c_void_p()
+        check(lib().keto_host_alloc(self.nbytes, ctypes.byref(p)))
+        self.ptr = p
+        buf = (ctypes.c_uint8 * self.nbytes).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=np.uint8, count=n * dtype.itemsize).view(dtype)
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            lib().keto_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
 class CheckEngine:
     """check.Engine over the GPU snapshot (limits = limit.max_read_depth/max_read_width)."""
 
@@ -218,6 +241,15 @@ class CheckEngine:
         check(lib().keto_check_batch(self.snapshot.handle, self.stream.handle, q.ctypes.data, len(q),
                                      ctypes.byref(self.limits), allowed.ctypes.data, err.ctypes.data, flags))
         return allowed, err
+
+    def check_batch_async(self, queries: np.ndarray, allowed: np.ndarray, err: np.ndarray):
+        """KETO_F_ASYNC over host buffers (pinned: PinnedArray): H2D of the queries, the kernels
+        and D2H of the decisions are enqueued on the stream and the call returns; the outputs are
+        valid after stream.sync()."""
+        assert queries.dtype == _abi.QUERY_DT and queries.flags.c_contiguous
+        assert len(allowed) >= len(queries) and len(err) >= len(queries)
+        check(lib().keto_check_batch(self.snapshot.handle, self.stream.handle, queries.ctypes.data, len(queries),
+                                     ctypes.byref(self.limits), allowed.ctypes.data, err.ctypes.data, _abi.F_ASYNC))
 
     def check_batch_device(self, d_queries: DeviceBuffer, n: int, d_allowed: DeviceBuffer, d_err: DeviceBuffer,
                            sync: bool = True, count_work: bool = False):

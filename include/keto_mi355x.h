@@ -136,7 +136,14 @@ typedef struct keto_stream keto_stream;
 
 /* flags for keto_check_batch / keto_expand_batch */
 #define KETO_F_DEVICE_PTRS 0x1u  /* query / output pointers are device memory */
-#define KETO_F_ASYNC 0x2u        /* enqueue only; pair with keto_stream_sync */
+/* KETO_F_ASYNC: enqueue only, no host synchronisation inside the call; pair with
+ * keto_stream_sync before reading the outputs.  With host buffers the copies in and out are
+ * enqueued on the stream too (pinned memory, keto_host_alloc, makes them truly asynchronous);
+ * the buffers must stay valid until the stream is synchronised.  The frontier engine launches
+ * the generations the stream's last synchronous batch needed plus a margin; a query deeper than
+ * that is answered by the DFS interpreter (same answers).  keto_frontier_stats counts these
+ * batches in async_batches only. */
+#define KETO_F_ASYNC 0x2u
 #define KETO_F_COUNT_WORK 0x4u   /* accumulate keto_work_counters on the stream */
 /* keto_check_batch: for KETO_QERR_NO_RELATION, out_err[i] = 1 | (relation name id << 8), the
  * relation ASTRelationFor rejected -- not always the query's own (a subject set deeper in the
@@ -171,7 +178,8 @@ int keto_stream_last_kernel_ms(keto_stream *s, double *ms);
  * decisive occurrence, the goal budget, the generation cap or the arena), goals spawned and
  * generations run (sum and max).  reset != 0 zeroes them afterwards. */
 typedef struct keto_frontier_stats {
-    uint64_t batches, queries, routed, goals, generations, max_generations;
+    uint64_t batches, queries, routed, goals, generations, max_generations;  /* synchronous batches */
+    uint64_t async_batches;  /* KETO_F_ASYNC batches (their counts stay on the device) */
 } keto_frontier_stats;
 int keto_stream_frontier_stats(keto_stream *s, keto_frontier_stats *out, int32_t reset);
 /* Synchronises the stream, then reports the summed device time (ms) and count of the main
@@ -317,6 +325,9 @@ int keto_partition_expand_result(keto_partition *p, keto_tree_node *out_nodes, u
 int keto_partition_stats_get(keto_partition *p, keto_partition_stats *out);
 int keto_partition_free(keto_partition *p);
 
+/* pinned host memory (hipHostMalloc) for the query / output buffers of KETO_F_ASYNC batches */
+int keto_host_alloc(uint64_t bytes, void **out);
+int keto_host_free(void *p);
 /* device memory helpers (for callers without their own allocator) */
 int keto_device_alloc(int32_t device, uint64_t bytes, void **out);
 int keto_device_free(void *p);

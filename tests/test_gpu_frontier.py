@@ -164,3 +164,32 @@ def test_every_query_routed_matches_oracle(budget):
     np.testing.assert_array_equal(gerr, err)
     np.testing.assert_array_equal(allowed, dec)
     assert fs["routed"] == len(q)
+
+
+@pytest.mark.parametrize("seed", [3, 17, 41])
+def test_async_batches_match_sync(seed):
+    """KETO_F_ASYNC: H2D, the speculated generations, the reductions, the DFS on the device-side
+    routed count and D2H are all enqueued with no host read-back; two streams' batches in flight
+    at once give the synchronous answers.  A fresh stream has no depth history (24 generations
+    speculated); the deep random worlds route what lies deeper and the interpreter answers it."""
+    w, t, q, _ = random_world(seed, rewrites=True)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(w.max_depth, w.max_width)
+    dec, err, _ = orc.check_batch(q, threads=4)
+    snap = product_snapshot(w, t)
+    qp = queries_to_product(q)
+    streams = [km.Stream(0), km.Stream(0)]
+    engs = [km.CheckEngine(snap, s, max_read_depth=w.max_depth, max_read_width=w.max_width) for s in streams]
+    qs = [km.PinnedArray(len(qp), km.QUERY_DT) for _ in range(2)]
+    outs = [(km.PinnedArray(len(qp), np.uint8), km.PinnedArray(len(qp), np.int32)) for _ in range(2)]
+    for i in range(2):
+        qs[i].array[:] = qp
+        engs[i].check_batch_async(qs[i].array, outs[i][0].array, outs[i][1].array)
+    for i in range(2):
+        streams[i].sync()
+        np.testing.assert_array_equal(outs[i][1].array, err)
+        np.testing.assert_array_equal(outs[i][0].array, dec)
+        fs = streams[i].frontier_stats()
+        assert fs["async_batches"] == 1 and fs["batches"] == 0
+    for s in streams:
+        s.close()

@@ -148,3 +148,23 @@ def test_collective_adapter_two_gloo_ranks():
         assert mx == 100 + world - 1
         assert rc1 == 0 and b == [7 * r + rank for r in range(world)]
         assert rc2 == 0 and v == 5 + world - 1
+
+
+def test_generator_rows_give_the_same_closure():
+    """synth.drive_object_tuples (the generator's rows of given objects, used for config 5 at x40
+    where the graph is never held whole) against the materialized graph: same closure, same rows"""
+    from closure_ref import closure
+    from keto_mi355x import synth
+    wl = synth.drive(depth=5, fanout=4, n_groups=2000, n_users=5000, seed=6)
+    q = synth.drive_queries(wl, 3000, seed=2)
+    sub = q["s_obj"][q["subj_kind"] == 0]
+    a = closure(wl.tuples, q["ns"], q["obj"], wl.max_depth + 1, subjects=sub)
+    b = closure(lambda k: synth.drive_object_tuples(wl, k), q["ns"], q["obj"], wl.max_depth + 1, subjects=sub)
+    assert len(a) == len(b) > 0
+    ka = np.sort(a.view(np.uint8).reshape(len(a), -1), axis=0)
+    kb = np.sort(b.view(np.uint8).reshape(len(b), -1), axis=0)
+    # same multiset of records (the generator emits objects in key order, the array in tuple order)
+    sa = np.unique(a.view(np.dtype((np.void, a.dtype.itemsize))))
+    sb = np.unique(b.view(np.dtype((np.void, b.dtype.itemsize))))
+    assert len(sa) == len(a) and np.array_equal(sa, sb)
+    assert ka.shape == kb.shape

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-3 GPU pass: the -m gpu suite without config 5 at x40, then config 5 at x40
+# (tests/test_gpu_c5.py), then the default bench line.  Every GPU step bounded; the first
+# failure ends the run.   usage: tools/gpu_r03_suite.sh [tag] [skip-c5]
+set -u
+cd "$(dirname "$0")/.." && mkdir -p gpurun_out && export TMPDIR=/tmp
+TAG=${1:-r03s}
+O=gpurun_out/$TAG && rm -rf $O && mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  --deselect tests/test_gpu_c5.py::test_c5_x40_eight_ranks_matches_oracle > $O/tests.log 2>&1
+rc=$?; tail -4 $O/tests.log
+[ $rc -ne 0 ] && { grep -E "Error|error|assert" $O/tests.log | head -30; exit $rc; }
+if [ -z "${2:-}" ]; then
+  timeout -k 10 900 python3 -u -m pytest -x -v -s --timeout 880 --timeout-method thread tests/test_gpu_c5.py > $O/c5x40.log 2>&1
+  rc=$?; grep -E "^\[c5|passed|failed|Error|assert|^[0-9] \{" $O/c5x40.log | tail -60
+  [ $rc -ne 0 ] && { tail -30 $O/c5x40.log; exit $rc; }
+fi
+timeout -k 10 300 python3 -u bench.py --no-cpu-baseline > $O/bench.log 2>&1 || { echo "bench failed"; tail -5 $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-600
