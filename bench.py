@@ -566,6 +566,9 @@ def main(argv=None):
     errs = de.download(stream, np.zeros(len(q), np.int32))
     assert (errs == 0).all(), "unexpected query errors"
 
+    dev = f"cuda:{device}" if dist_on else "cpu"
+    # (1) device-resident: queries already in HBM, one synchronous batch per step -- the kernels'
+    # own time (HIP events on the engine's stream around every batch's check path) for the roofline
     for _ in range(args.warmup):
         eng.check_batch_device(dq, len(q), da, de, sync=True)
     if dist_on:
@@ -581,10 +584,8 @@ def main(argv=None):
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
-    elapsed_local = time.perf_counter() - t_start
-    value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps,
-                                     f"cuda:{device}" if dist_on else "cpu")
-    ranks_ms = per_rank_ms(elapsed_local / args.steps * 1e3, f"cuda:{device}" if dist_on else "cpu")
+    resident_local = time.perf_counter() - t_start
+    resident_rate, resident_el, _ = job_rate(resident_local, args.batch * args.steps, dev)
     # average device time of a batch's check path over the timed region: HIP event pairs recorded
     # on the engine's own stream around every batch (rewrite snapshots: the frontier engine's
     # generations plus the DFS interpreter on the routed queries; C2: the union kernel's tier 0)
@@ -592,20 +593,61 @@ def main(argv=None):
     assert k_n == args.steps, f"timed {k_n} kernel launches, expected {args.steps}"
     kernel_ms = k_sum / k_n
     fr = stream.frontier_stats(reset=True)
-    # the timed batches' decisions (the measured path): the CPU parity sample checks these, and
-    # they must equal the counted batch's DFS decisions on the same queries
+    # the timed batches' decisions: they must equal the counted batch's DFS decisions on the same
+    # queries
     allowed = da.download(stream, np.zeros(len(q), np.uint8))
     errs = de.download(stream, np.zeros(len(q), np.int32))
     assert (errs == 0).all(), "unexpected query errors"
     dfs_mismatches = int((allowed != dfs_allowed).sum())
-
-    log(f"[rank {rank}] timed: {elapsed_local / args.steps * 1e3:.2f} ms/step, kernel {kernel_ms:.2f} ms "
+    log(f"[rank {rank}] device-resident: {resident_local / args.steps * 1e3:.2f} ms/step, kernel {kernel_ms:.2f} ms "
         f"({time.perf_counter() - t_setup:.1f}s since start)")
-    # PCIe-inclusive rate (host buffers: H2D queries, kernels, D2H decisions) -- never `value`
-    t1 = time.perf_counter()
-    for _ in range(3):
-        eng.check_batch(q)
-    pcie_rate = 3 * len(q) / (time.perf_counter() - t1)
+
+    # (2) `value` -- the metric's pipeline (BASELINE.md:46-51): per step a fresh seeded batch in
+    # (pinned) host memory, H2D of the queries + the check kernels + D2H of the decisions, all
+    # enqueued with KETO_F_ASYNC on two streams alternately, so batch k+1's copies overlap batch
+    # k's kernels.  Timed from the first enqueue to both streams drained.
+    nb = min(args.steps, 32)  # distinct batches (cycled beyond 32 steps)
+    if args.workload == "c2":
+        qgen = lambda k: synth.nested_groups_queries(wl, args.batch, seed=shard_seed(7, rank) + 1000 * (k + 1))  # noqa: E731
+    else:
+        qgen = lambda k: synth.drive_queries(wl, args.batch, seed=shard_seed(11, rank) + 1000 * (k + 1))  # noqa: E731
+    qb = [km.PinnedArray(args.batch, km.QUERY_DT) for _ in range(nb)]
+    ab = [km.PinnedArray(args.batch, np.uint8) for _ in range(nb)]
+    eb = [km.PinnedArray(args.batch, np.int32) for _ in range(nb)]
+    for k in range(nb):
+        qb[k].array[:] = qgen(k)
+    streams = [stream, km.Stream(device)]
+    engs = [eng, km.CheckEngine(snap, streams[1], max_read_depth=wl.max_depth, max_read_width=wl.max_width)]
+    engs[1].check_batch(qb[0].array)  # (a synchronous batch: the second stream learns the depth)
+    for k in range(max(1, args.warmup)):
+        engs[k % 2].check_batch_async(qb[k % nb].array, ab[k % nb].array, eb[k % nb].array)
+    for s_ in streams:
+        s_.sync()
+    for s_ in streams:
+        s_.kernel_time(reset=True)
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        engs[k % 2].check_batch_async(qb[k % nb].array, ab[k % nb].array, eb[k % nb].array)
+    for s_ in streams:
+        s_.sync()
+    if dist_on:
+        dist.barrier()
+    elapsed_local = time.perf_counter() - t_start
+    value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps, dev)
+    ranks_ms = per_rank_ms(elapsed_local / args.steps * 1e3, dev)
+    pipe_kernel = [s_.kernel_time(reset=True) for s_ in streams]
+    pipe_allowed = [ab[k].array.copy() for k in range(nb)]
+    pipe_err = np.concatenate([eb[k].array for k in range(nb)])
+    assert (pipe_err == 0).all(), "unexpected query errors"
+    # the pipeline's first batch again, synchronously on the device-resident path: same decisions
+    dq.upload(stream, qb[0].array)
+    eng.check_batch_device(dq, len(q), da, de, sync=True)
+    pipe_vs_resident = int((da.download(stream, np.zeros(len(q), np.uint8)) != pipe_allowed[0]).sum())
+    log(f"[rank {rank}] pipelined: {elapsed_local / args.steps * 1e3:.2f} ms/step "
+        f"({time.perf_counter() - t_setup:.1f}s since start)")
     # p99 batch latency over >= 100 batches of 64Ki queries (one rank's stream)
     lat = []
     nl = min(args.latency_batch, len(q))
@@ -657,8 +699,18 @@ def main(argv=None):
         "latency_batch": nl,
         "allowed_fraction": float(allowed.mean()),
         "timed_vs_dfs": {"n": int(len(q)), "mismatches": dfs_mismatches,
-                         "note": "timed batches' decisions vs the counted batch's DFS interpreter, same queries"},
-        "pcie_inclusive_checks_per_s": pcie_rate,
+                         "note": "device-resident batches' decisions vs the counted batch's DFS interpreter, same queries"},
+        "pipeline": {"what": "value: per step a fresh seeded batch in pinned host memory, H2D + check kernels + D2H "
+                             "enqueued (KETO_F_ASYNC) on two streams alternately; timed from the first enqueue until "
+                             "both streams drained",
+                     "distinct_batches": nb, "streams": 2,
+                     "kernel_ms_per_batch": [ks / max(1, kn) for ks, kn in pipe_kernel],
+                     "first_batch_vs_device_resident_mismatches": pipe_vs_resident,
+                     "allowed_fraction": float(np.mean([a.mean() for a in pipe_allowed]))},
+        "device_resident": {"checks_per_s": resident_rate, "ms_per_step": resident_el / args.steps * 1e3,
+                            "kernel_ms": kernel_ms,
+                            "what": "the same step with the queries already in HBM and outputs left there, one "
+                                    "synchronous batch per step (KETO_F_DEVICE_PTRS): the roofline's timing"},
         "serving": serving,
         "expand": expand,
         "snapshot_build_s": info["build_seconds"],
