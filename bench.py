@@ -284,14 +284,26 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
     xe = km.ExpandEngine(snap, stream, max_read_depth=wl.max_depth)
     nodes, offs, err = xe.build_trees(r)  # warm-up (sizes the output buffer)
     stream.counters(reset=True)
+    stream.expand_time(reset=True)
     t0 = time.perf_counter()
     for _ in range(reps):
         nodes, offs, err = xe.build_trees(r)
     dt = (time.perf_counter() - t0) / reps
     c = stream.counters(reset=True)
+    ms, nb = stream.expand_time(reset=True)
+    kms = ms / max(1, nb)
+    # algorithmic bytes: 8*rows + 4*edges + 12*out_nodes per batch
+    xbytes = (8 * c["rows"][0] + 4 * c["edges"][0] + 12 * c["out_nodes"][0]) / reps
     return {"roots_per_batch": n, "ms_per_batch": dt * 1e3, "trees_per_s": n / dt, "nodes_per_batch": int(offs[n]),
             "errors": int((err != 0).sum()), "max_read_depth": wl.max_depth,
-            "note": "host buffers in/out, count + emit passes; roots: Group#members and Folder#viewers"}
+            "traversal_kernel_ms": kms,
+            "roofline": {"bound": "hbm", "achieved": xbytes / (kms * 1e-3) / 1e9 if kms else None, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": xbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS if kms else None,
+                         "algorithmic_bytes_per_batch": xbytes,
+                         "bytes_model": "8*rows + 4*edges + 12*out_nodes (SURVEY.md 8.1 (d))",
+                         "kernel": "expand_wave (wave per root, one traversal) + fallback count pass if any"},
+            "note": "ms_per_batch: host roots in, trees out (API form, root order) incl. PCIe; roots: Group#members "
+                    "and Folder#viewers"}
 
 
 def serving_probe(km, snap, q, wl, clients: int, req: int, seconds: float):

@@ -52,6 +52,10 @@ Stream::~Stream() {
     if (union_scratch.mem) (void)hipFree(union_scratch.mem);
     if (frontier.mem) (void)hipFree(frontier.mem);
     if (frontier.host_ctrl) (void)hipHostFree(frontier.host_ctrl);
+    if (xw.mem) (void)hipFree(xw.mem);
+    if (xw.outbuf) (void)hipFree(xw.outbuf);
+    for (hipEvent_t e : xw.ev)
+        if (e) (void)hipEventDestroy(e);
     if (lists) (void)hipFree(lists);
     if (qbuf) (void)hipFree(qbuf);
     if (obuf) (void)hipFree(obuf);
@@ -234,6 +238,18 @@ int keto_stream_frontier_stats(keto_stream *hs, keto_frontier_stats *out, int32_
     });
 }
 
+int keto_stream_expand_time(keto_stream *hs, double *ms_sum, uint64_t *batches, int32_t reset) {
+    keto::Stream *s = ST(hs);
+    if (!s) return fail(KETO_E_INVALID, "null stream");
+    if (ms_sum) *ms_sum = s->xw.ms_sum;
+    if (batches) *batches = s->xw.batches;
+    if (reset) {
+        s->xw.ms_sum = 0;
+        s->xw.batches = 0;
+    }
+    return KETO_OK;
+}
+
 int keto_stream_last_kernel_ms(keto_stream *hs, double *ms) {
     keto::Stream *s = ST(hs);
     if (!s || !ms) return fail(KETO_E_INVALID, "null argument");
@@ -315,44 +331,11 @@ int keto_expand_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_
         KETO_HIP(hipSetDevice(s->device));
         out_offsets[0] = 0;
         if (n == 0) return;
-        // device buffers: roots | sizes | offsets | err
-        const size_t rb = (n * sizeof(keto_subject_set) + 255) / 256 * 256;
-        const size_t sb = (n * 8 + 255) / 256 * 256;
-        const size_t eb = (n * 4 + 255) / 256 * 256;
-        grow(s->qbuf, s->qbuf_bytes, rb + 2 * sb + eb);
-        char *base = static_cast<char *>(s->qbuf);
-        auto *d_roots = reinterpret_cast<keto_subject_set *>(base);
-        auto *d_sizes = reinterpret_cast<uint64_t *>(base + rb);
-        auto *d_offs = reinterpret_cast<uint64_t *>(base + rb + sb);
-        auto *d_err = reinterpret_cast<int32_t *>(base + rb + 2 * sb);
+        grow(s->qbuf, s->qbuf_bytes, n * sizeof(keto_subject_set));
+        auto *d_roots = static_cast<keto_subject_set *>(s->qbuf);
         KETO_HIP(hipMemcpyAsync(d_roots, roots, n * sizeof(keto_subject_set), hipMemcpyHostToDevice, s->stream));
-        keto::ExpandLaunch L{};
-        L.roots = d_roots;
-        L.n = n;
-        L.max_depth = lim.max_read_depth;
-        L.sizes = d_sizes;
-        L.offsets = d_offs;
-        L.err = d_err;
-        L.emit = false;
-        keto::run_expand(*snap, *s, L);  // pass 1: count nodes per tree
-        std::vector<uint64_t> sizes(n);
-        KETO_HIP(hipMemcpyAsync(sizes.data(), d_sizes, n * 8, hipMemcpyDeviceToHost, s->stream));
-        KETO_HIP(hipMemcpyAsync(out_err, d_err, n * 4, hipMemcpyDeviceToHost, s->stream));
-        KETO_HIP(hipStreamSynchronize(s->stream));
-        for (uint64_t i = 0; i < n; i++) out_offsets[i + 1] = out_offsets[i] + (out_err[i] ? 0 : sizes[i]);
-        const uint64_t total = out_offsets[n];
-        if (total > out_cap || (total && !out_nodes)) {
-            rc = fail(KETO_E_CAPACITY, "expand output needs " + std::to_string(total) + " nodes");
-            return;
-        }
-        if (total == 0) return;
-        grow(s->obuf, s->obuf_bytes, total * sizeof(keto_tree_node));
-        KETO_HIP(hipMemcpyAsync(d_offs, out_offsets, n * 8, hipMemcpyHostToDevice, s->stream));
-        L.emit = true;
-        L.out = static_cast<keto_tree_node *>(s->obuf);
-        keto::run_expand(*snap, *s, L);  // pass 2: emit pre-order nodes, already in API form
-        KETO_HIP(hipMemcpyAsync(out_nodes, s->obuf, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, s->stream));
-        KETO_HIP(hipStreamSynchronize(s->stream));
+        if (!keto::expand_batch(*snap, *s, d_roots, n, lim.max_read_depth, out_nodes, out_cap, out_offsets, out_err))
+            rc = fail(KETO_E_CAPACITY, "expand output needs " + std::to_string(out_offsets[n]) + " nodes");
     });
     return g != KETO_OK ? g : rc;
 }

@@ -150,6 +150,20 @@ struct Stream {
     void harvest();     // accumulate every completed pair (call after a stream sync)
     // device workspace (allocated on first use, never inside a launch sequence)
     Scratch check_scratch, union_scratch, expand_scratch;
+    // expand_wave workspace (expand.hip): per-wave staging, the batch's stage, per-root arrays
+    struct {
+        void *mem = nullptr, *roots_mem = nullptr;
+        uint64_t grid = 0, stage_cap = 0, ncap = 0;
+        keto_tree_node *priv = nullptr, *stage = nullptr, *outbuf = nullptr;
+        uint64_t out_cap = 0;
+        unsigned long long *sizes = nullptr, *soff = nullptr, *ctrl = nullptr;
+        uint64_t *offsets = nullptr;
+        int32_t *err = nullptr;
+        uint32_t *fb_list = nullptr;
+        hipEvent_t ev[2] = {nullptr, nullptr};  // around the traversal (expand_wave + the fallback's count pass)
+        double ms_sum = 0;
+        uint64_t batches = 0;
+    } xw;
     FrontierScratch frontier;
     // per-batch workspace of list_cap queries, one allocation:
     uint32_t *lists = nullptr;       // two overflow hand-off lists (of start-record positions)
@@ -204,8 +218,16 @@ struct ExpandLaunch {
     keto_tree_node *out;  // device nodes in API form (emit pass)
     int32_t *err;       // device [n]
     bool emit;
+    const uint32_t *list = nullptr, *list_count = nullptr;  // only these roots (device list + count; nl roots at most)
+    uint64_t nl = 0;
 };
+// the lane-per-root two-pass kernel (expand_kernel): expand_batch's fallback
 void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L);
+// keto_expand_batch's device path (expand_wave, fallback expand_kernel): the trees of the n
+// device roots into out_nodes (host, root order) with out_offsets / out_err; false (and the
+// offsets filled) when out_cap is too small
+bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth,
+                  keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets, int32_t *out_err);
 
 // treefmt.cpp: Expand trees -> API form (Mapper.ToTree + JSON / Tree.ToProto), host only
 void trees_to_json(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,

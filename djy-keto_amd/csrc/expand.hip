@@ -1,9 +1,22 @@
-// gfx950 batched Expand (expand/engine.go:54-124): one lane per root, explicit DFS stack,
-// global per-call visited set (root included), two passes -- count, then emit into the
-// exclusive-scan offsets -- so the pre-order output needs no device-side allocation.
+// gfx950 batched Expand (expand/engine.go:54-124).
+//
+// expand_wave (the default): one wavefront per root.  The walk is the reference's DFS in
+// pre-order -- a child's subtree is finished before its next sibling is looked at, because the
+// visited set (global per call, root included, :69-72, :112-117) decides what a later sibling
+// becomes -- but every row is read by the whole wave at once: 64 entries per coalesced load,
+// with the entries' own loads (row bounds, visited alias, the API form's entity and relation
+// name) issued together.  Only the decision per subject-set entry (visited? expand?) is
+// sequential, in LDS: the visited set (open addressing) and the DFS stack live there.  Nodes are
+// written once, in pre-order, to the wave's staging region; a finished tree moves to the batch's
+// stage in one coalesced copy, and the host's offsets place the trees in root order.
+//
+// expand_kernel: one lane per root, two passes (count, emit), per-lane visited tables in HBM --
+// the fallback for the rare root whose visited set, stack or tree outgrows expand_wave's LDS /
+// staging space (tiered scratch up to 2^23 visited nodes).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "device_common.hpp"
 
@@ -194,6 +207,207 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams P) {
     }
 }
 
+constexpr uint32_t XW_VIS = 2048;   // visited keys per wave (LDS, half full at most)
+constexpr uint32_t XW_STACK = 64;   // DFS frames per wave (LDS): the walk is at most max_read_depth deep
+constexpr uint32_t XW_PRIV = 8192;  // staged nodes per wave; a larger tree goes to the fallback
+constexpr uint32_t XW_EMPTY = NONE32;
+#ifdef KETO_CPUEMU
+constexpr uint32_t XWW = 1;  // the CPU emulation runs one-lane waves (tools/cpuemu)
+#else
+constexpr uint32_t XWW = 64;  // wavefront width: the lanes that read one row chunk
+#endif
+
+struct ExpandWaveParams {
+    DevSnapshot s;
+    const keto_subject_set *roots;
+    uint32_t n;
+    int32_t max_depth;
+    uint32_t priv_cap;              // <= XW_PRIV (tests lower it: KETO_XW_PRIV, mixed wave / fallback batches)
+    keto_tree_node *priv;           // [grid][XW_PRIV]: the tree being walked
+    keto_tree_node *stage;          // finished trees, in completion order
+    unsigned long long stage_cap;
+    unsigned long long *stage_top;
+    unsigned long long *sizes, *soff;  // [n]: nodes of each tree, its offset in `stage` (NONE: fallback)
+    int32_t *err;
+    uint32_t *next;                 // root queue
+    uint32_t *fb_list, *fb_count;   // roots for expand_kernel
+    unsigned long long *counters;   // rows, edges, -, out nodes
+};
+
+// one root per wavefront: see the file comment
+__global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
+    __shared__ uint32_t vis[XW_VIS];
+    __shared__ uint4 stk[XW_STACK];
+    const DevSnapshot &s = P.s;
+    const uint32_t lane = threadIdx.x;
+    keto_tree_node *priv = P.priv + (size_t)blockIdx.x * XW_PRIV;
+    unsigned long long c_rows = 0, c_edges = 0, c_out = 0;
+    for (;;) {
+        uint32_t q = 0;
+        if (lane == 0) q = atomicAdd(P.next, 1u);
+        q = __shfl(q, 0);
+        if (q >= P.n) break;
+        for (uint32_t i = lane; i < XW_VIS; i += XWW) vis[i] = XW_EMPTY;
+        __syncthreads();
+        const keto_subject_set R = P.roots[q];
+        int32_t d = R.max_depth;
+        if (d <= 0 || P.max_depth < d) d = P.max_depth;  // :56-58
+        const uint32_t root = resolve_node(s, R.ns, R.obj, R.rel);
+        uint32_t cnt = 0, vcount = 0, sp = 0;
+        uint64_t rows = 0, edges = 0;
+        bool fail = false;
+        // visited check-and-insert (CheckAndAddVisited), in walk order: lane 0 decides, all learn
+        auto visit = [&](uint32_t key) -> bool {
+            uint32_t seen = 0;
+            if (lane == 0) {
+                uint32_t h = (uint32_t)mix64(key) & (XW_VIS - 1);
+                for (;;) {
+                    const uint32_t v = vis[h];
+                    if (v == key) {
+                        seen = 1;
+                        break;
+                    }
+                    if (v == XW_EMPTY) {
+                        if (2 * (vcount + 1) > XW_VIS) seen = 2;  // table full: the fallback walks this root
+                        else vis[h] = key;
+                        break;
+                    }
+                    h = (h + 1) & (XW_VIS - 1);
+                }
+            }
+            seen = __shfl(seen, 0);
+            if (seen == 2) fail = true;
+            else if (!seen) vcount++;
+            return seen == 1;
+        };
+        if (!(root & VIRT_BIT)) {
+            uint32_t key = root;
+            if (s.vkey && ri_shared(node_ri(s, root))) key = s.vkey[root];
+            visit(key);  // the root is visited (:69-72)
+            const uint32_t b = s.all_off[root], e = s.all_off[root + 1];
+            rows++;
+            if (b != e) {  // no tuples on the first page -> nil (:97-99)
+                if (lane == 0) priv[0] = api_node(s, d <= 1 ? 4u : 1u, SKEY_SET | root, d <= 1 ? 0u : e - b);  // :101-104
+                cnt = 1;
+                uint4 top = make_uint4(b, e, (uint32_t)d, 0);
+                while (d > 1 && !fail) {
+                    if (top.x == top.y) {
+                        if (sp == 0) break;
+                        top = stk[--sp];
+                        continue;
+                    }
+                    // the next (up to) 64 entries of the row, and each entry's own loads, together
+                    const uint32_t m = std::min<uint32_t>(XWW, top.y - top.x);
+                    const bool in = lane < m;
+                    const uint32_t sk = in ? s.all_subj[top.x + lane] : 0u;
+                    const bool set = in && (sk & SKEY_SET);
+                    uint32_t ck = 0, cb = 0, ce = 0;
+                    keto_tree_node nd{};
+                    if (in) nd = api_node(s, 4, sk, 0);
+                    if (set) {
+                        const uint32_t c = sk & ~SKEY_SET;
+                        ck = c;
+                        if (s.vkey && ri_shared(node_ri(s, c))) ck = s.vkey[c];
+                        cb = s.all_off[c];
+                        ce = s.all_off[c + 1];
+                    }
+                    const unsigned long long setm = __ballot(set);
+                    uint32_t pos = 0;
+                    for (;;) {
+                        const unsigned long long rest = pos < XWW ? setm & (~0ull << pos) : 0ull;
+                        const uint32_t j = rest ? (uint32_t)__ffsll((long long)rest) - 1 : m;
+                        // subject ids before the next subject set: leaves (:60-67), written together
+                        const uint32_t nl = j - pos;
+                        if (lane >= pos && lane < j && cnt + (lane - pos) < P.priv_cap) priv[cnt + (lane - pos)] = nd;
+                        cnt += nl;
+                        edges += nl;
+                        if (cnt > P.priv_cap) {
+                            fail = true;
+                            break;
+                        }
+                        if (j >= m) {
+                            top.x += m;
+                            break;
+                        }
+                        // the subject set at j, in walk order
+                        const uint32_t ckj = __shfl(ck, j), cbj = __shfl(cb, j), cej = __shfl(ce, j);
+                        edges++;
+                        pos = j + 1;
+                        keto_tree_node leaf = nd;  // (lane j's record)
+                        bool expand = false;
+                        if (!visit(ckj)) {  // a revisit is nil -> a leaf (:112-117)
+                            if (fail) break;
+                            rows++;
+                            expand = cbj != cej && top.z - 1 > 1;
+                        }
+                        if (lane == j) {
+                            if (expand) {
+                                leaf.type = 1;
+                                leaf.n_children = cej - cbj;
+                            }
+                            if (cnt < P.priv_cap) priv[cnt] = leaf;
+                        }
+                        if (++cnt > P.priv_cap) {
+                            fail = true;
+                            break;
+                        }
+                        if (expand) {  // the child's subtree before the next sibling
+                            if (sp >= XW_STACK) {
+                                fail = true;
+                                break;
+                            }
+                            if (lane == 0) stk[sp] = make_uint4(top.x + pos, top.y, top.z, 0);
+                            sp++;
+                            top = make_uint4(cbj, cej, top.z - 1, 0);
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();  // (the wave's LDS writes before the next root clears them)
+        unsigned long long off = 0;
+        if (!fail && cnt) {
+            if (lane == 0) off = atomicAdd(P.stage_top, (unsigned long long)cnt);
+            off = __shfl(off, 0);
+            if (off + cnt > P.stage_cap) fail = true;
+        }
+        if (fail) {
+            if (lane == 0) {
+                P.soff[q] = ~0ull;
+                P.fb_list[atomicAdd(P.fb_count, 1u)] = q;
+            }
+            continue;
+        }
+        for (uint32_t i = lane; i < cnt; i += XWW) P.stage[off + i] = priv[i];
+        if (lane == 0) {
+            P.sizes[q] = cnt;
+            P.soff[q] = off;
+            P.err[q] = 0;
+        }
+        c_rows += rows;
+        c_edges += edges;
+        c_out += cnt;
+    }
+    if (P.counters && lane == 0) {
+        atomicAdd(&P.counters[0], c_rows);
+        atomicAdd(&P.counters[1], c_edges);
+        atomicAdd(&P.counters[3], c_out);
+    }
+}
+
+// trees from the stage into their root-order positions of the output
+__global__ __launch_bounds__(256) void expand_place(const keto_tree_node *stage, const unsigned long long *soff,
+                                                    const unsigned long long *sizes, const uint64_t *offsets, uint32_t n,
+                                                    keto_tree_node *out) {
+    for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
+        const unsigned long long so = soff[q];
+        if (so == ~0ull) continue;  // a fallback root: expand_kernel's emit pass writes it
+        const unsigned long long c = sizes[q];
+        for (unsigned long long i = threadIdx.x; i < c; i += blockDim.x) out[offsets[q] + i] = stage[so + i];
+    }
+}
+
 }  // namespace
 
 void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
@@ -211,8 +425,8 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
         ExpandParams P{};
         P.s = s.dev;
         P.roots = L.roots;
-        P.qlist = tier == 0 ? nullptr : list[tier - 1];
-        P.qlist_count = tier == 0 ? nullptr : &sc.ctrl[3 + tier - 1];
+        P.qlist = tier == 0 ? L.list : list[tier - 1];
+        P.qlist_count = tier == 0 ? L.list_count : &sc.ctrl[3 + tier - 1];
         P.n = (uint32_t)L.n;
         P.max_depth = L.max_depth;
         P.sizes = reinterpret_cast<unsigned long long *>(L.sizes);
@@ -237,14 +451,140 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
         // lane's DFS then shares its wave's issue with fewer divergent walks
         P.live_lanes = 64;
         if (tier == 0) {
-            const uint64_t waves = lanes / 64;
-            P.live_lanes = (uint32_t)std::min<uint64_t>(64, (L.n + waves - 1) / waves);
-            lanes = (uint32_t)std::min<uint64_t>(lanes, (L.n + P.live_lanes - 1) / P.live_lanes * 64);
+            const uint64_t waves = lanes / 64, nr = L.list ? L.nl : L.n;
+            P.live_lanes = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, (nr + waves - 1) / waves));
+            lanes = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(lanes, (nr + P.live_lanes - 1) / P.live_lanes * 64));
         }
         const uint32_t bs = std::min<uint32_t>(tier == 0 ? 64 : BLOCK, lanes);  // every launched lane owns scratch
         hipLaunchKernelGGL(expand_kernel, dim3(lanes / bs), dim3(bs), 0, st.stream, P);
         KETO_HIP(hipGetLastError());
     }
+}
+
+static size_t xal(size_t b) { return (b + 255) / 256 * 256; }
+
+bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth,
+                  keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets, int32_t *out_err) {
+    out_offsets[0] = 0;
+    if (n == 0) return true;
+    if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
+    auto &X = st.xw;
+    const uint32_t cus = (uint32_t)num_cus(s.device);
+    const uint64_t grid = (uint64_t)cus * 8;  // 8 one-wave blocks per CU (a few KB of LDS each)
+    if (!X.mem || X.ncap < n) {
+        if (X.mem) KETO_HIP(hipFree(X.mem));
+        X.mem = nullptr;
+        uint64_t nc = 1;
+        while (nc < n) nc <<= 1;
+        const uint64_t sc = std::max<uint64_t>(X.stage_cap, 1u << 22);
+        const size_t bytes = xal(64) + xal(grid * XW_PRIV * sizeof(keto_tree_node)) + xal(sc * sizeof(keto_tree_node)) +
+                             3 * xal(nc * 8) + xal(nc * 4) + xal(nc * 4);
+        KETO_HIP(hipMalloc(&X.mem, bytes));
+        char *p = static_cast<char *>(X.mem);
+        X.ctrl = reinterpret_cast<unsigned long long *>(p);
+        p += xal(64);
+        X.priv = reinterpret_cast<keto_tree_node *>(p);
+        p += xal(grid * XW_PRIV * sizeof(keto_tree_node));
+        X.stage = reinterpret_cast<keto_tree_node *>(p);
+        p += xal(sc * sizeof(keto_tree_node));
+        X.sizes = reinterpret_cast<unsigned long long *>(p);
+        p += xal(nc * 8);
+        X.soff = reinterpret_cast<unsigned long long *>(p);
+        p += xal(nc * 8);
+        X.offsets = reinterpret_cast<uint64_t *>(p);
+        p += xal(nc * 8);
+        X.err = reinterpret_cast<int32_t *>(p);
+        p += xal(nc * 4);
+        X.fb_list = reinterpret_cast<uint32_t *>(p);
+        X.grid = grid;
+        X.stage_cap = sc;
+        X.ncap = nc;
+    }
+    KETO_HIP(hipMemsetAsync(X.ctrl, 0, 64, st.stream));
+    // KETO_EXPAND_WAVE=0 (A/B, tests): every root through the lane kernel
+    const char *ew = getenv("KETO_EXPAND_WAVE");
+    const bool wave = !(ew && ew[0] == '0');
+    ExpandWaveParams P{};
+    P.s = s.dev;
+    P.roots = d_roots;
+    P.n = (uint32_t)n;
+    P.max_depth = max_depth;
+    const char *pc = getenv("KETO_XW_PRIV");
+    P.priv_cap = pc ? (uint32_t)std::max(1, std::min(atoi(pc), (int)XW_PRIV)) : XW_PRIV;
+    P.priv = X.priv;
+    P.stage = X.stage;
+    P.stage_cap = X.stage_cap;
+    P.stage_top = X.ctrl;
+    P.next = reinterpret_cast<uint32_t *>(X.ctrl + 1);
+    P.fb_count = reinterpret_cast<uint32_t *>(X.ctrl + 2);
+    P.fb_list = X.fb_list;
+    P.sizes = X.sizes;
+    P.soff = X.soff;
+    P.err = X.err;
+    P.counters = st.counters;
+    if (!X.ev[0]) {
+        KETO_HIP(hipEventCreate(&X.ev[0]));
+        KETO_HIP(hipEventCreate(&X.ev[1]));
+    }
+    KETO_HIP(hipEventRecord(X.ev[0], st.stream));
+    if (wave) {
+        hipLaunchKernelGGL(expand_wave, dim3((uint32_t)std::min<uint64_t>(grid, n)), dim3(XWW), 0, st.stream, P);
+        KETO_HIP(hipGetLastError());
+    } else {
+        KETO_HIP(hipMemsetAsync(X.soff, 0xFF, n * 8, st.stream));
+    }
+    unsigned long long h[3] = {0, 0, 0};
+    KETO_HIP(hipMemcpyAsync(h, X.ctrl, 24, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipStreamSynchronize(st.stream));
+    const uint32_t nfb = wave ? (uint32_t)h[2] : (uint32_t)n;
+    ExpandLaunch F{};
+    F.roots = d_roots;
+    F.n = n;
+    F.max_depth = max_depth;
+    F.sizes = reinterpret_cast<uint64_t *>(X.sizes);
+    F.offsets = X.offsets;
+    F.err = X.err;
+    F.list = wave ? X.fb_list : nullptr;
+    F.list_count = wave ? P.fb_count : nullptr;
+    F.nl = nfb;
+    if (nfb) {  // roots past the wave kernel's LDS / staging space: the lane kernel counts them
+        F.emit = false;
+        run_expand(s, st, F);
+    }
+    KETO_HIP(hipEventRecord(X.ev[1], st.stream));
+    std::vector<unsigned long long> sizes(n);
+    KETO_HIP(hipMemcpyAsync(sizes.data(), X.sizes, n * 8, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipMemcpyAsync(out_err, X.err, n * 4, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipStreamSynchronize(st.stream));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, X.ev[0], X.ev[1]) == hipSuccess) {
+        X.ms_sum += ms;
+        X.batches++;
+    }
+    for (uint64_t i = 0; i < n; i++) out_offsets[i + 1] = out_offsets[i] + (out_err[i] ? 0 : sizes[i]);
+    const uint64_t total = out_offsets[n];
+    if (h[0] > X.stage_cap / 2) X.stage_cap = std::max<uint64_t>(X.stage_cap, 2 * h[0]), X.ncap = 0;  // (regrown next batch)
+    if (total > out_cap || (total && !out_nodes)) return false;
+    if (total == 0) return true;
+    if (X.out_cap < total) {
+        if (X.outbuf) KETO_HIP(hipFree(X.outbuf));
+        X.outbuf = nullptr;
+        X.out_cap = 0;
+        KETO_HIP(hipMalloc(&X.outbuf, total * sizeof(keto_tree_node)));
+        X.out_cap = total;
+    }
+    KETO_HIP(hipMemcpyAsync(X.offsets, out_offsets, n * 8, hipMemcpyHostToDevice, st.stream));
+    hipLaunchKernelGGL(expand_place, dim3((uint32_t)std::min<uint64_t>(n, cus * 16)), dim3(256), 0, st.stream, X.stage, X.soff,
+                       X.sizes, X.offsets, (uint32_t)n, X.outbuf);
+    KETO_HIP(hipGetLastError());
+    if (nfb) {
+        F.emit = true;
+        F.out = X.outbuf;
+        run_expand(s, st, F);
+    }
+    KETO_HIP(hipMemcpyAsync(out_nodes, X.outbuf, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipStreamSynchronize(st.stream));
+    return true;
 }
 
 }  // namespace keto

@@ -103,6 +103,7 @@ SIGNATURES = {
     "keto_stream_last_kernel_ms": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double)]),
     "keto_stream_frontier_stats": (ctypes.c_int, [_VP, ctypes.POINTER(FrontierStats), _I32]),
     "keto_host_alloc": (ctypes.c_int, [_U64, ctypes.POINTER(ctypes.c_void_p)]),
+    "keto_stream_expand_time": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64), _I32]),
     "keto_host_free": (ctypes.c_int, [_VP]),
     "keto_stream_kernel_time": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64), _I32]),
     "keto_check_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),

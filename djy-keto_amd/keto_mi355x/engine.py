@@ -153,6 +153,12 @@ class Stream:
         check(lib().keto_stream_frontier_stats(self.handle, ctypes.byref(c), int(reset)))
         return {k: int(getattr(c, k)) for k, _ in c._fields_}
 
+    def expand_time(self, reset: bool = False) -> tuple:
+        """(ms summed, batches) of the Expand traversals on this stream (keto_stream_expand_time)"""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        check(lib().keto_stream_expand_time(self.handle, ctypes.byref(ms), ctypes.byref(n), int(reset)))
+        return ms.value, n.value
+
     def kernel_time(self, reset: bool = False) -> tuple:
         """(summed main-kernel ms, launches) timed with HIP events on this stream"""
         ms, n = ctypes.c_double(), ctypes.c_uint64()

@@ -187,6 +187,11 @@ int keto_stream_frontier_stats(keto_stream *s, keto_frontier_stats *out, int32_t
  * included); reset != 0 zeroes the sums afterwards. */
 int keto_stream_kernel_time(keto_stream *s, double *ms_sum, uint64_t *launches, int32_t reset);
 
+/* Device time (ms, HIP events on the stream) of the Expand traversals since the last reset:
+ * the wave-per-root kernel plus, for roots it hands on, the fallback's count pass -- not the
+ * copies placing the trees in root order. */
+int keto_stream_expand_time(keto_stream *s, double *ms_sum, uint64_t *batches, int32_t reset);
+
 /* Check n queries: out_allowed[i] = CheckIsMember's bool, out_err[i] = error code.
  * Replaces check.Engine.CheckIsMember (engine.go:65-71) for a whole batch. */
 int keto_check_batch(keto_snapshot *snap, keto_stream *s, const keto_query *queries, uint64_t n,

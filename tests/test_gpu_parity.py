@@ -1,5 +1,7 @@
 """GPU parity: the HIP engine (through the C ABI) against the reference's known answers
 and against the oracle on the same seeded inputs.  Integer/boolean work: bit-exact."""
+import os
+
 import numpy as np
 import pytest
 
@@ -412,3 +414,47 @@ def test_regrouped_interpreter_drive(stream, regroup_forced):
     np.testing.assert_array_equal(e, err)
     assert (c["rows"], c["edges"], c["probes"]) == (st.rows, st.edges, st.probes)
     assert c["per_tier"]["queries"][0] > 0
+
+
+@pytest.mark.parametrize("mode", ["wave", "mixed", "lane"])
+def test_expand_drive_trees_wave_and_fallback(stream, mode):
+    """Expand on a Drive world: the wave-per-root kernel (every root), a batch where trees larger
+    than a lowered staging capacity fall back to the lane kernel (both paths in one batch, placed
+    in root order), and the lane kernel alone -- exact trees, child order included, vs the oracle"""
+    from keto_mi355x import synth
+    wl = synth.drive(depth=5, n_groups=400, members_per_group=6, n_users=3000, seed=13)
+    w, t = world_from_workload(wl)
+    orc = refsem.Oracle(w, t)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    rng = np.random.default_rng(3)
+    n = 300
+    roots = np.zeros(n, dtype=km.SUBJSET_DT)
+    h = n // 2
+    roots["ns"][:h], roots["rel"][:h] = wl.ns_names.index("Group"), wl.rel_names.index("members")
+    roots["obj"][:h] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], h)
+    roots["ns"][h:], roots["rel"][h:] = wl.ns_names.index("Folder"), wl.rel_names.index("viewers")
+    roots["obj"][h:] = rng.integers(0, wl.meta["folders_per_root"], n - h)
+    roots["max_depth"] = rng.integers(0, 8, n)
+    env = {"wave": {}, "mixed": {"KETO_XW_PRIV": "12"}, "lane": {"KETO_EXPAND_WAVE": "0"}}[mode]
+    old = {k: os.environ.get(k) for k in ("KETO_XW_PRIV", "KETO_EXPAND_WAVE")}
+    os.environ.update(env)
+    try:
+        nodes, offs, err = km.ExpandEngine(snap, stream, max_read_depth=6).build_trees(roots)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert (err == 0).all()
+    big = 0
+    for i, r in enumerate(roots):
+        d = int(r["max_depth"])
+        on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), d if 0 < d <= 6 else 6)
+        mine = nodes[int(offs[i]):int(offs[i + 1])]
+        assert len(mine) == len(on), i
+        big += len(on) > 12
+        for f_p, f_o in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"),
+                         ("s_rel", "srel"), ("n_children", "n_children")):
+            np.testing.assert_array_equal(mine[f_p], on[f_o])
+    assert big > 10  # the mixed batch really sends trees to the fallback
