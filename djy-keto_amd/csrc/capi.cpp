@@ -52,6 +52,9 @@ Stream::~Stream() {
     if (union_scratch.mem) (void)hipFree(union_scratch.mem);
     if (frontier.mem) (void)hipFree(frontier.mem);
     if (frontier.host_ctrl) (void)hipHostFree(frontier.host_ctrl);
+    if (frontier_block.mem) (void)hipFree(frontier_block.mem);
+    if (frontier_block.fb_list) (void)hipFree(frontier_block.fb_list);
+    if (frontier_block.host) (void)hipHostFree(frontier_block.host);
     if (xw.mem) (void)hipFree(xw.mem);
     if (xw.outbuf) (void)hipFree(xw.outbuf);
     for (hipEvent_t e : xw.ev)

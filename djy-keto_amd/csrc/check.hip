@@ -525,16 +525,20 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         run_dfs(s, st, L, nullptr, nullptr, L.n, true);
         return;
     }
+    // KETO_FR_ENGINE=gen: the generation engine (frontier.hip, A/B); default: the block engine
+    const char *ee = getenv("KETO_FR_ENGINE");
+    const bool gen = ee && ee[0] == 'g';
     st.mark_begin();
     run_resolve(s, st, L.queries, L.n, L.max_depth, false);
     for (uint64_t off = 0; off < L.n; off += FR_MAX_BATCH) {
         CheckLaunch Lp = L;
         Lp.n = std::min<uint64_t>(FR_MAX_BATCH, L.n - off);
-        const uint32_t routed = run_frontier(s, st, Lp, off);
+        const uint32_t routed = gen ? run_frontier(s, st, Lp, off) : run_frontier_block(s, st, Lp, off);
+        const uint32_t *fl = gen ? st.frontier.fb_list : st.frontier_block.fb_list;
+        const uint32_t *fc = gen ? st.frontier.fb_count : st.frontier_block.fb_count;
         // asynchronous: the interpreter is sized for the whole pass and reads the routed count on
         // the device (its lanes find an empty list and leave)
-        if (routed) run_dfs(s, st, L, st.frontier.fb_list, st.frontier.fb_count, routed == FR_ROUTED_ON_DEVICE ? Lp.n : routed,
-                            false);
+        if (routed) run_dfs(s, st, L, fl, fc, routed == FR_ROUTED_ON_DEVICE ? Lp.n : routed, false);
     }
     st.mark_end();
 }

@@ -136,6 +136,15 @@ struct FrontierScratch {
     keto_frontier_stats stats{};
 };
 
+// per-stream workspace of the block frontier engine (frontier_block.hip)
+struct FrontierBlockScratch {
+    void *mem = nullptr, *gpool = nullptr, *opool = nullptr;
+    uint32_t *ctrl = nullptr, *host = nullptr;  // host: pinned read-back of ctrl
+    uint32_t gpool_cap = 0, opool_cap = 0;
+    uint32_t *fb_list = nullptr, *fb_count = nullptr;
+    uint64_t fb_cap = 0;
+};
+
 struct Stream {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -165,6 +174,7 @@ struct Stream {
         uint64_t batches = 0;
     } xw;
     FrontierScratch frontier;
+    FrontierBlockScratch frontier_block;
     // per-batch workspace of list_cap queries, one allocation:
     uint32_t *lists = nullptr;       // two overflow hand-off lists (of start-record positions)
     uint4 *resolved = nullptr;       // 2 x 16 B start record per query, longest-first (resolve.hip)
@@ -208,6 +218,9 @@ void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // r
 constexpr uint64_t FR_MAX_BATCH = 1ull << 21;
 constexpr uint32_t FR_ROUTED_ON_DEVICE = 0xFFFFFFFFu;  // run_frontier, asynchronous: the count stays on the device
 uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint64_t pos_base);
+// frontier_block.hip: the same evaluation with a workgroup per chunk of queries (the default
+// engine); routed batch positions in st.frontier_block.fb_list
+uint32_t run_frontier_block(const Snapshot &s, Stream &st, const CheckLaunch &L, uint64_t pos_base);
 
 struct ExpandLaunch {
     const keto_subject_set *roots;  // device

@@ -43,18 +43,8 @@
 namespace keto {
 namespace {
 
-constexpr uint32_t M_UNK = 0, M_IS = 1, M_NOT = 2;
-__device__ __forceinline__ uint32_t mk_err(uint32_t e) { return e << 8; }
-__device__ __forceinline__ bool decisive(uint32_t r) { return (r >> 8) != 0 || (r & 3u) == M_IS; }
+#include "frontier_goal.inc"
 
-enum GoalKind : uint32_t { G_IA = 0, G_ES = 1, G_RW = 2, G_TTU = 3, G_INV = 4, G_DEAD = 7 };
-constexpr uint32_t GD_MAX = 0xFFFu;
-constexpr uint32_t GF_SKIP = 1u << 15, GF_ESCHILD = 1u << 16, GF_ALIAS = 1u << 17;
-// gfn.y: children (< 2^24) | reduce op << 24
-enum ReduceOp : uint32_t { R_FIRST = 0, R_AND = 1, R_NOT = 2, R_FIRST_AND = 3 };  // (R_FIRST_AND: and_merge)
-constexpr uint32_t NC_MAX = (1u << 24) - 1;
-constexpr uint32_t GFN_CHAIN = 1u << 28;  // gfn.y: an ES goal that ran its one child's expand-subject
-constexpr uint32_t MAX_GEN = 192;
 // The arena is cut into FR_SHARDS slices of `scap` goals; a block spawns into slice
 // blockIdx % FR_SHARDS, so the allocation counters of a generation are FR_SHARDS addresses,
 // not one (a single counter serialises every block's atomic: ~60M/s).  A generation is the
@@ -64,9 +54,6 @@ constexpr uint32_t GEN_STRIDE = MAX_GEN + 2;
 // ctrl: gbase[FR_SHARDS][GEN_STRIDE] | gcount[FR_SHARDS][GEN_STRIDE] | fallback count (+3) |
 // occurrence counts[FR_SHARDS]
 constexpr size_t FR_CTRL_BYTES = (2 * FR_SHARDS * GEN_STRIDE + 4 + FR_SHARDS) * 4;
-__device__ __forceinline__ uint32_t gword(uint32_t kind, uint32_t d, uint32_t op = 0, uint32_t flags = 0) {
-    return (d & GD_MAX) | (kind << 12) | flags | (op << 16);
-}
 
 struct FrontierParams {
     DevSnapshot s;
@@ -109,57 +96,9 @@ struct FrontierParams {
 #define FR_MARK(n) ((void)0)
 #endif
 
-// the query subject's membership test (checkDirect / the found-lookahead / the IN shortcut):
-// a short reverse row sits in the start record, a long one is answered by the probe hash
-struct Subject {
-    uint32_t sidx;
-    bool heavy;
-    uint4 R;
-};
 __device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_t pos) {
-    const uint4 b = P.start[2 * (size_t)pos + 1];  // one load: resolve.hip packs a heavy subject here too
-    return Subject{b.x, b.y == START_R_HEAVY, b};
+    return subject_of(P.start[2 * (size_t)pos + 1]);  // one load
 }
-// can node c's rows hold the query subject at all: a subject id needs a slot with subject-id
-// tuples, a subject set one with subject-set tuples (RI_IDROWS / RI_SETROWS, per snapshot).
-// Only a heavy subject's probe is worth skipping (a light one's entries are registers, and its
-// record holds them in place of the subject index).
-__device__ __forceinline__ bool may_hold(const DevSnapshot &s, const Subject &q, uint32_t ri) {
-    return !q.heavy || (q.sidx < s.n_uuids ? ri_idrows(ri) : ri_setrows(ri));
-}
-__device__ __forceinline__ bool member(const DevSnapshot &s, const Subject &q, uint32_t c) {
-    if (!q.heavy) return c == q.R.x || c == q.R.y || c == q.R.z || c == q.R.w;
-    const uint64_t fb = subj_filter_bits(c), f = (uint64_t)q.R.z | ((uint64_t)q.R.w << 32);
-    if ((f & fb) != fb) return false;  // not in the subject's reverse row: no probe load
-    const uint64_t key = (((uint64_t)q.sidx << 32) | c) + 1;
-    uint32_t b = (uint32_t)mix64(key) & s.probe_mask;
-    for (;;) {  // the table keeps empty slots: every probe sequence ends
-        const uint4 v = s.probe[b];
-        const uint64_t k0 = (uint64_t)v.x | ((uint64_t)v.y << 32), k1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
-        if (k0 == key || k1 == key) return true;
-        if (k0 == 0 || k1 == 0) return false;
-        b = (b + 1) & s.probe_mask;
-    }
-}
-
-// the edges [cur, end) of a subject-set row in shard order, through 16-byte windows; the
-// row descriptor holds its first two edges
-struct Edges {
-    const uint32_t *dst;
-    uint32_t cur, end, lo, hi;
-    uint4 w;
-    __device__ __forceinline__ Edges(const DevSnapshot &s, const uint4 &row)
-        : dst(s.set_dst), cur(row.x), end(row.y), lo(row.x), hi(row.x + 2), w(make_uint4(row.z, row.w, 0, 0)) {}
-    __device__ __forceinline__ uint32_t next() {  // caller checks cur < end
-        if (cur < lo || cur >= hi) {
-            w = *win(dst, cur);
-            lo = cur - (uint32_t)((reinterpret_cast<uintptr_t>(dst + cur) >> 2) & 3);
-            hi = lo + 4;
-        }
-        return wword(w, cur++ - lo);
-    }
-};
-
 // Decisive-key table: keys carry the batch's epoch (1..TAB_EPOCHS) in bits 61-63 (scope < 2^29:
 // a goal index), so the table is cleared once every TAB_EPOCHS batches instead of after each one:
 // a slot holding 0 or another epoch's key is free.  Within a batch a slot only ever goes from
@@ -195,101 +134,6 @@ __device__ __forceinline__ int64_t tab_insert(unsigned long long *tk, uint32_t m
     return -1;
 }
 
-// A sub-check checkIsAllowed(c, dc, skip) shaped when its parent spawns it (oracle u_sub): a
-// relation with a rewrite is an IA goal; one without is decided on the spot (dc <= 0: Unknown;
-// an error; a direct tuple: IsMember) or is just its expand-subject, an ES(dc-1) goal -- or
-// NotMember when no row of the relation holds a subject set.  `esf` (an ES's children:
-// GF_ESCHILD [| GF_ALIAS]) makes an error a goal too, so every decisive occurrence of a scope
-// key is a goal, and goes into the word.  word != 0: spawn it; else `leaf` is the result.
-// `row`: what is known of c's own subject-set row -- ROW_ANY (nothing: its relation's flag
-// decides), ROW_EMPTY (an ES child's edge says so, EDGE_LEAF), ROW_LOAD (load it): an
-// expand-subject of an empty row is NotMember, decided here (oracle u_sub `node_check`).
-enum RowHint : uint32_t { ROW_ANY = 0, ROW_EMPTY = 1, ROW_LOAD = 2 };
-struct Sub {
-    uint32_t word, leaf;
-};
-__device__ __forceinline__ Sub sub_check(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t c, uint32_t dc,
-                                         bool skip, uint32_t esf, uint32_t row = ROW_ANY) {
-    if (dc == 0) return Sub{0, M_UNK};
-    const NodeInfo ni = t_node_info(T, c);
-    const bool err = ri_status(ni.ri) == REL_ERROR;
-    if (ri_rw(ni.ri) && !esf) {
-        // with neither a direct check (engine.go:239-243) nor an expand-subject (:244-246) to
-        // run, checkIsAllowed is its rewrite's result (an OR / AND never yields a bare Unknown):
-        // the RW goal is spawned in the IA's place, one generation earlier (oracle u_sub)
-        const bool direct = !s.strict && !skip && dc > 1 && !(c & VIRT_BIT) && may_hold(s, q, ni.ri) && member(s, q, c);
-        if (!direct && !(ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri))) return Sub{gword(G_RW, dc, ri_op(ni.ri)), 0};
-    }
-    if (ri_rw(ni.ri) || (err && esf)) return Sub{gword(G_IA, dc, 0, (skip ? GF_SKIP : 0u) | esf), 0};
-    if (err) return Sub{0, mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, c, ni) << 16)};
-    if (!skip && dc > 1 && !(c & VIRT_BIT) && may_hold(s, q, ni.ri) && member(s, q, c)) return Sub{0, M_IS};
-    if (ri_ss(ni.ri) && dc > 1 && ri_setrows(ni.ri)) {
-        if (row == ROW_EMPTY || (row == ROW_LOAD && ((c & VIRT_BIT) || s.set_row[c].x == s.set_row[c].y))) return Sub{0, M_NOT};
-        return Sub{gword(G_ES, dc - 1, 0, esf), 0};
-    }
-    return Sub{0, M_NOT};
-}
-// the row hint of an ES child from its edge
-__device__ __forceinline__ uint32_t edge_row(const DevSnapshot &s, uint32_t raw) {
-    return (s.edge_leaf && (raw & EDGE_LEAF)) ? ROW_EMPTY : ROW_ANY;
-}
-
-// AND maps a non-member (an error kept) to NotMember (binop.go:52-54)
-__device__ __forceinline__ uint32_t and_map(uint32_t x) { return ((x >> 8) != 0 || (x & 3u) != M_IS) ? ((x & ~3u) | M_NOT) : x; }
-
-// A NOT decided where it is spawned (a malformed NOT, a computed userset that is a leaf, a
-// rewrite at rest depth 0) is folded into its parent: its result, or NONE32 when it must be an
-// INV goal (oracle u_inv_folds; the G_INV case of fr_expand evaluates the same way)
-__device__ __forceinline__ uint32_t inv_leaf(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
-                                             uint32_t op, uint32_t d) {
-    const Op o = T.ops[op];
-    if (o.child_count != 1) return mk_err(KETO_QERR_NOT_IMPLEMENTED);
-    const Op ch = T.ops[T.op_children[o.child_begin]];
-    const uint32_t ct = ch.type_kind & 0xFFu;
-    uint32_t leaf = NONE32;
-    if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
-    else if (ct == OP_CSS) {
-        const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
-        if (!sb.word) leaf = sb.leaf;
-    }
-    if (leaf == NONE32) return NONE32;
-    const uint32_t m = leaf & 3u;  // NOT: IsMember <-> NotMember, Unknown / errors kept (rewrites.go:183-199)
-    return m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
-}
-
-// An AND at rest depth d > 1 whose children are one nested OR (a goal at d-1, rewrites.go:118)
-// and leaves that are all IsMember without an error is that OR mapped through AND (and_map; the
-// OR never yields a bare Unknown): the AND's goal runs the OR's items itself, reduced by
-// R_FIRST_AND, and no goal is spawned for the OR (oracle u_and_merge).  Returns the OR's op,
-// NONE32 when the AND is not of that form.  One goal and one generation less per level of
-// `(a | b | parents.traverse(...)) & !banned`.
-__device__ __forceinline__ uint32_t and_merge(const DevSnapshot &s, const Tables &T, const Subject &q, uint32_t node,
-                                              const NodeInfo &ni, const Op &o, uint32_t d) {
-#ifdef KETO_FR_NOMERGE  // measurement builds only (tools/ab)
-    return NONE32;
-#endif
-    if (d <= 1) return NONE32;
-    uint32_t orop = NONE32;
-    for (uint32_t c = 0; c < o.child_count; c++) {
-        const uint32_t ci = T.op_children[o.child_begin + c];
-        const Op ch = T.ops[ci];
-        const uint32_t ct = ch.type_kind & 0xFFu;
-        if (ct == OP_REWRITE) {
-            if (orop != NONE32 || ((ch.type_kind >> 8) & 0xFFu) != OPK_OR) return NONE32;
-            orop = ci;
-        } else if (ct == OP_CSS) {
-            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
-            if (sb.word || sb.leaf != M_IS) return NONE32;
-        } else if (ct == OP_INVERT) {
-            if (inv_leaf(s, T, q, node, ci, d) != M_IS) return NONE32;
-        } else {
-            return NONE32;  // a tuple-to-userset is always a goal
-        }
-    }
-    return orop;
-}
-
-
 __device__ __forceinline__ uint32_t tab_hash(unsigned long long key, uint32_t mask) {
     return (uint32_t)mix64(key & ((1ull << 61) - 1ull)) & mask;  // the epoch does not move a key
 }
@@ -314,18 +158,6 @@ __device__ __forceinline__ void spawn(const FrontierParams &P, uint32_t c, uint3
     P.g0[c] = make_uint4(node, pos, word, scope);
 }
 
-
-// wave-wide exclusive prefix sum of v; *total = the wave's sum
-__device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t &total) {
-    uint32_t x = v;
-    const uint32_t lane = __lane_id();
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
-    total = __shfl(x, 63);
-    return x - v;
-}
 
 // a generation's slices: exclusive prefix of their counts and their slice-local bases (LDS)
 struct GenMap {
@@ -355,6 +187,18 @@ __device__ __forceinline__ uint32_t gen_goal(const FrontierParams &P, const GenM
     return lo * P.scap + m.base[lo] + (j - m.pre[lo]);
 }
 
+// the generation engine's sink: goal records into the arena, occurrences into the sliced list
+struct GlobalSink {
+    const FrontierParams &P;
+    __device__ __forceinline__ void spawn(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope) const {
+        P.g0[c] = make_uint4(node, pos, word, scope);
+    }
+    __device__ __forceinline__ void spawn_es(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope,
+                                             uint32_t) const {
+        spawn(c, node, pos, word, scope);
+    }
+    __device__ __forceinline__ void occ(uint32_t o, uint32_t scope, uint32_t key) const { P.occ[o] = make_uint2(scope, key); }
+};
 // generation 0: query position i in slice i / chunk
 __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -468,254 +312,11 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         const Subject q = live ? load_subject(P, pos) : Subject{0, false, make_uint4(0, 0, 0, 0)};
         FR_MARK(0);
         // ---- phase A: decide, or count the children -------------------------------------------
-        uint32_t nc = 0, val = M_NOT;  // value if nc == 0, else the partial (tail) for fr_reduce
-        uint32_t rop = kind == G_INV ? R_NOT : R_FIRST;
-        uint32_t pat = 0;              // per kind: which children (phase B regenerates them)
-        uint32_t sc = scope, xrel = 0;
-        bool chain = false;            // G_ES: the one child's expand-subject runs in this goal
-        if (live) {
-            switch (kind) {
-            case G_IA: {  // checkIsAllowed (engine.go:214-249)
-                if (d == 0) {
-                    val = M_UNK;
-                    break;
-                }
-                const NodeInfo ni = t_node_info(T, node);
-                if (ri_status(ni.ri) == REL_ERROR) {  // :228-232
-                    val = mk_err(KETO_QERR_NO_RELATION) | (t_relname(s, T, node, ni) << 16);
-                    break;
-                }
-                const bool rw = ri_rw(ni.ri);
-                bool direct = false;
-                if ((!s.strict || !rw) && !(w & GF_SKIP) && d > 1 && !(node & VIRT_BIT) && may_hold(s, q, ni.ri))  // :239-243
-                    direct = member(s, q, node);
-                // expand-subject(d-1) (:244-246), unless no row of the relation holds a subject set
-                const bool es = ri_ss(ni.ri) && d > 1 && !direct && ri_setrows(ni.ri);
-                pat = (rw ? 1u : 0u) | (es ? 2u : 0u);
-                xrel = ri_op(ni.ri);
-                nc = (rw ? 1u : 0u) + (es ? 1u : 0u);
-                val = nc == 0 ? (direct ? M_IS : M_NOT) : (direct ? M_IS : NONE32);
-                break;
-            }
-            case G_ES: {  // checkExpandSubject (engine.go:102-164)
-                if (row.x == row.y) break;  // (virtual nodes have no row)
-                uint32_t keep = row.y - row.x;
-                if (keep > W) keep = W > 0 ? W - 1 : 0;  // results[:maxWidth-1] (engine.go:141-150)
-                Edges it(s, row);
-                bool found = false;  // found-lookahead over every row (traverser.go:73-80, 109-111)
-                uint32_t cw = 0;
-                for (uint32_t e = 0; it.cur < it.end && !found; e++) {
-                    const uint32_t raw = it.next(), c = raw & s.edge_mask;
-                    found = member(s, q, c);
-                    if (e < keep) {
-                        cw = sub_check(s, T, q, c, d, true, GF_ESCHILD, edge_row(s, raw)).word;
-                        if (cw) nc++;  // the children that are goals
-                    }
-                }
-                if (found) {
-                    val = M_IS;
-                    nc = 0;
-                    break;
-                }
-                if (scope == NONE32) sc = i;  // graph.InitVisited (graph_utils.go:38-43)
-                if (row.y - row.x == 1 && keep == 1 && cw && ((cw >> 12) & 7u) == G_ES) {
-                    // chain (oracle u_es): the one child is an expand-subject goal; run its
-                    // expand-subject here instead -- its key stays an occurrence of the scope,
-                    // its children are this goal's, and this goal's result is the child's
-                    const uint4 rc = s.set_row[row.z & s.edge_mask];
-                    uint32_t kc = rc.y - rc.x;
-                    if (kc > W) kc = W > 0 ? W - 1 : 0;
-                    Edges ic(s, rc);
-                    bool fc = false;
-                    nc = 0;
-                    for (uint32_t e = 0; ic.cur < ic.end && !fc; e++) {
-                        const uint32_t raw = ic.next(), g = raw & s.edge_mask;
-                        fc = member(s, q, g);
-                        if (e < kc && sub_check(s, T, q, g, d - 1, true, GF_ESCHILD, edge_row(s, raw)).word) nc++;
-                    }
-                    if (fc) {  // the child's found-lookahead: IsMember, only the child's key is an occurrence
-                        nc = 0;
-                        kc = 0;
-                    }
-                    chain = true;
-                    pat = kc;
-                    val = fc ? M_IS : (nc ? NONE32 : M_NOT);
-                    xrel = 1;  // phase B writes the occurrences
-                    break;
-                }
-                pat = keep;
-                val = nc ? NONE32 : M_NOT;  // (leaf children are NotMember: they only mark their key)
-                xrel = (!nc && keep) ? 1u : 0u;  // phase B still marks the leaf children's keys
-                break;
-            }
-            case G_RW: {  // checkSubjectSetRewrite (rewrites.go:33-134) + or/and (binop.go:18-73)
-                if (d == 0) {
-                    val = M_UNK;
-                    break;
-                }
-                const Op o = T.ops[op];
-                const uint32_t okind = (o.type_kind >> 8) & 0xFFu;
-                if (okind == OPK_BAD) {  // :58-59
-                    val = mk_err(KETO_QERR_NOT_IMPLEMENTED);
-                    break;
-                }
-                const bool is_or = okind == OPK_OR;
-                const NodeInfo ni = t_node_info(T, node);
-                uint32_t tail = NONE32;
-                xrel = NONE32;  // OR: parents of the stopping TTU item phase B spawns (NONE32: all)
-                uint32_t xop = op, xd = d;  // the OR whose items run here (an and_merge: the AND's OR)
-                const uint32_t mo = is_or ? NONE32 : and_merge(s, T, q, node, ni, o, d);
-                if (mo != NONE32) {
-                    xop = mo;
-                    xd = d - 1;
-                    rop = R_FIRST_AND;
-                }
-                if (is_or || mo != NONE32) {  // the flattened items (layout.hpp IT_*), nested ORs spliced in
-                    const uint32_t oi = T.op_items[xop], end = (oi & 0xFFFFu) + (oi >> 16);
-                    uint32_t it = oi & 0xFFFFu;
-                    while (it < end) {
-                        const uint2 item = T.or_items[it];
-                        const uint32_t ik = it_kind(item.x), kk = it_k(item.x);
-                        if (ik == IT_NEST) {  // a nested OR at rest depth d - k <= 0 is Unknown (:39-42)
-                            it = xd <= kk ? it_end(item.x) : it + 1;
-                            continue;
-                        }
-                        const uint32_t dk = xd - kk;
-                        uint32_t leaf = NONE32;
-                        if (ik == IT_SHORT) {  // the IN shortcut (rewrites.go:62-92, traverser.go:123-191)
-                            const Op x = T.ops[item.y];
-                            for (uint32_t c = 0; c < x.child_count; c++) {
-                                const Op ch = T.ops[T.op_children[x.child_begin + c]];
-                                if ((ch.type_kind & 0xFFu) != OP_CSS) continue;
-                                const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
-                                if (t & VIRT_BIT) continue;
-                                if (s.strict) {  // traverser.go:137-139
-                                    const NodeInfo ti = t_node_info(T, t);
-                                    if (ri_status(ti.ri) == REL_DECLARED && ri_rw(ti.ri)) continue;
-                                }
-                                if (member(s, q, t)) {
-                                    leaf = M_IS;
-                                    break;
-                                }
-                            }
-                        } else if (ik == IT_CAND) {  // checkIsAllowed(c, d-1, skipDirect) (rewrites.go:88-90)
-                            if (dk > 1) {
-                                const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, item.y), dk - 1, true, 0, ROW_LOAD);
-                                if (sb.word) nc++;
-                                else leaf = sb.leaf;
-                            }
-                        } else if (ik == IT_RW) {
-                            if (dk > 1) nc++;  // nested AND: its own goal at d-1 (:118)
-                        } else if (ik == IT_TTU) {
-                            // spliced: a tuple-to-userset is the first decisive of its parents'
-                            // checks in row order, so they are this OR's own items (rewrites.go:
-                            // 242-293; oracle u_or_items); d - 1 <= 0 makes each one Unknown
-                            if (dk > 1) {
-                                const uint32_t rc = T.ops[item.y].rel_computed;
-                                const uint32_t ts = t_sibling(T, node, ni, rc & 0xFFFFu);
-                                if (!(ts & VIRT_BIT)) {
-                                    Edges et(s, s.set_row[ts]);
-                                    for (uint32_t e = 0; et.cur < et.end; e++) {
-                                        const uint32_t pn = et.next() & s.edge_mask;
-                                        const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), rc >> 16), dk - 1, false, 0);
-                                        if (sb.word) nc++;
-                                        else if (decisive(sb.leaf)) {
-                                            leaf = sb.leaf;
-                                            xrel = e;
-                                            break;
-                                        }
-                                    }
-                                }
-                            }
-                        } else {  // NOT: a leaf when decided here, else its own goal
-                            leaf = inv_leaf(s, T, q, node, item.y, dk);
-                            if (leaf == NONE32) nc++;
-                        }
-                        if (leaf != NONE32 && decisive(leaf)) {  // binop.go:23-26: nothing after it runs
-                            tail = leaf;
-                            break;
-                        }
-                        it++;
-                    }
-                    pat = it;  // fr_expand's second walk stops here
-                } else {
-                    rop = R_AND;
-                    // the children in AST order, up to a leaf that decides the group
-                    uint32_t kend = o.child_count;
-                    for (uint32_t c = 0; c < o.child_count; c++) {
-                        const Op ch = T.ops[T.op_children[o.child_begin + c]];
-                        const uint32_t ct = ch.type_kind & 0xFFu;
-                        uint32_t leaf = NONE32;
-                        if (ct == OP_REWRITE && d <= 1) leaf = M_UNK;  // nested rewrite at d-1 <= 0 (:39-42)
-                        else if (ct == OP_CSS) {  // checkComputedSubjectSet (rewrites.go:208-230)
-                            const Sub sb = sub_check(s, T, q, t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu), d, false, 0);
-                            if (!sb.word) leaf = sb.leaf;
-                        } else if (ct == OP_INVERT)
-                            leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin + c], d);
-                        if (leaf == NONE32) {
-                            nc++;
-                            continue;
-                        }
-                        if ((leaf >> 8) != 0 || (leaf & 3u) != M_IS) {  // binop.go:52-54
-                            tail = (leaf & ~3u) | M_NOT;
-                            kend = c;
-                            break;
-                        }
-                    }
-                    pat = kend;
-                }
-                if (nc == 0) val = tail != NONE32 ? tail : ((!is_or && mo == NONE32 && o.child_count > 0) ? M_IS : M_NOT);
-                else val = tail;
-                if (mo != NONE32 && nc == 0) val = and_map(val);
-                break;
-            }
-            case G_TTU: {  // checkTupleToSubjectSet (rewrites.go:242-293)
-                // row: the tupleset relation's row (none when virtual, or when d <= 1 makes every
-                // parent check Unknown); each parent: checkIsAllowed(S#computed, d-1) (:279-288)
-                xrel = T.ops[op].rel_computed >> 16;
-                Edges it(s, row);
-                uint32_t tail = NONE32, e = 0;
-                for (; it.cur < it.end; e++) {
-                    const uint32_t pn = it.next() & s.edge_mask;
-                    const Sub sb = sub_check(s, T, q, t_sibling(T, pn, t_node_info(T, pn), xrel), d - 1, false, 0);
-                    if (sb.word) nc++;
-                    else if (decisive(sb.leaf)) {
-                        tail = sb.leaf;
-                        e++;
-                        break;
-                    }
-                }
-                pat = e;  // parents phase B walks
-                val = nc ? tail : (tail != NONE32 ? tail : M_NOT);
-                break;
-            }
-            case G_INV: {  // checkInverted (rewrites.go:136-200)
-                const Op o = T.ops[op];
-                if (o.child_count != 1) {
-                    val = mk_err(KETO_QERR_NOT_IMPLEMENTED);
-                    break;
-                }
-                const Op ch = T.ops[T.op_children[o.child_begin]];
-                const uint32_t ct = ch.type_kind & 0xFFu;
-                uint32_t leaf = NONE32;
-                if (ct == OP_REWRITE && d == 0) leaf = M_UNK;
-                else if (ct == OP_CSS) {
-                    const Sub sb = sub_check(s, T, q, t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu), d, false, 0);
-                    if (!sb.word) leaf = sb.leaf;
-                } else if (ct == OP_INVERT) leaf = inv_leaf(s, T, q, node, T.op_children[o.child_begin], d);  // folded inner NOT
-                if (leaf != NONE32) {  // NOT of a result known now: IsMember <-> NotMember, Unknown / errors kept
-                    const uint32_t m = leaf & 3u;
-                    val = m == M_IS ? ((leaf & ~3u) | M_NOT) : (m == M_NOT ? ((leaf & ~3u) | M_IS) : leaf);
-                    break;
-                }
-                nc = 1;
-                val = NONE32;
-                break;
-            }
-            default:
-                val = mk_err(KETO_QERR_INTERNAL);
-            }
-        }
+        const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W);
+        uint32_t nc = pa.nc, val = pa.val;
+        const uint32_t rop = pa.rop, pat = pa.pat, sc = pa.sc, xrel = pa.xrel;
+        const bool chain = pa.chain;
+        (void)sc;
         if (nc > NC_MAX) {  // a row too long for the record: the DFS interpreter takes the query
             route(P, pos);
             nc = 0;
@@ -764,119 +365,11 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         oc += so * P.ocap;
         FR_MARK(3);
         // ---- phase B: write the children (the same walk as phase A) -------------------------------
-        if (nc || (kind == G_ES && xrel)) switch (kind) {
-        case G_IA:
-            if (pat & 1u) spawn(P, cb, node, pos, gword(G_RW, d, xrel), scope);
-            if (pat & 2u) spawn(P, cb + ((pat & 1u) ? 1 : 0), node, pos, gword(G_ES, d - 1), scope);
-            break;
-        case G_ES: {
-            uint4 r = row;
-            uint32_t o0 = oc, dd = d;
-            if (chain) {  // the one child: its key, then its row's children one level down
-                const uint32_t rawc = row.z, cc = rawc & s.edge_mask;
-                if (occ_ok) P.occ[oc] = make_uint2(sc, (rawc & EDGE_ALIAS) ? s.vkey[cc] : cc);
-                r = s.set_row[cc];
-                o0 = oc + 1;
-                dd = d - 1;
-            }
-            Edges it(s, r);
-            uint32_t c = cb;
-            for (uint32_t e = 0; e < pat; e++) {
-                const uint32_t raw = it.next(), cn = raw & s.edge_mask;
-                const uint32_t esf = GF_ESCHILD | ((raw & EDGE_ALIAS) ? GF_ALIAS : 0u);
-                // checkIsAllowed(c, d, skipDirect) (:161); every child's key is an occurrence
-                const Sub sb = sub_check(s, T, q, cn, dd, true, esf, edge_row(s, raw));
-                if (sb.word && nc) spawn(P, c++, cn, pos, sb.word, sc);
-                if (occ_ok) P.occ[o0 + e] = make_uint2(sc, (raw & EDGE_ALIAS) ? s.vkey[cn] : cn);
-            }
-            break;
-        }
-        case G_RW: {
-            const Op o = T.ops[op];
-            const NodeInfo ni = t_node_info(T, node);
-            uint32_t c = cb;
-            const bool is_or = ((o.type_kind >> 8) & 0xFFu) == OPK_OR;
-            const uint32_t mo = (is_or || rop != R_FIRST_AND) ? NONE32 : and_merge(s, T, q, node, ni, o, d);
-            if (is_or || mo != NONE32) {
-                const uint32_t xop = is_or ? op : mo, xd = is_or ? d : d - 1;
-                uint32_t it = T.op_items[xop] & 0xFFFFu;
-                while (it < pat || (it == pat && xrel != NONE32)) {  // (+ the stopping TTU item's parents)
-                    const uint2 item = T.or_items[it];
-                    const uint32_t ik = it_kind(item.x), kk = it_k(item.x);
-                    if (ik == IT_NEST) {
-                        it = xd <= kk ? it_end(item.x) : it + 1;
-                        continue;
-                    }
-                    const uint32_t dk = xd - kk;
-                    if (ik == IT_CAND) {
-                        if (dk > 1) {
-                            const uint32_t t = t_sibling(T, node, ni, item.y);
-                            const Sub sb = sub_check(s, T, q, t, dk - 1, true, 0, ROW_LOAD);
-                            if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
-                        }
-                    } else if (ik == IT_TTU) {
-                        if (dk > 1) {
-                            const uint32_t rc = T.ops[item.y].rel_computed;
-                            const uint32_t ts = t_sibling(T, node, ni, rc & 0xFFFFu);
-                            if (!(ts & VIRT_BIT)) {
-                                Edges et(s, s.set_row[ts]);
-                                const uint32_t lim = it == pat ? xrel : NONE32;
-                                for (uint32_t e = 0; et.cur < et.end && e < lim; e++) {
-                                    const uint32_t pn = et.next() & s.edge_mask;
-                                    const uint32_t t = t_sibling(T, pn, t_node_info(T, pn), rc >> 16);
-                                    const Sub sb = sub_check(s, T, q, t, dk - 1, false, 0);
-                                    if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
-                                }
-                            }
-                        }
-                    } else if (ik == IT_INV) {
-                        if (inv_leaf(s, T, q, node, item.y, dk) == NONE32) spawn(P, c++, node, pos, gword(G_INV, dk, item.y), scope);
-                    }
-                    else if (ik == IT_RW && dk > 1) spawn(P, c++, node, pos, gword(G_RW, dk - 1, item.y), scope);
-                    it++;
-                }
-                break;
-            }
-            for (uint32_t k2 = 0; k2 < pat; k2++) {  // AND: rewrites.go:95-129
-                const uint32_t ci = T.op_children[o.child_begin + k2];
-                const Op ch = T.ops[ci];
-                const uint32_t ct = ch.type_kind & 0xFFu;
-                if (ct == OP_TTU) spawn(P, c++, node, pos, gword(G_TTU, d, ci), scope);
-                else if (ct == OP_CSS) {
-                    const uint32_t t = t_sibling(T, node, ni, ch.rel_computed & 0xFFFFu);
-                    const Sub sb = sub_check(s, T, q, t, d, false, 0);
-                    if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
-                } else if (ct == OP_REWRITE) spawn(P, c++, node, pos, gword(G_RW, d - 1, ci), scope);  // :118
-                else if (inv_leaf(s, T, q, node, ci, d) == NONE32) spawn(P, c++, node, pos, gword(G_INV, d, ci), scope);
-            }
-            break;
-        }
-        case G_TTU: {
-            Edges it(s, row);
-            uint32_t c = cb;
-            for (uint32_t e = 0; e < pat; e++) {
-                const uint32_t pn = it.next() & s.edge_mask;
-                const uint32_t t = t_sibling(T, pn, t_node_info(T, pn), xrel);
-                const Sub sb = sub_check(s, T, q, t, d - 1, false, 0);
-                if (sb.word) spawn(P, c++, t, pos, sb.word, scope);
-            }
-            break;
-        }
-        case G_INV: {
-            const Op o = T.ops[op];
-            const uint32_t ci = T.op_children[o.child_begin];
-            const Op ch = T.ops[ci];
-            const uint32_t ct = ch.type_kind & 0xFFu;
-            if (ct == OP_TTU) spawn(P, cb, node, pos, gword(G_TTU, d, ci), scope);
-            else if (ct == OP_CSS) {
-                const uint32_t t = t_sibling(T, node, t_node_info(T, node), ch.rel_computed & 0xFFFFu);
-                spawn(P, cb, t, pos, sub_check(s, T, q, t, d, false, 0).word, scope);
-            } else if (ct == OP_REWRITE) spawn(P, cb, node, pos, gword(G_RW, d, ci), scope);  // keeps depth (:171)
-            else spawn(P, cb, node, pos, gword(G_INV, d, ci), scope);
-            break;
-        }
-        default:
-            break;
+        if (nc || (kind == G_ES && xrel)) {
+            GlobalSink gs{P};
+            PhaseA pb = pa;
+            pb.nc = nc;
+            phase_b(s, T, q, node, pos, w, scope, row, pb, cb, oc, occ_ok, gs);
         }
         FR_MARK(4);
     }
