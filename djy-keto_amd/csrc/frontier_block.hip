@@ -55,7 +55,7 @@ struct GoalPage {
 struct BlockParams {
     DevSnapshot s;
     const uint4 *start;  // resolve records, 2 per batch position of this pass
-    uint32_t n, budget, max_width, err_detail, pos_base;
+    uint32_t n, cq, budget, max_width, err_detail, pos_base;  // cq: queries per chunk (<= BQ)
     uint32_t *ctrl;      // [0] chunk queue, [1] goal pages taken, [2] occurrence pages taken
     GoalPage *gpool;
     uint32_t gpool_cap;
@@ -179,9 +179,9 @@ __global__ __launch_bounds__(BB, KETO_FRB_WAVES) void fr_block(BlockParams P) {
     for (;;) {
         if (tid == 0) C.chunk = atomicAdd(&P.ctrl[0], 1u);
         __syncthreads();
-        const uint32_t c0 = C.chunk * BQ;
+        const uint32_t c0 = C.chunk * P.cq;
         if (c0 >= P.n) break;
-        const uint32_t nq = std::min(BQ, P.n - c0);
+        const uint32_t nq = std::min(P.cq, P.n - c0);
         // generation 0: the chunk's queries
         for (uint32_t t = tid; t < nq; t += NT) {
             const uint4 r0 = P.start[2 * (size_t)(c0 + t)], r1 = P.start[2 * (size_t)(c0 + t) + 1];
@@ -402,8 +402,12 @@ uint32_t run_frontier_block(const Snapshot &s, Stream &st, const CheckLaunch &L,
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, BB, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
     per_cu = std::min(per_cu, 8);
-    const uint64_t chunks = (L.n + BQ - 1) / BQ;
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * per_cu, chunks));
+    // chunks of BQ queries; a batch too small to give every resident workgroup one gets smaller
+    // chunks (down to 16 queries), so its generations spread over more CUs
+    const uint64_t resident = (uint64_t)cus * per_cu;
+    const uint32_t cq = (uint32_t)std::min<uint64_t>(BQ, std::max<uint64_t>(16, (L.n + resident - 1) / resident));
+    const uint64_t chunks = (L.n + cq - 1) / cq;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, chunks));
     // pools: a workgroup keeps the pages its largest chunk needed; an average chunk needs one goal
     // page and one occurrence page, a worst-case chunk 64 of each (routed past what is left)
     const uint32_t gcap = std::max<uint32_t>(2048, 4 * grid), ocap = gcap;
@@ -436,6 +440,7 @@ uint32_t run_frontier_block(const Snapshot &s, Stream &st, const CheckLaunch &L,
     P.s = s.dev;
     P.start = st.resolved + 2 * pos_base;
     P.n = (uint32_t)L.n;
+    P.cq = cq;
     P.budget = L.budget;
     P.max_width = (uint32_t)L.max_width;
     P.err_detail = L.err_detail;
