@@ -324,11 +324,46 @@ def serving_probe(km, snap, q, wl, clients: int, req: int, seconds: float):
             "host_client": "native closed loop: C++ threads calling keto_dispatcher_check"}
 
 
+def c5_cpu_baseline(wl, q, budget_s: float):
+    """configs[4]'s CPU side: the oracle (oracle/refsem.c) over the closure of a sample of the
+    batch, computed on the host from the generator's own rows (tests/closure_ref.py with
+    synth.drive_object_tuples) -- the graph itself is never held on the host.  Returns the
+    baseline record and (sample indices, decisions) for the parity check."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refsem
+    from closure_ref import closure
+    from keto_mi355x import synth
+    from product_helpers import world_from_workload
+
+    cores = cpu_threads()
+    n = 1 << 11
+    while True:
+        qs = q[:n]
+        ct = closure(lambda k: synth.drive_object_tuples(wl, k), qs["ns"], qs["obj"], wl.max_depth + 1,
+                     subjects=qs["s_obj"][qs["subj_kind"] == 0])
+        w, _ = world_from_workload(wl, with_tuples=False)
+        orc = refsem.Oracle(w, ct.view(refsem.TUPLE_DT), shard_bytes=True)
+        orc.set_limits(wl.max_depth, wl.max_width)
+        t0 = time.perf_counter()
+        dec, _, _ = orc.check_batch(qs.view(refsem.QUERY_DT), threads=cores)
+        dt = time.perf_counter() - t0
+        orc.close()
+        if dt * 2.5 > budget_s or n >= len(q):
+            break
+        n = min(len(q), int(n * max(2.0, min(8.0, budget_s / 2.5 / max(dt, 1e-3)))))
+    return {"value": n / dt, "unit": "checks/s", "cores": cores, "kind": "port",
+            "sample": f"first {n} queries of rank 0's batch, oracle/refsem.c over their closure ({len(ct)} tuples, "
+                      f"generated from the Drive generator's rows on the host: the x{wl.meta['roots']} graph is never "
+                      f"held whole), {cores} threads, {dt:.2f} s (closure + index untimed)"}, dec
+
+
 def run_c5(args, rank, world, device, dist_on):
     """configs[4]: a graph partitioned by object over the ranks (keto_partition_*, csrc/partition.hip).
     One step = one batch of this rank's Checks: closure exchange (all-to-all per BFS level over
     the job's collective) -> device snapshot build of the closure -> the Check kernels.  Every
-    phase is inside the timed region."""
+    phase is inside the timed region.  Ranks sharing one GPU (KETO_BENCH_BACKEND=gloo, a
+    rehearsal) build their device stores one after another."""
     import torch
 
     import keto_mi355x as km
@@ -336,22 +371,33 @@ def run_c5(args, rank, world, device, dist_on):
 
     t0 = time.perf_counter()
     wl = synth.drive_scaled(args.scale, materialize=False)
-    part = synth.drive_partition(wl, world, rank)
-    n_part = len(part)
     coll = None
     if dist_on:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from torch_collective import TorchCollective  # keto_collective over the job's process group
         coll = TorchCollective()
-    eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
-                                      device=device, max_read_depth=wl.max_depth, max_read_width=wl.max_width,
-                                      collective=coll)
-    del part
+    shared = os.environ.get("KETO_BENCH_BACKEND", "nccl") == "gloo"
+    eng, n_part = None, 0
+    for r in range(world if (dist_on and shared) else 1):
+        if not (dist_on and shared) or r == rank:
+            part = synth.drive_partition(wl, world, rank)
+            n_part = len(part)
+            eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
+                                              device=device, max_read_depth=wl.max_depth,
+                                              max_read_width=wl.max_width, collective=coll)
+            del part
+        if dist_on and shared:
+            import torch.distributed as dist
+            dist.barrier()
     setup_s = time.perf_counter() - t0
     log(f"[rank {rank}] partition {rank}/{world}: {n_part} of {wl.meta['n_tuples']} tuples, setup {setup_s:.1f}s")
     q = synth.drive_queries(wl, args.batch, seed=shard_seed(11, rank))
-    allowed, err = eng.check_batch(q)  # first batch: warm-up and the decision summary
+    # algorithmic bytes: one counted batch (the check kernels' reference-traversal counters) plus
+    # the closure it moved
+    allowed, err = eng.check_batch(q, count_work=True)
     assert (err == 0).all(), "unexpected query errors"
+    cw = eng.last_work
+    closure_tuples = eng.last["tuples"]
     for _ in range(max(0, args.warmup - 1)):
         eng.check_batch(q)
     if dist_on:
@@ -370,6 +416,13 @@ def run_c5(args, rank, world, device, dist_on):
     elapsed_local = time.perf_counter() - t_start
     value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps, f"cuda:{device}" if dist_on else "cpu")
     ranks_ms = per_rank_ms(elapsed_local / args.steps * 1e3, f"cuda:{device}" if dist_on else "cpu")
+    ms_step = elapsed_local / args.steps * 1e3
+    # roofline of the step (this rank): the check's algorithmic bytes (BASELINE.md model, counted
+    # on the closure snapshot) + the closure the step moves (each tuple gathered -- read + written
+    # -- and read by the build: 3 x 48 B) over the whole step's time
+    check_bytes = 8 * cw["rows"][0] + 4 * cw["edges"][0] + 8 * cw["probes"][0] + 17 * cw["queries"][0]
+    step_bytes = check_bytes + 3 * 48 * closure_tuples
+    achieved = step_bytes / (ms_step * 1e-3) / 1e9
     out = {
         "metric": METRIC, "value": value, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "per_rank_ms_per_step": ranks_ms,
@@ -386,8 +439,19 @@ def run_c5(args, rank, world, device, dist_on):
         "closure": {"tuples": eng.last["tuples"], "objects": eng.last["objects"], "levels": eng.last["levels"],
                     "bytes_sent": eng.last["bytes_sent"],
                     "partition_tuples": n_part},
-        "roofline": None, "cpu_baseline": None,
+        "shared_gpu": bool(dist_on and shared),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "the whole step: closure exchange + closure build + check (one rank)",
+                     "algorithmic_bytes_per_step": int(step_bytes), "check_bytes": int(check_bytes),
+                     "closure_tuples": int(closure_tuples),
+                     "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (check) + 3*48*closure tuples"},
+        "cpu_baseline": None,
     }
+    if rank == 0 and not args.no_cpu_baseline:
+        cb, dec = c5_cpu_baseline(wl, q, args.cpu_budget)
+        out["cpu_baseline"] = cb
+        out["cpu_parity_sample"] = {"n": len(dec), "mismatches": int((dec != allowed[:len(dec)]).sum())}
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
@@ -412,7 +476,9 @@ def launch_ranks(args, argv) -> int:
     import subprocess
 
     n = args.gpus
-    have = n if args.dry_run else visible_gpus()
+    # KETO_BENCH_BACKEND=gloo: a rehearsal whose ranks share the visible GPUs (its line says so)
+    shared = os.environ.get("KETO_BENCH_BACKEND", "nccl") == "gloo"
+    have = n if (args.dry_run or shared) else visible_gpus()
     if have < n:
         log(f"bench.py --gpus {n}: only {have} GPU(s) visible -- refusing to report a {n}-GPU line")
         return 2

@@ -935,6 +935,15 @@ void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8
         sync(P);
     }
     st.run_s = secs(t0);
+    if (flags & KETO_F_COUNT_WORK) {
+        keto_work_counters wc{};
+        if (keto_stream_counters(P.kstream, &wc, 1) == KETO_OK) {
+            st.rows = wc.rows[0];
+            st.edges = wc.edges[0];
+            st.probes = wc.probes[0];
+            st.queries = wc.queries[0];
+        }
+    }
     P.last = st;
 }
 

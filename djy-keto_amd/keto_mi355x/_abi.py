@@ -70,7 +70,8 @@ class DispatcherStats(ctypes.Structure):
 class PartitionStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("levels", ctypes.c_uint64), ("objects", ctypes.c_uint64),
                 ("tuples", ctypes.c_uint64), ("bytes_sent", ctypes.c_uint64), ("closure_s", ctypes.c_double),
-                ("build_s", ctypes.c_double), ("run_s", ctypes.c_double)]
+                ("build_s", ctypes.c_double), ("run_s", ctypes.c_double), ("rows", ctypes.c_uint64),
+                ("edges", ctypes.c_uint64), ("probes", ctypes.c_uint64), ("queries", ctypes.c_uint64)]
 
 
 # keto_collective callbacks

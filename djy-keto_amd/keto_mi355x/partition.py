@@ -131,6 +131,8 @@ class PartitionedEngine:
         check(lib().keto_partition_check(self.handle, q.ctypes.data if len(q) else None, len(q), allowed.ctypes.data,
                                          err.ctypes.data, _abi.F_COUNT_WORK if count_work else 0))
         self._stats()
+        if count_work:  # the check kernels' counters, keto_work_counters-shaped (tier 0 only)
+            self.last_work = {k: [self.last[k], 0, 0] for k in ("rows", "edges", "probes", "queries")}
         return allowed, err[:len(q)]
 
     def expand_batch(self, roots: np.ndarray):

@@ -310,6 +310,8 @@ typedef struct keto_collective {
 typedef struct keto_partition_stats {
     uint64_t batches, levels, objects, tuples, bytes_sent;
     double closure_s, build_s, run_s;
+    /* a KETO_F_COUNT_WORK batch: the check kernels' work counters (keto_work_counters, tier 0) */
+    uint64_t rows, edges, probes, queries;
 } keto_partition_stats;
 typedef struct keto_partition keto_partition;
 /* tuples: this rank's partition (host, or device memory of cfg->device with
