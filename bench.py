@@ -794,11 +794,17 @@ def main(argv=None):
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "check path: resolve_kernel, frontier generations (fr_init, fr_expand, fr_reduce, fr_repeat) "
-                               "+ DFS on routed",
+                     "kernel": ("check path: resolve_kernel + fr_block (one launch) + DFS on routed"
+                                if os.environ.get("KETO_FR_ENGINE", "block")[0] != "g" else
+                                "check path: resolve_kernel + frontier generations (fr_init, fr_expand, fr_reduce, "
+                                "fr_repeat) + DFS on routed"),
                      "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": int(bytes_t0),
-                     "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (BASELINE.md)",
+                     "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (BASELINE.md) of the REFERENCE's "
+                                    "traversal -- the rows, edges and probes Keto's engine reads for these queries "
+                                    "(the DFS interpreter's counters of a counted batch, equal to the oracle's) -- "
+                                    "over the engine's measured check-path time; the engine itself reads a "
+                                    "different (unpruned, breadth-first) set",
                      "work": {"rows": pt["rows"][0], "edges": pt["edges"][0], "probes": pt["probes"][0],
                               "queries_tier0": pt["queries"][0], "queries_tier1": pt["queries"][1],
                               "queries_tier2": pt["queries"][2]}},

@@ -19,5 +19,8 @@ if [ -z "${2:-}" ]; then
   timeout -k 10 900 python3 -u -m pytest -x -v -s --timeout 880 --timeout-method thread tests/test_gpu_c5.py > $O/c5x40.log 2>&1
   rc=$?; grep -E "^\[c5|passed|failed|Error|assert|^[0-9] \{" $O/c5x40.log | tail -60
   [ $rc -ne 0 ] && { tail -30 $O/c5x40.log; exit $rc; }
+  KETO_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u bench.py --workload c5 --gpus 8 --steps 3 --warmup 1 > $O/bench_c5.log 2>&1 \
+    || { echo "c5 bench failed"; tail -8 $O/bench_c5.log; exit 1; }
+  grep '^{' $O/bench_c5.log | cut -c1-1500
 fi
 exit 0
