@@ -145,6 +145,17 @@ int keto_snapshot_build_device(const keto_snapshot_config *cfg, const keto_tuple
     });
 }
 
+int keto_snapshot_save(const keto_snapshot *snap, const char *path) {
+    if (!snap || !path) return fail(KETO_E_INVALID, "null argument");
+    return guarded([&] { keto::save_snapshot(*SN(snap), path); });
+}
+
+int keto_snapshot_load(const char *path, int32_t device, keto_snapshot **out) {
+    if (!out || !path) return fail(KETO_E_INVALID, "null argument");
+    *out = nullptr;
+    return guarded([&] { *out = reinterpret_cast<keto_snapshot *>(keto::load_snapshot(path, device)); });
+}
+
 int keto_snapshot_free(keto_snapshot *snap) {
     delete SN(snap);
     return KETO_OK;

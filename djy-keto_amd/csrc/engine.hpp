@@ -41,6 +41,7 @@ struct Snapshot {
     std::vector<uint2> or_items;
     DevSnapshot dev{};
     std::vector<void *> allocs;
+    std::vector<size_t> alloc_bytes;  // (parallel to allocs: what keto_snapshot_save writes)
     keto_snapshot_info info{};
 
     ~Snapshot();
@@ -50,6 +51,9 @@ struct Snapshot {
 
 Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
                          bool sched_weights = true);
+// snapshot.cpp: a built snapshot to a file and back (keto_snapshot_save / _load)
+void save_snapshot(const Snapshot &s, const char *path);
+Snapshot *load_snapshot(const char *path, int device);
 
 // build.hip: device-side snapshot construction (one-thread-per-item kernels)
 namespace build {

@@ -207,6 +207,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         void *p = nullptr;
         KETO_HIP(hipMalloc(&p, bytes));
         s.allocs.push_back(p);
+        s.alloc_bytes.push_back(bytes);
         KETO_HIP(hipMemset(p, 0, bytes));
         s.info.device_bytes += bytes;
         return p;
@@ -214,6 +215,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     auto adopt = [&](DevBuf &b) -> void * {
         s.info.device_bytes += b.bytes;
         s.allocs.push_back(b.p);
+        s.alloc_bytes.push_back(b.bytes);
         return b.release();
     };
 
@@ -529,6 +531,206 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     s.info.n_entities = ent_total;
     s.info.n_tuples = n;
     s.info.n_nodes = N;
+    s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return S.release();
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Snapshot files (keto_snapshot_save / keto_snapshot_load): the restart artefact SURVEY.md section
+// 5 names.  The reference keeps no such state -- its SQL database is the state and a restart
+// re-reads it -- so a file stands for "the store at this snaptoken, already compiled": a header,
+// the host tables, then every device array (the DevSnapshot pointers as array indices).
+// Little-endian, this library's layout only (the magic carries the ABI version).
+
+namespace {
+constexpr uint64_t SNAP_MAGIC = 0x31534F54454B0000ull | KETO_ABI_VERSION;  // "\0\0KETOS1" + ABI
+
+struct File {
+    FILE *f = nullptr;
+    File(const char *path, const char *mode) : f(fopen(path, mode)) {
+        if (!f) throw Error(KETO_E_INVALID, std::string("cannot open ") + path);
+    }
+    ~File() {
+        if (f) fclose(f);
+    }
+    void put(const void *p, size_t n) {
+        if (n && fwrite(p, 1, n, f) != n) throw Error(KETO_E_INVALID, "snapshot file write failed");
+    }
+    void get(void *p, size_t n) {
+        if (n && fread(p, 1, n, f) != n) throw Error(KETO_E_INVALID, "snapshot file truncated");
+    }
+    template <class T>
+    void put_v(const std::vector<T> &v) {
+        const uint64_t n = v.size();
+        put(&n, 8);
+        put(v.data(), n * sizeof(T));
+    }
+    template <class T>
+    void get_v(std::vector<T> &v) {
+        uint64_t n = 0;
+        get(&n, 8);
+        if (n > (1ull << 34) / sizeof(T)) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+        v.resize(n);
+        get(v.data(), n * sizeof(T));
+    }
+    void put_s(const std::vector<std::string> &v) {
+        const uint64_t n = v.size();
+        put(&n, 8);
+        for (auto &x : v) {
+            const uint64_t l = x.size();
+            put(&l, 8);
+            put(x.data(), l);
+        }
+    }
+    void get_s(std::vector<std::string> &v) {
+        uint64_t n = 0;
+        get(&n, 8);
+        if (n > (1u << 24)) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+        v.resize(n);
+        for (auto &x : v) {
+            uint64_t l = 0;
+            get(&l, 8);
+            if (l > (1u << 20)) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+            x.resize(l);
+            get(&x[0], l);
+        }
+    }
+};
+
+// the DevSnapshot pointer fields, in file order
+template <class F>
+void dev_ptrs(DevSnapshot &D, F &&f) {
+    f(reinterpret_cast<const void *&>(D.set_row));
+    f(reinterpret_cast<const void *&>(D.set_dst));
+    f(reinterpret_cast<const void *&>(D.weight));
+    f(reinterpret_cast<const void *&>(D.ent_obj));
+    f(reinterpret_cast<const void *&>(D.slot_rel));
+    f(reinterpret_cast<const void *&>(D.vkey));
+    f(reinterpret_cast<const void *&>(D.all_off));
+    f(reinterpret_cast<const void *&>(D.all_subj));
+    f(reinterpret_cast<const void *&>(D.rev_off));
+    f(reinterpret_cast<const void *&>(D.rev_nodes));
+    f(reinterpret_cast<const void *&>(D.ns));
+    f(reinterpret_cast<const void *&>(D.relinfo));
+    f(reinterpret_cast<const void *&>(D.nsrel));
+    f(reinterpret_cast<const void *&>(D.ops));
+    f(reinterpret_cast<const void *&>(D.op_children));
+    f(reinterpret_cast<const void *&>(D.op_items));
+    f(reinterpret_cast<const void *&>(D.or_items));
+    f(reinterpret_cast<const void *&>(D.ent_rank));
+    f(reinterpret_cast<const void *&>(D.probe));
+}
+constexpr size_t STAGE = 64u << 20;  // device <-> file through a pinned buffer of this size
+}  // namespace
+
+void save_snapshot(const Snapshot &s, const char *path) {
+    KETO_HIP(hipSetDevice(s.device));
+    File F(path, "wb");
+    const uint64_t magic = SNAP_MAGIC;
+    F.put(&magic, 8);
+    const uint32_t hdr[6] = {s.n_ns, s.n_rel, s.n_rel_caller, s.n_uuids, (uint32_t)s.strict, 0};
+    F.put(hdr, sizeof hdr);
+    F.put(&s.info, sizeof s.info);
+    DevSnapshot D = s.dev;
+    F.put(&D, sizeof D);  // (its scalars; the pointers are replaced below by array indices)
+    F.put_s(s.ns_names);
+    F.put_s(s.rel_names);
+    F.put_v(s.ns);
+    F.put_v(s.ent_obj);
+    F.put_v(s.slot_rel);
+    F.put_v(s.relinfo);
+    F.put_v(s.nsrel);
+    F.put_v(s.ops);
+    F.put_v(s.op_children);
+    F.put_v(s.op_items);
+    F.put_v(s.or_items);
+    std::vector<int64_t> idx;
+    dev_ptrs(D, [&](const void *&p) {
+        int64_t k = -1;
+        for (size_t i = 0; i < s.allocs.size(); i++)
+            if (s.allocs[i] == p) k = (int64_t)i;
+        if (p && k < 0) throw Error(KETO_E_INVALID, "snapshot array outside its allocations");
+        idx.push_back(k);
+    });
+    F.put_v(idx);
+    F.put_v(s.alloc_bytes);
+    void *stage = nullptr;
+    KETO_HIP(hipHostMalloc(&stage, STAGE, 0));
+    try {
+        for (size_t i = 0; i < s.allocs.size(); i++)
+            for (size_t off = 0; off < s.alloc_bytes[i]; off += STAGE) {
+                const size_t b = std::min(STAGE, s.alloc_bytes[i] - off);
+                KETO_HIP(hipMemcpy(stage, static_cast<const char *>(s.allocs[i]) + off, b, hipMemcpyDeviceToHost));
+                F.put(stage, b);
+            }
+    } catch (...) {
+        (void)hipHostFree(stage);
+        throw;
+    }
+    KETO_HIP(hipHostFree(stage));
+}
+
+Snapshot *load_snapshot(const char *path, int device) {
+    auto t0 = std::chrono::steady_clock::now();
+    KETO_HIP(hipSetDevice(device));
+    File F(path, "rb");
+    uint64_t magic = 0;
+    F.get(&magic, 8);
+    if (magic != SNAP_MAGIC) throw Error(KETO_E_INVALID, "not a snapshot file of this library version");
+    auto S = std::make_unique<Snapshot>();
+    Snapshot &s = *S;
+    s.device = device;
+    uint32_t hdr[6];
+    F.get(hdr, sizeof hdr);
+    s.n_ns = hdr[0];
+    s.n_rel = hdr[1];
+    s.n_rel_caller = hdr[2];
+    s.n_uuids = hdr[3];
+    s.strict = hdr[4] != 0;
+    F.get(&s.info, sizeof s.info);
+    F.get(&s.dev, sizeof s.dev);
+    F.get_s(s.ns_names);
+    F.get_s(s.rel_names);
+    F.get_v(s.ns);
+    F.get_v(s.ent_obj);
+    F.get_v(s.slot_rel);
+    F.get_v(s.relinfo);
+    F.get_v(s.nsrel);
+    F.get_v(s.ops);
+    F.get_v(s.op_children);
+    F.get_v(s.op_items);
+    F.get_v(s.or_items);
+    std::vector<int64_t> idx;
+    std::vector<size_t> bytes;
+    F.get_v(idx);
+    F.get_v(bytes);
+    if (idx.size() != 19) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+    void *stage = nullptr;
+    KETO_HIP(hipHostMalloc(&stage, STAGE, 0));
+    try {
+        for (size_t i = 0; i < bytes.size(); i++) {
+            void *p = nullptr;
+            KETO_HIP(hipMalloc(&p, std::max<size_t>(16, bytes[i])));
+            s.allocs.push_back(p);
+            s.alloc_bytes.push_back(bytes[i]);
+            for (size_t off = 0; off < bytes[i]; off += STAGE) {
+                const size_t b = std::min(STAGE, bytes[i] - off);
+                F.get(stage, b);
+                KETO_HIP(hipMemcpy(static_cast<char *>(p) + off, stage, b, hipMemcpyHostToDevice));
+            }
+        }
+    } catch (...) {
+        (void)hipHostFree(stage);
+        throw;
+    }
+    KETO_HIP(hipHostFree(stage));
+    size_t k = 0;
+    dev_ptrs(s.dev, [&](const void *&p) {
+        const int64_t i = idx[k++];
+        if (i >= (int64_t)s.allocs.size()) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+        p = i < 0 ? nullptr : s.allocs[(size_t)i];
+    });
     s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return S.release();
 }

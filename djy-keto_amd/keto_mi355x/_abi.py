@@ -96,6 +96,8 @@ SIGNATURES = {
     "keto_snapshot_build": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, ctypes.POINTER(_VP)]),
     "keto_snapshot_build_device": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, ctypes.POINTER(_VP)]),
     "keto_snapshot_free": (ctypes.c_int, [_VP]),
+    "keto_snapshot_save": (ctypes.c_int, [_VP, ctypes.c_char_p]),
+    "keto_snapshot_load": (ctypes.c_int, [ctypes.c_char_p, _I32, ctypes.POINTER(_VP)]),
     "keto_snapshot_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(SnapshotInfo)]),
     "keto_stream_create": (ctypes.c_int, [_I32, ctypes.POINTER(_VP)]),
     "keto_stream_destroy": (ctypes.c_int, [_VP]),

@@ -89,6 +89,20 @@ class Snapshot:
         check(lib().keto_snapshot_info_get(self.handle, ctypes.byref(inf)))
         return {k: getattr(inf, k) for k, _ in inf._fields_}
 
+    def save(self, path: str):
+        """the snapshot to a file (keto_snapshot_save): the restart artefact"""
+        check(lib().keto_snapshot_save(self.handle, str(path).encode()))
+
+    @classmethod
+    def load(cls, path: str, ns_names: list, rel_names: list, device: int = 0) -> "Snapshot":
+        """a saved snapshot back onto `device` (keto_snapshot_load), without a rebuild"""
+        self = cls.__new__(cls)
+        h = ctypes.c_void_p()
+        check(lib().keto_snapshot_load(str(path).encode(), device, ctypes.byref(h)))
+        self.handle, self.device = h, device
+        self.ns_names, self.rel_names = list(ns_names), list(rel_names)
+        return self
+
     def close(self):
         if getattr(self, "handle", None):
             lib().keto_snapshot_free(self.handle)

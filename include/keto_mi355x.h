@@ -163,6 +163,14 @@ int keto_snapshot_build(const keto_snapshot_config *cfg, const keto_tuple *tuple
  * keeps them alive for the duration of the call only. */
 int keto_snapshot_build_device(const keto_snapshot_config *cfg, const keto_tuple *device_tuples, uint64_t n_tuples,
                                keto_snapshot **out);
+/* A built snapshot to a file and back: the restart artefact (checkpoint).
+ * The reference's state is its SQL database (internal/driver/registry_default.go:247-292) and a
+ * restart re-reads it; here a restart can load the snapshot of the last snaptoken instead of
+ * rebuilding it.  The file holds the compiled namespace tables and every device array of this
+ * library's layout (its ABI version is checked on load); load onto any device.  The store
+ * version (info.version) travels with it; build_seconds of a loaded snapshot = the load time. */
+int keto_snapshot_save(const keto_snapshot *snap, const char *path);
+int keto_snapshot_load(const char *path, int32_t device, keto_snapshot **out);
 int keto_snapshot_free(keto_snapshot *snap);
 int keto_snapshot_info_get(const keto_snapshot *snap, keto_snapshot_info *out);
 
