@@ -92,7 +92,13 @@ struct Dispatcher {
     bool stop = false;
     std::vector<std::unique_ptr<Slot>> slots;
     keto_dispatcher_stats stats{};
+    keto_batch_hook on_batch = nullptr;
+    void *hook_ctx = nullptr;
 };
+
+double ms_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
 
 // one packed batch through the device: async copies around the kernels, one sync
 int Slot::launch(keto_snapshot *snap, uint64_t n, std::string &msg) {
@@ -106,7 +112,7 @@ int Slot::launch(keto_snapshot *snap, uint64_t n, std::string &msg) {
         if (rc == KETO_OK) {
             KETO_HIP(hipMemcpyAsync(ha, da, n, hipMemcpyDeviceToHost, hs));
             KETO_HIP(hipMemcpyAsync(he, de, n * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-            KETO_HIP(hipStreamSynchronize(hs));
+            if (keto_stream_sync(stream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream synchronisation failed");
         } else {
             char buf[512];
             keto_last_error(buf, sizeof(buf));
@@ -122,6 +128,7 @@ int Slot::launch(keto_snapshot *snap, uint64_t n, std::string &msg) {
 // Expand batch for every taken request: one keto_expand_batch over all roots, then each
 // caller's trees are copied to its buffer with offsets rebased to it
 void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
+    const auto t0 = std::chrono::steady_clock::now();
     uint64_t n = 0;
     for (auto *r : take) n += r->n;
     int rc = KETO_OK;
@@ -133,6 +140,7 @@ void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
     xerr.assign(n, 0);
     if (xnodes.empty()) xnodes.resize(1u << 16);
     for (int attempt = 0; attempt < 2; attempt++) {
+        keto_stream_expand_time(stream, nullptr, nullptr, 1);
         rc = keto_expand_batch(snap, stream, roots.data(), n, &d->limits, xnodes.data(), xnodes.size(), xoffs.data(),
                                xerr.data());
         if (rc != KETO_E_CAPACITY) break;
@@ -143,8 +151,11 @@ void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
         keto_last_error(buf, sizeof(buf));
         msg = buf;
     }
+    double dms = 0;
+    keto_stream_expand_time(stream, &dms, nullptr, 1);
+    const keto_batch_event ev{1, (uint32_t)take.size(), n, ms_since(t0), dms, rc};
     uint64_t o = 0;
-    std::lock_guard<std::mutex> lk(d->m);
+    std::unique_lock<std::mutex> lk(d->m);
     for (auto *r : take) {
         int rrc = rc;
         std::string rmsg = msg;
@@ -168,7 +179,11 @@ void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
     d->stats.batches++;
     d->stats.queries += n;
     d->stats.requests += take.size();
+    d->stats.wall_ms_sum += ev.wall_ms;
+    d->stats.device_ms_sum += ev.device_ms;
     if (n > d->stats.max_batch_seen) d->stats.max_batch_seen = n;
+    lk.unlock();
+    if (d->on_batch) d->on_batch(d->hook_ctx, &ev);
 }
 
 void Slot::run() {
@@ -211,6 +226,7 @@ void Slot::run() {
             release();
             continue;
         }
+        const auto t0 = std::chrono::steady_clock::now();
         uint64_t n = 0;
         for (auto *r : take) n += r->n;
         int rc = KETO_OK;
@@ -232,8 +248,11 @@ void Slot::run() {
                 msg = buf;
             }
         }
+        double dms = 0;
+        keto_stream_last_kernel_ms(stream, &dms);
+        const keto_batch_event ev{0, (uint32_t)take.size(), n, ms_since(t0), dms, rc};
         uint64_t o = 0;
-        std::lock_guard<std::mutex> lk(d->m);
+        std::unique_lock<std::mutex> lk(d->m);
         release();
         for (auto *r : take) {
             if (rc == KETO_OK && staged) {
@@ -249,7 +268,11 @@ void Slot::run() {
         d->stats.batches++;
         d->stats.queries += n;
         d->stats.requests += take.size();
+        d->stats.wall_ms_sum += ev.wall_ms;
+        d->stats.device_ms_sum += ev.device_ms;
         if (n > d->stats.max_batch_seen) d->stats.max_batch_seen = n;
+        lk.unlock();
+        if (d->on_batch) d->on_batch(d->hook_ctx, &ev);
     }
 }
 
@@ -292,6 +315,8 @@ void dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, k
     d->max_batch = cfg->max_batch;
     d->max_wait_us = cfg->max_wait_us;
     d->flags = cfg->flags & KETO_F_ERR_DETAIL;
+    d->on_batch = cfg->on_batch;
+    d->hook_ctx = cfg->hook_ctx;
     d->device = reinterpret_cast<Snapshot *>(snap)->device;
     try {
         KETO_HIP(hipSetDevice(d->device));

@@ -57,14 +57,24 @@ class FrontierStats(ctypes.Structure):
                                                "max_generations", "async_batches")]
 
 
+class BatchEvent(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("requests", ctypes.c_uint32), ("queries", ctypes.c_uint64),
+                ("wall_ms", ctypes.c_double), ("device_ms", ctypes.c_double), ("rc", ctypes.c_int32)]
+
+
+BATCH_HOOK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(BatchEvent))
+
+
 class DispatcherConfig(ctypes.Structure):
     _fields_ = [("limits", Limits), ("max_batch", ctypes.c_uint32), ("max_wait_us", ctypes.c_uint32),
-                ("inflight", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("inflight", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("on_batch", BATCH_HOOK_FN),
+                ("hook_ctx", ctypes.c_void_p)]
 
 
 class DispatcherStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("queries", ctypes.c_uint64),
-                ("max_batch_seen", ctypes.c_uint64)]
+                ("max_batch_seen", ctypes.c_uint64), ("wall_ms_sum", ctypes.c_double),
+                ("device_ms_sum", ctypes.c_double)]
 
 
 class PartitionStats(ctypes.Structure):
@@ -160,7 +170,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.keto_abi_version() != 1:
+        if L.keto_abi_version() != 2:
             raise RuntimeError("libketo_mi355x ABI version mismatch")
         _lib = L
     return _lib

@@ -340,9 +340,19 @@ class Dispatcher:
     GIL for the blocking call, so Python threads coalesce like goroutines in the Go shim."""
 
     def __init__(self, snapshot: Snapshot, max_read_depth: int = 5, max_read_width: int = 100,
-                 max_batch: int = 1 << 16, max_wait_us: int = 0, inflight: int = 4, err_detail: bool = False):
+                 max_batch: int = 1 << 16, max_wait_us: int = 0, inflight: int = 4, err_detail: bool = False,
+                 on_batch=None):
+        """on_batch(event dict): called by the library's slot threads after every batch
+        (keto_dispatcher_config.on_batch) -- where a Go shim feeds its Prometheus histograms"""
+        self._hook = None
+        if on_batch is not None:
+            def hook(_ctx, ev):
+                e = ev.contents
+                on_batch({k: getattr(e, k) for k, _ in e._fields_})
+            self._hook = _abi.BATCH_HOOK_FN(hook)
         cfg = _abi.DispatcherConfig(_abi.Limits(max_read_depth, max_read_width), max_batch, max_wait_us, inflight,
-                                    _abi.F_ERR_DETAIL if err_detail else 0)
+                                    _abi.F_ERR_DETAIL if err_detail else 0,
+                                    self._hook if self._hook else _abi.BATCH_HOOK_FN(), None)
         h = ctypes.c_void_p()
         check(lib().keto_dispatcher_create(snapshot.handle, ctypes.byref(cfg), ctypes.byref(h)))
         self.handle = h

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 1
+#define KETO_ABI_VERSION 2
 
 /* status codes */
 #define KETO_OK 0
@@ -230,15 +230,30 @@ int keto_store_free(keto_store *st);
 /* Request coalescing for serving: concurrent callers, one batch per launch (the
  * dispatcher a Go shim puts behind CheckService, check/handler.go:304-331). */
 typedef struct keto_dispatcher keto_dispatcher;
+/* One finished dispatcher batch, for the caller's metrics (the reference's Prometheus / otel
+ * hooks, internal/driver/registry_default.go:170-182, count requests above the engine; this is
+ * what happens below it). */
+typedef struct keto_batch_event {
+    uint32_t kind;      /* 0 Check, 1 Expand */
+    uint32_t requests;  /* callers coalesced into the batch */
+    uint64_t queries;   /* queries / roots */
+    double wall_ms;     /* the slot's copies + kernels + copies, host clock */
+    double device_ms;   /* the check path / Expand traversal on the device (HIP events) */
+    int32_t rc;         /* KETO_OK or the batch's error */
+} keto_batch_event;
+typedef void (*keto_batch_hook)(void *ctx, const keto_batch_event *ev);
 typedef struct keto_dispatcher_config {
     keto_limits limits;
     uint32_t max_batch;   /* queries per launch (staging size); a larger request runs alone */
     uint32_t max_wait_us; /* 0: launch as soon as a slot is free with whatever is queued */
     uint32_t inflight;    /* batches in flight on their own streams (0 -> 4, at most 16) */
     uint32_t flags;       /* KETO_F_ERR_DETAIL: out_err as keto_check_batch with that flag */
+    keto_batch_hook on_batch;  /* optional: called by the slot thread after each batch, callers released */
+    void *hook_ctx;
 } keto_dispatcher_config;
 typedef struct keto_dispatcher_stats {
     uint64_t batches, requests, queries, max_batch_seen;
+    double wall_ms_sum, device_ms_sum;  /* summed over the batches */
 } keto_dispatcher_stats;
 
 /* The snapshot must outlive the dispatcher (or be replaced with set_snapshot first). */

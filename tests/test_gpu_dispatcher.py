@@ -34,7 +34,8 @@ def test_concurrent_callers_match_oracle():
     q["max_depth"][:500] = np.random.default_rng(1).integers(1, 5, 500)
     snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
     want, werr = _oracle_answers(_oracle(wl), q)
-    d = km.Dispatcher(snap, wl.max_depth, wl.max_width, max_batch=4096)
+    events = []
+    d = km.Dispatcher(snap, wl.max_depth, wl.max_width, max_batch=4096, on_batch=events.append)
     got = np.full(len(q), 7, np.uint8)
     gerr = np.full(len(q), -1, np.int32)
     errors = []
@@ -61,6 +62,10 @@ def test_concurrent_callers_match_oracle():
     st = d.stats()
     assert st["batches"] < st["requests"]  # requests really were coalesced
     assert st["max_batch_seen"] <= 4096
+    # the per-batch hook (the shim's metrics): one event per batch, the same totals as the stats
+    assert len(events) == st["batches"] and sum(e["queries"] for e in events) == st["queries"]
+    assert all(e["kind"] == 0 and e["rc"] == 0 and e["wall_ms"] > 0 for e in events)
+    assert sum(e["device_ms"] for e in events) > 0
     covered = got != 7
     assert covered.sum() > len(q) // 2
     np.testing.assert_array_equal(got[covered], want[covered])
