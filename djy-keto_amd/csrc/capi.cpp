@@ -49,7 +49,6 @@ Stream::~Stream() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (check_scratch.mem) (void)hipFree(check_scratch.mem);
     if (expand_scratch.mem) (void)hipFree(expand_scratch.mem);
-    if (union_scratch.mem) (void)hipFree(union_scratch.mem);
     if (frontier.mem) (void)hipFree(frontier.mem);
     if (frontier.host_ctrl) (void)hipHostFree(frontier.host_ctrl);
     if (frontier_block.mem) (void)hipFree(frontier_block.mem);
@@ -271,15 +270,6 @@ int keto_stream_last_kernel_ms(keto_stream *hs, double *ms) {
     return KETO_OK;
 }
 
-// Every snapshot runs the frontier engine (+ the DFS interpreter on routed queries): on the C2
-// nested-group batch it is 3.4x the rewrite-free lane interpreter (2.15 vs 8.32 ms).
-// KETO_UNION_FRONTIER=0 keeps rewrite-free snapshots on that interpreter (A/B, tests).
-static void (*check_engine(const keto::Snapshot &snap))(const keto::Snapshot &, keto::Stream &, const keto::CheckLaunch &) {
-    const char *e = getenv("KETO_UNION_FRONTIER");  // read per batch: tests switch it
-    if (snap.ops.empty() && e && e[0] == '0') return keto::run_check_union;
-    return keto::run_check;
-}
-
 int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *queries, uint64_t n,
                      const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags) {
     keto::Snapshot *snap = SN(hsnap);
@@ -304,7 +294,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
             L.queries = queries;
             L.out_allowed = out_allowed;
             L.out_err = out_err;
-            check_engine(*snap)(*snap, *s, L);
+            keto::run_check(*snap, *s, L);
             if (!(flags & KETO_F_ASYNC)) {
                 KETO_HIP(hipStreamSynchronize(s->stream));
                 s->harvest();
@@ -321,7 +311,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         L.queries = static_cast<const keto_query *>(s->qbuf);
         L.out_allowed = d_allowed;
         L.out_err = d_err;
-        check_engine(*snap)(*snap, *s, L);
+        keto::run_check(*snap, *s, L);
         KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
         if (flags & KETO_F_ASYNC) return;  // the caller synchronises the stream (keto_stream_sync)

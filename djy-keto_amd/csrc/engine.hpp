@@ -162,7 +162,7 @@ struct Stream {
     void mark_end();    // after it
     void harvest();     // accumulate every completed pair (call after a stream sync)
     // device workspace (allocated on first use, never inside a launch sequence)
-    Scratch check_scratch, union_scratch, expand_scratch;
+    Scratch check_scratch, expand_scratch;
     // expand_wave workspace (expand.hip): per-wave staging, the batch's stage, per-root arrays
     struct {
         void *mem = nullptr, *roots_mem = nullptr;
@@ -215,7 +215,6 @@ struct CheckLaunch {
 void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth,
                  bool ordered = true);
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
-void run_check_union(const Snapshot &s, Stream &st, const CheckLaunch &L);  // rewrite-free snapshots
 // frontier.hip: L.n resolved queries from batch position pos_base on, breadth-first; returns the
 // number of queries routed to the DFS interpreter (batch positions in st.frontier.fb_list).
 // Batches above FR_MAX_BATCH run as several passes: the arena's goal indices stay in range.

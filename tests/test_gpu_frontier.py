@@ -125,29 +125,6 @@ def test_nested_groups_small_frontier_vs_oracle(stream):
     assert 0.05 < allowed.mean() < 0.95
 
 
-@pytest.mark.parametrize("seed", list(range(0, 60, 3)))
-def test_union_interpreter_opt_out_vs_oracle(stream, seed):
-    """KETO_UNION_FRONTIER=0 keeps rewrite-free snapshots on the lane interpreter (check_union.hip)"""
-    w, t, q, _ = random_world(seed, rewrites=False)
-    orc = refsem.Oracle(w, t)
-    orc.set_limits(w.max_depth, w.max_width)
-    dec, err, _ = orc.check_batch(q, threads=4)
-    snap = product_snapshot(w, t)
-    eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
-    old = os.environ.get("KETO_UNION_FRONTIER")
-    os.environ["KETO_UNION_FRONTIER"] = "0"
-    try:
-        allowed, gerr, fs = _frontier_batch(stream, eng, queries_to_product(q))
-    finally:
-        if old is None:
-            os.environ.pop("KETO_UNION_FRONTIER")
-        else:
-            os.environ["KETO_UNION_FRONTIER"] = old
-    np.testing.assert_array_equal(gerr, err)
-    np.testing.assert_array_equal(allowed, dec)
-    assert fs["batches"] == 0  # the frontier engine did not run
-
-
 def test_every_query_routed_matches_oracle(budget):
     """budget 1: every query with a sub-check goes to the DFS interpreter through the routed list"""
     from keto_mi355x import synth
