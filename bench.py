@@ -82,8 +82,12 @@ def schedule_report(orc, q, gpu_allowed, n: int, cores: int):
             "sequential_schedule_differs": int(diff.sum()),
             "gpu_mismatches_on_flagged": int((dec[sens] != gpu_allowed[:n][sens]).sum()),
             "gpu_mismatches": int((dec != gpu_allowed[:n]).sum()),
-            "criterion": "a visited scope pruned a sibling and saw width truncation / an error / AND-NOT, or "
-                         "pruned occurrences at different rest depths plus depth truncation (oracle/refsem.c)"}
+            "flagged_by_maximal_exploration": int(((flags & refsem.F_MAXEXP) != 0).sum()),
+            "criterion": "a visited scope reached a key twice and saw width truncation / an error / AND-NOT, or "
+                         "reached it at different rest depths plus depth truncation -- in either simulated "
+                         "schedule or in the tree of every check the reference's eager construction can start "
+                         "(oracle/refsem.c); sound against oracle/refconc.py's goroutine-level interleavings "
+                         "(tests/test_schedule.py)"}
 
 
 SQL_MAX_ROWS = 2_000_000  # per worker: the rows become Python tuples before they reach SQLite
@@ -293,7 +297,7 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
     ms, nb = stream.expand_time(reset=True)
     kms = ms / max(1, nb)
     # algorithmic bytes: 8*rows + 4*edges + 12*out_nodes per batch
-    xbytes = (8 * c["rows"][0] + 4 * c["edges"][0] + 12 * c["out_nodes"][0]) / reps
+    xbytes = (8 * c["rows"] + 4 * c["edges"] + 12 * c["out_nodes"]) / reps
     return {"roots_per_batch": n, "ms_per_batch": dt * 1e3, "trees_per_s": n / dt, "nodes_per_batch": int(offs[n]),
             "errors": int((err != 0).sum()), "max_read_depth": wl.max_depth,
             "traversal_kernel_ms": kms,

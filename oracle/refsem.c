@@ -402,6 +402,7 @@ typedef struct {
     int depth_guard;
     int sched;
     uint32_t flags; /* RS_F_SENSITIVE */
+    uint64_t mx_nodes; /* maximal exploration: checks built so far */
 } qctx;
 
 /* an order-sensitive event inside the current visited scope (if any) */
@@ -841,7 +842,7 @@ done:
 static int check_sched(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, int sched, uint32_t *flags) {
     rs_stats dummy = {0, 0, 0, 0};
     qctx c = {db, q->kind, q->sid, q->kind == 1 ? q->sns : 0, q->kind == 1 ? q->srel : 0,
-              st ? st : &dummy, 0, sched, 0};
+              st ? st : &dummy, 0, sched, 0, 0};
     int d = q->depth;
     if (d <= 0 || db->max_depth < d) d = db->max_depth; /* :82-84 */
     res r = check_is_allowed(&c, q->ns, q->obj, q->rel, d, 0, NULL);
@@ -854,13 +855,188 @@ int rs_check(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st) {
     return check_sched(db, q, err, st, SCHED_EAGER, NULL);
 }
 
+/* ------------------------------------------------------------------ */
+/* Maximal exploration: every check some legal schedule of the reference can start.          */
+/*
+ * The two simulated schedules only explore what the recursion reads.  The reference starts
+ * more, because its checks are built eagerly (oracle/refconc.py restates it goroutine by
+ * goroutine):
+ *   - building checkIsAllowed Adds its first sub-check at once (engine.go:226-246), so an
+ *     expand-subject (engine.go:161), tuple-to-userset (rewrites.go:281-286) or OR-shortcut
+ *     (rewrites.go:88-90) loop starts child k+1 while child k runs -- even when k decides;
+ *   - checkSubjectSetRewrite builds its computed-subject-set, nested rewrite and NOT children
+ *     when it is built (rewrites.go:94-125, 153-178), so an AND or NOT child runs even where
+ *     binop.go's loop never reads it.
+ * Those checks mark visited keys too.  So the flag looks at the tree of every check that can
+ * be started: no visited pruning, no short-circuit, only the static cut-offs (depth, width,
+ * a found-lookahead, a shortcut IN hit).  A scope whose key is reached twice in that tree,
+ * together with an order-sensitive event (or a rest-depth difference plus depth truncation),
+ * may answer differently under some interleaving.  Trees past MX_NODE_CAP checks, and
+ * recursions that never end (an AND's computed subject set reaching its own relation keeps
+ * restDepth: the reference overflows its stack), are flagged as they are. */
+#define MX_NODE_CAP 2000000u
+
+static void mx_ia(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip_direct, vset *vs);
+static void mx_rewrite(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs);
+
+static int mx_enter(qctx *c) {
+    if (++c->mx_nodes > MX_NODE_CAP || c->depth_guard + 1 > MAX_RECURSION) {
+        c->flags |= RS_F_SENSITIVE | RS_F_MAXEXP;
+        return 0;
+    }
+    c->depth_guard++;
+    return 1;
+}
+
+static void mx_es(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, vset *vs) {
+    if (d <= 0) {
+        scope_trunc(vs);
+        return;
+    }
+    const rs_db *db = c->db;
+    vset *own = NULL;
+    if (!vs) vs = own = vset_new();
+    size_t lo, hi;
+    node_rows(db, ns, obj, rel, &lo, &hi);
+    size_t nres = 0;
+    for (size_t i = lo; i < hi; i++) {
+        const key7 *t = ROW(db, i);
+        if (t->kind != 1) continue;
+        nres++;
+        if (exists(c, t->sns, t->sid, t->srel)) { /* found: no child is built (engine.go:133-138) */
+            if (own && ((own->skips && own->events) || (own->dskips && own->trunc))) c->flags |= RS_F_MAXEXP;
+            scope_close(&c->flags, own);
+            return;
+        }
+    }
+    size_t left = nres;
+    if ((long)nres > (long)db->max_width) {
+        left = db->max_width > 0 ? (size_t)(db->max_width - 1) : 0;
+        scope_event(vs);
+    }
+    for (size_t i = lo; i < hi && left; i++) {
+        const key7 *t = ROW(db, i);
+        if (t->kind != 1) continue;
+        left--;
+        int32_t prev = d;
+        if (vset_add_d(vs, vkey(db, t->sns, t->sid, t->srel), d, &prev)) { /* reached again: explored anyway */
+            vs->skips++;
+            if (prev != d) vs->dskips++;
+        }
+        mx_ia(c, t->sns, t->sid, t->srel, d, 1, vs);
+    }
+    if (own && ((own->skips && own->events) || (own->dskips && own->trunc))) c->flags |= RS_F_MAXEXP;
+    scope_close(&c->flags, own);
+}
+
+static void mx_child(qctx *c, uint32_t ns, uint32_t obj, int ci, int d, int nested_cost, vset *vs) {
+    const rs_db *db = c->db;
+    const rs_ast *ch = &db->ast[ci];
+    switch (ch->type) {
+    case RS_TTU: {
+        if (d < 0) {
+            scope_trunc(vs);
+            return;
+        }
+        size_t lo, hi;
+        node_rows(db, ns, obj, ch->rel, &lo, &hi);
+        for (size_t i = lo; i < hi; i++) {
+            const key7 *t = ROW(db, i);
+            if (t->kind == 1) mx_ia(c, t->sns, t->sid, ch->computed, d - 1, 0, vs);
+        }
+        return;
+    }
+    case RS_CSS:
+        if (d < 0) scope_trunc(vs);
+        else mx_ia(c, ns, obj, ch->rel, d, 0, vs);
+        return;
+    case RS_REWRITE:
+        mx_rewrite(c, ns, obj, ci, d - nested_cost, vs);
+        return;
+    case RS_INVERT:
+        scope_event(vs);
+        if (d >= 0 && ch->child_count == 1 && mx_enter(c)) {
+            mx_child(c, ns, obj, db->children[ch->child_begin], d, 0, vs);
+            c->depth_guard--;
+        }
+        return;
+    default:
+        scope_event(vs);
+    }
+}
+
+static void mx_rewrite(qctx *c, uint32_t ns, uint32_t obj, int ai, int d, vset *vs) {
+    if (d <= 0) {
+        scope_trunc(vs);
+        return;
+    }
+    const rs_db *db = c->db;
+    const rs_ast *a = &db->ast[ai];
+    if (a->op != RS_OP_OR) scope_event(vs); /* AND, and not-implemented operators: order-sensitive */
+    if (a->op != RS_OP_OR && a->op != RS_OP_AND) return;
+    if (!mx_enter(c)) return;
+    if (a->op == RS_OP_OR) {
+        int found = 0, has_css = 0;
+        for (int k = 0; k < a->child_count; k++) {
+            const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+            if (ch->type != RS_CSS) continue;
+            has_css = 1;
+            int err;
+            int ri = ast_relation_for(db, ns, ch->rel, &err);
+            if (db->strict && ri >= 0 && db->rels[ri].rewrite >= 0) continue;
+            if (!found && exists(c, ns, obj, ch->rel)) found = 1;
+        }
+        if (has_css && !found)
+            for (int k = 0; k < a->child_count; k++) {
+                const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
+                if (ch->type == RS_CSS) mx_ia(c, ns, obj, ch->rel, d - 1, 1, vs);
+            }
+    }
+    for (int k = 0; k < a->child_count; k++) {
+        int ci = db->children[a->child_begin + k];
+        if (a->op == RS_OP_OR && db->ast[ci].type == RS_CSS) continue;
+        mx_child(c, ns, obj, ci, d, 1, vs);
+    }
+    c->depth_guard--;
+}
+
+static void mx_ia(qctx *c, uint32_t ns, uint32_t obj, uint32_t rel, int d, int skip_direct, vset *vs) {
+    if (d <= 0) {
+        scope_trunc(vs);
+        return;
+    }
+    const rs_db *db = c->db;
+    if (!mx_enter(c)) return;
+    int err;
+    int ri = ast_relation_for(db, ns, rel, &err);
+    if (err) {
+        scope_event(vs);
+    } else {
+        int has_rewrite = ri >= 0 && db->rels[ri].rewrite >= 0;
+        int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
+        if (has_rewrite) mx_rewrite(c, ns, obj, db->rels[ri].rewrite, d, vs);
+        if ((!db->strict || !has_rewrite) && !skip_direct && d - 1 <= 0) scope_trunc(vs);
+        if (can_ss) mx_es(c, ns, obj, rel, d - 1, vs);
+    }
+    c->depth_guard--;
+}
+
+static uint32_t max_exploration_flags(rs_db *db, const rs_query *q) {
+    rs_stats dummy = {0, 0, 0, 0};
+    qctx c = {db, q->kind, q->sid, q->kind == 1 ? q->sns : 0, q->kind == 1 ? q->srel : 0, &dummy, 0, SCHED_EAGER, 0, 0};
+    int d = q->depth;
+    if (d <= 0 || db->max_depth < d) d = db->max_depth;
+    mx_ia(&c, q->ns, q->obj, q->rel, d, 0, NULL);
+    return c.flags & (RS_F_SENSITIVE | RS_F_MAXEXP);
+}
+
 int rs_check_ex(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, uint32_t *flags) {
     uint32_t f0 = 0, f1 = 0;
     int32_t e0 = 0, e1 = 0;
     const int m0 = check_sched(db, q, &e0, st, SCHED_EAGER, &f0);
     const int m1 = check_sched(db, q, &e1, NULL, SCHED_SEQUENTIAL, &f1);
     const int a0 = e0 == 0 && m0 == RS_IS_MEMBER, a1 = e1 == 0 && m1 == RS_IS_MEMBER;
-    uint32_t f = (f0 | f1) & RS_F_SENSITIVE;
+    uint32_t f = ((f0 | f1) & RS_F_SENSITIVE) | max_exploration_flags(db, q);
     if (a0 != a1 || e0 != e1) f |= RS_F_SEQ_DIFFERS;
     if (err) *err = e0;
     if (flags) *flags = f;
@@ -1347,7 +1523,7 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
 int rs_check_u(rs_db *db, const rs_query *q, uint32_t budget, int32_t *err, uint32_t *routed, uint32_t *goals,
                uint32_t *gens) {
     rs_stats dummy = {0, 0, 0, 0};
-    qctx c = {db, q->kind, q->sid, q->kind == 1 ? q->sns : 0, q->kind == 1 ? q->srel : 0, &dummy, 0, SCHED_EAGER, 0};
+    qctx c = {db, q->kind, q->sid, q->kind == 1 ? q->sns : 0, q->kind == 1 ? q->srel : 0, &dummy, 0, SCHED_EAGER, 0, 0};
     uctx u;
     memset(&u, 0, sizeof u);
     u.c = &c;

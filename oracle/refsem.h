@@ -119,11 +119,15 @@ void rs_check_batch(rs_db *db, const rs_query *q, size_t n, int threads,
 /* Schedule-sensitivity report.  The canonical (eager-marking) result,
  * plus flags: RS_F_SENSITIVE when some visited scope both pruned a sibling as already
  * visited and saw an order-sensitive event (depth or width truncation, an error, AND / NOT)
- * under either simulated schedule (the conservative criterion); RS_F_SEQ_DIFFERS when the
+ * under either simulated schedule or in the maximal-exploration tree (the conservative
+ * criterion); RS_F_SEQ_DIFFERS when the
  * sequential schedule (every child done before the next sibling is marked) decides
- * differently.  Runs each query twice. */
+ * differently.  Runs each query three times (two schedules, the maximal-exploration tree). */
 #define RS_F_SENSITIVE 1u
 #define RS_F_SEQ_DIFFERS 2u
+/* set (with RS_F_SENSITIVE) when the maximal-exploration criterion fired: the tree of every
+ * check the reference's eager construction can start (refsem.c "Maximal exploration") */
+#define RS_F_MAXEXP 4u
 int rs_check_ex(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st, uint32_t *flags);
 void rs_check_batch_ex(rs_db *db, const rs_query *q, size_t n, int threads, uint8_t *decision,
                        int32_t *err, uint32_t *flags, rs_stats *st);

@@ -33,7 +33,7 @@ TREE_DT = np.dtype([("type", "<u4"), ("kind", "<u4"), ("sid", "<u4"), ("sns", "<
                     ("n_children", "<u4")])
 
 REWRITE, CSS, TTU, INVERT = 0, 1, 2, 3
-F_SENSITIVE, F_SEQ_DIFFERS = 1, 2  # rs_check_ex flags
+F_SENSITIVE, F_SEQ_DIFFERS, F_MAXEXP = 1, 2, 4  # rs_check_ex flags
 IS_MEMBER, NOT_MEMBER, UNKNOWN = 1, 2, 0
 
 

@@ -8,10 +8,16 @@ in practice.  rs_check_ex re-runs each query under the other extreme (SCHED_SEQU
 k finishes before its sibling is marked) and flags a query as schedule-sensitive when some
 visited scope both pruned a sibling and saw depth / width truncation, an error or AND / NOT.
 These tests pin that the flag is sound for the two schedules (every disagreement is flagged)
-and that it stays rare on the BASELINE workloads."""
+and that it stays rare on the BASELINE workloads.
+
+The second half runs the reference's real concurrency: oracle/refconc.py restates the engine
+goroutine by goroutine (eager construction of checkIsAllowed and of rewrite children, one
+reservation per checkgroup, shared visited sets, cancellation) under seeded schedulers that
+interleave at hop granularity.  No unflagged query may change its answer under any of them."""
 import numpy as np
 import pytest
 
+import refconc
 import refsem
 from fixtures import load, world_for
 from product_helpers import queries_to_oracle, world_from_workload
@@ -74,3 +80,123 @@ def test_sensitivity_rate_on_baseline_generators(wl_name):
     assert not (diff & ~sens).any()
     assert sens.mean() < 0.25
     assert diff.mean() < 0.01
+
+
+POLICIES = ("random", "newest", "oldest")
+
+
+def _interleavings(eng, q, dec, err, flags, runs_flagged, runs_unflagged, seed0):
+    """every query under several seeded interleavings: (unflagged answers that changed, flagged
+    queries whose answer changed under some interleaving, queries without a reference answer)"""
+    bad, flagged_changed, crashed = [], 0, 0
+    for i in range(len(q)):
+        f = bool(flags[i] & refsem.F_SENSITIVE)
+        changed = False
+        for s in range(runs_flagged if f else runs_unflagged):
+            r = eng.allowed(q[i], seed0 + 97 * i + s, POLICIES[s % 3])
+            if r is None:  # the reference's construction recurses without end: no answer to compare
+                crashed += 1
+                break
+            if r != (int(dec[i]), int(err[i])):
+                changed = True
+                if not f:
+                    bad.append((i, r, int(dec[i]), int(err[i])))
+                break
+        flagged_changed += changed and f
+    return bad, flagged_changed, crashed
+
+
+def test_interleavings_reproduce_the_reference_answers():
+    """the goroutine-level restatement gives the reference's own asserted answers (every check
+    fixture transcribed from its tests and docs, and the H3 alias fixture) under every schedule"""
+    import glob
+    import os
+    from fixtures import GOLDEN
+    n = 0
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "*.json"))):
+        name = os.path.basename(path)[:-5]
+        fx = load(name)
+        if not fx.get("checks") or name == "sibling_marking_order":  # (its timing-decided query: below)
+            continue
+        w, t, q = world_for(fx)
+        eng = refconc.Engine(w, t)
+        for i, c in enumerate(fx["checks"]):
+            for s in range(6):
+                r = eng.allowed(q[i], s, POLICIES[s % 3])
+                assert r is not None and bool(r[0]) == c["allowed"], (path, i, s, r)
+                n += 1
+    assert n > 200
+
+
+def test_interleavings_reach_both_answers_of_the_sibling_fixture():
+    """the hand-derived sibling-order fixture: its depth-3 query (flagged) really is decided by
+    timing in the reference -- both answers occur -- and the unflagged ones never move"""
+    fx = load("sibling_marking_order")
+    w, t, q = world_for(fx)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(5, 100)
+    dec, err, flags, _ = orc.check_batch_ex(q, threads=1)
+    eng = refconc.Engine(w, t, max_depth=5, max_width=100)
+    seen = {eng.allowed(q[0], s, POLICIES[s % 3]) for s in range(60)}
+    assert seen == {(0, 0), (1, 0)}
+    assert flags[0] & refsem.F_SENSITIVE
+    bad, _, _ = _interleavings(eng, q, dec, err, flags, 1, 40, 0)
+    assert not bad
+
+
+@pytest.mark.parametrize("rewrites", [True, False])
+def test_no_unflagged_answer_changes_under_interleaving_random_worlds(rewrites):
+    """the 120 random worlds (60 seeds x rewrites on / off), every query under 3 interleavings
+    (9 when flagged)"""
+    bad, changed, flagged = [], 0, 0
+    for seed in range(60):
+        w, t, q, _ = random_world(seed, rewrites=rewrites)
+        orc = refsem.Oracle(w, t)
+        orc.set_limits(w.max_depth, w.max_width)
+        dec, err, flags, _ = orc.check_batch_ex(q, threads=2)
+        b, c, _ = _interleavings(refconc.Engine(w, t), q, dec, err, flags, 9, 3, seed * 100_000)
+        bad += [(seed,) + x for x in b]
+        changed += c
+        flagged += int((flags & refsem.F_SENSITIVE).astype(bool).sum())
+    assert not bad, f"unflagged answers changed under an interleaving: {bad[:5]}"
+    assert changed <= flagged
+
+
+@pytest.mark.parametrize("seed0", [0, 1])
+def test_no_unflagged_answer_changes_dense_random_worlds(seed0):
+    """denser worlds (5 objects, 3 users, 90 tuples: many keys reached twice per scope), where
+    interleavings do change flagged answers -- and never an unflagged one"""
+    bad, changed = [], 0
+    for seed in range(seed0, 60, 2):
+        for rewrites in (True, False):
+            w, t, q, _ = random_world(seed, n_obj=5, n_users=3, n_tuples=90, rewrites=rewrites)
+            orc = refsem.Oracle(w, t)
+            orc.set_limits(w.max_depth, w.max_width)
+            dec, err, flags, _ = orc.check_batch_ex(q, threads=2)
+            b, c, _ = _interleavings(refconc.Engine(w, t), q, dec, err, flags, 12, 3, seed * 100_000 + 7)
+            bad += [(seed, rewrites) + x for x in b]
+            changed += c
+    assert not bad, f"unflagged answers changed under an interleaving: {bad[:5]}"
+
+
+@pytest.mark.parametrize("wl_name", ["nested_groups", "drive"])
+def test_no_unflagged_answer_changes_under_interleaving_baseline_generators(wl_name):
+    """small instances of the C2 / C3 generators: 600 queries, 2 interleavings each (12 when
+    flagged)"""
+    from keto_mi355x import synth
+    if wl_name == "nested_groups":
+        wl = synth.nested_groups(200_000, seed=5)
+        q = synth.nested_groups_queries(wl, 600, seed=9, trunc_frac=0.05)
+    else:
+        wl = synth.drive(depth=6, n_groups=5000, n_users=20000, seed=11)
+        q = synth.drive_queries(wl, 600, seed=4)
+        q["max_depth"][:30] = np.random.default_rng(0).integers(1, 5, 30)
+    w, _ = world_from_workload(wl, with_tuples=False)
+    orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    qo = queries_to_oracle(q)
+    dec, err, flags, _ = orc.check_batch_ex(qo, threads=4)
+    eng = refconc.Engine(w, wl.tuples, shard_bytes=True, max_depth=wl.max_depth, max_width=wl.max_width)
+    bad, _, crashed = _interleavings(eng, qo, dec, err, flags, 12, 2, 31)
+    assert not bad, f"unflagged answers changed under an interleaving: {bad[:5]}"
+    assert crashed == 0
