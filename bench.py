@@ -310,6 +310,58 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
                     "and Folder#viewers"}
 
 
+def store_probe(km, wl, q, n_ins: int = 600, n_del: int = 400):
+    """Incremental snapshots at the workload's size: the graph in a
+    device tuple store (keto_store_*), a TransactRelationTuples of n_ins + n_del rows (new ACL rows
+    on existing objects, deletes of stored rows), then the new version cut by patching the previous
+    snapshot (keto_store_snapshot_patch) -- timed beside the full device build of the same version,
+    and checked against it on the bench's query batch."""
+    import torch
+
+    rng = np.random.default_rng(21)
+    t = wl.tuples
+    t0 = time.perf_counter()
+    st = km.TupleStore(t)
+    load_s = time.perf_counter() - t0
+    base = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict, store=st)
+    ins = t[rng.choice(len(t), n_ins, replace=False)].copy()
+    acl = (ins["ns"] >= 2) & (ins["rel"] != wl.rel_names.index("parents"))
+    ins["subj_kind"][acl], ins["s_ns"][acl], ins["s_rel"][acl] = 0, 0, 0
+    ins["s_obj"][acl] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], int(acl.sum()))
+    ins["shard_id"] = rng.integers(0, 256, (n_ins, 16), dtype=np.uint8)
+    dele = t[rng.choice(len(t), n_del, replace=False)].copy()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st.transact(ins, dele)
+    transact_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    patched = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict, store=st,
+                          base=base)
+    patch_ms = (time.perf_counter() - t0) * 1e3
+    was_patched = patched.patched
+    base.close()
+    t0 = time.perf_counter()
+    full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict, store=st)
+    full_ms = (time.perf_counter() - t0) * 1e3
+    res = []
+    for snap in (patched, full):
+        a, e = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+        res.append((a, e))
+    pi, fi = patched.info(), full.info()
+    out = {"transaction_rows": n_ins + n_del, "patched": was_patched, "patch_ms": patch_ms, "full_build_ms": full_ms,
+           "transact_ms": transact_ms, "store_load_s": load_s, "version": int(pi["version"]),
+           "n_tuples_equal": pi["n_tuples"] == fi["n_tuples"],
+           "checks_vs_full_build": {"n": int(len(q)), "mismatches": int((res[0][0] != res[1][0]).sum()
+                                                                         + (res[0][1] != res[1][1]).sum())},
+           "what": "keto_store_transact of the rows, then keto_store_snapshot_patch of the previous snapshot "
+                   "(host API call to a usable snapshot); full_build_ms: keto_store_snapshot of the same version"}
+    patched.close()
+    full.close()
+    st.close()
+    torch.cuda.empty_cache()
+    return out
+
+
 def serving_probe(km, snap, q, wl, clients: int, req: int, seconds: float):
     """Closed-loop serving load through the coalescing dispatcher (keto_dispatcher_*): `clients`
     native threads (synth.closed_loop, C++) each send `req`-query requests back to back, the way
@@ -580,6 +632,7 @@ def main(argv=None):
     ap.add_argument("--serve-clients", type=int, default=128, help="0 skips the dispatcher probe")
     ap.add_argument("--serve-request", type=int, default=64)
     ap.add_argument("--serve-seconds", type=float, default=3.0)
+    ap.add_argument("--no-store-probe", action="store_true", help="skip the incremental-snapshot probe")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # CPU: launcher + rank protocol only
     argv = sys.argv[1:] if argv is None else list(argv)
     args = ap.parse_args(argv)
@@ -748,6 +801,11 @@ def main(argv=None):
     serving = serving_probe(km, snap, q, wl, args.serve_clients, args.serve_request, args.serve_seconds) \
         if args.serve_clients > 0 else None
     log(f"[rank {rank}] expand + serving probes done ({time.perf_counter() - t_setup:.1f}s since start)")
+    store = None
+    if rank == 0 and world == 1 and not args.no_store_probe and args.workload in ("c3", "c4"):
+        store = store_probe(km, wl, q)
+        log(f"[rank {rank}] store probe: patch {store['patch_ms']:.1f} ms (patched {store['patched']}), full build "
+            f"{store['full_build_ms']:.0f} ms ({time.perf_counter() - t_setup:.1f}s since start)")
 
     achieved = bytes_t0 / (kernel_ms * 1e-3) / 1e9
     kname = "frontier"
@@ -795,11 +853,12 @@ def main(argv=None):
                                     "synchronous batch per step (KETO_F_DEVICE_PTRS): the roofline's timing"},
         "serving": serving,
         "expand": expand,
+        "incremental_snapshot": store,
         "snapshot_build_s": info["build_seconds"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": ("check path: resolve_kernel + fr_block (one launch) + DFS on routed"
-                                if os.environ.get("KETO_FR_ENGINE", "block")[0] != "g" else
+                                if os.environ.get("KETO_FR_ENGINE", "gen")[0] == "b" else
                                 "check path: resolve_kernel + frontier generations (fr_init, fr_expand, fr_reduce, "
                                 "fr_repeat) + DFS on routed"),
                      "kernel_ms": kernel_ms,

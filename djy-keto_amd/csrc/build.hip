@@ -535,6 +535,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         uint64_t buckets = 1;
         while (buckets * 2 < h * 2 + 2) buckets <<= 1;  // load factor <= 1/2
         out.probe_buckets = buckets;
+        out.probe_keys = h;
         out.probe = DevBuf(16 * buckets);
         KETO_HIP(hipMemset(out.probe.p, 0, 16 * buckets));
         DevBuf cur(4 * (M + 1));

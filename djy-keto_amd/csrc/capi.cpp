@@ -507,6 +507,18 @@ int keto_store_snapshot(keto_store *st, const keto_snapshot_config *cfg, keto_sn
     });
 }
 
+int keto_store_snapshot_patch(keto_store *st, const keto_snapshot *base, const keto_snapshot_config *cfg,
+                              keto_snapshot **out, int32_t *patched) {
+    if (!st || !base || !out) return fail(KETO_E_INVALID, "null argument");
+    *out = nullptr;
+    return guarded([&] {
+        bool p = false;
+        *out = reinterpret_cast<keto_snapshot *>(
+            keto::store_snapshot_patch(*reinterpret_cast<keto::TupleStore *>(st), *SN(base), cfg, &p));
+        if (patched) *patched = p ? 1 : 0;
+    });
+}
+
 int keto_store_info(keto_store *st, uint64_t *n_tuples, uint64_t *version) {
     if (!st) return fail(KETO_E_INVALID, "null store");
     keto::store_info(*reinterpret_cast<keto::TupleStore *>(st), n_tuples, version);

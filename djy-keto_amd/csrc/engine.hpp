@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -42,9 +43,15 @@ struct Snapshot {
     DevSnapshot dev{};
     std::vector<void *> allocs;
     std::vector<size_t> alloc_bytes;  // (parallel to allocs: what keto_snapshot_save writes)
+    std::vector<std::shared_ptr<void>> owned;  // (parallel to allocs: a patched snapshot shares its base's unchanged arrays)
     keto_snapshot_info info{};
+    uint64_t store_id = 0;     // the keto_store it was cut from (0: built directly)
+    uint64_t probe_used = 0;   // probe-hash slots holding a key or a tombstone (patches keep the load bounded)
 
-    ~Snapshot();
+    // a device allocation of this snapshot (freed with its last sharer)
+    void own(void *p, size_t bytes);
+    // the allocation of `o` holding p, shared (p must be one of o's arrays)
+    void share(const Snapshot &o, const void *p);
     // node -> (ns, entity, slot) on the host (for Expand output conversion)
     uint32_t ns_of(uint32_t node) const;
 };
@@ -95,7 +102,7 @@ struct RowsOut {
     uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *weight;  // caller-allocated
     uint4 *set_row;
     DevBuf set_dst, probe;
-    uint64_t n_set = 0, probe_buckets = 0;
+    uint64_t n_set = 0, probe_buckets = 0, probe_keys = 0;
 };
 void rows(const RowsIn &in, RowsOut &out);
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows);
@@ -127,8 +134,8 @@ struct FrontierScratch {
     void *mem = nullptr;
     uint64_t cap = 0, ncap = 0, dcap = 0, ocap = 0;  // goals, queries, decisive-key slots, occurrences per slice
     uint32_t *ctrl = nullptr;              // [gbase | gcount | fallback count]
-    uint32_t *qgoals = nullptr, *qroute = nullptr, *fb_list = nullptr, *fb_count = nullptr;
-    uint4 *g0 = nullptr;
+    uint32_t *qrouted = nullptr, *fb_list = nullptr, *fb_count = nullptr;  // qrouted: a bit per query
+    uint4 *g0 = nullptr, *g1 = nullptr;
     uint2 *gfn = nullptr;
     uint2 *gvs = nullptr;  // {value, goals below} per goal
     unsigned long long *dkeys = nullptr;
@@ -267,6 +274,13 @@ TupleStore *store_create(int device, const keto_tuple *tuples, uint64_t n, bool 
 void store_transact(TupleStore &st, const keto_tuple *ins, uint64_t n_ins, const keto_tuple *del, uint64_t n_del,
                     bool device_ptrs);
 Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg);
+// the store's current content by patching `base` (cut from this store earlier); *patched = false
+// when the full device build ran instead
+Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const keto_snapshot_config *cfg, bool *patched);
+// patch.hip: base + the rows the touched tuples name, rebuilt from the store's content (nullptr:
+// base has no node for some touched tuple, or its probe hash is too full -- build in full)
+Snapshot *patch_snapshot(const Snapshot &base, const keto_tuple *store_rows, uint64_t n_store, const keto_tuple *touched,
+                         const uint8_t *touched_is_ins, uint64_t n_touched);
 void store_free(TupleStore *st);
 void store_info(const TupleStore &st, uint64_t *n, uint64_t *version);
 

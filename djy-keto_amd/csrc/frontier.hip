@@ -60,13 +60,14 @@ struct FrontierParams {
     const uint4 *start;  // resolve records: 2 per query position (resolve.hip)
     uint32_t n;
     uint4 *g0;
+    uint4 *g1;                   // KETO_FR_G1: the query subject's start record, copied into every goal by its parent
     uint2 *gfn;
     uint2 *gvs;                  // {value, goals below (fr_reduce): the root's is the query's count}
     uint32_t cap, scap;          // arena goals, goals per slice
     uint32_t *gbase, *gcount;    // [FR_SHARDS][GEN_STRIDE]: slice-local base and count per generation
     uint32_t gen;
     uint32_t gen_cap;            // generations this batch may run (MAX_GEN; asynchronous batches: the speculated count)
-    uint32_t *qgoals, *qroute;   // [n] per query position
+    uint32_t *qrouted;           // [n / 32] one bit per query position: routed to the DFS interpreter (L2-resident)
     uint32_t budget;
     unsigned long long *dkeys;   // decisive (scope, visited key) pairs of the batch (epoch-tagged)
     uint32_t *dcnt;              // their occurrences, counted by fr_repeat
@@ -96,7 +97,11 @@ struct FrontierParams {
 #define FR_MARK(n) ((void)0)
 #endif
 
-__device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_t pos) {
+#ifndef KETO_FR_G1
+#define KETO_FR_G1 0
+#endif
+__device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_t pos, uint32_t i) {
+    if (KETO_FR_G1) return subject_of(P.g1[i]);  // the goal's own copy (coalesced with the generation)
     return subject_of(P.start[2 * (size_t)pos + 1]);  // one load
 }
 // Decisive-key table: keys carry the batch's epoch (1..TAB_EPOCHS) in bits 61-63 (scope < 2^29:
@@ -146,12 +151,13 @@ __device__ __forceinline__ uint32_t dbit(unsigned long long key) {
     return (uint32_t)(mix64(key & ((1ull << 61) - 1ull)) >> 40) & ((1u << DBITS_LOG2) - 1u);
 }
 
-// a routed query also saturates its goal count, so the budget atomic of any later spawn refuses
-constexpr uint32_t QG_ROUTED = 0x40000000u;
+// a routed query: its bit (every later goal of it stops spawning; generation 0 hands it over).
+// One bit per query keeps the flags every goal reads in L2 (128 KB per 2^20 queries) instead of
+// a 4-byte word per query that every goal fetched as a random line from HBM.
 __device__ __forceinline__ void route(const FrontierParams &P, uint32_t pos) {
-    P.qroute[pos] = 1;
-    P.qgoals[pos] = QG_ROUTED;
+    atomicOr(&P.qrouted[pos >> 5], 1u << (pos & 31u));
 }
+__device__ __forceinline__ bool routed(const FrontierParams &P, uint32_t pos) { return (P.qrouted[pos >> 5] >> (pos & 31u)) & 1u; }
 
 __device__ __forceinline__ void spawn(const FrontierParams &P, uint32_t c, uint32_t node, uint32_t pos, uint32_t word,
                                       uint32_t scope) {
@@ -190,8 +196,10 @@ __device__ __forceinline__ uint32_t gen_goal(const FrontierParams &P, const GenM
 // the generation engine's sink: goal records into the arena, occurrences into the sliced list
 struct GlobalSink {
     const FrontierParams &P;
+    uint4 subj;
     __device__ __forceinline__ void spawn(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope) const {
         P.g0[c] = make_uint4(node, pos, word, scope);
+        if (KETO_FR_G1) P.g1[c] = subj;
     }
     __device__ __forceinline__ void spawn_es(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope,
                                              uint32_t) const {
@@ -211,8 +219,8 @@ __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
     const uint4 r0 = P.start[2 * (size_t)i];
     const uint32_t d = r0.z & 0xFFFFu;
     P.g0[(i / chunk) * P.scap + i % chunk] = make_uint4(r0.x, i, gword(G_IA, d), NONE32);
-    P.qgoals[i] = d > GD_MAX ? QG_ROUTED : 0u;
-    P.qroute[i] = d > GD_MAX ? 1u : 0u;
+    if (KETO_FR_G1) P.g1[(i / chunk) * P.scap + i % chunk] = P.start[2 * (size_t)i + 1];
+    if (d > GD_MAX) route(P, i);  // (the bits were cleared before the launch)
 }
 
 // One generation: every goal decides what it can and spawns its children into the next.
@@ -299,7 +307,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
 #endif
         const uint32_t node = g.x, pos = g.y, w = g.z, scope = g.w;
         const uint32_t d = w & GD_MAX, kind = (w >> 12) & 7u, op = w >> 16;
-        const uint32_t qg = live ? P.qgoals[pos] : 0u;
+        const bool qr = live && routed(P, pos);
         // The loads the goal kinds start from, issued together: the row an ES / TTU reads, and
         // the subject's membership record (IA direct check, ES lookahead, OR shortcut).
         uint32_t rnode = NONE32;
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             if (!(ts & VIRT_BIT)) rnode = ts;
         }
         const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
-        const Subject q = live ? load_subject(P, pos) : Subject{0, false, make_uint4(0, 0, 0, 0)};
+        const Subject q = live ? load_subject(P, pos, i) : Subject{0, false, make_uint4(0, 0, 0, 0)};
         FR_MARK(0);
         // ---- phase A: decide, or count the children -------------------------------------------
         const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W);
@@ -324,11 +332,11 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         FR_MARK(1);
         // ---- budget and generation cap.  A query's goal count is its root's subtree count, summed
         // bottom-up by fr_reduce (gvs.y) without atomics, and compared with the budget at
-        // generation 0; here a routed query (qgoals saturated by route) stops spawning, as does
+        // generation 0; here a routed query (its bit set by route) stops spawning, as does
         // a goal with more children than the budget or at the last generation.  A query past its
         // budget spawns on meanwhile (bounded by MAX_GEN and its arena slice) -----------------------
         const uint32_t lane = __lane_id();
-        if (nc && (qg > P.budget || nc > P.budget || last)) {
+        if (nc && (qr || nc > P.budget || last)) {
             route(P, pos);
             nc = 0;
         }
@@ -366,7 +374,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         FR_MARK(3);
         // ---- phase B: write the children (the same walk as phase A) -------------------------------
         if (nc || (kind == G_ES && xrel)) {
-            GlobalSink gs{P};
+            GlobalSink gs{P, q.R};
             PhaseA pb = pa;
             pb.nc = nc;
             phase_b(s, T, q, node, pos, w, scope, row, pb, cb, oc, occ_ok, gs);
@@ -439,7 +447,7 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         }
         if (k == 0) {  // generation 0: one goal per query position
             const uint32_t pos = P.g0[i].y;
-            if (P.qroute[pos] || 1u + sub > P.budget) {
+            if (routed(P, pos) || 1u + sub > P.budget) {
                 P.fb_list[atomicAdd(P.fb_count, 1u)] = P.pos_base + pos;
                 continue;
             }
@@ -533,7 +541,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     while (dcap < 4 * ncap) dcap <<= 1;
     const uint64_t ocap = cap / 2 / FR_SHARDS;  // per slice
     const size_t ctrl = al256(FR_CTRL_BYTES);
-    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 8) + al256(dcap * 12) +
+    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) * (KETO_FR_G1 ? 2 : 1) + al256(cap * 8) + al256(cap * 8) + al256(dcap * 12) +
                          al256(ocap * FR_SHARDS * 8) + (1u << DBITS_LOG2) / 8;
     KETO_HIP(hipMalloc(&f.mem, bytes));
     char *p = static_cast<char *>(f.mem);
@@ -541,12 +549,15 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     f.fb_count = f.ctrl + 2 * FR_SHARDS * GEN_STRIDE;
     f.occ_count = f.fb_count + 4;
     p += ctrl;
-    f.qgoals = reinterpret_cast<uint32_t *>(p);
-    f.qroute = f.qgoals + ncap;
-    f.fb_list = f.qroute + ncap;
+    f.qrouted = reinterpret_cast<uint32_t *>(p);
+    f.fb_list = f.qrouted + 2 * ncap;
     p += al256(ncap * 12);
     f.g0 = reinterpret_cast<uint4 *>(p);
     p += al256(cap * 16);
+    if (KETO_FR_G1) {
+        f.g1 = reinterpret_cast<uint4 *>(p);
+        p += al256(cap * 16);
+    }
     f.gfn = reinterpret_cast<uint2 *>(p);
     p += al256(cap * 8);
     f.gvs = reinterpret_cast<uint2 *>(p);
@@ -578,20 +589,21 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     uint32_t *gbase = f.ctrl, *gcount = f.ctrl + FR_SHARDS * GEN_STRIDE, *fb_count = f.fb_count;
     KETO_HIP(hipMemsetAsync(f.ctrl, 0, FR_CTRL_BYTES, st.stream));
     KETO_HIP(hipMemsetAsync(f.dbits, 0, (1u << DBITS_LOG2) / 8, st.stream));
+    KETO_HIP(hipMemsetAsync(f.qrouted, 0, (L.n + 31) / 32 * 4, st.stream));
     FrontierParams P{};
     P.s = s.dev;
     P.start = st.resolved + 2 * pos_base;
     P.pos_base = (uint32_t)pos_base;
     P.n = (uint32_t)L.n;
     P.g0 = f.g0;
+    P.g1 = f.g1;
     P.gfn = f.gfn;
     P.gvs = f.gvs;
     P.cap = (uint32_t)f.cap;
     P.scap = (uint32_t)(f.cap / FR_SHARDS);
     P.gbase = gbase;
     P.gcount = gcount;
-    P.qgoals = f.qgoals;
-    P.qroute = f.qroute;
+    P.qrouted = f.qrouted;
     P.budget = L.budget;
     P.dkeys = f.dkeys;
     P.dcnt = f.dcnt;

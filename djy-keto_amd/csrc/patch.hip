@@ -1,0 +1,698 @@
+// Incremental snapshots (keto_store_snapshot_patch): the store's
+// content after some transactions, cut by patching the snapshot of an earlier version instead of
+// building it again.
+//
+// The reference's write path touches single rows (persistence/sql/relationtuples.go:104-126
+// WriteRelationTuples, :168-189 DeleteRelationTuples, :277-287 TransactRelationTuples); a read
+// after it sees exactly the new rows.  Here the touched tuples (every insert and delete since the
+// base version, kept by the store) name the rows that can differ:
+//   - the rows of their objects' nodes (set rows for expand-subject / tuple-to-userset, all-rows
+//     for Expand) and the reverse rows of their subjects (checkDirect, the found-lookahead, the
+//     OR shortcut's IN);
+//   - those rows are rebuilt from the store's current content -- one streaming pass over the
+//     store finds their tuples (a small hash of the touched keys, a bit filter in LDS first) --
+//     in shard order (traverser.go:88, relationtuples.go:216), ties by store position as the
+//     full build breaks them;
+//   - every other row keeps its content: the CSR arrays are copied with each row shifted by the
+//     size change of the touched rows before it (one bandwidth-bound pass per array);
+//   - the probe hash gets the heavy subjects' new (subject, node) keys and tombstones for the
+//     keys that went away (member() walks past a tombstone: it is neither empty nor the key);
+//   - the EDGE_LEAF flags of edges into nodes whose set row became empty / non-empty are fixed
+//     through the new reverse rows, RI_SETROWS is recounted, RI_IDROWS only grows;
+//   - node space, entities, visited keys, scheduling weights and the rewrite program are
+//     shared with the base snapshot (same allocations).
+// A touched tuple whose object, subject set or relation slot has no node in the base (a new
+// object, a new (namespace, relation) pair, a uuid past n_uuids) cannot be placed: the caller
+// builds in full.  The base stays untouched (a batch may still be running on it).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iterator>
+#include <memory>
+#include <unordered_map>
+#include <vector>
+
+#include "device_common.hpp"
+
+namespace keto {
+namespace {
+
+constexpr uint32_t BLK = 256;
+constexpr uint32_t ITEMS = 16;  // elements per thread of the copy passes
+inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, (n + BLK - 1) / BLK)); }
+inline dim3 grid_items(uint64_t n) {
+    return dim3((uint32_t)std::max<uint64_t>(1, (n + (uint64_t)BLK * ITEMS - 1) / ((uint64_t)BLK * ITEMS)));
+}
+__device__ __forceinline__ uint64_t gid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+constexpr unsigned long long PROBE_TOMB = ~0ull;  // a removed probe key (never a key: subject < 2^32 - 2)
+
+// ---- keys of the store scan ------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t key4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return mix64(((uint64_t)a << 32 | b) ^ mix64((uint64_t)c << 32 | d) ^ 0x51ED27u);
+}
+// a row's key (ns, obj, rel) and a subject's (kind, id, ns, rel) -- a subject id matches on
+// its id alone, as the delete does (persistence/sql/relationtuples.go:128-150)
+__host__ __device__ __forceinline__ void row_key(const keto_tuple &t, uint4 &k) { k = make_uint4(t.ns, t.obj, t.rel, 0xFFFFFFFFu); }
+__host__ __device__ __forceinline__ void subj_key(const keto_tuple &t, uint4 &k) {
+    k = t.subj_kind == 1 ? make_uint4(1u, t.s_obj, t.s_ns, t.s_rel) : make_uint4(0u, t.s_obj, 0u, 0u);
+}
+struct KeyTab {  // open addressing over power-of-two slots {key, value}; value NONE32 = empty
+    const uint4 *key;
+    const uint32_t *val;
+    uint32_t mask;
+};
+__device__ __forceinline__ uint32_t tab_find(const KeyTab &T, const uint4 &k, uint64_t h) {
+    for (uint32_t b = (uint32_t)h & T.mask;; b = (b + 1) & T.mask) {
+        const uint32_t v = T.val[b];
+        if (v == NONE32) return NONE32;
+        const uint4 x = T.key[b];
+        if (x.x == k.x && x.y == k.y && x.z == k.z && x.w == k.w) return v;
+    }
+}
+
+// ---- node / subject index of raw ids in the base snapshot --------------------------------------
+__device__ __forceinline__ uint32_t node_in(const DevSnapshot &s, uint32_t ns, uint32_t obj, uint32_t rel) {
+    if (ns >= s.n_ns || rel >= s.n_rel) return NONE32;
+    const uint32_t e = ent_lookup(s, ns, obj);
+    if (e == NONE32) return NONE32;
+    const uint32_t slot = nr_slot(s.nsrel[(size_t)ns * s.n_rel + rel]);
+    if (slot == NO_SLOT) return NONE32;
+    const NsDev nd = s.ns[ns];
+    return nd.node_base + (e - nd.ent_base) * nd.n_slots + slot;
+}
+// {row node, subject value (id, or SKEY_SET | node), subject index (rev_off space), 0}
+__device__ __forceinline__ uint4 place(const DevSnapshot &s, const keto_tuple &t) {
+    const uint32_t node = node_in(s, t.ns, t.obj, t.rel);
+    if (t.subj_kind == 1) {
+        const uint32_t c = node_in(s, t.s_ns, t.s_obj, t.s_rel);
+        if (c == NONE32) return make_uint4(node, NONE32, NONE32, 0);
+        return make_uint4(node, c | SKEY_SET, s.n_uuids + c, 0);
+    }
+    if (t.subj_kind != 0 || t.s_obj >= s.n_uuids) return make_uint4(node, NONE32, NONE32, 0);
+    return make_uint4(node, t.s_obj, t.s_obj, 0);
+}
+
+__global__ __launch_bounds__(BLK) void k_place(DevSnapshot s, const keto_tuple *t, uint64_t n, uint4 *out) {
+    const uint64_t i = gid();
+    if (i < n) out[i] = place(s, t[i]);
+}
+
+// one pass over the store: the positions of tuples of a touched row / with a touched subject
+constexpr uint32_t FILTER_WORDS = 8192;  // 256 Kbit LDS filter of both key sets
+__global__ __launch_bounds__(BLK) void k_scan(const keto_tuple *t, uint64_t n, const uint32_t *filter, KeyTab rows,
+                                              KeyTab subj, uint32_t *rlist, uint32_t *slist, uint32_t cap,
+                                              uint32_t *counts) {
+    __shared__ uint32_t f[FILTER_WORDS];
+    for (uint32_t i = threadIdx.x; i < FILTER_WORDS; i += blockDim.x) f[i] = filter[i];
+    __syncthreads();
+    for (uint64_t i = gid(); i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const keto_tuple x = t[i];
+        uint4 k;
+        row_key(x, k);
+        uint64_t h = key4(k.x, k.y, k.z, k.w);
+        uint32_t b = (uint32_t)(h >> 40) & (FILTER_WORDS * 32 - 1);
+        if ((f[b >> 5] >> (b & 31)) & 1u)
+            if (tab_find(rows, k, h) != NONE32) {
+                const uint32_t at = atomicAdd(&counts[0], 1u);
+                if (at < cap) rlist[at] = (uint32_t)i;
+            }
+        subj_key(x, k);
+        h = key4(k.x, k.y, k.z, k.w);
+        b = (uint32_t)(h >> 40) & (FILTER_WORDS * 32 - 1);
+        if ((f[b >> 5] >> (b & 31)) & 1u)
+            if (tab_find(subj, k, h) != NONE32) {
+                const uint32_t at = atomicAdd(&counts[1], 1u);
+                if (at < cap) slist[at] = (uint32_t)i;
+            }
+    }
+}
+
+// matched store tuples -> {place, shard hi, shard lo} for the host
+struct Match {
+    uint4 p;
+    uint32_t pos;
+    unsigned long long hi, lo;
+};
+__global__ __launch_bounds__(BLK) void k_matches(DevSnapshot s, const keto_tuple *t, const uint32_t *list, uint32_t n,
+                                                 Match *out) {
+    const uint64_t i = gid();
+    if (i >= n) return;
+    const keto_tuple x = t[list[i]];
+    unsigned long long hi = 0, lo = 0;
+    for (int k = 0; k < 8; k++) hi = (hi << 8) | x.shard_id[k];
+    for (int k = 8; k < 16; k++) lo = (lo << 8) | x.shard_id[k];
+    out[i] = Match{place(s, x), list[i], hi, lo};
+}
+
+// base rows of the touched nodes / subjects: {all begin, all end, set begin, set end}
+__global__ __launch_bounds__(BLK) void k_old_rows(DevSnapshot s, const uint32_t *nodes, uint32_t m, uint4 *out) {
+    const uint64_t i = gid();
+    if (i >= m) return;
+    const uint32_t c = nodes[i];
+    const uint4 r = s.set_row[c];
+    out[i] = make_uint4(s.all_off[c], s.all_off[c + 1], r.x, r.y);
+}
+__global__ __launch_bounds__(BLK) void k_old_rev(DevSnapshot s, const uint32_t *subj, uint32_t m, uint2 *out) {
+    const uint64_t i = gid();
+    if (i < m) out[i] = make_uint2(s.rev_off[subj[i]], s.rev_off[subj[i] + 1]);
+}
+__global__ __launch_bounds__(BLK) void k_gather_ranges(const uint32_t *src, const uint2 *ranges, const uint32_t *dst_off,
+                                                       uint32_t m, uint32_t *dst) {
+    const uint64_t i = gid();
+    if (i >= m) return;
+    for (uint32_t k = ranges[i].x, o = dst_off[i]; k < ranges[i].y; k++, o++) dst[o] = src[k];
+}
+
+// ---- the shifted copies ---------------------------------------------------------------------
+// rows are touched at sorted indices key[0..m); cum[j] = size change of touched rows 0..j
+__device__ __forceinline__ uint32_t upper(const uint32_t *a, uint32_t m, uint64_t x) {  // # of a[j] <= x
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// offsets: dst[x] = src[x] + the change of the touched rows before x (x in [0, n])
+__global__ __launch_bounds__(BLK) void k_shift_off(uint32_t *dst, const uint32_t *src, uint64_t n, const uint32_t *key,
+                                                   const long long *cum, uint32_t m) {
+    const uint64_t x0 = (uint64_t)blockIdx.x * blockDim.x * ITEMS + threadIdx.x;
+    if (x0 > n) return;
+    uint32_t j = x0 ? upper(key, m, x0 - 1) : 0;  // # of key < x0
+    for (uint32_t it = 0; it < ITEMS; it++) {
+        const uint64_t x = x0 + (uint64_t)it * blockDim.x;
+        if (x > n) break;
+        while (j < m && key[j] < x) j++;
+        dst[x] = (uint32_t)((long long)src[x] + (j ? cum[j - 1] : 0));
+    }
+}
+// values outside the touched rows, moved by the change of the touched rows before them;
+// touched row j holds [beg[j], end[j]) in src
+__global__ __launch_bounds__(BLK) void k_shift_vals(uint32_t *dst, const uint32_t *src, uint64_t n, const uint32_t *beg,
+                                                    const uint32_t *end, const long long *cum, uint32_t m) {
+    const uint64_t e0 = (uint64_t)blockIdx.x * blockDim.x * ITEMS + threadIdx.x;
+    if (e0 >= n) return;
+    uint32_t j = upper(beg, m, e0);  // touched rows starting at or before e0
+    for (uint32_t it = 0; it < ITEMS; it++) {
+        const uint64_t e = e0 + (uint64_t)it * blockDim.x;
+        if (e >= n) break;
+        while (j < m && beg[j] <= e) j++;
+        if (j && e < end[j - 1]) continue;  // inside touched row j-1: rewritten
+        dst[(long long)e + (j ? cum[j - 1] : 0)] = src[e];
+    }
+}
+// set rows of untouched nodes: begin / end moved (inline edges kept)
+__global__ __launch_bounds__(BLK) void k_shift_setrow(uint4 *dst, const uint4 *src, uint64_t n, const uint32_t *key,
+                                                      const long long *cum, uint32_t m) {
+    const uint64_t x0 = (uint64_t)blockIdx.x * blockDim.x * ITEMS + threadIdx.x;
+    if (x0 >= n) return;
+    uint32_t j = x0 ? upper(key, m, x0 - 1) : 0;  // # of key < x0
+    for (uint32_t it = 0; it < ITEMS; it++) {
+        const uint64_t x = x0 + (uint64_t)it * blockDim.x;
+        if (x >= n) break;
+        while (j < m && key[j] < x) j++;
+        if (j < m && key[j] == x) continue;  // touched: written from its new row
+        uint4 r = src[x];
+        const long long d = j ? cum[j - 1] : 0;
+        r.x = (uint32_t)((long long)r.x + d);
+        r.y = (uint32_t)((long long)r.y + d);
+        dst[x] = r;
+    }
+}
+// the touched rows' new content: values [voff[j], voff[j+1]) at dst_off[key[j]]
+__global__ __launch_bounds__(BLK) void k_put_rows(uint32_t *dst, const uint32_t *dst_off, const uint32_t *key,
+                                                  const uint32_t *vals, const uint32_t *voff, uint32_t m) {
+    const uint64_t j = gid();
+    if (j >= m) return;
+    for (uint32_t k = voff[j], o = dst_off[key[j]]; k < voff[j + 1]; k++, o++) dst[o] = vals[k];
+}
+// the touched nodes' set rows: begin / end (the edges follow once every row's extent is known)
+__global__ __launch_bounds__(BLK) void k_put_setrow_extent(uint4 *set_row, const uint32_t *key, const uint32_t *begin,
+                                                           const uint32_t *len, uint32_t m) {
+    const uint64_t j = gid();
+    if (j < m) set_row[key[j]] = make_uint4(begin[j], begin[j] + len[j], NONE32, NONE32);
+}
+__device__ __forceinline__ uint32_t edge_flags(const DevSnapshot &s, const uint4 *set_row, uint32_t c) {
+    uint32_t f = 0;
+    if (s.vkey && s.vkey[c] != c) f |= EDGE_ALIAS;
+    if (s.edge_leaf && set_row[c].x == set_row[c].y) f |= EDGE_LEAF;
+    return c | f;
+}
+// the touched rows' edges (alias / leaf flags from the new rows) and their inline copies
+__global__ __launch_bounds__(BLK) void k_put_edges(DevSnapshot s, uint4 *set_row, uint32_t *set_dst, const uint32_t *key,
+                                                   const uint32_t *vals, const uint32_t *voff, uint32_t m) {
+    const uint64_t j = gid();
+    if (j >= m) return;
+    uint4 r = set_row[key[j]];
+    for (uint32_t k = voff[j], o = r.x; k < voff[j + 1]; k++, o++) set_dst[o] = edge_flags(s, set_row, vals[k]);
+    r.z = r.y > r.x ? set_dst[r.x] : NONE32;
+    r.w = r.y > r.x + 1 ? set_dst[r.x + 1] : NONE32;
+    set_row[key[j]] = r;
+}
+// edges into a node whose set row became empty / non-empty: its parents are the reverse row of
+// the subject set (n_uuids + c); one block per such node
+__global__ __launch_bounds__(BLK) void k_fix_leaf(DevSnapshot s, uint4 *set_row, uint32_t *set_dst, const uint32_t *rev_off,
+                                                  const uint32_t *rev_nodes, const uint32_t *flip, uint32_t m) {
+    if (blockIdx.x >= m) return;
+    const uint32_t c = flip[blockIdx.x];
+    const bool leaf = set_row[c].x == set_row[c].y;
+    const uint64_t v = (uint64_t)s.n_uuids + c;
+    for (uint32_t r = rev_off[v] + threadIdx.x; r < rev_off[v + 1]; r += blockDim.x) {
+        const uint32_t p = rev_nodes[r];
+        uint4 row = set_row[p];
+        bool changed = false;
+        for (uint32_t k = row.x; k < row.y; k++) {
+            const uint32_t e = set_dst[k];
+            if ((e & s.edge_mask) != c) continue;
+            const uint32_t ne = leaf ? (e | EDGE_LEAF) : (e & ~EDGE_LEAF);
+            if (ne != e) {
+                set_dst[k] = ne;
+                changed = true;
+            }
+        }
+        if (changed) {  // (one parent row may list c twice: every thread of p writes the same words)
+            row.z = row.y > row.x ? set_dst[row.x] : NONE32;
+            row.w = row.y > row.x + 1 ? set_dst[row.x + 1] : NONE32;
+            set_row[p] = row;
+        }
+    }
+}
+// probe keys: inserts into empty slots (or found present), removals to tombstones
+__global__ __launch_bounds__(BLK) void k_probe_apply(unsigned long long *probe, uint64_t bmask, const unsigned long long *keys,
+                                                     uint32_t n_ins, uint32_t n_del) {
+    const uint64_t i = gid();
+    if (i >= (uint64_t)n_ins + n_del) return;
+    const unsigned long long key = keys[i];
+    for (uint64_t b = mix64(key) & bmask;; b = (b + 1) & bmask) {
+        for (int k = 0; k < 2; k++) {
+            unsigned long long *slot = &probe[2 * b + k];
+            if (i < n_ins) {
+                const unsigned long long old = atomicCAS(slot, 0ull, key);
+                if (old == 0 || old == key) return;
+            } else {
+                const unsigned long long cur = *slot;
+                if (cur == key) {
+                    *slot = PROBE_TOMB;
+                    return;
+                }
+                if (cur == 0) return;  // not there
+            }
+        }
+    }
+}
+
+struct Touched {  // a touched row or subject, keyed for the scan
+    uint4 key;
+    uint32_t idx;  // node / subject index
+};
+
+}  // namespace
+
+Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_store, const keto_tuple *touched,
+                         const uint8_t *is_ins, uint64_t n_touched) {
+    using build::DevBuf;
+    auto t0 = std::chrono::steady_clock::now();
+    KETO_HIP(hipSetDevice(B.device));
+    static const bool verbose = getenv("KETO_PATCH_VERBOSE") != nullptr;
+    auto tp = t0;
+    auto phase = [&](const char *what) {  // KETO_PATCH_VERBOSE: where the time goes
+        if (!verbose) return;
+        KETO_HIP(hipDeviceSynchronize());
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[keto patch]   %-10s %.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
+    const DevSnapshot &D = B.dev;
+    const uint32_t N = D.n_nodes;
+    const uint64_t M = (uint64_t)D.n_uuids + N;  // subject index space
+    if (n_store >= (1ull << 32) || n_touched >= (1ull << 31)) return nullptr;
+    // ---- 1. place the touched tuples in the base's node space -----------------------------------
+    std::vector<keto_tuple> ht(n_touched);
+    std::vector<uint4> pl(n_touched);
+    if (n_touched) {
+        DevBuf d_pl(sizeof(uint4) * n_touched);
+        KETO_HIP(hipMemcpy(ht.data(), touched, sizeof(keto_tuple) * n_touched, hipMemcpyDeviceToHost));
+        hipLaunchKernelGGL(k_place, grid_for(n_touched), dim3(BLK), 0, 0, D, touched, n_touched, static_cast<uint4 *>(d_pl.p));
+        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemcpy(pl.data(), d_pl.p, sizeof(uint4) * n_touched, hipMemcpyDeviceToHost));
+    }
+    std::unordered_map<uint32_t, size_t> node_at, subj_at;  // node / subject index -> position in the sorted lists
+    std::vector<Touched> tn, ts;
+    std::vector<uint32_t> idrow_slots;
+    for (uint64_t i = 0; i < n_touched; i++) {
+        const keto_tuple &t = ht[i];
+        if (pl[i].x == NONE32 || pl[i].y == NONE32) {
+            if (is_ins[i]) return nullptr;  // an insert with no place in the base: build in full
+            continue;                       // a delete naming no node deletes nothing the base holds
+        }
+        Touched a{}, b{};
+        row_key(t, a.key);
+        a.idx = pl[i].x;
+        subj_key(t, b.key);
+        b.idx = pl[i].z;
+        if (node_at.emplace(a.idx, 0).second) tn.push_back(a);
+        if (subj_at.emplace(b.idx, 0).second) ts.push_back(b);
+        if (is_ins[i] && t.subj_kind == 0) idrow_slots.push_back(pl[i].x);
+    }
+    std::sort(tn.begin(), tn.end(), [](const Touched &x, const Touched &y) { return x.idx < y.idx; });
+    std::sort(ts.begin(), ts.end(), [](const Touched &x, const Touched &y) { return x.idx < y.idx; });
+    for (size_t j = 0; j < tn.size(); j++) node_at[tn[j].idx] = j;
+    for (size_t j = 0; j < ts.size(); j++) subj_at[ts[j].idx] = j;
+    const uint32_t m = (uint32_t)tn.size(), ms = (uint32_t)ts.size();
+
+    phase("place");
+    // ---- 2. the touched rows' tuples: one pass over the store ------------------------------------
+    std::vector<Match> rmatch, smatch;
+    if (m) {
+        auto tab = [&](const std::vector<Touched> &v, DevBuf &kb, DevBuf &vb, std::vector<uint32_t> &filter) -> KeyTab {
+            uint32_t size = 64;
+            while (size < 4 * v.size()) size <<= 1;
+            std::vector<uint4> keys(size, make_uint4(0, 0, 0, 0));
+            std::vector<uint32_t> vals(size, NONE32);
+            for (size_t j = 0; j < v.size(); j++) {
+                const uint64_t h = key4(v[j].key.x, v[j].key.y, v[j].key.z, v[j].key.w);
+                uint32_t b = (uint32_t)h & (size - 1);
+                while (vals[b] != NONE32) b = (b + 1) & (size - 1);
+                keys[b] = v[j].key;
+                vals[b] = (uint32_t)j;
+                const uint32_t fb = (uint32_t)(h >> 40) & (FILTER_WORDS * 32 - 1);
+                filter[fb >> 5] |= 1u << (fb & 31);
+            }
+            kb = DevBuf(16ull * size);
+            vb = DevBuf(4ull * size);
+            KETO_HIP(hipMemcpy(kb.p, keys.data(), 16ull * size, hipMemcpyHostToDevice));
+            KETO_HIP(hipMemcpy(vb.p, vals.data(), 4ull * size, hipMemcpyHostToDevice));
+            return KeyTab{static_cast<const uint4 *>(kb.p), vb.u32(), size - 1};
+        };
+        std::vector<uint32_t> filter(FILTER_WORDS, 0);
+        DevBuf rk, rv, sk, sv;
+        const KeyTab RT = tab(tn, rk, rv, filter), ST = tab(ts, sk, sv, filter);
+        DevBuf d_filter(4ull * FILTER_WORDS), counts(16);
+        KETO_HIP(hipMemcpy(d_filter.p, filter.data(), 4ull * FILTER_WORDS, hipMemcpyHostToDevice));
+        int per_cu = 0;
+        KETO_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_scan), BLK, 0));
+        const uint32_t grid = (uint32_t)std::max(1, num_cus(B.device) * std::max(per_cu, 1));
+        uint32_t cap = 1u << 20;
+        for (;;) {
+            DevBuf rl(4ull * cap), sl(4ull * cap);
+            KETO_HIP(hipMemset(counts.p, 0, 16));
+            hipLaunchKernelGGL(k_scan, dim3(grid), dim3(BLK), 0, 0, rows, n_store, d_filter.u32(), RT, ST, rl.u32(), sl.u32(),
+                               cap, counts.u32());
+            KETO_HIP(hipGetLastError());
+            uint32_t c[2];
+            KETO_HIP(hipMemcpy(c, counts.p, 8, hipMemcpyDeviceToHost));
+            if (c[0] > cap || c[1] > cap) {
+                cap = std::max(c[0], c[1]);
+                continue;
+            }
+            for (int w = 0; w < 2; w++) {
+                std::vector<Match> &out = w ? smatch : rmatch;
+                out.resize(c[w]);
+                if (!c[w]) continue;
+                DevBuf mb(sizeof(Match) * c[w]);
+                hipLaunchKernelGGL(k_matches, grid_for(c[w]), dim3(BLK), 0, 0, D, rows, w ? sl.u32() : rl.u32(), c[w],
+                                   static_cast<Match *>(mb.p));
+                KETO_HIP(hipGetLastError());
+                KETO_HIP(hipMemcpy(out.data(), mb.p, sizeof(Match) * c[w], hipMemcpyDeviceToHost));
+            }
+            break;
+        }
+    }
+    for (const Match &x : rmatch)  // (store tuples of touched rows were placed by step 1 or the base build)
+        if (x.p.x == NONE32 || x.p.y == NONE32) return nullptr;
+    for (const Match &x : smatch)
+        if (x.p.x == NONE32 || x.p.z == NONE32) return nullptr;
+
+    phase("scan");
+    // ---- 3. the touched rows' new content (host: a few rows) --------------------------------------
+    std::vector<std::vector<const Match *>> per_node(m);
+    for (const Match &x : rmatch) {
+        auto it = node_at.find(x.p.x);
+        if (it != node_at.end()) per_node[it->second].push_back(&x);
+    }
+    std::vector<uint32_t> key_n(m), all_vals, all_voff(m + 1, 0), set_vals, set_voff(m + 1, 0), set_len(m);
+    for (uint32_t j = 0; j < m; j++) {
+        key_n[j] = tn[j].idx;
+        auto &v = per_node[j];
+        std::sort(v.begin(), v.end(), [](const Match *a, const Match *b) {
+            return a->hi != b->hi ? a->hi < b->hi : (a->lo != b->lo ? a->lo < b->lo : a->pos < b->pos);
+        });
+        for (const Match *x : v) {
+            all_vals.push_back(x->p.y);
+            if (x->p.y & SKEY_SET) set_vals.push_back(x->p.y & ~SKEY_SET);
+        }
+        all_voff[j + 1] = (uint32_t)all_vals.size();
+        set_voff[j + 1] = (uint32_t)set_vals.size();
+        set_len[j] = set_voff[j + 1] - set_voff[j];
+    }
+    std::vector<std::vector<uint32_t>> per_subj(ms);
+    for (const Match &x : smatch) {
+        auto it = subj_at.find(x.p.z);
+        if (it != subj_at.end()) per_subj[it->second].push_back(x.p.x);
+    }
+    std::vector<uint32_t> key_s(ms), rev_vals, rev_voff(ms + 1, 0);
+    for (uint32_t j = 0; j < ms; j++) {
+        key_s[j] = ts[j].idx;
+        std::sort(per_subj[j].begin(), per_subj[j].end());
+        rev_vals.insert(rev_vals.end(), per_subj[j].begin(), per_subj[j].end());
+        rev_voff[j + 1] = (uint32_t)rev_vals.size();
+    }
+    // the base's extents of those rows
+    std::vector<uint4> old_n(m);
+    std::vector<uint2> old_s(ms);
+    auto up = [](const auto &v) {
+        using T = typename std::decay_t<decltype(v)>::value_type;
+        DevBuf b(std::max<size_t>(1, v.size()) * sizeof(T));
+        if (!v.empty()) KETO_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+        return b;
+    };
+    DevBuf d_key_n = up(key_n), d_key_s = up(key_s);
+    if (m) {
+        DevBuf o(sizeof(uint4) * m);
+        hipLaunchKernelGGL(k_old_rows, grid_for(m), dim3(BLK), 0, 0, D, d_key_n.u32(), m, static_cast<uint4 *>(o.p));
+        KETO_HIP(hipMemcpy(old_n.data(), o.p, sizeof(uint4) * m, hipMemcpyDeviceToHost));
+    }
+    if (ms) {
+        DevBuf o(sizeof(uint2) * ms);
+        hipLaunchKernelGGL(k_old_rev, grid_for(ms), dim3(BLK), 0, 0, D, d_key_s.u32(), ms, static_cast<uint2 *>(o.p));
+        KETO_HIP(hipMemcpy(old_s.data(), o.p, sizeof(uint2) * ms, hipMemcpyDeviceToHost));
+    }
+    // the heavy subjects' old reverse rows (their probe keys)
+    std::vector<uint2> heavy_rng;
+    std::vector<uint32_t> heavy_off(1, 0), heavy_j;
+    for (uint32_t j = 0; j < ms; j++)
+        if (old_s[j].y - old_s[j].x > PROBE_K) {
+            heavy_rng.push_back(old_s[j]);
+            heavy_j.push_back(j);
+            heavy_off.push_back(heavy_off.back() + (old_s[j].y - old_s[j].x));
+        }
+    std::vector<uint32_t> heavy_old(heavy_off.back());
+    if (!heavy_j.empty()) {
+        DevBuf r = up(heavy_rng), o = up(heavy_off), g(4ull * std::max<uint32_t>(1, heavy_off.back()));
+        hipLaunchKernelGGL(k_gather_ranges, grid_for(heavy_j.size()), dim3(BLK), 0, 0, D.rev_nodes,
+                           static_cast<const uint2 *>(r.p), o.u32(), (uint32_t)heavy_j.size(), g.u32());
+        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemcpy(heavy_old.data(), g.p, 4ull * heavy_off.back(), hipMemcpyDeviceToHost));
+    }
+    // probe key changes: a heavy subject's keys are exactly the distinct nodes of its reverse row
+    std::vector<unsigned long long> ins_keys, del_keys;
+    {
+        std::vector<int64_t> hj(ms, -1);
+        for (size_t h = 0; h < heavy_j.size(); h++) hj[heavy_j[h]] = (int64_t)h;
+        for (uint32_t j = 0; j < ms; j++) {
+            std::vector<uint32_t> nw(rev_vals.begin() + rev_voff[j], rev_vals.begin() + rev_voff[j + 1]), old;
+            const bool new_heavy = nw.size() > PROBE_K;
+            if (hj[j] >= 0) old.assign(heavy_old.begin() + heavy_off[hj[j]], heavy_old.begin() + heavy_off[hj[j] + 1]);
+            std::sort(old.begin(), old.end());
+            old.erase(std::unique(old.begin(), old.end()), old.end());
+            nw.erase(std::unique(nw.begin(), nw.end()), nw.end());
+            if (!new_heavy) nw.clear();
+            const uint64_t v = key_s[j];
+            auto key = [&](uint32_t node) { return ((v << 32) | node) + 1; };
+            std::vector<uint32_t> d;
+            std::set_difference(nw.begin(), nw.end(), old.begin(), old.end(), std::back_inserter(d));
+            for (uint32_t x : d) ins_keys.push_back(key(x));
+            d.clear();
+            std::set_difference(old.begin(), old.end(), nw.begin(), nw.end(), std::back_inserter(d));
+            for (uint32_t x : d) del_keys.push_back(key(x));
+        }
+    }
+    const uint64_t probe_slots = 2ull * ((uint64_t)D.probe_mask + 1);
+    if (B.probe_used + ins_keys.size() > probe_slots * 3 / 4) return nullptr;  // too full: build in full
+
+    phase("rows");
+    // ---- 4. the new snapshot: shifted copies, the touched rows, the probe keys ---------------------
+    auto S = std::make_unique<Snapshot>();
+    Snapshot &s = *S;
+    s.device = B.device;
+    s.n_ns = B.n_ns;
+    s.n_rel = B.n_rel;
+    s.n_rel_caller = B.n_rel_caller;
+    s.n_uuids = B.n_uuids;
+    s.strict = B.strict;
+    s.ns_names = B.ns_names;
+    s.rel_names = B.rel_names;
+    s.ns = B.ns;
+    s.ent_obj = B.ent_obj;
+    s.slot_rel = B.slot_rel;
+    s.relinfo = B.relinfo;
+    s.nsrel = B.nsrel;
+    s.ops = B.ops;
+    s.op_children = B.op_children;
+    s.op_items = B.op_items;
+    s.or_items = B.or_items;
+    s.info = B.info;
+    s.info.device_bytes = 0;
+    s.store_id = B.store_id;
+    s.probe_used = B.probe_used + ins_keys.size();
+    DevSnapshot &X = s.dev;
+    X = D;
+    for (const void *p : {(const void *)D.weight, (const void *)D.ent_obj, (const void *)D.slot_rel, (const void *)D.vkey,
+                          (const void *)D.ns, (const void *)D.nsrel, (const void *)D.ops, (const void *)D.op_children,
+                          (const void *)D.op_items, (const void *)D.or_items, (const void *)D.ent_rank})
+        s.share(B, p);
+    auto fresh = [&](size_t bytes) -> void * {
+        bytes = (bytes + 31) / 16 * 16;
+        void *p = nullptr;
+        KETO_HIP(hipMalloc(&p, bytes));
+        s.own(p, bytes);
+        return p;
+    };
+    // size change per touched row, cumulative
+    std::vector<long long> cum_all(m), cum_set(m), cum_rev(ms);
+    std::vector<uint32_t> beg_all(m), end_all(m), beg_set(m), end_set(m), beg_rev(ms), end_rev(ms);
+    long long ca = 0, cs = 0, cr = 0;
+    for (uint32_t j = 0; j < m; j++) {
+        beg_all[j] = old_n[j].x;
+        end_all[j] = old_n[j].y;
+        beg_set[j] = old_n[j].z;
+        end_set[j] = old_n[j].w;
+        ca += (long long)(all_voff[j + 1] - all_voff[j]) - (old_n[j].y - old_n[j].x);
+        cs += (long long)set_len[j] - (old_n[j].w - old_n[j].z);
+        cum_all[j] = ca;
+        cum_set[j] = cs;
+    }
+    for (uint32_t j = 0; j < ms; j++) {
+        beg_rev[j] = old_s[j].x;
+        end_rev[j] = old_s[j].y;
+        cr += (long long)(rev_voff[j + 1] - rev_voff[j]) - (old_s[j].y - old_s[j].x);
+        cum_rev[j] = cr;
+    }
+    const uint64_t n_all_old = B.info.n_tuples, n_set_old = B.info.n_set_edges;
+    const uint64_t n_all = (uint64_t)((long long)n_all_old + ca), n_set = (uint64_t)((long long)n_set_old + cs);
+    if (n_all != n_store || (uint64_t)((long long)n_all_old + cr) != n_store) return nullptr;  // (the log and the store disagree)
+    DevBuf d_cum_all = up(cum_all), d_cum_set = up(cum_set), d_cum_rev = up(cum_rev);
+    DevBuf d_beg_all = up(beg_all), d_end_all = up(end_all), d_beg_set = up(beg_set), d_end_set = up(end_set);
+    DevBuf d_beg_rev = up(beg_rev), d_end_rev = up(end_rev);
+    DevBuf d_all_vals = up(all_vals), d_all_voff = up(all_voff), d_set_vals = up(set_vals), d_set_voff = up(set_voff);
+    DevBuf d_rev_vals = up(rev_vals), d_rev_voff = up(rev_voff), d_set_len = up(set_len);
+    const long long *CA = static_cast<const long long *>(d_cum_all.p), *CS = static_cast<const long long *>(d_cum_set.p),
+                    *CR = static_cast<const long long *>(d_cum_rev.p);
+    // all-rows (Expand)
+    uint32_t *all_off = static_cast<uint32_t *>(fresh(4ull * (N + 1)));
+    uint32_t *all_subj = static_cast<uint32_t *>(fresh(4ull * std::max<uint64_t>(1, n_all)));
+    hipLaunchKernelGGL(k_shift_off, grid_items(N + 1), dim3(BLK), 0, 0, all_off, D.all_off, (uint64_t)N, d_key_n.u32(), CA, m);
+    hipLaunchKernelGGL(k_shift_vals, grid_items(n_all_old), dim3(BLK), 0, 0, all_subj, D.all_subj, n_all_old, d_beg_all.u32(),
+                       d_end_all.u32(), CA, m);
+    hipLaunchKernelGGL(k_put_rows, grid_for(m), dim3(BLK), 0, 0, all_subj, all_off, d_key_n.u32(), d_all_vals.u32(),
+                       d_all_voff.u32(), m);
+    KETO_HIP(hipGetLastError());
+    phase("all-rows");
+    // reverse rows (membership)
+    uint32_t *rev_off = static_cast<uint32_t *>(fresh(4ull * (M + 1)));
+    uint32_t *rev_nodes = static_cast<uint32_t *>(fresh(4ull * std::max<uint64_t>(1, n_all)));
+    hipLaunchKernelGGL(k_shift_off, grid_items(M + 1), dim3(BLK), 0, 0, rev_off, D.rev_off, M, d_key_s.u32(), CR, ms);
+    hipLaunchKernelGGL(k_shift_vals, grid_items(n_all_old), dim3(BLK), 0, 0, rev_nodes, D.rev_nodes, n_all_old, d_beg_rev.u32(),
+                       d_end_rev.u32(), CR, ms);
+    hipLaunchKernelGGL(k_put_rows, grid_for(ms), dim3(BLK), 0, 0, rev_nodes, rev_off, d_key_s.u32(), d_rev_vals.u32(),
+                       d_rev_voff.u32(), ms);
+    KETO_HIP(hipGetLastError());
+    phase("rev-rows");
+    // set rows (expand-subject, tuple-to-userset): extents, then the touched rows' edges
+    uint4 *set_row = static_cast<uint4 *>(fresh(16ull * N));
+    uint32_t *set_dst = static_cast<uint32_t *>(fresh(4ull * n_set + 16));
+    hipLaunchKernelGGL(k_shift_setrow, grid_items(N), dim3(BLK), 0, 0, set_row, D.set_row, (uint64_t)N, d_key_n.u32(), CS, m);
+    hipLaunchKernelGGL(k_shift_vals, grid_items(n_set_old), dim3(BLK), 0, 0, set_dst, D.set_dst, n_set_old, d_beg_set.u32(),
+                       d_end_set.u32(), CS, m);
+    {
+        std::vector<uint32_t> nb(m);  // new begin of each touched set row: old begin + change before it
+        for (uint32_t j = 0; j < m; j++) nb[j] = (uint32_t)((long long)beg_set[j] + (j ? cum_set[j - 1] : 0));
+        DevBuf d_nb = up(nb);
+        hipLaunchKernelGGL(k_put_setrow_extent, grid_for(m), dim3(BLK), 0, 0, set_row, d_key_n.u32(), d_nb.u32(), d_set_len.u32(), m);
+        KETO_HIP(hipGetLastError());
+        X.set_row = set_row;
+        hipLaunchKernelGGL(k_put_edges, grid_for(m), dim3(BLK), 0, 0, X, set_row, set_dst, d_key_n.u32(), d_set_vals.u32(),
+                           d_set_voff.u32(), m);
+        KETO_HIP(hipGetLastError());
+    }
+    phase("set-rows");
+    // leaf flags of the edges into nodes whose set row changed between empty and non-empty
+    std::vector<uint32_t> flip;
+    for (uint32_t j = 0; j < m; j++)
+        if ((set_len[j] == 0) != (old_n[j].w == old_n[j].z)) flip.push_back(key_n[j]);
+    if (D.edge_leaf && !flip.empty()) {
+        DevBuf d_flip = up(flip);
+        hipLaunchKernelGGL(k_fix_leaf, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, X, set_row, set_dst, rev_off, rev_nodes,
+                           d_flip.u32(), (uint32_t)flip.size());
+        KETO_HIP(hipGetLastError());
+    }
+    phase("leaf");
+    // probe hash: a copy with the heavy subjects' key changes
+    void *probe = fresh(16ull * ((uint64_t)D.probe_mask + 1));
+    KETO_HIP(hipMemcpyAsync(probe, D.probe, 16ull * ((uint64_t)D.probe_mask + 1), hipMemcpyDeviceToDevice, 0));
+    if (!ins_keys.empty() || !del_keys.empty()) {
+        std::vector<unsigned long long> keys(ins_keys);
+        keys.insert(keys.end(), del_keys.begin(), del_keys.end());
+        DevBuf d_keys = up(keys);
+        hipLaunchKernelGGL(k_probe_apply, grid_for(keys.size()), dim3(BLK), 0, 0, static_cast<unsigned long long *>(probe),
+                           (uint64_t)D.probe_mask, static_cast<const unsigned long long *>(d_keys.p), (uint32_t)ins_keys.size(),
+                           (uint32_t)del_keys.size());
+        KETO_HIP(hipGetLastError());
+    }
+    phase("probe");
+    // relation info: RI_SETROWS recounted over the new set rows, RI_IDROWS grown by the inserts
+    {
+        const uint32_t total_slots = (uint32_t)s.relinfo.size();
+        if (total_slots) {
+            DevBuf flag(4ull * total_slots);
+            KETO_HIP(hipMemset(flag.p, 0, 4ull * total_slots));
+            build::slot_setrows(set_row, N, D.ns, s.n_ns, flag.u32());
+            std::vector<uint32_t> hf(total_slots);
+            KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
+            for (uint32_t gs = 0; gs < total_slots; gs++) s.relinfo[gs] = (s.relinfo[gs] & ~RI_SETROWS) | (hf[gs] ? RI_SETROWS : 0u);
+            for (uint32_t node : idrow_slots) {
+                const uint32_t ns = B.ns_of(node);
+                s.relinfo[s.ns[ns].slot_base + (node - s.ns[ns].node_base) % s.ns[ns].n_slots] |= RI_IDROWS;
+            }
+        }
+        uint32_t *ri = static_cast<uint32_t *>(fresh(std::max<size_t>(1, s.relinfo.size()) * 4));
+        if (!s.relinfo.empty()) KETO_HIP(hipMemcpy(ri, s.relinfo.data(), 4 * s.relinfo.size(), hipMemcpyHostToDevice));
+        X.relinfo = ri;
+    }
+    KETO_HIP(hipDeviceSynchronize());
+    phase("relinfo");
+    X.all_off = all_off;
+    X.all_subj = all_subj;
+    X.rev_off = rev_off;
+    X.rev_nodes = rev_nodes;
+    X.set_row = set_row;
+    X.set_dst = set_dst;
+    X.probe = static_cast<const uint4 *>(probe);
+    s.info.n_tuples = n_all;
+    s.info.n_set_edges = n_set;
+    s.info.n_rev_entries = n_all;
+    s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (verbose)
+        fprintf(stderr, "[keto patch] %llu touched tuples: %u rows, %u subjects, %llu store matches, %zu leaf flips, "
+                        "probe +%zu -%zu keys, %.2f ms\n", (unsigned long long)n_touched, m, ms,
+                (unsigned long long)(rmatch.size() + smatch.size()), flip.size(), ins_keys.size(), del_keys.size(),
+                s.info.build_seconds * 1e3);
+    return S.release();
+}
+
+}  // namespace keto

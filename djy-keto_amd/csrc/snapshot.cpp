@@ -104,8 +104,24 @@ uint32_t bytes16(const std::vector<T> &v) {
 
 }  // namespace
 
-Snapshot::~Snapshot() {
-    for (void *p : allocs) (void)hipFree(p);
+void Snapshot::own(void *p, size_t bytes) {
+    allocs.push_back(p);
+    alloc_bytes.push_back(bytes);
+    owned.emplace_back(p, [](void *q) { (void)hipFree(q); });
+    info.device_bytes += bytes;
+}
+
+void Snapshot::share(const Snapshot &o, const void *p) {
+    if (!p) return;
+    for (size_t i = 0; i < o.allocs.size(); i++)
+        if (o.allocs[i] == p) {
+            allocs.push_back(o.allocs[i]);
+            alloc_bytes.push_back(o.alloc_bytes[i]);
+            owned.push_back(o.owned[i]);
+            info.device_bytes += o.alloc_bytes[i];
+            return;
+        }
+    throw Error(KETO_E_INVALID, "shared array outside the base snapshot's allocations");
 }
 
 uint32_t Snapshot::ns_of(uint32_t node) const {
@@ -206,17 +222,15 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         bytes = (bytes + 31) / 16 * 16;
         void *p = nullptr;
         KETO_HIP(hipMalloc(&p, bytes));
-        s.allocs.push_back(p);
-        s.alloc_bytes.push_back(bytes);
+        s.own(p, bytes);
         KETO_HIP(hipMemset(p, 0, bytes));
-        s.info.device_bytes += bytes;
         return p;
     };
     auto adopt = [&](DevBuf &b) -> void * {
-        s.info.device_bytes += b.bytes;
-        s.allocs.push_back(b.p);
-        s.alloc_bytes.push_back(b.bytes);
-        return b.release();
+        const size_t bytes = b.bytes;
+        void *p = b.release();
+        s.own(p, bytes);
+        return p;
     };
 
     // ---- validate tuples, collect (ns, rel) pairs ------------------------------
@@ -391,6 +405,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.set_dst = static_cast<const uint32_t *>(adopt(ro.set_dst));
     D.probe = static_cast<const uint4 *>(adopt(ro.probe));
     D.probe_mask = (uint32_t)(ro.probe_buckets - 1);
+    s.probe_used = ro.probe_keys;
     D.probe_k = PROBE_K;
     s.info.n_set_edges = ro.n_set;
     s.info.n_rev_entries = n;
@@ -712,8 +727,9 @@ Snapshot *load_snapshot(const char *path, int device) {
         for (size_t i = 0; i < bytes.size(); i++) {
             void *p = nullptr;
             KETO_HIP(hipMalloc(&p, std::max<size_t>(16, bytes[i])));
-            s.allocs.push_back(p);
-            s.alloc_bytes.push_back(bytes[i]);
+            const uint64_t keep = s.info.device_bytes;
+            s.own(p, bytes[i]);
+            s.info.device_bytes = keep;  // (the file's info already counts every array)
             for (size_t off = 0; off < bytes[i]; off += STAGE) {
                 const size_t b = std::min(STAGE, bytes[i] - off);
                 F.get(stage, b);
@@ -731,6 +747,7 @@ Snapshot *load_snapshot(const char *path, int device) {
         if (i >= (int64_t)s.allocs.size()) throw Error(KETO_E_INVALID, "snapshot file corrupt");
         p = i < 0 ? nullptr : s.allocs[(size_t)i];
     });
+    s.probe_used = (uint64_t)s.dev.probe_mask + 1;  // (not in the file: assume the build's bound, half the slots)
     s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return S.release();
 }

@@ -15,13 +15,18 @@
 // delete keys and one pass over the store that flags matching rows.  Survivors are then
 // compacted in place: the deleted slots below the new length are filled with the live rows
 // above it.  Row order does not matter, because the snapshot builder orders every row by
-// shard_id.  A snapshot of the current content is one device build
-// (keto_snapshot_build_device, ~2 s at 1B tuples), stamped with the store's version: the
-// snaptoken the reference leaves unimplemented (check/handler.go:327-330).
+// shard_id.  A snapshot of the current content is stamped with the store's version: the
+// snaptoken the reference leaves unimplemented (check/handler.go:327-330).  It is either one
+// device build (keto_snapshot_build_device, ~2 s at 1B tuples) or a patch of an earlier
+// snapshot of this store (patch.hip): the store keeps every transaction's rows in a change log
+// (bounded), and the rows they name are the only ones a patch rebuilds.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <deque>
 #include <memory>
+#include <vector>
 
 #include "engine.hpp"
 
@@ -108,6 +113,15 @@ struct TupleStore {
     int device = 0;
     build::DevBuf buf;  // capacity in rows = buf.bytes / sizeof(keto_tuple)
     uint64_t n = 0, version = 0;
+    uint64_t id = 0;  // stamped on its snapshots: a patch only takes a base cut from this store
+    // change log: the rows of the last transactions (inserts then deletes), oldest first
+    struct Change {
+        uint64_t version, n_ins, n_del;
+        build::DevBuf rows;
+    };
+    std::deque<Change> log;
+    uint64_t log_rows = 0;
+    static constexpr uint64_t LOG_MAX_ROWS = 1ull << 22;
     keto_tuple *rows() const { return static_cast<keto_tuple *>(buf.p); }
     uint64_t cap() const { return buf.bytes / sizeof(keto_tuple); }
     void reserve(uint64_t need) {
@@ -120,8 +134,10 @@ struct TupleStore {
 
 TupleStore *store_create(int device, const keto_tuple *tuples, uint64_t n, bool device_ptrs) {
     KETO_HIP(hipSetDevice(device));
+    static std::atomic<uint64_t> next_id{1};
     auto st = std::make_unique<TupleStore>();
     st->device = device;
+    st->id = next_id++;
     st->reserve(std::max<uint64_t>(n, 64));
     if (n)
         KETO_HIP(hipMemcpy(st->rows(), tuples, n * sizeof(keto_tuple),
@@ -134,6 +150,18 @@ void store_transact(TupleStore &st, const keto_tuple *ins, uint64_t n_ins, const
                     bool device_ptrs) {
     KETO_HIP(hipSetDevice(st.device));
     const hipMemcpyKind kind = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    {   // the change log entry of this version (a transaction larger than the log holds none: a
+        // snapshot across it is a full build)
+        TupleStore::Change c{st.version + 1, n_ins, n_del, build::DevBuf(sizeof(keto_tuple) * std::max<uint64_t>(1, n_ins + n_del))};
+        if (n_ins) KETO_HIP(hipMemcpy(c.rows.p, ins, n_ins * sizeof(keto_tuple), kind));
+        if (n_del) KETO_HIP(hipMemcpy(static_cast<keto_tuple *>(c.rows.p) + n_ins, del, n_del * sizeof(keto_tuple), kind));
+        st.log_rows += n_ins + n_del;
+        st.log.push_back(std::move(c));
+        while (!st.log.empty() && st.log_rows > TupleStore::LOG_MAX_ROWS) {
+            st.log_rows -= st.log.front().n_ins + st.log.front().n_del;
+            st.log.pop_front();
+        }
+    }
     if (n_ins) {  // WriteRelationTuples: appended rows, fresh shard_ids from the caller
         st.reserve(st.n + n_ins);
         KETO_HIP(hipMemcpy(st.rows() + st.n, ins, n_ins * sizeof(keto_tuple), kind));
@@ -187,7 +215,46 @@ Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg) 
     if (!cfg || cfg->device != st.device) throw Error(KETO_E_INVALID, "config names another device");
     Snapshot *s = build_snapshot(cfg, st.rows(), st.n, true);
     s->info.version = st.version;
+    s->store_id = st.id;
     return s;
+}
+
+Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const keto_snapshot_config *cfg, bool *patched) {
+    if (!cfg || cfg->device != st.device) throw Error(KETO_E_INVALID, "config names another device");
+    if (base.store_id == st.id && base.device == st.device && base.info.version <= st.version) {
+        // the log must hold every version after the base's
+        uint64_t want = base.info.version + 1, n_rows = 0;
+        bool covered = true;
+        for (const auto &c : st.log)
+            if (c.version >= want) {
+                if (c.version != want) covered = false;
+                want++;
+                n_rows += c.n_ins + c.n_del;
+            }
+        covered = covered && want == st.version + 1;
+        if (covered) {
+            KETO_HIP(hipSetDevice(st.device));
+            build::DevBuf rows(sizeof(keto_tuple) * std::max<uint64_t>(1, n_rows));
+            std::vector<uint8_t> is_ins(n_rows);
+            uint64_t at = 0;
+            for (const auto &c : st.log) {
+                if (c.version <= base.info.version) continue;
+                const uint64_t k = c.n_ins + c.n_del;
+                if (k) KETO_HIP(hipMemcpy(static_cast<keto_tuple *>(rows.p) + at, c.rows.p, k * sizeof(keto_tuple), hipMemcpyDeviceToDevice));
+                std::fill(is_ins.begin() + at, is_ins.begin() + at + c.n_ins, 1);
+                at += k;
+            }
+            Snapshot *s = patch_snapshot(base, st.rows(), st.n, static_cast<const keto_tuple *>(rows.p), is_ins.data(), n_rows);
+            if (s) {
+                s->info.version = st.version;
+                s->store_id = st.id;
+                if (patched) *patched = true;
+                return s;
+            }
+        }
+    }
+    if (patched) *patched = false;
+    return store_snapshot(st, cfg);
 }
 
 }  // namespace keto

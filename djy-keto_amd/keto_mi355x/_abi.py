@@ -129,6 +129,8 @@ SIGNATURES = {
     "keto_store_create": (ctypes.c_int, [_I32, _VP, _U64, _U32, ctypes.POINTER(_VP)]),
     "keto_store_transact": (ctypes.c_int, [_VP, _VP, _U64, _VP, _U64, _U32]),
     "keto_store_snapshot": (ctypes.c_int, [_VP, ctypes.POINTER(SnapshotConfig), ctypes.POINTER(_VP)]),
+    "keto_store_snapshot_patch": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(SnapshotConfig), ctypes.POINTER(_VP),
+                                                 ctypes.POINTER(_I32)]),
     "keto_store_info": (ctypes.c_int, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "keto_store_free": (ctypes.c_int, [_VP]),
     "keto_dispatcher_create": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherConfig), ctypes.POINTER(_VP)]),

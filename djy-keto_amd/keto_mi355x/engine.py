@@ -60,10 +60,12 @@ class Snapshot:
 
     def __init__(self, namespaces_json: str | dict, tuples: np.ndarray, ns_names: list, rel_names: list,
                  n_uuids: int, strict: bool = False, device: int = 0, device_tuples: tuple | None = None,
-                 store: "TupleStore | None" = None):
+                 store: "TupleStore | None" = None, base: "Snapshot | None" = None):
         """tuples: host TUPLE_DT array; or tuples=None and device_tuples=(device pointer, count)
         for records already resident on `device` (keto_snapshot_build_device); or tuples=None
-        and store=TupleStore for its current content (keto_store_snapshot)."""
+        and store=TupleStore for its current content (keto_store_snapshot) -- with base= an
+        earlier snapshot of that store, by patching it (keto_store_snapshot_patch; `patched`
+        says whether the patch ran or the full build)."""
         if isinstance(namespaces_json, dict):
             namespaces_json = json.dumps(namespaces_json)
         self._ns = (ctypes.c_char_p * max(1, len(ns_names)))(*[n.encode() for n in ns_names])
@@ -72,7 +74,13 @@ class Snapshot:
         cfg = _abi.SnapshotConfig(len(ns_names), self._ns, len(rel_names), self._rel, n_uuids, self._json,
                                   int(strict), device)
         h = ctypes.c_void_p()
-        if store is not None:
+        self.patched = False
+        if store is not None and base is not None:
+            p = ctypes.c_int32()
+            check(lib().keto_store_snapshot_patch(store.handle, base.handle, ctypes.byref(cfg), ctypes.byref(h),
+                                                  ctypes.byref(p)))
+            self.patched = bool(p.value)
+        elif store is not None:
             check(lib().keto_store_snapshot(store.handle, ctypes.byref(cfg), ctypes.byref(h)))
         elif device_tuples is not None:
             ptr, count = device_tuples

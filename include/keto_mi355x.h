@@ -224,6 +224,18 @@ int keto_store_transact(keto_store *st, const keto_tuple *ins, uint64_t n_ins, c
                         uint32_t flags);
 /* cfg->device must be the store's device; cfg->n_uuids must cover every id written so far */
 int keto_store_snapshot(keto_store *st, const keto_snapshot_config *cfg, keto_snapshot **out);
+/* The store's current content cut by patching `base`, a snapshot this store cut earlier (by
+ * keto_store_snapshot or this call) whose version is still in the store's change log (the rows
+ * of the last 4M inserted or deleted tuples).  Only the rows the transactions since base name
+ * are rebuilt -- their nodes' set and Expand rows, their subjects' reverse rows and probe keys
+ * (the reference's per-row write path: persistence/sql/relationtuples.go:104-126, 168-189,
+ * 277-287) --; every other row is copied shifted, and node space, entities and the rewrite
+ * program are shared with base.  Equal in every answer to keto_store_snapshot of the same
+ * version.  When a transaction wrote something base has no node for (a new object, a new
+ * (namespace, relation) pair, a uuid >= n_uuids), or base is not this store's or too old, the
+ * full device build runs instead; *patched (optional) says which ran.  base stays valid. */
+int keto_store_snapshot_patch(keto_store *st, const keto_snapshot *base, const keto_snapshot_config *cfg,
+                              keto_snapshot **out, int32_t *patched);
 int keto_store_info(keto_store *st, uint64_t *n_tuples, uint64_t *version);
 int keto_store_free(keto_store *st);
 

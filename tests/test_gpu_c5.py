@@ -150,6 +150,10 @@ def _worker(rank, world, port, out):
             "host_closure": len(ct), "tree_mis": tree_mis, "xerr": int((xerr != 0).sum()), "tree_nodes": n_nodes,
         }
         eng.close()
+    except BaseException:
+        import traceback
+        _log(rank, "failed:\n" + traceback.format_exc())  # (spawn reports one rank's error: maybe a peer's)
+        raise
     finally:
         dist.destroy_process_group()
 

@@ -174,18 +174,19 @@ def test_async_batches_match_sync(seed):
 
 @pytest.mark.parametrize("seed", list(range(0, 60, 4)))
 def test_generation_engine_matches_block_engine(stream, seed):
-    """KETO_FR_ENGINE=gen keeps the generation engine (frontier.hip, one launch per generation over
-    the whole batch) as an A/B path: the same decisions, routed queries and goal counts as the
-    default block engine (frontier_block.hip) -- both evaluate frontier_goal.inc's phases"""
+    """KETO_FR_ENGINE=block keeps the block engine (frontier_block.hip, a workgroup per chunk of
+    queries runs all its generations) as an A/B path: the same decisions, routed queries and goal
+    counts as the default generation engine (frontier.hip) -- both evaluate frontier_goal.inc's
+    phases"""
     w, t, q, _ = random_world(seed, rewrites=True)
     snap = product_snapshot(w, t)
     eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
     qp = queries_to_product(q)
-    a_b, e_b, fs_b = _frontier_batch(stream, eng, qp)
+    a_g, e_g, fs_g = _frontier_batch(stream, eng, qp)
     old = os.environ.get("KETO_FR_ENGINE")
-    os.environ["KETO_FR_ENGINE"] = "gen"
+    os.environ["KETO_FR_ENGINE"] = "block"
     try:
-        a_g, e_g, fs_g = _frontier_batch(stream, eng, qp)
+        a_b, e_b, fs_b = _frontier_batch(stream, eng, qp)
     finally:
         if old is None:
             os.environ.pop("KETO_FR_ENGINE")

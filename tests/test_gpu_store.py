@@ -2,6 +2,8 @@
 give exactly the snapshot a full rebuild from the host-side transaction result gives, and
 the oracle agrees on it; versions count transactions; a dispatcher picks the new snapshot
 up between batches."""
+import os
+
 import numpy as np
 import pytest
 
@@ -110,3 +112,129 @@ def test_snapshot_save_load_round_trip(tmp_path):
     with pytest.raises(km.KetoError):
         km.Snapshot.load(bad, wl.ns_names, wl.rel_names)
     st.close()
+
+
+def _edge_delta(wl, rng, t_now):
+    """subject-set edges in and out: nested-group rows emptied (their parents' edges become
+    leaves) and leaf groups given a nested group (their parents' edges stop being leaves), one
+    user made heavy (> 4 reverse entries: probe keys) and a heavy subject made light again"""
+    g_ns, mem = wl.ns_names.index("Group"), wl.rel_names.index("members")
+    nested = t_now[(t_now["ns"] == g_ns) & (t_now["rel"] == mem) & (t_now["subj_kind"] == 1)]
+    dele = nested[rng.choice(len(nested), min(40, len(nested)), replace=False)].copy()
+    groups = wl.meta["gbase"] + rng.choice(wl.meta["n_groups"], 40, replace=False)
+    ins = np.zeros(80, dtype=t_now.dtype)
+    ins["ns"][:40], ins["obj"][:40], ins["rel"][:40] = g_ns, groups, mem
+    ins["subj_kind"][:40], ins["s_ns"][:40], ins["s_rel"][:40] = 1, g_ns, mem
+    ins["s_obj"][:40] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], 40)
+    acl = t_now[(t_now["ns"] >= 2) & (t_now["rel"] != wl.rel_names.index("parents"))]
+    pick = acl[rng.choice(len(acl), 40, replace=False)].copy()
+    pick["subj_kind"], pick["s_obj"], pick["s_ns"], pick["s_rel"] = 0, wl.meta["ubase"] + 7, 0, 0
+    ins[40:] = pick
+    ins["shard_id"] = rng.integers(0, 256, (80, 16), dtype=np.uint8)
+    # a subject with many reverse entries loses all of them but two
+    subj, cnt = np.unique(t_now["s_obj"][t_now["subj_kind"] == 0], return_counts=True)
+    heavy = subj[np.argmax(cnt)]
+    rows = t_now[(t_now["subj_kind"] == 0) & (t_now["s_obj"] == heavy)]
+    dele = np.concatenate([dele, rows[2:]])
+    dele["shard_id"] = 0
+    return ins, dele
+
+
+def _compare(wl, a, b, q, roots):
+    """every Check answer (and the frontier's routed count, and its goal count -- the flags it
+    reads: RI_SETROWS, EDGE_LEAF -- when no query is routed: a routed query stops spawning when
+    its bit is seen, so its goals vary with timing on the GPU; the CPU emulation, one lane at a
+    time, compares them exactly: tests/test_kernel_emulation.py) and every Expand tree of
+    snapshot a equal b's"""
+    out = []
+    for snap in (a, b):
+        stream = km.Stream(0)
+        eng = km.CheckEngine(snap, stream, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+        stream.frontier_stats(reset=True)
+        al, er = eng.check_batch(q)
+        fs = stream.frontier_stats(reset=True)
+        nodes, offs, xerr = km.ExpandEngine(snap, stream, max_read_depth=wl.max_depth).build_trees(roots)
+        out.append((al, er, fs["goals"], fs["routed"], nodes.tobytes(), offs, xerr))
+        stream.close()
+    (a1, e1, g1, r1, n1, o1, x1), (a2, e2, g2, r2, n2, o2, x2) = out
+    np.testing.assert_array_equal(a1, a2)
+    np.testing.assert_array_equal(e1, e2)
+    assert r1 == r2
+    if r1 == 0 or os.environ.get("KETO_MI355X_LIB_OVERRIDE"):
+        assert g1 == g2
+    np.testing.assert_array_equal(o1, o2)
+    np.testing.assert_array_equal(x1, x2)
+    assert n1 == n2
+    return a1
+
+
+def _roots(wl, rng, n=256):
+    r = np.zeros(n, dtype=km.SUBJSET_DT)
+    h = n // 2
+    r["ns"][:h], r["rel"][:h] = wl.ns_names.index("Group"), wl.rel_names.index("members")
+    r["obj"][:h] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], h)
+    r["ns"][h:], r["rel"][h:] = wl.ns_names.index("Folder"), wl.rel_names.index("viewers")
+    r["obj"][h:] = rng.integers(0, wl.meta["folders_per_root"], n - h)
+    return r
+
+
+def test_patched_snapshots_equal_full_builds():
+    """keto_store_snapshot_patch: a chain of transactions -- ACL rows in and out, duplicates,
+    nested-group edges in and out (leaf flags), subjects crossing the heavy threshold (probe keys
+    and tombstones) -- each cut by patching the previous snapshot: every Check (with depth
+    truncation), frontier goal count and Expand tree equals a full build of the same store
+    version, and the oracle over the host-side transaction result agrees"""
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=8)
+    rng = np.random.default_rng(3)
+    st = km.TupleStore(wl.tuples)
+    host = wl.tuples.copy()
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    q = synth.drive_queries(wl, 20_000, seed=6)
+    q["max_depth"][:500] = rng.integers(1, 5, 500)
+    roots = _roots(wl, rng)
+    w, _ = world_from_workload(wl)
+    for step in range(4):
+        ins, dele = _delta(wl, rng, 1500, 1000) if step % 2 == 0 else _edge_delta(wl, rng, host)
+        st.transact(ins, dele)
+        host = transact(host, ins, dele)
+        prev = snap
+        snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=prev)
+        assert snap.patched, f"step {step}: the full build ran"
+        full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+        pi, fi = snap.info(), full.info()
+        for k in ("n_tuples", "n_set_edges", "version"):
+            assert pi[k] == fi[k], (step, k)
+        allowed = _compare(wl, snap, full, q, roots)
+        orc = refsem.Oracle(w, host.view(refsem.TUPLE_DT).copy(), shard_bytes=True)
+        orc.set_limits(wl.max_depth, wl.max_width)
+        dec, err, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+        np.testing.assert_array_equal(allowed, dec)
+        full.close()
+        prev.close()
+    # the patch is not a no-op: answers moved since the first version
+    base = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    a0, _ = km.CheckEngine(base, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    assert (a0 != allowed).any()
+    st.close()
+
+
+def test_patch_falls_back_when_base_has_no_node():
+    """a transaction naming an object the base snapshot has never seen cannot be patched in: the
+    full build runs (patched = False) and the result is still the store's content; a snapshot of
+    another store is never patched"""
+    wl = synth.drive(depth=4, n_groups=300, n_users=1000, seed=5)
+    st = km.TupleStore(wl.tuples[: len(wl.tuples) // 2])
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    rest = wl.tuples[len(wl.tuples) // 2:]
+    st.transact(rest, None)
+    nxt = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=snap)
+    assert not nxt.patched
+    full = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    q = synth.drive_queries(wl, 4096, seed=2)
+    rng = np.random.default_rng(0)
+    _compare(wl, nxt, full, q, _roots(wl, rng, 64))
+    other = km.TupleStore(wl.tuples)
+    o2 = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=other, base=nxt)
+    assert not o2.patched
+    st.close()
+    other.close()
