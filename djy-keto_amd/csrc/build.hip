@@ -357,7 +357,14 @@ __global__ __launch_bounds__(BLK) void k_leaf_mark(uint32_t *set_dst, uint64_t n
 
 // ---------------------------------------------------------------- host side
 DevBuf::DevBuf(size_t b) : bytes(b) {
-    KETO_HIP(hipMalloc(&p, std::max<size_t>(bytes, 16) + 16));
+    const size_t n = std::max<size_t>(bytes, 16) + 16;
+    if (hipMalloc(&p, n) != hipSuccess) {  // out of memory: the snapshot pool's spare blocks go first
+        (void)hipGetLastError();
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        pool_trim(dev);
+        KETO_HIP(hipMalloc(&p, n));
+    }
 }
 DevBuf::~DevBuf() {
     if (p) (void)hipFree(p);

@@ -61,6 +61,17 @@ Stream::~Stream() {
     if (lists) (void)hipFree(lists);
     if (qbuf) (void)hipFree(qbuf);
     if (obuf) (void)hipFree(obuf);
+    for (hipStream_t c : {h2d, d2h})
+        if (c) {
+            (void)hipStreamSynchronize(c);
+            (void)hipStreamDestroy(c);
+        }
+    for (Slot &sl : slot) {
+        if (sl.q) (void)hipFree(sl.q);
+        if (sl.o) (void)hipFree(sl.o);
+        for (hipEvent_t e : {sl.in, sl.out, sl.free})
+            if (e) (void)hipEventDestroy(e);
+    }
     if (counters) (void)hipFree(counters);
     for (int i = 0; i < TIMER_SLOTS; i++) {
         if (ev_a[i]) (void)hipEventDestroy(ev_a[i]);
@@ -197,6 +208,7 @@ int keto_stream_sync(keto_stream *hs) {
     return guarded([&] {
         KETO_HIP(hipSetDevice(s->device));
         KETO_HIP(hipStreamSynchronize(s->stream));
+        if (s->d2h) KETO_HIP(hipStreamSynchronize(s->d2h));  // (an asynchronous batch's last copy)
         s->harvest();
     });
 }
@@ -301,8 +313,42 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
             }
             return;
         }
-        // host buffers: stage through device memory owned by the stream
         const size_t qb = n * sizeof(keto_query), ob = n * (1 + sizeof(int32_t));
+        if (flags & KETO_F_ASYNC) {
+            // host buffers, enqueue only: slot b's H2D on the h2d stream (after the slot's previous
+            // D2H), the kernels on the compute stream (after the H2D), the D2H on the d2h stream
+            // (after the kernels).  Consecutive batches alternate slots, so the copies of one
+            // overlap the kernels of its neighbours and the kernels never share the GPU.
+            if (!s->h2d) {
+                KETO_HIP(hipStreamCreateWithFlags(&s->h2d, hipStreamNonBlocking));
+                KETO_HIP(hipStreamCreateWithFlags(&s->d2h, hipStreamNonBlocking));
+                for (auto &sl : s->slot)
+                    for (hipEvent_t *e : {&sl.in, &sl.out, &sl.free}) KETO_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            }
+            keto::Stream::Slot &sl = s->slot[s->slot_seq++ & 1];
+            if (sl.qb < qb || sl.ob < ob + 64) {  // (growing a slot: wait until its last batch is done)
+                KETO_HIP(hipStreamSynchronize(s->d2h));
+                grow(sl.q, sl.qb, std::max<size_t>(qb, 64));
+                grow(sl.o, sl.ob, std::max<size_t>(ob + 64, 64));
+            }
+            auto *d_allowed = static_cast<uint8_t *>(sl.o);
+            auto *d_err = reinterpret_cast<int32_t *>(static_cast<char *>(sl.o) + ((n + 63) / 64) * 64);
+            KETO_HIP(hipStreamWaitEvent(s->h2d, sl.free, 0));
+            KETO_HIP(hipMemcpyAsync(sl.q, queries, qb, hipMemcpyHostToDevice, s->h2d));
+            KETO_HIP(hipEventRecord(sl.in, s->h2d));
+            KETO_HIP(hipStreamWaitEvent(s->stream, sl.in, 0));
+            L.queries = static_cast<const keto_query *>(sl.q);
+            L.out_allowed = d_allowed;
+            L.out_err = d_err;
+            keto::run_check(*snap, *s, L);
+            KETO_HIP(hipEventRecord(sl.out, s->stream));
+            KETO_HIP(hipStreamWaitEvent(s->d2h, sl.out, 0));
+            KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->d2h));
+            KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->d2h));
+            KETO_HIP(hipEventRecord(sl.free, s->d2h));
+            return;  // the caller synchronises the stream (keto_stream_sync)
+        }
+        // host buffers: stage through device memory owned by the stream
         grow(s->qbuf, s->qbuf_bytes, std::max<size_t>(qb, 64));
         grow(s->obuf, s->obuf_bytes, std::max<size_t>(ob + 64, 64));
         auto *d_allowed = static_cast<uint8_t *>(s->obuf);
@@ -314,7 +360,6 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         keto::run_check(*snap, *s, L);
         KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->stream));
         KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
-        if (flags & KETO_F_ASYNC) return;  // the caller synchronises the stream (keto_stream_sync)
         KETO_HIP(hipStreamSynchronize(s->stream));
         s->harvest();
     });

@@ -48,8 +48,9 @@ struct Snapshot {
     uint64_t store_id = 0;     // the keto_store it was cut from (0: built directly)
     uint64_t probe_used = 0;   // probe-hash slots holding a key or a tombstone (patches keep the load bounded)
 
-    // a device allocation of this snapshot (freed with its last sharer)
+    // a device allocation of this snapshot (back to the pool with its last sharer)
     void own(void *p, size_t bytes);
+    void *alloc(size_t bytes);  // own(pool_acquire(bytes))
     // the allocation of `o` holding p, shared (p must be one of o's arrays)
     void share(const Snapshot &o, const void *p);
     // node -> (ns, entity, slot) on the host (for Expand output conversion)
@@ -135,7 +136,7 @@ struct FrontierScratch {
     uint64_t cap = 0, ncap = 0, dcap = 0, ocap = 0;  // goals, queries, decisive-key slots, occurrences per slice
     uint32_t *ctrl = nullptr;              // [gbase | gcount | fallback count]
     uint32_t *qrouted = nullptr, *fb_list = nullptr, *fb_count = nullptr;  // qrouted: a bit per query
-    uint4 *g0 = nullptr, *g1 = nullptr;
+    uint4 *g0 = nullptr;
     uint2 *gfn = nullptr;
     uint2 *gvs = nullptr;  // {value, goals below} per goal
     unsigned long long *dkeys = nullptr;
@@ -193,6 +194,16 @@ struct Stream {
     uint64_t list_cap = 0;
     void *qbuf = nullptr, *obuf = nullptr;  // staging for host-pointer batches
     size_t qbuf_bytes = 0, obuf_bytes = 0;
+    // KETO_F_ASYNC host-pointer batches: their copies run on two copy streams beside the compute
+    // stream, through two staging slots, so batch k+1's H2D and batch k-1's D2H overlap batch k's
+    // kernels (events order each slot's H2D -> kernels -> D2H -> next H2D)
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    struct Slot {
+        void *q = nullptr, *o = nullptr;
+        size_t qb = 0, ob = 0;
+        hipEvent_t in = nullptr, out = nullptr, free = nullptr;
+    } slot[2];
+    uint64_t slot_seq = 0;
     unsigned long long *counters = nullptr;  // device [3 tiers][8]
     keto_work_counters host_counters{};
     double last_kernel_ms = 0;
@@ -202,6 +213,13 @@ struct Stream {
 
 // scratch.cpp
 int num_cus(int device);
+// snapshot arrays: a block of >= bytes from the device's pool of released arrays, else hipMalloc
+// (*got: the block's size); release returns it (after a device sync) or frees it; reserve makes
+// sure a free block of each size exists (allocated and touched now)
+void *pool_acquire(int device, size_t bytes, size_t *got);
+void pool_release(int device, void *p, size_t bytes);
+void pool_reserve(int device, const std::vector<size_t> &sizes);
+void pool_trim(int device);  // every pooled block freed (any allocation that runs out of memory calls it)
 void ensure_scratch(Scratch &sc, const Tier t[3]);
 void ensure_lists(Stream &st, uint64_t n);
 

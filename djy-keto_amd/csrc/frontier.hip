@@ -60,7 +60,6 @@ struct FrontierParams {
     const uint4 *start;  // resolve records: 2 per query position (resolve.hip)
     uint32_t n;
     uint4 *g0;
-    uint4 *g1;                   // KETO_FR_G1: the query subject's start record, copied into every goal by its parent
     uint2 *gfn;
     uint2 *gvs;                  // {value, goals below (fr_reduce): the root's is the query's count}
     uint32_t cap, scap;          // arena goals, goals per slice
@@ -97,11 +96,7 @@ struct FrontierParams {
 #define FR_MARK(n) ((void)0)
 #endif
 
-#ifndef KETO_FR_G1
-#define KETO_FR_G1 0
-#endif
-__device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_t pos, uint32_t i) {
-    if (KETO_FR_G1) return subject_of(P.g1[i]);  // the goal's own copy (coalesced with the generation)
+__device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_t pos) {
     return subject_of(P.start[2 * (size_t)pos + 1]);  // one load
 }
 // Decisive-key table: keys carry the batch's epoch (1..TAB_EPOCHS) in bits 61-63 (scope < 2^29:
@@ -196,10 +191,8 @@ __device__ __forceinline__ uint32_t gen_goal(const FrontierParams &P, const GenM
 // the generation engine's sink: goal records into the arena, occurrences into the sliced list
 struct GlobalSink {
     const FrontierParams &P;
-    uint4 subj;
     __device__ __forceinline__ void spawn(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope) const {
         P.g0[c] = make_uint4(node, pos, word, scope);
-        if (KETO_FR_G1) P.g1[c] = subj;
     }
     __device__ __forceinline__ void spawn_es(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope,
                                              uint32_t) const {
@@ -219,7 +212,6 @@ __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
     const uint4 r0 = P.start[2 * (size_t)i];
     const uint32_t d = r0.z & 0xFFFFu;
     P.g0[(i / chunk) * P.scap + i % chunk] = make_uint4(r0.x, i, gword(G_IA, d), NONE32);
-    if (KETO_FR_G1) P.g1[(i / chunk) * P.scap + i % chunk] = P.start[2 * (size_t)i + 1];
     if (d > GD_MAX) route(P, i);  // (the bits were cleared before the launch)
 }
 
@@ -264,6 +256,12 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
     constexpr uint32_t NB = KETO_FR_RG_BUCKETS;  // goal classes; dead lanes are one more
     __shared__ uint4 rg_g[XBLOCK];
     __shared__ uint32_t rg_i[XBLOCK], rg_n[XBLOCK / 64][NB + 1];
+#endif
+#if KETO_FR_STASH
+    __shared__ uint2 stash_lds[XBLOCK * STASH_K];
+    uint2 *const stash = stash_lds + threadIdx.x * STASH_K;
+#else
+    uint2 *const stash = nullptr;
 #endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
@@ -317,10 +315,10 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             if (!(ts & VIRT_BIT)) rnode = ts;
         }
         const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
-        const Subject q = live ? load_subject(P, pos, i) : Subject{0, false, make_uint4(0, 0, 0, 0)};
+        const Subject q = live ? load_subject(P, pos) : Subject{0, false, make_uint4(0, 0, 0, 0)};
         FR_MARK(0);
         // ---- phase A: decide, or count the children -------------------------------------------
-        const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W);
+        const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W, stash);
         uint32_t nc = pa.nc, val = pa.val;
         const uint32_t rop = pa.rop, pat = pa.pat, sc = pa.sc, xrel = pa.xrel;
         const bool chain = pa.chain;
@@ -374,10 +372,10 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         FR_MARK(3);
         // ---- phase B: write the children (the same walk as phase A) -------------------------------
         if (nc || (kind == G_ES && xrel)) {
-            GlobalSink gs{P, q.R};
+            GlobalSink gs{P};
             PhaseA pb = pa;
             pb.nc = nc;
-            phase_b(s, T, q, node, pos, w, scope, row, pb, cb, oc, occ_ok, gs);
+            phase_b(s, T, q, node, pos, w, scope, row, pb, cb, oc, occ_ok, gs, stash);
         }
         FR_MARK(4);
     }
@@ -541,7 +539,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     while (dcap < 4 * ncap) dcap <<= 1;
     const uint64_t ocap = cap / 2 / FR_SHARDS;  // per slice
     const size_t ctrl = al256(FR_CTRL_BYTES);
-    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) * (KETO_FR_G1 ? 2 : 1) + al256(cap * 8) + al256(cap * 8) + al256(dcap * 12) +
+    const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 8) + al256(dcap * 12) +
                          al256(ocap * FR_SHARDS * 8) + (1u << DBITS_LOG2) / 8;
     KETO_HIP(hipMalloc(&f.mem, bytes));
     char *p = static_cast<char *>(f.mem);
@@ -554,10 +552,6 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     p += al256(ncap * 12);
     f.g0 = reinterpret_cast<uint4 *>(p);
     p += al256(cap * 16);
-    if (KETO_FR_G1) {
-        f.g1 = reinterpret_cast<uint4 *>(p);
-        p += al256(cap * 16);
-    }
     f.gfn = reinterpret_cast<uint2 *>(p);
     p += al256(cap * 8);
     f.gvs = reinterpret_cast<uint2 *>(p);
@@ -596,7 +590,6 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     P.pos_base = (uint32_t)pos_base;
     P.n = (uint32_t)L.n;
     P.g0 = f.g0;
-    P.g1 = f.g1;
     P.gfn = f.gfn;
     P.gvs = f.gvs;
     P.cap = (uint32_t)f.cap;

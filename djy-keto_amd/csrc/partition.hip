@@ -481,7 +481,9 @@ uint64_t allreduce_max(Partition &P, uint64_t v) {
 
 // all-to-all-v of device records grouped by destination (send_cnt[r] records of `rec` bytes
 // for rank r): received records land in `dst` (grown), grouped by source; returns per-source
-// counts.  Host-staged, so any collective (RCCL, gloo, MPI) can carry it.
+// counts.  With the collective's alltoallv_device the bytes go device to device on the
+// partition's stream (RCCL over xGMI); otherwise host-staged, so any collective (gloo, MPI) can
+// carry it.
 std::vector<uint64_t> exchange(Partition &P, const void *src, const std::vector<uint64_t> &send_cnt, size_t rec,
                                DevBuf &dst, uint64_t &bytes_sent) {
     const uint32_t W = P.world;
@@ -499,6 +501,11 @@ std::vector<uint64_t> exchange(Partition &P, const void *src, const std::vector<
         ns += sb[r];
         nr += rb[r];
         if (r != P.rank) bytes_sent += sb[r];
+    }
+    if (P.coll.alltoallv_device) {
+        ensure(dst, nr);
+        coll_check(P.coll.alltoallv_device(P.coll.ctx, src, sb.data(), dst.p, rb.data(), P.hs), "alltoallv_device");
+        return recv_cnt;
     }
     std::vector<uint8_t> hsend(ns), hrecv(nr);
     if (ns) KETO_HIP(hipMemcpyAsync(hsend.data(), src, ns, hipMemcpyDeviceToHost, P.hs));

@@ -282,6 +282,24 @@ __global__ __launch_bounds__(BLK) void k_fix_leaf(DevSnapshot s, uint4 *set_row,
         }
     }
 }
+// does any node of a slot still hold a subject-set row: job {slot, first node, nodes, stride};
+// every thread walks each job's nodes grid-strided and stops once the job's flag is set
+__global__ __launch_bounds__(BLK) void k_slot_any(const uint4 *set_row, const uint4 *job, uint32_t njobs, uint32_t *flag) {
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    for (uint32_t j = 0; j < njobs; j++) {
+        const uint4 J = job[j];
+        volatile uint32_t *f = flag + j;
+        uint32_t it = 0;
+        for (uint64_t k = gid(); k < J.z; k += T, it++) {
+            if ((it & 63) == 0 && *f) break;
+            const uint4 r = set_row[J.y + k * J.w];
+            if (r.x != r.y) {
+                atomicOr(&flag[j], 1u);
+                break;
+            }
+        }
+    }
+}
 // probe keys: inserts into empty slots (or found present), removals to tombstones
 __global__ __launch_bounds__(BLK) void k_probe_apply(unsigned long long *probe, uint64_t bmask, const unsigned long long *keys,
                                                      uint32_t n_ins, uint32_t n_del) {
@@ -556,13 +574,7 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
                           (const void *)D.ns, (const void *)D.nsrel, (const void *)D.ops, (const void *)D.op_children,
                           (const void *)D.op_items, (const void *)D.or_items, (const void *)D.ent_rank})
         s.share(B, p);
-    auto fresh = [&](size_t bytes) -> void * {
-        bytes = (bytes + 31) / 16 * 16;
-        void *p = nullptr;
-        KETO_HIP(hipMalloc(&p, bytes));
-        s.own(p, bytes);
-        return p;
-    };
+    auto fresh = [&](size_t bytes) -> void * { return s.alloc((bytes + 31) / 16 * 16); };
     // size change per touched row, cumulative
     std::vector<long long> cum_all(m), cum_set(m), cum_rev(ms);
     std::vector<uint32_t> beg_all(m), end_all(m), beg_set(m), end_set(m), beg_rev(ms), end_rev(ms);
@@ -655,21 +667,44 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
         KETO_HIP(hipGetLastError());
     }
     phase("probe");
-    // relation info: RI_SETROWS recounted over the new set rows, RI_IDROWS grown by the inserts
+    // relation info: RI_SETROWS can only change on the slots of the touched nodes whose set row
+    // flipped -- set where one became non-empty; where one became empty, kept only if another row
+    // of the slot still holds a subject set (a scan of that slot's nodes, stopping at the first);
+    // RI_IDROWS grows by the inserts (a stale bit only costs a probe)
     {
-        const uint32_t total_slots = (uint32_t)s.relinfo.size();
-        if (total_slots) {
-            DevBuf flag(4ull * total_slots);
-            KETO_HIP(hipMemset(flag.p, 0, 4ull * total_slots));
-            build::slot_setrows(set_row, N, D.ns, s.n_ns, flag.u32());
-            std::vector<uint32_t> hf(total_slots);
-            KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
-            for (uint32_t gs = 0; gs < total_slots; gs++) s.relinfo[gs] = (s.relinfo[gs] & ~RI_SETROWS) | (hf[gs] ? RI_SETROWS : 0u);
-            for (uint32_t node : idrow_slots) {
-                const uint32_t ns = B.ns_of(node);
-                s.relinfo[s.ns[ns].slot_base + (node - s.ns[ns].node_base) % s.ns[ns].n_slots] |= RI_IDROWS;
-            }
+        auto slot_of = [&](uint32_t node) {
+            const uint32_t ns = B.ns_of(node);
+            return s.ns[ns].slot_base + (node - s.ns[ns].node_base) % s.ns[ns].n_slots;
+        };
+        std::vector<uint32_t> emptied;
+        for (uint32_t j = 0; j < m; j++) {
+            if ((set_len[j] == 0) == (old_n[j].w == old_n[j].z)) continue;
+            const uint32_t gs = slot_of(key_n[j]);
+            if (set_len[j]) s.relinfo[gs] |= RI_SETROWS;
+            else emptied.push_back(gs);
         }
+        std::sort(emptied.begin(), emptied.end());
+        emptied.erase(std::unique(emptied.begin(), emptied.end()), emptied.end());
+        if (!emptied.empty()) {
+            std::vector<uint4> job;  // {global slot, first node, nodes, stride}
+            for (uint32_t gs : emptied) {
+                uint32_t ns = 0;
+                while (ns + 1 < s.n_ns && s.ns[ns + 1].slot_base <= gs) ns++;
+                const NsDev &nd = s.ns[ns];
+                const uint32_t ents = (s.ns[ns + 1].node_base - nd.node_base) / std::max(1u, nd.n_slots);
+                job.push_back(make_uint4(gs, nd.node_base + (gs - nd.slot_base), ents, nd.n_slots));
+            }
+            DevBuf d_job = up(job), flag(4ull * job.size());
+            KETO_HIP(hipMemset(flag.p, 0, 4ull * job.size()));
+            hipLaunchKernelGGL(k_slot_any, dim3((uint32_t)num_cus(B.device) * 4), dim3(BLK), 0, 0, set_row,
+                               static_cast<const uint4 *>(d_job.p), (uint32_t)job.size(), flag.u32());
+            KETO_HIP(hipGetLastError());
+            std::vector<uint32_t> hf(job.size());
+            KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * job.size(), hipMemcpyDeviceToHost));
+            for (size_t k = 0; k < job.size(); k++)
+                s.relinfo[job[k].x] = (s.relinfo[job[k].x] & ~RI_SETROWS) | (hf[k] ? RI_SETROWS : 0u);
+        }
+        for (uint32_t node : idrow_slots) s.relinfo[slot_of(node)] |= RI_IDROWS;
         uint32_t *ri = static_cast<uint32_t *>(fresh(std::max<size_t>(1, s.relinfo.size()) * 4));
         if (!s.relinfo.empty()) KETO_HIP(hipMemcpy(ri, s.relinfo.data(), 4 * s.relinfo.size(), hipMemcpyHostToDevice));
         X.relinfo = ri;

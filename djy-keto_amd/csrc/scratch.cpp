@@ -2,6 +2,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "engine.hpp"
 
@@ -60,5 +62,112 @@ void ensure_lists(Stream &st, uint64_t n) {
     st.list_cap = n;
 }
 
+// ---- snapshot array pool ----------------------------------------------------------------------
+// A fresh multi-GB device allocation is cleared by the driver before first use (~10 GB/s), so a
+// snapshot patched from a base pays seconds for its new arrays unless they come from memory
+// the process already holds.  Released snapshot arrays therefore go back to a per-device pool
+// (capped at a third of the device), and a store reserves the blocks its next patch needs when
+// it cuts a snapshot -- off the transaction path.
+namespace {
+struct PoolBlock {
+    void *p;
+    size_t bytes;
+};
+struct DevicePool {
+    std::mutex mu;
+    std::vector<PoolBlock> free;
+    size_t held = 0, cap = 0;
+};
+DevicePool &pool(int device) {
+    static DevicePool pools[64];
+    DevicePool &P = pools[std::clamp(device, 0, 63)];
+    if (!P.cap) {
+        size_t fr = 0, total = 0;
+        P.cap = hipMemGetInfo(&fr, &total) == hipSuccess ? total / 3 : (size_t)32 << 30;
+    }
+    return P;
+}
+// a free block holding `bytes` without wasting more than half of it
+bool take(DevicePool &P, size_t bytes, void **out, size_t *got) {
+    size_t best = SIZE_MAX, at = 0;
+    for (size_t i = 0; i < P.free.size(); i++)
+        if (P.free[i].bytes >= bytes && P.free[i].bytes <= bytes + bytes / 2 && P.free[i].bytes < best) {
+            best = P.free[i].bytes;
+            at = i;
+        }
+    if (best == SIZE_MAX) return false;
+    *out = P.free[at].p;
+    *got = best;
+    P.held -= best;
+    P.free.erase(P.free.begin() + (ptrdiff_t)at);
+    return true;
+}
+}  // namespace
+
+void *pool_acquire(int device, size_t bytes, size_t *got) {
+    DevicePool &P = pool(device);
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        void *q = nullptr;
+        if (take(P, bytes, &q, got)) return q;
+    }
+    void *q = nullptr;
+    if (hipMalloc(&q, bytes) != hipSuccess) {  // out of memory: hand the pool back and try again
+        (void)hipGetLastError();
+        pool_trim(device);
+        KETO_HIP(hipMalloc(&q, bytes));
+    }
+    *got = bytes;
+    return q;
+}
+
+void pool_trim(int device) {
+    DevicePool &P = pool(device);
+    std::lock_guard<std::mutex> g(P.mu);
+    if (P.free.empty()) return;
+    (void)hipDeviceSynchronize();
+    for (auto &b : P.free) (void)hipFree(b.p);
+    P.free.clear();
+    P.held = 0;
+}
+
+void pool_release(int device, void *p, size_t bytes) {
+    if (!p) return;
+    DevicePool &P = pool(device);
+    (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();  // (as hipFree would: no kernel may still read it)
+    std::lock_guard<std::mutex> g(P.mu);
+    if (bytes >= ((size_t)64 << 20) && P.held + bytes <= P.cap) {
+        P.free.push_back(PoolBlock{p, bytes});
+        P.held += bytes;
+    } else {
+        (void)hipFree(p);
+    }
+}
+
+void pool_reserve(int device, const std::vector<size_t> &sizes) {
+    DevicePool &P = pool(device);
+    std::vector<size_t> need;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        std::vector<bool> used(P.free.size(), false);
+        for (size_t want : sizes) {
+            if (want < ((size_t)64 << 20)) continue;
+            bool ok = false;
+            for (size_t i = 0; i < P.free.size() && !ok; i++)
+                if (!used[i] && P.free[i].bytes >= want && P.free[i].bytes <= want + want / 2) used[i] = ok = true;
+            if (!ok) need.push_back(want);
+        }
+    }
+    for (size_t want : need) {
+        void *q = nullptr;
+        if (hipMalloc(&q, want) != hipSuccess) {
+            (void)hipGetLastError();
+            return;  // no room for the spare: the patch allocates when it runs
+        }
+        KETO_HIP(hipMemset(q, 0, want));  // (first touch now, not in the patch)
+        pool_release(device, q, want);
+    }
+}
 
 }  // namespace keto

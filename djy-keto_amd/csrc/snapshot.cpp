@@ -107,8 +107,16 @@ uint32_t bytes16(const std::vector<T> &v) {
 void Snapshot::own(void *p, size_t bytes) {
     allocs.push_back(p);
     alloc_bytes.push_back(bytes);
-    owned.emplace_back(p, [](void *q) { (void)hipFree(q); });
+    const int dev = device;
+    owned.emplace_back(p, [dev, bytes](void *q) { pool_release(dev, q, bytes); });
     info.device_bytes += bytes;
+}
+
+void *Snapshot::alloc(size_t bytes) {
+    size_t got = 0;
+    void *p = pool_acquire(device, bytes, &got);
+    own(p, got);
+    return p;
 }
 
 void Snapshot::share(const Snapshot &o, const void *p) {
@@ -220,9 +228,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     // final device arrays: zero-filled, 16 bytes of slack for window loads past the end
     auto dalloc = [&](size_t bytes) -> void * {
         bytes = (bytes + 31) / 16 * 16;
-        void *p = nullptr;
-        KETO_HIP(hipMalloc(&p, bytes));
-        s.own(p, bytes);
+        void *p = s.alloc(bytes);
         KETO_HIP(hipMemset(p, 0, bytes));
         return p;
     };

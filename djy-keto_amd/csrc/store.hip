@@ -138,7 +138,7 @@ TupleStore *store_create(int device, const keto_tuple *tuples, uint64_t n, bool 
     auto st = std::make_unique<TupleStore>();
     st->device = device;
     st->id = next_id++;
-    st->reserve(std::max<uint64_t>(n, 64));
+    st->reserve(std::max<uint64_t>(n + n / 16 + (1u << 16), 64));  // (room for transactions: no regrowth copy)
     if (n)
         KETO_HIP(hipMemcpy(st->rows(), tuples, n * sizeof(keto_tuple),
                            device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
@@ -211,11 +211,24 @@ void store_info(const TupleStore &st, uint64_t *n, uint64_t *version) {
     if (version) *version = st.version;
 }
 
+// the arrays a patch of snapshot s will allocate, reserved in the device pool now (a fresh
+// multi-GB allocation is cleared by the driver at first use: seconds at 1B tuples), with room
+// for the row arrays to grow.  Only at a full cut: in a chain of patches each released version
+// hands its arrays to the next patch.
+static void reserve_next_patch(const Snapshot &s) {
+    const uint64_t N = s.dev.n_nodes, M = (uint64_t)s.dev.n_uuids + N, n = s.info.n_tuples, ne = s.info.n_set_edges;
+    auto r = [](uint64_t b) { return (size_t)((b + 31) / 16 * 16); };
+    auto grow = [&](uint64_t b) { return r(b + b / 16 + (1u << 20)); };
+    pool_reserve(s.device, {r(16 * N), r(4 * (N + 1)), grow(4 * n), r(4 * (M + 1)), grow(4 * n), grow(4 * ne + 16),
+                            r(16 * ((uint64_t)s.dev.probe_mask + 1))});
+}
+
 Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg) {
     if (!cfg || cfg->device != st.device) throw Error(KETO_E_INVALID, "config names another device");
     Snapshot *s = build_snapshot(cfg, st.rows(), st.n, true);
     s->info.version = st.version;
     s->store_id = st.id;
+    reserve_next_patch(*s);
     return s;
 }
 
@@ -248,7 +261,7 @@ Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const
             if (s) {
                 s->info.version = st.version;
                 s->store_id = st.id;
-                if (patched) *patched = true;
+                if (patched) *patched = true;  // (the next patch takes this one's base's arrays once it is released)
                 return s;
             }
         }

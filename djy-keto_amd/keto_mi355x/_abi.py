@@ -85,11 +85,15 @@ class PartitionStats(ctypes.Structure):
 
 
 # keto_collective callbacks
+ABI_VERSION = 3  # include/keto_mi355x.h KETO_ABI_VERSION
+
 ALLTOALL_U64_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                    ctypes.POINTER(ctypes.c_uint64))
 ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                 ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
 ALLREDUCE_MAX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+ALLTOALLV_DEV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p)
 
 
 class NameTables(ctypes.Structure):
@@ -172,7 +176,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.keto_abi_version() != 2:
+        if L.keto_abi_version() != ABI_VERSION:
             raise RuntimeError("libketo_mi355x ABI version mismatch")
         _lib = L
     return _lib

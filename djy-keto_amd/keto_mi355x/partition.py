@@ -13,6 +13,10 @@ whole graph's.  The collective is the caller's: `collective` is any object with
     alltoallv(send: np.ndarray uint8, send_bytes: list, recv: np.ndarray uint8, recv_bytes: list) -> None
     allreduce_max_u64(v: int) -> int
 
+and optionally, to move the exchange's bytes device to device (keto_collective.alltoallv_device),
+
+    alltoallv_device(send_ptr: int, send_bytes: list, recv_ptr: int, recv_bytes: list, stream: int) -> None
+
 (tests/torch_collective.py wraps torch.distributed: gloo in the tests, RCCL in bench.py; a Go
 host wraps its own communicator).  No collective = one rank.  This module imports no torch.
 """
@@ -39,7 +43,7 @@ def object_owner(ns: np.ndarray, obj: np.ndarray, nparts: int) -> np.ndarray:
 class _CCollective(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("alltoall_u64", _abi.ALLTOALL_U64_FN), ("alltoallv", _abi.ALLTOALLV_FN),
-                ("allreduce_max_u64", _abi.ALLREDUCE_MAX_FN)]
+                ("allreduce_max_u64", _abi.ALLREDUCE_MAX_FN), ("alltoallv_device", _abi.ALLTOALLV_DEV_FN)]
 
 
 def _c_collective(coll):
@@ -74,7 +78,18 @@ def _c_collective(coll):
         except Exception:
             return -1
 
-    fns = (_abi.ALLTOALL_U64_FN(a2a), _abi.ALLTOALLV_FN(a2av), _abi.ALLREDUCE_MAX_FN(amax))
+    def a2av_dev(_ctx, send, send_bytes, recv, recv_bytes, stream):
+        try:
+            sb = [int(x) for x in np.ctypeslib.as_array(send_bytes, shape=(W,))]
+            rb = [int(x) for x in np.ctypeslib.as_array(recv_bytes, shape=(W,))]
+            coll.alltoallv_device(int(send or 0), sb, int(recv or 0), rb, int(stream or 0))
+            return 0
+        except Exception:
+            return -1
+
+    use_dev = callable(getattr(coll, "alltoallv_device", None)) and getattr(coll, "device_buffers", True)
+    dev = _abi.ALLTOALLV_DEV_FN(a2av_dev) if use_dev else _abi.ALLTOALLV_DEV_FN()
+    fns = (_abi.ALLTOALL_U64_FN(a2a), _abi.ALLTOALLV_FN(a2av), _abi.ALLREDUCE_MAX_FN(amax), dev)
     c = _CCollective(None, int(coll.rank), W, *fns)
     return c, fns
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 2
+#define KETO_ABI_VERSION 3
 
 /* status codes */
 #define KETO_OK 0
@@ -341,6 +341,14 @@ typedef struct keto_collective {
     int (*alltoallv)(void *ctx, const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes);
     /* *value <- max over ranks */
     int (*allreduce_max_u64)(void *ctx, uint64_t *value);
+    /* optional (NULL: alltoallv over host copies): the same all-to-all-v over DEVICE buffers of
+     * the library's device, ordered on `stream` (the library's hipStream_t): the send bytes are
+     * complete in stream order when it is called, and the library's later work on the stream
+     * reads the received bytes.  An RCCL host enqueues ncclGroupStart, one ncclSend / ncclRecv
+     * per peer and ncclGroupEnd on that stream -- the bytes move GPU to GPU over xGMI, no host
+     * copy, no host synchronisation. */
+    int (*alltoallv_device)(void *ctx, const void *send, const uint64_t *send_bytes, void *recv,
+                            const uint64_t *recv_bytes, void *stream);
 } keto_collective;
 typedef struct keto_partition_stats {
     uint64_t batches, levels, objects, tuples, bytes_sent;

@@ -102,7 +102,7 @@ def _worker(rank, world, port, out):
                 t1 = time.perf_counter()
                 eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
                                                   max_read_depth=wl.max_depth, max_read_width=wl.max_width,
-                                                  collective=TorchCollective())
+                                                  collective=TorchCollective(device_buffers=True))
                 del part
                 _log(rank, f"partition {n_part} tuples: generated {t1 - t0:.1f} s, device store {time.perf_counter() - t1:.1f} s")
             dist.barrier()

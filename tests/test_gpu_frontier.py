@@ -198,3 +198,30 @@ def test_generation_engine_matches_block_engine(stream, seed):
     assert fs_b["max_generations"] == fs_g["max_generations"]
     if not fs_b["routed"]:
         assert fs_b["goals"] == fs_g["goals"]
+
+
+def test_async_batches_in_flight_on_one_stream():
+    """KETO_F_ASYNC host batches queued back to back on one stream: the library overlaps their
+    copies with the kernels through two staging slots (H2D and D2H on copy streams, ordered by
+    events); five batches in flight -- each slot reused -- all give the oracle's answers"""
+    w, t, q, _ = random_world(29, rewrites=True)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(w.max_depth, w.max_width)
+    snap = product_snapshot(w, t)
+    stream = km.Stream(0)
+    eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+    rng = np.random.default_rng(5)
+    batches = []
+    for k in range(5):
+        sub = q[rng.permutation(len(q))[: 40 + 15 * k]]
+        qa = km.PinnedArray(len(sub), km.QUERY_DT)
+        qa.array[:] = queries_to_product(sub)
+        out = (km.PinnedArray(len(sub), np.uint8), km.PinnedArray(len(sub), np.int32))
+        eng.check_batch_async(qa.array, out[0].array, out[1].array)
+        batches.append((sub, qa, out))
+    stream.sync()
+    for sub, _, (a, e) in batches:
+        dec, err, _ = orc.check_batch(sub, threads=2)
+        np.testing.assert_array_equal(e.array, err)
+        np.testing.assert_array_equal(a.array, dec)
+    stream.close()

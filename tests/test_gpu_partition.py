@@ -84,7 +84,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, device_buffers=False):
     for p in (ROOT, os.path.join(ROOT, "djy-keto_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -95,7 +95,8 @@ def _worker(rank, world, port, out):
         wl = _wl()
         eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids,
                                           synth.drive_partition(wl, world, rank), max_read_depth=wl.max_depth,
-                                          max_read_width=wl.max_width, collective=TorchCollective())
+                                          max_read_width=wl.max_width,
+                                          collective=TorchCollective(device_buffers=device_buffers))
         q = synth.drive_queries(wl, 8192, seed=40 + rank)
         allowed, err = eng.check_batch(q)
         st = dict(eng.last)
@@ -115,11 +116,15 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_two_rank_partitioned_matches_oracle():
+@pytest.mark.parametrize("device_buffers", [False, True])
+def test_two_rank_partitioned_matches_oracle(device_buffers):
+    """two ranks sharing the GPU: the exchange over host copies (keto_collective.alltoallv), and
+    over the library's device buffers on its stream (alltoallv_device; gloo stages on the
+    adapter's side, RCCL would move the bytes GPU to GPU)"""
     world = 2
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), out, device_buffers), nprocs=world, join=True)
         res = dict(out)
     for r in range(world):
         dmis, emis, n_allowed, sent, tree_mis, xerr = res[r]

@@ -5,7 +5,7 @@
 #   usage: tools/gpu_c4_ab.sh [name ...]
 set -u
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out && export TMPDIR=/tmp
-ARGS="--no-cpu-baseline --serve-clients 0 --latency-iters 0"
+ARGS="--no-cpu-baseline --serve-clients 0 --latency-iters 0 --no-store-probe"
 for name in base "$@"; do
   if [ $name = base ]; then lib=$PWD/djy-keto_amd/keto_mi355x/libketo_mi355x.so; else lib=$PWD/tools/ab/libketo_$name.so; fi
   export KETO_MI355X_ALLOW_OVERRIDE=tools KETO_MI355X_LIB_OVERRIDE=$lib
