@@ -257,12 +257,6 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
     __shared__ uint4 rg_g[XBLOCK];
     __shared__ uint32_t rg_i[XBLOCK], rg_n[XBLOCK / 64][NB + 1];
 #endif
-#if KETO_FR_STASH
-    __shared__ uint2 stash_lds[XBLOCK * STASH_K];
-    uint2 *const stash = stash_lds + threadIdx.x * STASH_K;
-#else
-    uint2 *const stash = nullptr;
-#endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
         // goals of queries routed meanwhile still run (rare); they can no longer spawn
@@ -318,7 +312,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         const Subject q = live ? load_subject(P, pos) : Subject{0, false, make_uint4(0, 0, 0, 0)};
         FR_MARK(0);
         // ---- phase A: decide, or count the children -------------------------------------------
-        const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W, stash);
+        const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W);
         uint32_t nc = pa.nc, val = pa.val;
         const uint32_t rop = pa.rop, pat = pa.pat, sc = pa.sc, xrel = pa.xrel;
         const bool chain = pa.chain;
@@ -375,7 +369,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             GlobalSink gs{P};
             PhaseA pb = pa;
             pb.nc = nc;
-            phase_b(s, T, q, node, pos, w, scope, row, pb, cb, oc, occ_ok, gs, stash);
+            phase_b(s, T, q, node, pos, w, scope, row, pb, cb, oc, occ_ok, gs);
         }
         FR_MARK(4);
     }
@@ -631,7 +625,14 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
         // tables).  A query that would spawn past G is routed: the DFS interpreter, launched on
         // the device-side count, answers it.  So the answers are the synchronous path's; only a
         // deeper-than-speculated query costs the slower engine.
-        const uint32_t G = std::min<uint32_t>(MAX_GEN, std::max<uint32_t>(f.last_gens + 4, 24));
+#ifndef KETO_FR_SPEC_MARGIN
+#define KETO_FR_SPEC_MARGIN 2  // (4 and 8 reduce blocks per CU: 1 % slower per step on C4)
+#endif
+#ifndef KETO_FR_RGRID
+#define KETO_FR_RGRID 4
+#endif
+        // (a stream with no history speculates 24; every empty generation still costs two launches)
+        const uint32_t G = std::min<uint32_t>(MAX_GEN, f.last_gens ? f.last_gens + KETO_FR_SPEC_MARGIN : 24);
         P.gen_cap = G;
         for (uint32_t k = 0; k < G; k++) {
             P.gen = k;
@@ -645,7 +646,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
                 hipLaunchKernelGGL(fr_repeat, dim3(cus * 2), dim3(REPEAT_BLOCK), 0, st.stream, P);
                 KETO_HIP(hipGetLastError());
             }
-            hipLaunchKernelGGL(fr_reduce, dim3(cus * 8), eb, 0, st.stream, P);
+            hipLaunchKernelGGL(fr_reduce, dim3(cus * KETO_FR_RGRID), eb, 0, st.stream, P);
             KETO_HIP(hipGetLastError());
         }
         if (++f.epoch > TAB_EPOCHS) {

@@ -17,5 +17,4 @@ timeout -k 10 420 python3 -u bench.py > $O/bench.log 2>&1 || { echo "bench faile
 tail -1 $O/bench.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read())
 for k in ['value','ms_per_step','device_resident','pipeline','incremental_snapshot','cpu_baseline','schedule_sensitivity','roofline']: print(k, json.dumps(d.get(k))[:500])"
-bash tools/gpu_pcsample.sh $TAG/pcs || echo "pc sampling failed (not fatal)"
 exit 0
