@@ -854,7 +854,8 @@ def main(argv=None):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": ("check path: resolve_kernel + fr_block (one launch) + DFS on routed"
-                                if os.environ.get("KETO_FR_ENGINE", "gen")[0] == "b" else
+                                if os.environ.get("KETO_FR_ENGINE", "b" if args.batch <= int(os.environ.get(
+                                    "KETO_FR_BLOCK_MAX", 1 << 16)) else "g")[0] == "b" else
                                 "check path: resolve_kernel + frontier generations (fr_init, fr_expand, fr_reduce, "
                                 "fr_repeat) + DFS on routed"),
                      "kernel_ms": kernel_ms,

@@ -525,10 +525,18 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         run_dfs(s, st, L, nullptr, nullptr, L.n, true);
         return;
     }
-    // default: the generation engine (frontier.hip); KETO_FR_ENGINE=block: the block engine
-    // (frontier_block.hip, the A/B path -- on C4 4.6 vs 3.7 ms per 2^20 batch)
+    // Two engines evaluate the same goals (frontier_goal.inc): the generation engine (frontier.hip,
+    // a launch per generation over the whole batch) for large batches -- C4 3.7 vs 4.6 ms per 2^20
+    // batch -- and the block engine (frontier_block.hip, one launch, a workgroup per chunk of
+    // queries) for batches of up to KETO_FR_BLOCK_MAX queries, whose ~32 launches per batch would
+    // otherwise set their latency (serving, small batches).  KETO_FR_ENGINE=gen /
+    // block forces one.
+    static const uint64_t block_max = [] {
+        const char *e = getenv("KETO_FR_BLOCK_MAX");
+        return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)1 << 16;
+    }();
     const char *ee = getenv("KETO_FR_ENGINE");
-    const bool gen = !(ee && ee[0] == 'b');
+    const bool gen = ee ? ee[0] != 'b' : L.n > block_max;
     st.mark_begin();
     run_resolve(s, st, L.queries, L.n, L.max_depth, false);
     for (uint64_t off = 0; off < L.n; off += FR_MAX_BATCH) {

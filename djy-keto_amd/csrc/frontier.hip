@@ -510,17 +510,32 @@ __global__ __launch_bounds__(REPEAT_BLOCK) void fr_repeat(FrontierParams P) {
 
 static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
+// Arena: 64 goals per query of the batch (C4 spawns 21, C2 6), or twice the stream's last batch if
+// that was more; a slice that still fills routes its overflowing queries to the DFS interpreter.
+// Occurrences (every kept child of an expand-subject, subject-id leaves included) outnumber goals
+// on member-heavy rows: their list holds KETO_FR_OCC_PER_GOAL per goal (8 B each against a goal's
+// 32 B).  (C4 at 64 goals per query with half as many occurrences routed 28 % of its queries.)
+// KETO_FR_GOALS_PER_QUERY in the environment overrides the goal count: processes sharing one
+// device (the eight ranks of tests/test_gpu_c5.py) hold less.
 #ifndef KETO_FR_GOALS_PER_QUERY
-#define KETO_FR_GOALS_PER_QUERY 256
+#define KETO_FR_GOALS_PER_QUERY 64
+#endif
+#ifndef KETO_FR_OCC_PER_GOAL
+#define KETO_FR_OCC_PER_GOAL 2
 #endif
 
 void ensure_frontier(FrontierScratch &f, uint64_t n) {
     // sized for the next power of two of the batch: a growing stream of batches reallocates (and
     // synchronises the device) O(log n) times, not at every new largest batch
+    static const uint64_t per_query = [] {
+        const char *e = getenv("KETO_FR_GOALS_PER_QUERY");
+        return e ? std::max<uint64_t>(1, strtoull(e, nullptr, 10)) : (uint64_t)KETO_FR_GOALS_PER_QUERY;
+    }();
     uint64_t np = 1;
     while (np < n) np <<= 1;
     n = std::min(np, FR_MAX_BATCH);
-    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n * KETO_FR_GOALS_PER_QUERY, 1u << 20), 1ull << 29) / FR_SHARDS *
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>({n * per_query, 2ull * f.last_goals, 1u << 20}),
+                                             1ull << 29) / FR_SHARDS *
                           FR_SHARDS;
     if (f.mem && f.cap >= want && f.ncap >= n) return;
     if (f.mem) KETO_HIP(hipFree(f.mem));
@@ -531,7 +546,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     // table routes (never seen); the occurrence list: half the arena's goal count
     uint64_t dcap = 1u << 16;
     while (dcap < 4 * ncap) dcap <<= 1;
-    const uint64_t ocap = cap / 2 / FR_SHARDS;  // per slice
+    const uint64_t ocap = cap * KETO_FR_OCC_PER_GOAL / FR_SHARDS;  // per slice
     const size_t ctrl = al256(FR_CTRL_BYTES);
     const size_t bytes = ctrl + al256(ncap * 12) + al256(cap * 16) + al256(cap * 8) + al256(cap * 8) + al256(dcap * 12) +
                          al256(ocap * FR_SHARDS * 8) + (1u << DBITS_LOG2) / 8;

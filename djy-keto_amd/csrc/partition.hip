@@ -440,6 +440,7 @@ struct Partition {
     uint64_t n_local = 0;
     DevBuf bq, braw, bsorted, bkeys, bsubj, bsubj_src, bhist;  // per-batch inputs, reused
     bool verbose = false;
+    bool trim = false;  // KETO_PART_TRIM: the engine stream's scratch is released after every batch
     uint64_t table_mask = 0, n_seen = 0;
     keto_partition_stats last{};
     // Expand results between keto_partition_expand and keto_partition_expand_result
@@ -783,6 +784,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     P->cfg.namespaces_json = P->json.c_str();
     KETO_HIP(hipStreamCreateWithFlags(&P->hs, hipStreamNonBlocking));
     P->verbose = getenv("KETO_PART_VERBOSE") != nullptr;
+    P->trim = getenv("KETO_PART_TRIM") != nullptr;
     if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
     // the partition, grouped by object key (stable radix sort of (key, index), then a gather)
     P->n = n;
@@ -902,6 +904,16 @@ void remap_ids(Partition &P, uint64_t nt, keto_query *q, keto_subject_set *r, ui
     }
 }
 
+// Processes sharing one device (tests/test_gpu_c5.py: eight ranks on the box's GPU) cannot each keep
+// a 2^20-query stream's scratch (frontier arena, DFS tiers: ~7 GB) between batches: with
+// KETO_PART_TRIM the stream is recreated after a batch, its scratch allocated again by the next.
+void trim_stream(Partition &P) {
+    if (!P.trim) return;
+    keto_stream_destroy(P.kstream);
+    P.kstream = nullptr;
+    if (keto_stream_create(P.device, &P.kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
+}
+
 Snapshot *closure_snapshot(Partition &P, uint64_t n_tuples) {
     keto_snapshot_config cfg = P.cfg;
     cfg.n_uuids = (uint32_t)std::max<uint64_t>(1, P.n_local);
@@ -951,6 +963,8 @@ void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8
             st.queries = wc.queries[0];
         }
     }
+    snap.reset();
+    trim_stream(P);
     P.last = st;
 }
 
@@ -994,6 +1008,8 @@ uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, ui
     for (uint64_t i = 0; i < P.xoffs[n]; i++)  // the trees' subject ids back to the global id space
         if (P.xnodes[i].s_obj < P.n_local) P.xnodes[i].s_obj = uniq[P.xnodes[i].s_obj];
     st.run_s = secs(t0);
+    snap.reset();
+    trim_stream(P);
     P.last = st;
     return P.xoffs[n];
 }

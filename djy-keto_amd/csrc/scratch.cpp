@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -81,9 +82,11 @@ struct DevicePool {
 DevicePool &pool(int device) {
     static DevicePool pools[64];
     DevicePool &P = pools[std::clamp(device, 0, 63)];
-    if (!P.cap) {
+    if (!P.cap) {  // (KETO_POOL_CAP_MB: processes that share one device, e.g. test ranks, each hold less)
         size_t fr = 0, total = 0;
-        P.cap = hipMemGetInfo(&fr, &total) == hipSuccess ? total / 3 : (size_t)32 << 30;
+        const char *e = getenv("KETO_POOL_CAP_MB");
+        P.cap = e ? std::max<size_t>((size_t)strtoull(e, nullptr, 10) << 20, 1)
+                  : hipMemGetInfo(&fr, &total) == hipSuccess ? total / 3 : (size_t)32 << 30;
     }
     return P;
 }

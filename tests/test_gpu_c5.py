@@ -74,13 +74,23 @@ def _roots(km, wl, n, seed):
     return r
 
 
+def _free_gib():
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    fr, tot = ctypes.c_size_t(), ctypes.c_size_t()
+    hip.hipMemGetInfo(ctypes.byref(fr), ctypes.byref(tot))
+    return f"{fr.value / 2**30:.1f} of {tot.value / 2**30:.0f} GiB free"
+
+
 def _worker(rank, world, port, out):
     for p in (ROOT, os.path.join(ROOT, "djy-keto_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
     import datetime
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # pool cap and stream scratch assume one process per device; eight ranks share this one
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KETO_POOL_CAP_MB="1",
+                      KETO_PART_TRIM="1")
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=20))
     try:
         import keto_mi355x as km
@@ -104,14 +114,14 @@ def _worker(rank, world, port, out):
                                                   max_read_depth=wl.max_depth, max_read_width=wl.max_width,
                                                   collective=TorchCollective(device_buffers=True))
                 del part
-                _log(rank, f"partition {n_part} tuples: generated {t1 - t0:.1f} s, device store {time.perf_counter() - t1:.1f} s")
+                _log(rank, f"partition {n_part} tuples: generated {t1 - t0:.1f} s, device store {time.perf_counter() - t1:.1f} s, {_free_gib()}")
             dist.barrier()
         total = int(wl.meta["n_tuples"])
         q = _batch(synth, wl, 70 + rank)
         t0 = time.perf_counter()
         a1, e1 = eng.check_batch(q)
         st1 = dict(eng.last)
-        _log(rank, f"batch 1: {time.perf_counter() - t0:.1f} s, closure {st1['tuples']} tuples / {st1['levels']} levels")
+        _log(rank, f"batch 1: {time.perf_counter() - t0:.1f} s, closure {st1['tuples']} tuples / {st1['levels']} levels, {_free_gib()}")
         a2, e2 = eng.check_batch(q)
         idx = _sample(70 + rank)
         qs = q[idx]

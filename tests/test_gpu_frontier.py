@@ -174,18 +174,19 @@ def test_async_batches_match_sync(seed):
 
 @pytest.mark.parametrize("seed", list(range(0, 60, 4)))
 def test_generation_engine_matches_block_engine(stream, seed):
-    """KETO_FR_ENGINE=block keeps the block engine (frontier_block.hip, a workgroup per chunk of
-    queries runs all its generations) as an A/B path: the same decisions, routed queries and goal
-    counts as the default generation engine (frontier.hip) -- both evaluate frontier_goal.inc's
-    phases"""
+    """the block engine (frontier_block.hip, a workgroup per chunk of queries runs all its
+    generations: batches up to KETO_FR_BLOCK_MAX queries) and the generation engine
+    (frontier.hip, larger batches), each forced with KETO_FR_ENGINE: the same decisions, routed
+    queries and goal counts -- both evaluate frontier_goal.inc's phases"""
     w, t, q, _ = random_world(seed, rewrites=True)
     snap = product_snapshot(w, t)
     eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
     qp = queries_to_product(q)
-    a_g, e_g, fs_g = _frontier_batch(stream, eng, qp)
     old = os.environ.get("KETO_FR_ENGINE")
-    os.environ["KETO_FR_ENGINE"] = "block"
     try:
+        os.environ["KETO_FR_ENGINE"] = "gen"
+        a_g, e_g, fs_g = _frontier_batch(stream, eng, qp)
+        os.environ["KETO_FR_ENGINE"] = "block"
         a_b, e_b, fs_b = _frontier_batch(stream, eng, qp)
     finally:
         if old is None:
