@@ -26,9 +26,13 @@ namespace build {
 namespace {
 
 constexpr uint32_t BLK = 256;
-constexpr uint32_t SCAN_CHUNK = 64;
+constexpr uint32_t SCAN_TILE = 4096;  // elements per block of the scan
+constexpr uint32_t SCAN_RUN = 16;     // consecutive elements per thread
+constexpr uint32_t FLAG_GRID = 1024;  // blocks of the flag-marking kernels (one flush per block)
+constexpr uint32_t LDS_FLAGS = 2048;  // flags deduplicated in LDS before the global stores
 
 inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, (n + BLK - 1) / BLK)); }
+inline dim3 grid_cap(uint64_t n, uint32_t cap) { return dim3((uint32_t)std::min<uint64_t>(grid_for(n).x, cap)); }
 
 __device__ __forceinline__ uint64_t gid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
@@ -43,35 +47,107 @@ __device__ __forceinline__ uint64_t shard_lo(const keto_tuple &t) {
     return h;
 }
 
+// ---------------------------------------------------------------- block helpers
+// Written against blockDim.x (not BLK) so the CPU emulation (one thread per block) runs them.
+// Block sum of one value per thread (power-of-two blockDim); every thread gets the total.
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *red) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t s = blockDim.x >> 1; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    const uint32_t t = red[0];
+    __syncthreads();
+    return t;
+}
+// Block exclusive scan of one value per thread (Hillis-Steele in LDS); *total = the block's sum.
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *buf, uint32_t *total) {
+    buf[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t off = 1; off < blockDim.x; off <<= 1) {
+        const uint32_t y = threadIdx.x >= off ? buf[threadIdx.x - off] : 0u;
+        __syncthreads();
+        buf[threadIdx.x] += y;
+        __syncthreads();
+    }
+    const uint32_t incl = buf[threadIdx.x];
+    *total = buf[blockDim.x - 1];
+    __syncthreads();
+    return incl - v;
+}
+// Lanes of a wave adding to the same counter in adjacent lanes (tuples of one row arrive
+// together) take one atomic per run instead of one each: returns the lane's old value.  Lanes
+// with !active neither add nor break the result of others.  Active lanes must be a prefix of the
+// wave (the grid's tail): the last run ends at the last active lane.
+__device__ __forceinline__ uint32_t run_atomic_inc(uint32_t *arr, uint32_t key, bool active) {
+    const uint32_t lane = __lane_id();
+    const uint32_t k = active ? key : NONE32;
+    const uint32_t prev = __shfl_up(k, 1);
+    const bool head = active && (lane == 0 || prev != k);
+    const unsigned long long heads = __ballot(head), live = __ballot(active);
+    const unsigned long long below = heads & ((2ull << lane) - 1ull);  // heads at or before this lane
+    const uint32_t h = below ? 63u - (uint32_t)__clzll((long long)below) : 0u;
+    const unsigned long long after = heads & ~((2ull << lane) - 1ull);
+    const uint32_t width = 64u - (uint32_t)__clzll((long long)live);
+    const uint32_t next = after ? (uint32_t)__ffsll((long long)after) - 1u : width;
+    uint32_t base = 0;
+    if (head) base = atomicAdd(&arr[key], next - lane);
+    base = __shfl(base, (int)h);
+    return base + (lane - h);
+}
+// the same for OR-ing bit masks into words (entity bits)
+__device__ __forceinline__ void run_atomic_or(unsigned long long *arr, uint64_t word, unsigned long long m, bool active) {
+    const uint32_t lane = __lane_id();
+    const uint64_t w = active ? word : ~0ull;
+    unsigned long long x = active ? m : 0ull;
+    for (uint32_t off = 1; off < 64; off <<= 1) {  // OR of the lanes at distance < 2*off with the same word
+        const unsigned long long y = __shfl_down(x, off);
+        const uint64_t wy = __shfl_down(w, off);
+        if (lane + off < 64 && wy == w) x |= y;
+    }
+    const uint64_t pw = __shfl_up(w, 1);  // (every lane shuffles: a lane left out of a shuffle reads as 0)
+    const bool head = active && (lane == 0 || pw != w);
+    if (head && (arr[w] & x) != x) atomicOr(&arr[w], x);
+}
+
 // ---------------------------------------------------------------- exclusive scan (u32)
-__global__ __launch_bounds__(BLK) void k_chunk_sum(const uint32_t *v, uint64_t n, uint32_t *sums, uint64_t nc) {
-    const uint64_t c = gid();
-    if (c >= nc) return;
-    const uint64_t b = c * SCAN_CHUNK, e = std::min<uint64_t>(n, b + SCAN_CHUNK);
+// Tile c = [c * SCAN_TILE, (c + 1) * SCAN_TILE): coalesced sums, then a carried block scan in
+// runs of SCAN_RUN consecutive elements per thread.
+__global__ __launch_bounds__(BLK) void k_tile_sum(const uint32_t *v, uint64_t n, uint32_t *sums, uint64_t nt) {
+    __shared__ uint32_t red[BLK];
+    const uint64_t c = blockIdx.x;
+    if (c >= nt) return;
+    const uint64_t b = c * SCAN_TILE, e = std::min<uint64_t>(n, b + SCAN_TILE);
     uint32_t acc = 0;
-    for (uint64_t i = b; i < e; i++) acc += v[i];
-    sums[c] = acc;
+    for (uint64_t i = b + threadIdx.x; i < e; i += blockDim.x) acc += v[i];
+    const uint32_t t = block_sum(acc, red);
+    if (threadIdx.x == 0) sums[c] = t;
 }
-__global__ __launch_bounds__(BLK) void k_chunk_apply(uint32_t *v, uint64_t n, const uint32_t *sums, uint64_t nc) {
-    const uint64_t c = gid();
-    if (c >= nc) return;
-    const uint64_t b = c * SCAN_CHUNK, e = std::min<uint64_t>(n, b + SCAN_CHUNK);
-    uint32_t acc = sums[c];
-    for (uint64_t i = b; i < e; i++) {
-        const uint32_t x = v[i];
-        v[i] = acc;
-        acc += x;
+// v[i] -> carry(c) + exclusive prefix within the tile; the last tile also writes v[n] = total
+__global__ __launch_bounds__(BLK) void k_tile_apply(uint32_t *v, uint64_t n, const uint32_t *sums, uint64_t nt) {
+    __shared__ uint32_t buf[BLK];
+    const uint64_t c = blockIdx.x;
+    if (c >= nt) return;
+    const uint64_t b = c * SCAN_TILE, e = std::min<uint64_t>(n, b + SCAN_TILE);
+    uint32_t carry = sums ? sums[c] : 0u;
+    for (uint64_t r = b; r < e; r += (uint64_t)blockDim.x * SCAN_RUN) {
+        const uint64_t i0 = r + (uint64_t)threadIdx.x * SCAN_RUN;
+        uint32_t x[SCAN_RUN], acc = 0;
+        for (uint32_t k = 0; k < SCAN_RUN; k++) {
+            x[k] = i0 + k < e ? v[i0 + k] : 0u;
+            acc += x[k];
+        }
+        uint32_t tot = 0;
+        uint32_t o = carry + block_excl(acc, buf, &tot);
+        for (uint32_t k = 0; k < SCAN_RUN; k++)
+            if (i0 + k < e) {
+                v[i0 + k] = o;
+                o += x[k];
+            }
+        carry += tot;
     }
-}
-__global__ void k_scan_serial(uint32_t *v, uint64_t n) {  // n <= SCAN_CHUNK; v[n] = total
-    if (gid() != 0) return;
-    uint32_t acc = 0;
-    for (uint64_t i = 0; i < n; i++) {
-        const uint32_t x = v[i];
-        v[i] = acc;
-        acc += x;
-    }
-    v[n] = acc;
+    if (c == nt - 1 && threadIdx.x == 0) v[n] = carry;
 }
 
 // ---------------------------------------------------------------- tuples
@@ -79,31 +155,56 @@ struct Limits {
     uint32_t n_ns, n_rel_caller, n_uuids, n_rel;
 };
 
-__global__ __launch_bounds__(BLK) void k_validate(const keto_tuple *t, uint64_t n, Limits L, uint32_t *used,
-                                                  unsigned long long *bad) {
-    const uint64_t i = gid();
-    if (i >= n) return;
-    const keto_tuple x = t[i];
-    if (x.ns >= L.n_ns || x.rel >= L.n_rel_caller || x.obj >= L.n_uuids || x.s_obj >= L.n_uuids || x.subj_kind > 1 ||
-        (x.subj_kind == 1 && (x.s_ns >= L.n_ns || x.s_rel >= L.n_rel_caller))) {
-        atomicMin(bad, (unsigned long long)i);
-        return;
+// flags marked by many threads (a handful of (namespace, relation) pairs / slots): deduplicated
+// in the block's LDS when there are at most LDS_FLAGS of them, stored once per block at the end
+struct BlockFlags {
+    uint32_t *lds;
+    uint32_t *g;
+    uint32_t n;
+    __device__ __forceinline__ void begin() {
+        if (n <= LDS_FLAGS) {
+            for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) lds[t] = 0;
+            __syncthreads();
+        }
     }
-    used[(size_t)x.ns * L.n_rel + x.rel] = 1;
-    if (x.subj_kind == 1) used[(size_t)x.s_ns * L.n_rel + x.s_rel] = 1;
+    __device__ __forceinline__ void set(uint32_t f) {
+        if (n <= LDS_FLAGS) lds[f] = 1;
+        else if (!g[f]) atomicOr(&g[f], 1u);
+    }
+    __device__ __forceinline__ void end() {
+        if (n > LDS_FLAGS) return;
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
+            if (lds[t] && !g[t]) g[t] = 1;
+    }
+};
+__global__ __launch_bounds__(BLK) void k_validate(const keto_tuple *t, uint64_t n, Limits L, uint32_t *used, uint32_t n_used,
+                                                  unsigned long long *bad) {
+    __shared__ uint32_t lf[LDS_FLAGS];
+    BlockFlags F{lf, used, n_used};
+    F.begin();
+    for (uint64_t i = gid(); i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const keto_tuple x = t[i];
+        if (x.ns >= L.n_ns || x.rel >= L.n_rel_caller || x.obj >= L.n_uuids || x.s_obj >= L.n_uuids || x.subj_kind > 1 ||
+            (x.subj_kind == 1 && (x.s_ns >= L.n_ns || x.s_rel >= L.n_rel_caller))) {
+            atomicMin(bad, (unsigned long long)i);
+            continue;
+        }
+        F.set(x.ns * L.n_rel + x.rel);
+        if (x.subj_kind == 1) F.set(x.s_ns * L.n_rel + x.s_rel);
+    }
+    F.end();
 }
 
-__device__ __forceinline__ void set_bit(unsigned long long *bits, uint64_t ck) {
-    const unsigned long long m = 1ull << (ck & 63);
-    if (!(bits[ck >> 6] & m)) atomicOr(&bits[ck >> 6], m);
-}
 __global__ __launch_bounds__(BLK) void k_entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride,
                                                      unsigned long long *bits) {
     const uint64_t i = gid();
-    if (i >= n) return;
-    const keto_tuple x = t[i];
-    set_bit(bits, x.ns * stride + x.obj);
-    if (x.subj_kind == 1) set_bit(bits, x.s_ns * stride + x.s_obj);
+    const bool in = i < n;
+    const keto_tuple x = in ? t[i] : keto_tuple{};
+    const uint64_t ck = x.ns * stride + x.obj;
+    run_atomic_or(bits, ck >> 6, 1ull << (ck & 63), in);
+    const uint64_t cs = x.s_ns * stride + x.s_obj;
+    run_atomic_or(bits, cs >> 6, 1ull << (cs & 63), in && x.subj_kind == 1);
 }
 __global__ __launch_bounds__(BLK) void k_popc(const unsigned long long *bits, uint64_t nblk, uint32_t *cnt) {
     const uint64_t i = gid();
@@ -155,20 +256,25 @@ __device__ __forceinline__ uint32_t node_of(const NodeMap &M, uint32_t ns, uint3
 __global__ __launch_bounds__(BLK) void k_src_dst(const keto_tuple *t, uint64_t n, NodeMap M, uint32_t *src, uint32_t *dst,
                                                  unsigned long long *skey, uint32_t *all_cnt, uint32_t *rev_cnt) {
     const uint64_t i = gid();
-    if (i >= n) return;
-    const keto_tuple x = t[i];
-    const uint32_t s = node_of(M, x.ns, x.obj, x.rel);
-    const uint32_t d = x.subj_kind == 1 ? node_of(M, x.s_ns, x.s_obj, x.s_rel) : x.s_obj;
-    src[i] = s;
-    dst[i] = x.subj_kind == 1 ? (d | SKEY_SET) : d;
-    skey[i] = shard_hi(x);
-    atomicAdd(&all_cnt[s], 1u);
-    atomicAdd(&rev_cnt[x.subj_kind == 1 ? M.n_uuids + d : d], 1u);
+    const bool in = i < n;
+    uint32_t s = 0;
+    if (in) {
+        const keto_tuple x = t[i];
+        s = node_of(M, x.ns, x.obj, x.rel);
+        const uint32_t d = x.subj_kind == 1 ? node_of(M, x.s_ns, x.s_obj, x.s_rel) : x.s_obj;
+        src[i] = s;
+        dst[i] = x.subj_kind == 1 ? (d | SKEY_SET) : d;
+        skey[i] = shard_hi(x);
+        atomicAdd(&rev_cnt[x.subj_kind == 1 ? M.n_uuids + d : d], 1u);
+    }
+    (void)run_atomic_inc(all_cnt, s, in);  // a row's tuples mostly arrive together
 }
 
 __global__ __launch_bounds__(BLK) void k_scatter_rows(const uint32_t *src, uint64_t n, uint32_t *cur, uint32_t *row_idx) {
     const uint64_t i = gid();
-    if (i < n) row_idx[atomicAdd(&cur[src[i]], 1u)] = (uint32_t)i;
+    const bool in = i < n;
+    const uint32_t p = run_atomic_inc(cur, in ? src[i] : 0u, in);
+    if (in) row_idx[p] = (uint32_t)i;
 }
 
 // shard order within one row: (shard_hi, shard_lo, tuple index)
@@ -272,10 +378,14 @@ __global__ __launch_bounds__(BLK) void k_row_inline(uint4 *set_row, uint64_t n_r
 
 // ---------------------------------------------------------------- reverse rows + probe hash
 __global__ __launch_bounds__(BLK) void k_heavy_count(const uint32_t *rev_off, uint64_t n_subj, unsigned long long *heavy) {
-    const uint64_t v = gid();
-    if (v >= n_subj) return;
-    const uint32_t len = rev_off[v + 1] - rev_off[v];
-    if (len > PROBE_K) atomicAdd(heavy, (unsigned long long)len);
+    __shared__ uint32_t red[BLK];
+    uint32_t acc = 0;  // (a block's heavy tuples fit: < 2^32 tuples in all)
+    for (uint64_t v = gid(); v < n_subj; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t len = rev_off[v + 1] - rev_off[v];
+        if (len > PROBE_K) acc += len;
+    }
+    const uint32_t t = block_sum(acc, red);
+    if (threadIdx.x == 0 && t) atomicAdd(heavy, (unsigned long long)t);
 }
 __global__ __launch_bounds__(BLK) void k_scatter_rev(const uint32_t *src, const uint32_t *dst, uint64_t n, uint32_t n_uuids,
                                                      const uint32_t *rev_off, uint32_t *cur, uint32_t *rev_nodes,
@@ -311,30 +421,36 @@ __global__ __launch_bounds__(BLK) void k_weight(const uint32_t *set_off, const u
 }
 // global slots whose rows hold a subject set somewhere (relinfo RI_SETROWS)
 __global__ __launch_bounds__(BLK) void k_slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns,
-                                                      uint32_t *flag) {
-    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i >= n_rows) return;
-    const uint4 r = set_row[i];
-    if (r.x == r.y) return;
-    uint32_t lo = 0, hi = n_ns;  // last namespace whose node_base <= i
-    while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (ns[m].node_base <= i) lo = m;
-        else hi = m;
+                                                      uint32_t *flag, uint32_t n_flags) {
+    __shared__ uint32_t lf[LDS_FLAGS];
+    BlockFlags F{lf, flag, n_flags};
+    F.begin();
+    for (uint64_t i = gid(); i < n_rows; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 r = set_row[i];
+        if (r.x == r.y) continue;
+        uint32_t lo = 0, hi = n_ns;  // last namespace whose node_base <= i
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (ns[m].node_base <= i) lo = m;
+            else hi = m;
+        }
+        F.set(ns[lo].slot_base + (uint32_t)((i - ns[lo].node_base) % ns[lo].n_slots));
     }
-    const uint32_t gs = ns[lo].slot_base + (uint32_t)((i - ns[lo].node_base) % ns[lo].n_slots);
-    if (!flag[gs]) atomicOr(&flag[gs], 1u);
+    F.end();
 }
 
 // slots holding a subject-id tuple: a direct check of any other slot against a subject id fails
 __global__ __launch_bounds__(BLK) void k_slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of,
-                                                     uint32_t n_rel, const NsDev *ns, uint32_t *flag) {
-    const uint64_t i = gid();
-    if (i >= n || t[i].subj_kind != 0) return;
-    const uint32_t k = slot_of[(size_t)t[i].ns * n_rel + t[i].rel];
-    if (k == NO_SLOT) return;
-    const uint32_t gs = ns[t[i].ns].slot_base + k;
-    if (!flag[gs]) atomicOr(&flag[gs], 1u);
+                                                     uint32_t n_rel, const NsDev *ns, uint32_t *flag, uint32_t n_flags) {
+    __shared__ uint32_t lf[LDS_FLAGS];
+    BlockFlags F{lf, flag, n_flags};
+    F.begin();
+    for (uint64_t i = gid(); i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (t[i].subj_kind != 0) continue;
+        const uint32_t k = slot_of[(size_t)t[i].ns * n_rel + t[i].rel];
+        if (k != NO_SLOT) F.set(ns[t[i].ns].slot_base + k);
+    }
+    F.end();
 }
 
 __global__ __launch_bounds__(BLK) void k_fill32(uint32_t *a, uint64_t n, uint32_t x) {
@@ -356,33 +472,23 @@ __global__ __launch_bounds__(BLK) void k_leaf_mark(uint32_t *set_dst, uint64_t n
 }  // namespace
 
 // ---------------------------------------------------------------- host side
-DevBuf::DevBuf(size_t b) : bytes(b) {
-    const size_t n = std::max<size_t>(bytes, 16) + 16;
-    if (hipMalloc(&p, n) != hipSuccess) {  // out of memory: the snapshot pool's spare blocks go first
-        (void)hipGetLastError();
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        pool_trim(dev);
-        KETO_HIP(hipMalloc(&p, n));
-    }
-}
-DevBuf::~DevBuf() {
-    if (p) (void)hipFree(p);
-}
-DevBuf::DevBuf(DevBuf &&o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; }
+DevBuf::DevBuf(size_t b) : bytes(b) { p = scratch_get(std::max<size_t>(bytes, 16) + 16, &cap); }
+DevBuf::~DevBuf() { scratch_put(p, cap); }
+DevBuf::DevBuf(DevBuf &&o) noexcept : p(o.p), bytes(o.bytes), cap(o.cap) { o.p = nullptr; }
 DevBuf &DevBuf::operator=(DevBuf &&o) noexcept {
     if (this != &o) {
         reset();
         p = o.p;
         bytes = o.bytes;
+        cap = o.cap;
         o.p = nullptr;
     }
     return *this;
 }
 void DevBuf::reset() {
-    if (p) (void)hipFree(p);
+    scratch_put(p, cap);
     p = nullptr;
-    bytes = 0;
+    bytes = cap = 0;
 }
 void *DevBuf::release() {
     void *q = p;
@@ -391,19 +497,18 @@ void *DevBuf::release() {
 }
 
 void scan_excl(uint32_t *v, uint64_t n) {
-    if (n <= SCAN_CHUNK) {
-        hipLaunchKernelGGL(k_scan_serial, dim3(1), dim3(1), 0, 0, v, n);
+    const uint64_t nt = std::max<uint64_t>(1, (n + SCAN_TILE - 1) / SCAN_TILE);
+    if (nt == 1) {
+        hipLaunchKernelGGL(k_tile_apply, dim3(1), dim3(BLK), 0, 0, v, n, nullptr, 1);
         KETO_HIP(hipGetLastError());
         return;
     }
-    const uint64_t nc = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
-    DevBuf sums(4 * (nc + 1));
-    hipLaunchKernelGGL(k_chunk_sum, grid_for(nc), dim3(BLK), 0, 0, v, n, sums.u32(), nc);
+    DevBuf sums(4 * (nt + 1));
+    hipLaunchKernelGGL(k_tile_sum, dim3((uint32_t)nt), dim3(BLK), 0, 0, v, n, sums.u32(), nt);
     KETO_HIP(hipGetLastError());
-    scan_excl(sums.u32(), nc);
-    hipLaunchKernelGGL(k_chunk_apply, grid_for(nc), dim3(BLK), 0, 0, v, n, sums.u32(), nc);
+    scan_excl(sums.u32(), nt);
+    hipLaunchKernelGGL(k_tile_apply, dim3((uint32_t)nt), dim3(BLK), 0, 0, v, n, sums.u32(), nt);
     KETO_HIP(hipGetLastError());
-    KETO_HIP(hipMemcpy(v + n, sums.u32() + nc, 4, hipMemcpyDeviceToDevice));
 }
 
 uint32_t read_u32(const uint32_t *d, uint64_t i) {
@@ -414,7 +519,8 @@ uint32_t read_u32(const uint32_t *d, uint64_t i) {
 
 void validate(const keto_tuple *t, uint64_t n, uint32_t n_ns, uint32_t n_rel_caller, uint32_t n_uuids, uint32_t n_rel,
               uint32_t *used, unsigned long long *bad) {
-    hipLaunchKernelGGL(k_validate, grid_for(n), dim3(BLK), 0, 0, t, n, Limits{n_ns, n_rel_caller, n_uuids, n_rel}, used, bad);
+    hipLaunchKernelGGL(k_validate, grid_cap(n, FLAG_GRID), dim3(BLK), 0, 0, t, n, Limits{n_ns, n_rel_caller, n_uuids, n_rel}, used,
+                       n_ns * n_rel, bad);
     KETO_HIP(hipGetLastError());
 }
 
@@ -534,7 +640,7 @@ void rows(const RowsIn &in, RowsOut &out) {
     {
         DevBuf heavy(8);
         KETO_HIP(hipMemset(heavy.p, 0, 8));
-        hipLaunchKernelGGL(k_heavy_count, grid_for(M), dim3(BLK), 0, 0, out.rev_off, M,
+        hipLaunchKernelGGL(k_heavy_count, grid_cap(M, FLAG_GRID), dim3(BLK), 0, 0, out.rev_off, M,
                            reinterpret_cast<unsigned long long *>(heavy.p));
         KETO_HIP(hipGetLastError());
         unsigned long long h = 0;
@@ -555,13 +661,14 @@ void rows(const RowsIn &in, RowsOut &out) {
     step("reverse+probe");
 }
 
-void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag) {
-    hipLaunchKernelGGL(k_slot_setrows, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, ns, n_ns, flag);
+void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag, uint32_t n_slots) {
+    hipLaunchKernelGGL(k_slot_setrows, grid_cap(n_rows, FLAG_GRID), dim3(BLK), 0, 0, set_row, n_rows, ns, n_ns, flag, n_slots);
     KETO_HIP(hipGetLastError());
 }
 
-void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag) {
-    if (n) hipLaunchKernelGGL(k_slot_idrows, grid_for(n), dim3(BLK), 0, 0, t, n, slot_of, n_rel, ns, flag);
+void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag,
+                 uint32_t n_slots) {
+    if (n) hipLaunchKernelGGL(k_slot_idrows, grid_cap(n, FLAG_GRID), dim3(BLK), 0, 0, t, n, slot_of, n_rel, ns, flag, n_slots);
     KETO_HIP(hipGetLastError());
 }
 

@@ -68,6 +68,7 @@ namespace build {
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
+    size_t cap = 0;  // the block's size (scratch_get may hand out a larger cached block)
     DevBuf() = default;
     explicit DevBuf(size_t b);  // hipMalloc(b + 16): 16-byte window loads past the end stay in bounds
     ~DevBuf();
@@ -109,8 +110,9 @@ void rows(const RowsIn &in, RowsOut &out);
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows);
 void leaf_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows);
 // flag[global slot] |= 1 where a row of the slot holds a subject set (flag zeroed by the caller)
-void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag);
-void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag);
+void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag, uint32_t n_slots);
+void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag,
+                 uint32_t n_slots);
 }  // namespace build
 
 // scratch tier: per-lane visited capacity (slots, pow2) and stack frames
@@ -219,7 +221,10 @@ int num_cus(int device);
 void *pool_acquire(int device, size_t bytes, size_t *got);
 void pool_release(int device, void *p, size_t bytes);
 void pool_reserve(int device, const std::vector<size_t> &sizes);
-void pool_trim(int device);  // every pooled block freed (any allocation that runs out of memory calls it)
+void pool_trim(int device);
+// builder temporaries (DevBuf): a per-device cache of freed blocks (scratch.cpp)
+void *scratch_get(size_t bytes, size_t *got);
+void scratch_put(void *p, size_t bytes);  // every pooled block freed (any allocation that runs out of memory calls it)
 void ensure_scratch(Scratch &sc, const Tier t[3]);
 void ensure_lists(Stream &st, uint64_t n);
 

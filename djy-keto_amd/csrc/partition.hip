@@ -66,24 +66,48 @@ __host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t wor
 
 // ------------------------------------------------------------------ kernels
 
-// append v (where `has`) to out[] with one atomic per wave instead of one per lane (a single
-// counter takes every append: per-lane atomics serialise at its L2 channel).  Every lane of the
-// wave calls it.
-template <class T>
-__device__ __forceinline__ void wave_append(bool has, T v, T *out, unsigned long long *n_out) {
-    const unsigned long long m = __ballot(has);
-    if (!m) return;
-    const uint32_t lane = __lane_id();
-    const int leader = __ffsll((long long)m) - 1;
-    unsigned long long base = 0;
-    if ((int)lane == leader) base = atomicAdd(n_out, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader);
-    if (has) out[base + __popcll(m & ((1ull << lane) - 1ull))] = v;
+// Appends to one counter: a block reserves its range with one atomic (per-wave atomics on a
+// single counter serialise at its L2 channel: k_next spent 3.3 ms of a C3 x10 batch on them).
+// Each thread offers up to K values (bit k of `mask`); every thread of the block calls it.
+constexpr uint32_t TILE_K = 8;  // values per thread per call: one atomic per BLK * TILE_K items
+__device__ __forceinline__ unsigned long long block_reserve(uint32_t cnt, unsigned long long *n_out,
+                                                            unsigned long long *s_base, uint32_t *s_wsum) {
+    const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    uint32_t x = cnt;  // inclusive scan over the wave
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wsum[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < nw; w++) {
+            const uint32_t v = s_wsum[w];
+            s_wsum[w] = (uint32_t)t;
+            t += v;
+        }
+        *s_base = t ? atomicAdd(n_out, t) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long o = *s_base + s_wsum[wv] + x - cnt;
+    __syncthreads();  // (the shared words are reused by the next call)
+    return o;
 }
-// grid-stride loop whose trip count is uniform per block (wave-level collectives inside)
-#define FOR_UNIFORM(i, n)                                                                                  \
-    for (uint64_t i##0 = (uint64_t)blockIdx.x * blockDim.x, i = i##0 + threadIdx.x; i##0 < (n);           \
-         i##0 += gstride(), i = i##0 + threadIdx.x)
+template <class T>
+__device__ __forceinline__ void block_append(const T (&v)[TILE_K], uint32_t mask, T *out, unsigned long long *n_out) {
+    __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_wsum[BLK / 64];
+    unsigned long long o = block_reserve((uint32_t)__popc(mask), n_out, &s_base, s_wsum);
+    for (uint32_t k = 0; k < TILE_K; k++)
+        if ((mask >> k) & 1u) out[o++] = v[k];
+}
+// grid-stride over tiles of blockDim * TILE_K items, uniform per block; item k of a thread's
+// tile is i = tile + k * blockDim + threadIdx (coalesced)
+#define FOR_TILES(t0, n)                                                                                  \
+    for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x * TILE_K; t0 < (n);                          \
+         t0 += (uint64_t)gridDim.x * blockDim.x * TILE_K)
+inline dim3 grid_tiles(uint64_t n) { return grid_for((n + TILE_K - 1) / TILE_K); }
 
 __global__ __launch_bounds__(BLK) void k_tuple_keys(const keto_tuple *t, uint64_t n, uint64_t *keys, uint32_t *idx) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
@@ -136,10 +160,19 @@ __global__ __launch_bounds__(BLK) void k_run_starts(const uint64_t *k, const uin
 }
 __global__ __launch_bounds__(BLK) void k_query_keys(const keto_query *q, uint64_t n, uint64_t *keys, uint32_t *subj,
                                                      unsigned long long *n_subj) {
-    FOR_UNIFORM(i, n) {
-        const bool in = i < n;
-        if (in) keys[i] = okey(q[i].ns, q[i].obj);
-        wave_append<uint32_t>(in && q[i].subj_kind == 0, in ? q[i].s_obj : 0u, subj, n_subj);
+    FOR_TILES(t0, n) {
+        uint32_t v[TILE_K], mask = 0;
+        for (uint32_t k = 0; k < TILE_K; k++) {
+            const uint64_t i = t0 + (uint64_t)k * blockDim.x + threadIdx.x;
+            v[k] = 0;
+            if (i >= n) continue;
+            keys[i] = okey(q[i].ns, q[i].obj);
+            if (q[i].subj_kind == 0) {
+                v[k] = q[i].s_obj;
+                mask |= 1u << k;
+            }
+        }
+        block_append<uint32_t>(v, mask, subj, n_subj);
     }
 }
 __global__ __launch_bounds__(BLK) void k_root_keys(const keto_subject_set *r, uint64_t n, uint64_t *keys) {
@@ -148,25 +181,30 @@ __global__ __launch_bounds__(BLK) void k_root_keys(const keto_subject_set *r, ui
 // seen-set insert: keys never asked for before go to `out` (each once)
 __global__ __launch_bounds__(BLK) void k_insert(const uint64_t *cand, uint64_t n, unsigned long long *table,
                                                  uint64_t mask, uint64_t *out, unsigned long long *n_out) {
-    FOR_UNIFORM(i, n) {
-        bool fresh = false;
-        const unsigned long long k = i < n ? cand[i] + 1 : 0ull;  // 0 = empty slot
-        if (i < n) {
-            uint64_t h = mix64(k) & mask;
+    FOR_TILES(t0, n) {
+        uint64_t v[TILE_K];
+        uint32_t fresh = 0;
+        for (uint32_t k = 0; k < TILE_K; k++) {
+            const uint64_t i = t0 + (uint64_t)k * blockDim.x + threadIdx.x;
+            v[k] = 0;
+            if (i >= n) continue;
+            const unsigned long long key = cand[i] + 1;  // 0 = empty slot
+            v[k] = cand[i];
+            uint64_t h = mix64(key) & mask;
             for (;;) {
                 // most candidates were seen before (popular groups, shared ancestors): a plain load
                 // answers them, the atomic is only for an empty slot
                 unsigned long long prev = __atomic_load_n(&table[h], __ATOMIC_RELAXED);
-                if (prev == 0ull) prev = atomicCAS(&table[h], 0ull, k);
+                if (prev == 0ull) prev = atomicCAS(&table[h], 0ull, key);
                 if (prev == 0ull) {
-                    fresh = true;
+                    fresh |= 1u << k;
                     break;
                 }
-                if (prev == k) break;
+                if (prev == key) break;
                 h = (h + 1) & mask;
             }
         }
-        wave_append<uint64_t>(fresh, k - 1, out, n_out);
+        block_append<uint64_t>(v, fresh, out, n_out);
     }
 }
 __global__ __launch_bounds__(BLK) void k_rehash(const uint64_t *keys, uint64_t n, unsigned long long *table,
@@ -301,7 +339,7 @@ __global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const
     }
 }
 // One pass for a rank gathering for itself (no grouping by source needed): each request counts
-// its kept tuples, takes its range with one atomic per wave, and copies them (the run is re-read
+// its kept tuples, takes its range with one atomic per block, and copies them (the run is re-read
 // from L2).  The closure's order is free: the builder sorts every row by shard_id.  A range past
 // `cap` sets *overflow and writes nothing; the host then reruns the level with the two passes.
 __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, keto_tuple *out, uint64_t cap,
@@ -315,18 +353,10 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, ket
                     c++;
                     if (j - b < 64) km |= 1ull << (j - b);
                 }
-        // wave-aggregated allocation
-        uint64_t x = c;
-        const uint32_t lane = __lane_id();
-        for (uint32_t off = 1; off < 64; off <<= 1) {
-            const uint64_t y = __shfl_up(x, off);
-            if (lane >= off) x += y;
-        }
-        const uint64_t wsum = __shfl(x, 63);
-        unsigned long long base = 0;
-        if (lane == 63 && wsum) base = atomicAdd(total, (unsigned long long)wsum);
-        base = __shfl(base, 63);
-        uint64_t o = base + x - c;
+        // block-aggregated allocation
+        __shared__ unsigned long long s_base;
+        __shared__ uint32_t s_wsum[BLK / 64];
+        uint64_t o = block_reserve((uint32_t)c, total, &s_base, s_wsum);
         if (!c) continue;
         if (o + c > cap) {
             atomicOr(overflow, 1ull);
@@ -342,9 +372,18 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, ket
 // next frontier: the subject-set objects of the tuples received
 __global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, uint64_t *cand,
                                                unsigned long long *n_cand) {
-    FOR_UNIFORM(i, n) {
-        const bool set = i < n && t[i].subj_kind == 1;
-        wave_append<uint64_t>(set, set ? okey(t[i].s_ns, t[i].s_obj) : 0ull, cand, n_cand);
+    FOR_TILES(t0, n) {
+        uint64_t v[TILE_K];
+        uint32_t mask = 0;
+        for (uint32_t k = 0; k < TILE_K; k++) {
+            const uint64_t i = t0 + (uint64_t)k * blockDim.x + threadIdx.x;
+            v[k] = 0;
+            if (i < n && t[i].subj_kind == 1) {
+                v[k] = okey(t[i].s_ns, t[i].s_obj);
+                mask |= 1u << k;
+            }
+        }
+        block_append<uint64_t>(v, mask, cand, n_cand);
     }
 }
 
@@ -609,7 +648,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         unsigned long long *c = dptr<unsigned long long>(P.ctr);
         KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
         if (n_cand)
-            hipLaunchKernelGGL(k_insert, grid_for(n_cand), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.cand), n_cand,
+            hipLaunchKernelGGL(k_insert, grid_tiles(n_cand), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.cand), n_cand,
                                dptr<unsigned long long>(P.table), P.table_mask, dptr<uint64_t>(P.fresh), c);
         const uint64_t n_new = d2h_u64(P, c);
         mark(0);
@@ -675,7 +714,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                 ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
                 KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
                 if (n_got)
-                    hipLaunchKernelGGL(k_next, grid_for(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total,
+                    hipLaunchKernelGGL(k_next, grid_tiles(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total,
                                        n_got, dptr<uint64_t>(P.cand), c);
                 n_cand = d2h_u64(P, c);
                 mark(4);
@@ -726,7 +765,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
         KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
         if (n_got)
-            hipLaunchKernelGGL(k_next, grid_for(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total, n_got,
+            hipLaunchKernelGGL(k_next, grid_tiles(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total, n_got,
                                dptr<uint64_t>(P.cand), c);
         n_cand = d2h_u64(P, c);
         mark(4);
@@ -859,7 +898,7 @@ uint64_t batch_keys(Partition &P, const keto_query *q, uint64_t n, DevBuf &keys,
     unsigned long long *c = dptr<unsigned long long>(P.ctr);
     KETO_HIP(hipMemsetAsync(c, 0, 16, P.hs));
     if (n)
-        hipLaunchKernelGGL(k_query_keys, grid_for(n), dim3(BLK), 0, P.hs, dptr<keto_query>(dq), n, dptr<uint64_t>(keys),
+        hipLaunchKernelGGL(k_query_keys, grid_tiles(n), dim3(BLK), 0, P.hs, dptr<keto_query>(dq), n, dptr<uint64_t>(keys),
                            dptr<uint32_t>(raw), c);
     const uint64_t ns = d2h_u64(P, c);
     if (!ns) return 0;

@@ -124,7 +124,96 @@ void *pool_acquire(int device, size_t bytes, size_t *got) {
     return q;
 }
 
+// ---- build scratch cache ----------------------------------------------------------------------
+// The builder's temporaries (DevBuf) come and go every build; hipFree of a large block unmaps it
+// (~0.3 ms each: 5 ms of a config-5 batch's closure build went to them).  Freed blocks stay in a
+// per-device cache instead (capped: KETO_SCRATCH_CAP_MB, default a sixteenth of the device) and
+// are handed out again best-fit within 2x.  A block may still be read by queued kernels when it
+// is returned, so the first reuse after any return synchronises the device once (as hipFree did).
+namespace {
+struct ScratchCache {
+    std::mutex mu;
+    std::vector<PoolBlock> free;
+    size_t held = 0, cap = 0;
+    bool dirty = false;
+};
+ScratchCache &scache(int device) {
+    static ScratchCache caches[64];
+    ScratchCache &C = caches[std::clamp(device, 0, 63)];
+    if (!C.cap) {
+        size_t fr = 0, total = 0;
+        const char *e = getenv("KETO_SCRATCH_CAP_MB");
+        C.cap = e ? std::max<size_t>((size_t)strtoull(e, nullptr, 10) << 20, 1)
+                  : hipMemGetInfo(&fr, &total) == hipSuccess ? total / 16 : (size_t)8 << 30;
+    }
+    return C;
+}
+constexpr size_t SCRATCH_MIN = (size_t)1 << 20;  // smaller blocks: plain hipMalloc / hipFree
+void scratch_trim(int device) {
+    ScratchCache &C = scache(device);
+    std::lock_guard<std::mutex> g(C.mu);
+    if (C.free.empty()) return;
+    (void)hipDeviceSynchronize();
+    for (auto &b : C.free) (void)hipFree(b.p);
+    C.free.clear();
+    C.held = 0;
+    C.dirty = false;
+}
+}  // namespace
+
+void *scratch_get(size_t bytes, size_t *got) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (bytes >= SCRATCH_MIN) {
+        ScratchCache &C = scache(dev);
+        std::lock_guard<std::mutex> g(C.mu);
+        size_t best = SIZE_MAX, at = 0;
+        for (size_t i = 0; i < C.free.size(); i++)
+            if (C.free[i].bytes >= bytes && C.free[i].bytes <= 2 * bytes && C.free[i].bytes < best) {
+                best = C.free[i].bytes;
+                at = i;
+            }
+        if (best != SIZE_MAX) {
+            if (C.dirty) {
+                KETO_HIP(hipDeviceSynchronize());
+                C.dirty = false;
+            }
+            void *q = C.free[at].p;
+            C.held -= best;
+            C.free.erase(C.free.begin() + (ptrdiff_t)at);
+            *got = best;
+            return q;
+        }
+    }
+    void *q = nullptr;
+    if (hipMalloc(&q, bytes) != hipSuccess) {  // out of memory: the caches' spare blocks go first
+        (void)hipGetLastError();
+        pool_trim(dev);
+        KETO_HIP(hipMalloc(&q, bytes));
+    }
+    *got = bytes;
+    return q;
+}
+
+void scratch_put(void *p, size_t bytes) {
+    if (!p) return;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (bytes >= SCRATCH_MIN) {
+        ScratchCache &C = scache(dev);
+        std::lock_guard<std::mutex> g(C.mu);
+        if (C.held + bytes <= C.cap) {
+            C.free.push_back(PoolBlock{p, bytes});
+            C.held += bytes;
+            C.dirty = true;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+
 void pool_trim(int device) {
+    scratch_trim(device);
     DevicePool &P = pool(device);
     std::lock_guard<std::mutex> g(P.mu);
     if (P.free.empty()) return;

@@ -394,7 +394,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         if (total_slots) {
             DevBuf flag(4ull * total_slots);
             KETO_HIP(hipMemset(flag.p, 0, 4ull * total_slots));
-            build::slot_idrows(dt, n, d_slot.u32(), s.n_rel, D.ns, flag.u32());
+            build::slot_idrows(dt, n, d_slot.u32(), s.n_rel, D.ns, flag.u32(), total_slots);
             KETO_HIP(hipMemcpy(idrows.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
         }
     }
@@ -476,7 +476,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     if (total_slots) {
         DevBuf flag(4ull * total_slots);
         KETO_HIP(hipMemset(flag.p, 0, 4ull * total_slots));
-        build::slot_setrows(ro.set_row, N, D.ns, s.n_ns, flag.u32());
+        build::slot_setrows(ro.set_row, N, D.ns, s.n_ns, flag.u32(), total_slots);
         std::vector<uint32_t> hf(total_slots);
         KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
         for (uint32_t gs = 0; gs < total_slots; gs++) {

@@ -88,8 +88,8 @@ def _worker(rank, world, port, out):
             sys.path.insert(0, p)
     import datetime
 
-    # pool cap and stream scratch assume one process per device; eight ranks share this one
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KETO_POOL_CAP_MB="1",
+    # the allocation caches and the stream scratch assume one process per device; eight ranks share this one
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KETO_POOL_CAP_MB="1", KETO_SCRATCH_CAP_MB="1",
                       KETO_PART_TRIM="1")
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=20))
     try:
