@@ -546,7 +546,7 @@ void rows(const RowsIn &in, RowsOut &out) {
     auto tp = std::chrono::steady_clock::now();
     auto step = [&](const char *what) {
         if (!verbose) return;
-        KETO_HIP(hipDeviceSynchronize());
+        KETO_HIP(hipStreamSynchronize(nullptr));
         const auto now = std::chrono::steady_clock::now();
         fprintf(stderr, "[keto build]   rows/%-12s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
         tp = now;
@@ -657,7 +657,7 @@ void rows(const RowsIn &in, RowsOut &out) {
                            cur.u32(), out.rev_nodes, reinterpret_cast<unsigned long long *>(out.probe.p), buckets - 1);
         KETO_HIP(hipGetLastError());
     }
-    KETO_HIP(hipDeviceSynchronize());
+    KETO_HIP(hipStreamSynchronize(nullptr));  // (the build's own stream: other work on the device runs on)
     step("reverse+probe");
 }
 

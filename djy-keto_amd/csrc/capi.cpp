@@ -501,6 +501,18 @@ int keto_partition_check(keto_partition *p, const keto_query *queries, uint64_t 
     });
 }
 
+int keto_partition_check_many(keto_partition *p, uint32_t n_batches, const keto_query *const *queries, const uint64_t *n,
+                              uint8_t *const *out_allowed, int32_t *const *out_err, uint32_t flags) {
+    if (!p) return fail(KETO_E_INVALID, "null partition");
+    if (n_batches && (!queries || !n || !out_allowed || !out_err)) return fail(KETO_E_INVALID, "null buffer");
+    for (uint32_t k = 0; k < n_batches; k++)
+        if (n[k] && (!queries[k] || !out_allowed[k] || !out_err[k])) return fail(KETO_E_INVALID, "null buffer");
+    return guarded([&] {
+        keto::partition_check_many(reinterpret_cast<keto::PartitionHandle *>(p), n_batches, queries, n, out_allowed, out_err,
+                                   flags);
+    });
+}
+
 int keto_partition_expand(keto_partition *p, const keto_subject_set *roots, uint64_t n, uint64_t *out_nodes_needed) {
     if (!p || !out_nodes_needed) return fail(KETO_E_INVALID, "null argument");
     if (n && !roots) return fail(KETO_E_INVALID, "null roots");

@@ -222,9 +222,17 @@ void *pool_acquire(int device, size_t bytes, size_t *got);
 void pool_release(int device, void *p, size_t bytes);
 void pool_reserve(int device, const std::vector<size_t> &sizes);
 void pool_trim(int device);
-// builder temporaries (DevBuf): a per-device cache of freed blocks (scratch.cpp)
+// builder temporaries (DevBuf): a per-device cache of freed blocks (scratch.cpp).  A block
+// returned by a thread is fenced by an event on that thread's stream (scratch_stream sets it;
+// returns the previous one), which its next user waits for.
 void *scratch_get(size_t bytes, size_t *got);
-void scratch_put(void *p, size_t bytes);  // every pooled block freed (any allocation that runs out of memory calls it)
+void scratch_put(void *p, size_t bytes);
+hipStream_t scratch_stream(hipStream_t s);
+struct ScratchStream {  // the calling thread's DevBufs live on stream s for this scope
+    hipStream_t old;
+    explicit ScratchStream(hipStream_t s) : old(scratch_stream(s)) {}
+    ~ScratchStream() { scratch_stream(old); }
+};  // every pooled block freed (any allocation that runs out of memory calls it)
 void ensure_scratch(Scratch &sc, const Tier t[3]);
 void ensure_lists(Stream &st, uint64_t n);
 
@@ -312,6 +320,8 @@ struct PartitionHandle;
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
                                   bool device_ptrs, const keto_collective *coll, const keto_limits *limits);
 void partition_check(PartitionHandle *p, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags);
+void partition_check_many(PartitionHandle *p, uint32_t nb, const keto_query *const *q, const uint64_t *n,
+                          uint8_t *const *allowed, int32_t *const *err, uint32_t flags);
 uint64_t partition_expand(PartitionHandle *p, const keto_subject_set *roots, uint64_t n);
 void partition_expand_result(PartitionHandle *p, keto_tree_node *nodes, uint64_t cap, uint64_t *offsets, int32_t *err);
 void partition_stats(PartitionHandle *p, keto_partition_stats *out);

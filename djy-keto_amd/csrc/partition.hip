@@ -40,8 +40,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "device_common.hpp"
@@ -179,8 +181,10 @@ __global__ __launch_bounds__(BLK) void k_root_keys(const keto_subject_set *r, ui
     for (uint64_t i = gid(); i < n; i += gstride()) keys[i] = okey(r[i].ns, r[i].obj);
 }
 // seen-set insert: keys never asked for before go to `out` (each once)
-__global__ __launch_bounds__(BLK) void k_insert(const uint64_t *cand, uint64_t n, unsigned long long *table,
-                                                 uint64_t mask, uint64_t *out, unsigned long long *n_out) {
+__global__ __launch_bounds__(BLK) void k_insert(const uint64_t *cand, uint64_t n, const unsigned long long *n_dev,
+                                                 unsigned long long *table, uint64_t mask, uint64_t *out,
+                                                 unsigned long long *n_out) {
+    if (n_dev) n = *n_dev;  // (a level launched before its count reached the host)
     FOR_TILES(t0, n) {
         uint64_t v[TILE_K];
         uint32_t fresh = 0;
@@ -338,40 +342,116 @@ __global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const
         }
     }
 }
-// One pass for a rank gathering for itself (no grouping by source needed): each request counts
-// its kept tuples, takes its range with one atomic per block, and copies them (the run is re-read
-// from L2).  The closure's order is free: the builder sorts every row by shard_id.  A range past
-// `cap` sets *overflow and writes nothing; the host then reruns the level with the two passes.
-__global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, keto_tuple *out, uint64_t cap,
-                                                        unsigned long long *total, unsigned long long *overflow) {
-    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += gstride()) {
-        const uint64_t i = i0 + threadIdx.x;
-        uint64_t b = 0, e = 0, c = 0, km = 0;  // km: which of a run's first 64 tuples are kept
-        if (i < n && run_of(L, L.req[i], b, e))
-            for (uint64_t j = b; j < e; j++)
-                if (keep(L, L.meta[j], 0)) {
-                    c++;
-                    if (j - b < 64) km |= 1ull << (j - b);
-                }
-        // block-aggregated allocation
-        __shared__ unsigned long long s_base;
-        __shared__ uint32_t s_wsum[BLK / 64];
-        uint64_t o = block_reserve((uint32_t)c, total, &s_base, s_wsum);
-        if (!c) continue;
-        if (o + c > cap) {
-            atomicOr(overflow, 1ull);
-            continue;
+// Block exclusive scan of one u32 per thread (wave scans + the waves' sums); *tot = the sum.
+__device__ __forceinline__ uint32_t block_excl_u32(uint32_t v, uint32_t *s_wsum, uint32_t *tot) {
+    const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    uint32_t x = v;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wsum[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < nw; w++) {
+            const uint32_t y = s_wsum[w];
+            s_wsum[w] = t;
+            t += y;
         }
-        for (uint64_t j = b; j < e; j++) {  // (the first pass's answers: no second probe of the filter)
-            const uint2 m = L.meta[j];
-            if (j - b < 64 ? ((km >> (j - b)) & 1ull) : keep(L, m, 0)) out[o++] = st_tuple(L.req[i], m, L.shard[j]);
+        s_wsum[nw] = t;
+    }
+    __syncthreads();
+    const uint32_t r = s_wsum[wv] + x - v;
+    *tot = s_wsum[nw];
+    __syncthreads();
+    return r;
+}
+// One pass for a rank gathering for itself (no grouping by source needed; the closure's order
+// is free: the builder sorts every row by shard_id).  A block takes BLK requests and lays their
+// runs end to end, a virtual list of tuples that all its threads then walk in segments of GSEG
+// items: a lane's work no longer depends on how long its own object's run is (folder runs of
+// hundreds of viewer tuples next to runs of one).  Per segment the kept tuples are marked in an
+// LDS bitmap, one range is reserved for them, and they are written in list order.  An item
+// past `cap` sets *overflow; the host then reruns the level with the two passes.
+constexpr uint32_t GSEG = BLK * 32;  // items per segment: one 32-bit bitmap word per thread
+__global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, const unsigned long long *n_dev, keto_tuple *out,
+                                                        uint64_t cap, unsigned long long *total,
+                                                        unsigned long long *overflow) {
+    if (n_dev) n = *n_dev;
+    __shared__ uint64_t s_b[BLK], s_key[BLK];
+    __shared__ uint32_t s_off[BLK + 1], s_bits[GSEG / 32], s_wsum[BLK / 64 + 1];
+    __shared__ unsigned long long s_wpos[GSEG / 32], s_base;
+    const uint32_t t = threadIdx.x;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * BLK; i0 < n; i0 += (uint64_t)gridDim.x * BLK) {
+        const uint64_t i = i0 + t;
+        uint64_t b = 0, e = 0;
+        const uint64_t key = i < n ? L.req[i] : 0ull;
+        if (i < n) run_of(L, key, b, e);
+        uint32_t T = 0;
+        const uint32_t off = block_excl_u32((uint32_t)(e - b), s_wsum, &T);
+        s_off[t] = off;
+        s_b[t] = b;
+        s_key[t] = key;
+        if (t == 0) s_off[BLK] = T;
+        __syncthreads();
+        for (uint32_t S0 = 0; S0 < T; S0 += GSEG) {
+            const uint32_t segn = min(GSEG, T - S0);
+            // marking pass: item v = k * BLK + t (consecutive lanes, consecutive tuples of a run);
+            // a wave's 64 answers are two bitmap words
+            for (uint32_t k = 0; k < GSEG / BLK; k++) {
+                const uint32_t v = k * BLK + t, x = S0 + v;
+                bool kp = false;
+                if (v < segn) {
+                    uint32_t lo = 0, hi = BLK;  // the request whose range holds x
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_off[mid] <= x) lo = mid;
+                        else hi = mid;
+                    }
+                    kp = keep(L, L.meta[s_b[lo] + (x - s_off[lo])], 0);
+                }
+                const unsigned long long m = __ballot(kp);
+                const uint32_t lane = __lane_id();
+                if (lane == 0) s_bits[v >> 5] = (uint32_t)m;
+                if (lane == 32) s_bits[v >> 5] = (uint32_t)(m >> 32);
+            }
+            __syncthreads();
+            const uint32_t word = s_bits[t];
+            const unsigned long long o = block_reserve((uint32_t)__popc(word), total, &s_base, s_wsum);
+            s_wpos[t] = o;
+            __syncthreads();
+            // write pass: consecutive threads take consecutive items (coalesced stores)
+            for (uint32_t v = t; v < segn; v += BLK) {
+                const uint32_t wd = s_bits[v >> 5], bit = v & 31u;
+                if (!((wd >> bit) & 1u)) continue;
+                const unsigned long long pos = s_wpos[v >> 5] + (uint32_t)__popc(wd & ((1u << bit) - 1u));
+                if (pos >= cap) {
+                    atomicOr(overflow, 1ull);
+                    continue;
+                }
+                const uint32_t x = S0 + v;
+                uint32_t lo = 0, hi = BLK;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_off[mid] <= x) lo = mid;
+                    else hi = mid;
+                }
+                const uint64_t j = s_b[lo] + (x - s_off[lo]);
+                out[pos] = st_tuple(s_key[lo], L.meta[j], L.shard[j]);
+            }
+            __syncthreads();
         }
     }
 }
 
 // next frontier: the subject-set objects of the tuples received
-__global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, uint64_t *cand,
-                                               unsigned long long *n_cand) {
+__global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, const unsigned long long *range_dev,
+                                               uint64_t *cand, unsigned long long *n_cand) {
+    if (range_dev) {  // the level's tuples: [range_dev[0], range_dev[1]) of the closure
+        t += range_dev[0];
+        n = range_dev[1] - range_dev[0];
+    }
     FOR_TILES(t0, n) {
         uint64_t v[TILE_K];
         uint32_t mask = 0;
@@ -385,6 +465,16 @@ __global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, u
         }
         block_append<uint64_t>(v, mask, cand, n_cand);
     }
+}
+
+// *any = 1 when some query of the batch has an error code
+__global__ __launch_bounds__(BLK) void k_any_nonzero(const int32_t *err, uint64_t n, unsigned long long *any) {
+    for (uint64_t i = gid(); i < n; i += gstride())
+        if (err[i] && !*any) atomicOr(any, 1ull);
+}
+// a device-side level boundary: *dst = min(*total, cap)
+__global__ void k_mark(const unsigned long long *total, unsigned long long *dst, unsigned long long cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *dst = *total < cap ? *total : cap;
 }
 
 // Compact id space of a closure (remap_ids): the uuid ids its tuples and the batch's queries /
@@ -472,11 +562,24 @@ struct Partition {
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
     DevBuf table, seen, cand, fresh, routed, req, req_off, subj, subj_off, subj_set, subj_bits, cnt, pos, out, got, scratch, ctr,
-        closure;
+        closure, lctr;
     uint64_t subj_mask = 0;
     // compact id space of the last closure (remap_ids): local id -> global uuid id
     DevBuf rm_ids, rm_pos, rm_ids2, rm_pos2, rm_flag, rm_rank, rm_lid, uniq, bout;
     uint64_t n_local = 0;
+    void *hpin = nullptr;  // pinned staging for a batch's decisions
+    size_t hpin_bytes = 0;
+    // batches in flight (partition_check_many): the closure of batch k+1 (stage 1: hs, the
+    // members above) runs while batch k is remapped, built and checked (stage 2: hs2, scratch2,
+    // ctr2, the remap buffers, kstream); each batch's closure and queries live in its slot
+    struct Slot {
+        DevBuf closure, bq;
+        uint64_t nt = 0;
+        keto_partition_stats st{};
+    };
+    Slot slots[2];
+    hipStream_t hs2 = nullptr;
+    DevBuf scratch2, ctr2;
     DevBuf bq, braw, bsorted, bkeys, bsubj, bsubj_src, bhist;  // per-batch inputs, reused
     bool verbose = false;
     bool trim = false;  // KETO_PART_TRIM: the engine stream's scratch is released after every batch
@@ -487,19 +590,25 @@ struct Partition {
     std::vector<uint64_t> xoffs;
     std::vector<int32_t> xerr;
     ~Partition() {
+        if (hpin) (void)hipHostFree(hpin);
         if (kstream) keto_stream_destroy(kstream);
         if (hs) (void)hipStreamDestroy(hs);
+        if (hs2) (void)hipStreamDestroy(hs2);
     }
 };
 
 void sync(Partition &P) { KETO_HIP(hipStreamSynchronize(P.hs)); }
 
 template <class F>
-void cub_call(Partition &P, F &&f) {  // hipCUB two-phase call with the shared scratch buffer
+void cub_call(DevBuf &scratch, F &&f) {  // hipCUB two-phase call with a reused scratch buffer
     size_t bytes = 0;
     KETO_HIP(f(nullptr, bytes));
-    ensure(P.scratch, bytes);
-    KETO_HIP(f(P.scratch.p, bytes));
+    ensure(scratch, bytes);
+    KETO_HIP(f(scratch.p, bytes));
+}
+template <class F>
+void cub_call(Partition &P, F &&f) {
+    cub_call(P.scratch, std::forward<F>(f));
 }
 
 uint64_t d2h_u64(Partition &P, const void *d) {
@@ -579,6 +688,60 @@ void ensure_table(Partition &P, uint64_t add) {
                            dptr<unsigned long long>(P.table), P.table_mask);
 }
 
+// One rank with a closure buffer from an earlier batch: every level is enqueued at once, its
+// kernels reading their counts from the device (no host round trip per level: 3 per level on the
+// synchronous path).  Buffers are sized for the worst case the buffer allows -- every candidate
+// is a batch key or the subject set of a gathered tuple -- and a closure that outgrows the
+// buffer returns UINT64_MAX (the caller reruns the batch's closure on the synchronous path).
+uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool filter, int levels, keto_partition_stats &st) {
+    using ull = unsigned long long;
+    const uint64_t cap = P.closure.bytes / sizeof(keto_tuple);
+    P.n_seen = 0;
+    ensure_table(P, n_keys + cap);
+    KETO_HIP(hipMemsetAsync(P.table.p, 0, (P.table_mask + 1) * 8, P.hs));
+    const uint64_t cc = std::max<uint64_t>(1, std::max(n_keys, cap));
+    ensure(P.cand, cc * 8);
+    ensure(P.fresh, cc * 8);
+    // [0] closure total, [1] overflow, [2] level 0's candidates; level L: {new, start, end, next}
+    const size_t nb = (3 + 4 * (size_t)levels) * 8;
+    ensure(P.lctr, nb);
+    ull *c = dptr<ull>(P.lctr), *lv = c + 3;
+    KETO_HIP(hipMemsetAsync(c, 0, nb, P.hs));
+    const ull nk = n_keys;
+    KETO_HIP(hipMemcpyAsync(c + 2, &nk, 8, hipMemcpyHostToDevice, P.hs));
+    if (n_keys) KETO_HIP(hipMemcpyAsync(P.cand.p, keys, n_keys * 8, hipMemcpyDeviceToDevice, P.hs));
+    Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
+             dptr<uint2>(P.meta), dptr<uint4>(P.shard), dptr<uint64_t>(P.fresh), dptr<uint64_t>(P.req_off),
+             dptr<ull>(P.subj_set), P.subj_mask, dptr<uint32_t>(P.subj_bits), 1u, filter ? 1 : 0};
+    const dim3 G(std::max(1, num_cus(P.device)) * 8u);
+    keto_tuple *cl = dptr<keto_tuple>(P.closure);
+    for (int l = 0; l < levels; l++) {
+        ull *m = lv + 4 * l;
+        const ull *n_cand = l ? lv + 4 * (l - 1) + 3 : c + 2;
+        hipLaunchKernelGGL(k_insert, G, dim3(BLK), 0, P.hs, dptr<uint64_t>(P.cand), 0, n_cand, dptr<ull>(P.table),
+                           P.table_mask, dptr<uint64_t>(P.fresh), m);
+        hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, P.hs, c, m + 1, (ull)cap);
+        hipLaunchKernelGGL(k_lookup_gather, G, dim3(BLK), 0, P.hs, L, 0, m, cl, cap, c, c + 1);
+        hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, P.hs, c, m + 2, (ull)cap);
+        hipLaunchKernelGGL(k_next, G, dim3(BLK), 0, P.hs, cl, 0, m + 1, dptr<uint64_t>(P.cand), m + 3);
+    }
+    KETO_HIP(hipGetLastError());
+    std::vector<ull> h(3 + 4 * (size_t)levels);
+    KETO_HIP(hipMemcpyAsync(h.data(), c, nb, hipMemcpyDeviceToHost, P.hs));
+    sync(P);
+    if (h[1]) return UINT64_MAX;
+    for (int l = 0; l < levels; l++) {
+        const ull nn = h[3 + 4 * l];
+        if (!nn) break;
+        st.levels++;
+        st.objects += nn;
+    }
+    if (P.verbose)
+        fprintf(stderr, "[keto partition] one-rank closure: %llu tuples, %llu levels, %llu objects (no per-level sync)\n",
+                (ull)h[0], (ull)st.levels, (ull)st.objects);
+    return h[0];
+}
+
 // Closure of the objects keyed in `keys` (device, n_keys): appended into P.closure, count returned.
 // subj (device, sorted unique, n_subj) filters subject-id tuples (Check); null ships everything.
 uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint32_t *subj, uint64_t n_subj,
@@ -615,6 +778,16 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                            dptr<uint64_t>(P.subj_off), W, soff[W], dptr<unsigned long long>(P.subj_set), P.subj_mask,
                            dptr<uint32_t>(P.subj_bits));
 
+    const int levels = P.limits.max_read_depth + 1;
+    if (W == 1 && P.closure.p && !getenv("KETO_PART_SYNC_LEVELS")) {
+        const uint64_t got = closure_self(P, keys, n_keys, filter, levels, st);
+        if (got != UINT64_MAX) {
+            st.tuples = got;
+            return got;
+        }
+        st.levels = 0;  // the buffer was too small: the synchronous levels below grow it
+        st.objects = 0;
+    }
     // seen set: fresh per batch
     P.n_seen = 0;
     ensure_table(P, n_keys);
@@ -623,7 +796,6 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
     ensure(P.cand, std::max<uint64_t>(1, n_keys) * 8);
     KETO_HIP(hipMemcpyAsync(P.cand.p, keys, n_keys * 8, hipMemcpyDeviceToDevice, P.hs));
     uint64_t n_cand = n_keys, total = 0;
-    const int levels = P.limits.max_read_depth + 1;
     auto tl = std::chrono::steady_clock::now();
     double step_ms[6] = {0, 0, 0, 0, 0, 0};  // verbose: insert, route+exchange, count+scan, fill, next, (spare)
     auto ts = std::chrono::steady_clock::now();
@@ -648,7 +820,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         unsigned long long *c = dptr<unsigned long long>(P.ctr);
         KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
         if (n_cand)
-            hipLaunchKernelGGL(k_insert, grid_tiles(n_cand), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.cand), n_cand,
+            hipLaunchKernelGGL(k_insert, grid_tiles(n_cand), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.cand), n_cand, nullptr,
                                dptr<unsigned long long>(P.table), P.table_mask, dptr<uint64_t>(P.fresh), c);
         const uint64_t n_new = d2h_u64(P, c);
         mark(0);
@@ -703,7 +875,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             unsigned long long *g = dptr<unsigned long long>(P.ctr) + 2;  // [2] total, [3] overflow
             KETO_HIP(hipMemsetAsync(g, 0, 16, P.hs));
             if (n_req)
-                hipLaunchKernelGGL(k_lookup_gather, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req,
+                hipLaunchKernelGGL(k_lookup_gather, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, nullptr,
                                    dptr<keto_tuple>(P.closure) + total, cap, g, g + 1);
             unsigned long long gv[2] = {0, 0};
             KETO_HIP(hipMemcpyAsync(gv, g, 16, hipMemcpyDeviceToHost, P.hs));
@@ -714,8 +886,8 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                 ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
                 KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
                 if (n_got)
-                    hipLaunchKernelGGL(k_next, grid_tiles(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total,
-                                       n_got, dptr<uint64_t>(P.cand), c);
+                    hipLaunchKernelGGL(k_next, grid_tiles(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total, n_got,
+                                       nullptr, dptr<uint64_t>(P.cand), c);
                 n_cand = d2h_u64(P, c);
                 mark(4);
                 total += n_got;
@@ -765,7 +937,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         ensure(P.cand, std::max<uint64_t>(1, n_got) * 8);
         KETO_HIP(hipMemsetAsync(c, 0, 8, P.hs));
         if (n_got)
-            hipLaunchKernelGGL(k_next, grid_tiles(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total, n_got,
+            hipLaunchKernelGGL(k_next, grid_tiles(n_got), dim3(BLK), 0, P.hs, dptr<keto_tuple>(P.closure) + total, n_got, nullptr,
                                dptr<uint64_t>(P.cand), c);
         n_cand = d2h_u64(P, c);
         mark(4);
@@ -822,6 +994,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     P->cfg.relation_names = P->rel_ptr.data();
     P->cfg.namespaces_json = P->json.c_str();
     KETO_HIP(hipStreamCreateWithFlags(&P->hs, hipStreamNonBlocking));
+    KETO_HIP(hipStreamCreateWithFlags(&P->hs2, hipStreamNonBlocking));
     P->verbose = getenv("KETO_PART_VERBOSE") != nullptr;
     P->trim = getenv("KETO_PART_TRIM") != nullptr;
     if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
@@ -912,7 +1085,8 @@ uint64_t batch_keys(Partition &P, const keto_query *q, uint64_t n, DevBuf &keys,
 
 // The closure's tuples plus the batch's queries (q, device) or Expand roots (r, device) over the
 // compact id space: rewritten in place, P.uniq[local] = global, P.n_local ids.
-void remap_ids(Partition &P, uint64_t nt, keto_query *q, keto_subject_set *r, uint64_t n) {
+void remap_ids(Partition &P, keto_tuple *t, uint64_t nt, keto_query *q, keto_subject_set *r, uint64_t n, hipStream_t hs,
+               DevBuf &scratch) {
     const uint64_t E = 2 * nt + (q ? 2 * n : n);
     if (E >= (1ull << 31)) throw Error(KETO_E_LIMIT, "closure too large for the compact id pass (2^31 ids)");
     for (DevBuf *b : {&P.rm_ids, &P.rm_pos, &P.rm_ids2, &P.rm_pos2, &P.rm_flag, &P.rm_rank, &P.rm_lid, &P.uniq})
@@ -920,25 +1094,24 @@ void remap_ids(Partition &P, uint64_t nt, keto_query *q, keto_subject_set *r, ui
     uint32_t *ids = dptr<uint32_t>(P.rm_ids), *pos = dptr<uint32_t>(P.rm_pos), *sk = dptr<uint32_t>(P.rm_ids2),
              *sp = dptr<uint32_t>(P.rm_pos2), *fl = dptr<uint32_t>(P.rm_flag), *rk = dptr<uint32_t>(P.rm_rank),
              *lid = dptr<uint32_t>(P.rm_lid);
-    keto_tuple *t = dptr<keto_tuple>(P.closure);
-    if (nt) hipLaunchKernelGGL(k_ids_tuples, grid_for(nt), dim3(BLK), 0, P.hs, t, nt, ids, pos);
-    if (n && q) hipLaunchKernelGGL(k_ids_queries, grid_for(n), dim3(BLK), 0, P.hs, q, n, 2 * nt, ids, pos);
-    if (n && r) hipLaunchKernelGGL(k_ids_roots, grid_for(n), dim3(BLK), 0, P.hs, r, n, 2 * nt, ids, pos);
+    if (nt) hipLaunchKernelGGL(k_ids_tuples, grid_for(nt), dim3(BLK), 0, hs, t, nt, ids, pos);
+    if (n && q) hipLaunchKernelGGL(k_ids_queries, grid_for(n), dim3(BLK), 0, hs, q, n, 2 * nt, ids, pos);
+    if (n && r) hipLaunchKernelGGL(k_ids_roots, grid_for(n), dim3(BLK), 0, hs, r, n, 2 * nt, ids, pos);
     P.n_local = 0;
     if (E) {
         const int ne = (int)E;
-        cub_call(P, [&](void *tmp, size_t &b) {
-            return hipcub::DeviceRadixSort::SortPairs(tmp, b, ids, sk, pos, sp, ne, 0, 32, P.hs);
+        cub_call(scratch, [&](void *tmp, size_t &b) {
+            return hipcub::DeviceRadixSort::SortPairs(tmp, b, ids, sk, pos, sp, ne, 0, 32, hs);
         });
-        hipLaunchKernelGGL(k_flags32, grid_for(E), dim3(BLK), 0, P.hs, sk, E, fl);
-        cub_call(P, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::InclusiveSum(tmp, b, fl, rk, ne, P.hs); });
-        hipLaunchKernelGGL(k_ids_assign, grid_for(E), dim3(BLK), 0, P.hs, sk, sp, fl, rk, E, lid, dptr<uint32_t>(P.uniq));
+        hipLaunchKernelGGL(k_flags32, grid_for(E), dim3(BLK), 0, hs, sk, E, fl);
+        cub_call(scratch, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::InclusiveSum(tmp, b, fl, rk, ne, hs); });
+        hipLaunchKernelGGL(k_ids_assign, grid_for(E), dim3(BLK), 0, hs, sk, sp, fl, rk, E, lid, dptr<uint32_t>(P.uniq));
         uint32_t m = 0;
-        KETO_HIP(hipMemcpyAsync(&m, rk + E - 1, 4, hipMemcpyDeviceToHost, P.hs));
-        if (nt) hipLaunchKernelGGL(k_apply_tuples, grid_for(nt), dim3(BLK), 0, P.hs, t, nt, lid);
-        if (n && q) hipLaunchKernelGGL(k_apply_queries, grid_for(n), dim3(BLK), 0, P.hs, q, n, 2 * nt, lid);
-        if (n && r) hipLaunchKernelGGL(k_apply_roots, grid_for(n), dim3(BLK), 0, P.hs, r, n, 2 * nt, lid);
-        sync(P);
+        KETO_HIP(hipMemcpyAsync(&m, rk + E - 1, 4, hipMemcpyDeviceToHost, hs));
+        if (nt) hipLaunchKernelGGL(k_apply_tuples, grid_for(nt), dim3(BLK), 0, hs, t, nt, lid);
+        if (n && q) hipLaunchKernelGGL(k_apply_queries, grid_for(n), dim3(BLK), 0, hs, q, n, 2 * nt, lid);
+        if (n && r) hipLaunchKernelGGL(k_apply_roots, grid_for(n), dim3(BLK), 0, hs, r, n, 2 * nt, lid);
+        KETO_HIP(hipStreamSynchronize(hs));
         P.n_local = m;
     }
 }
@@ -953,28 +1126,49 @@ void trim_stream(Partition &P) {
     if (keto_stream_create(P.device, &P.kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
 }
 
-Snapshot *closure_snapshot(Partition &P, uint64_t n_tuples) {
+Snapshot *closure_snapshot(Partition &P, const keto_tuple *t, uint64_t n_tuples) {
     keto_snapshot_config cfg = P.cfg;
     cfg.n_uuids = (uint32_t)std::max<uint64_t>(1, P.n_local);
-    return build_snapshot(&cfg, dptr<keto_tuple>(P.closure), n_tuples, true, false);  // (one batch: no weights)
+    return build_snapshot(&cfg, t, n_tuples, true, false);  // (one batch: no weights)
 }
 }  // namespace
 
-void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
-    Partition &P = *PH;
+namespace {
+// stage 1: the batch's keys, subjects and closure into slot S (the closure functions work on
+// P.closure / P.bq, so the slot's buffers are swapped in for the duration)
+void stage_closure(Partition &P, Partition::Slot &S, const keto_query *q, uint64_t n) {
     KETO_HIP(hipSetDevice(P.device));
-    keto_partition_stats st{};
-    st.batches = 1;
+    ScratchStream on_hs(P.hs);  // (the closure's buffers are used on P.hs)
+    S.st = keto_partition_stats{};
+    S.st.batches = 1;
+    std::swap(P.closure, S.closure);
+    std::swap(P.bq, S.bq);
+    try {
+        auto t0 = std::chrono::steady_clock::now();
+        DevBuf &keys = P.bkeys, &subj = P.bsubj;
+        const uint64_t n_subj = batch_keys(P, q, n, keys, subj);
+        if (P.verbose)
+            fprintf(stderr, "[keto partition] batch keys + %llu subjects: %.3f ms\n", (unsigned long long)n_subj, secs(t0) * 1e3);
+        S.nt = closure(P, dptr<uint64_t>(keys), n, dptr<uint32_t>(subj), n_subj, true, S.st);
+        S.st.closure_s = secs(t0);
+    } catch (...) {
+        std::swap(P.closure, S.closure);
+        std::swap(P.bq, S.bq);
+        throw;
+    }
+    std::swap(P.closure, S.closure);
+    std::swap(P.bq, S.bq);
+}
+
+// stage 2: slot S's closure over the compact id space, its snapshot, the Check kernels, the
+// decisions out
+void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
+    KETO_HIP(hipSetDevice(P.device));
+    keto_partition_stats &st = S.st;
     auto t0 = std::chrono::steady_clock::now();
-    DevBuf &keys = P.bkeys, &subj = P.bsubj;
-    const uint64_t n_subj = batch_keys(P, q, n, keys, subj);
-    if (P.verbose) fprintf(stderr, "[keto partition] batch keys + %llu subjects: %.3f ms\n", (unsigned long long)n_subj, secs(t0) * 1e3);
-    const uint64_t nt = closure(P, dptr<uint64_t>(keys), n, dptr<uint32_t>(subj), n_subj, true, st);
-    st.closure_s = secs(t0);
-    t0 = std::chrono::steady_clock::now();
-    keto_query *dq = dptr<keto_query>(P.bq);  // the batch, uploaded by batch_keys
-    remap_ids(P, nt, dq, nullptr, n);
-    std::unique_ptr<Snapshot> snap(closure_snapshot(P, nt));
+    keto_query *dq = dptr<keto_query>(S.bq);  // the batch, uploaded by batch_keys
+    remap_ids(P, dptr<keto_tuple>(S.closure), S.nt, dq, nullptr, n, P.hs2, P.scratch2);
+    std::unique_ptr<Snapshot> snap(closure_snapshot(P, dptr<keto_tuple>(S.closure), S.nt));
     st.build_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
     ensure(P.bout, std::max<uint64_t>(1, n) * 8 + 256);
@@ -988,9 +1182,34 @@ void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8
         throw Error(rc, buf);
     }
     if (n) {
-        KETO_HIP(hipMemcpyAsync(allowed, d_allowed, n, hipMemcpyDeviceToHost, P.hs));
-        KETO_HIP(hipMemcpyAsync(err, d_err, n * 4, hipMemcpyDeviceToHost, P.hs));
-        sync(P);
+        // decisions through pinned staging; the error codes only when a query has one (a 4n-byte
+        // pageable copy costs as much as the check kernels' tail)
+        const size_t need = (n + 7) / 8 * 8 + 8;
+        if (P.hpin_bytes < need) {
+            if (P.hpin) KETO_HIP(hipHostFree(P.hpin));
+            P.hpin = nullptr;
+            P.hpin_bytes = 0;
+            KETO_HIP(hipHostMalloc(&P.hpin, need * 2, 0));
+            P.hpin_bytes = need * 2;
+        }
+        uint8_t *hp = static_cast<uint8_t *>(P.hpin);
+        ensure(P.ctr2, 64);
+        unsigned long long *any = dptr<unsigned long long>(P.ctr2);
+        KETO_HIP(hipMemsetAsync(any, 0, 8, P.hs2));
+        hipLaunchKernelGGL(k_any_nonzero, grid_for(n), dim3(BLK), 0, P.hs2, d_err, n, any);
+        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemcpyAsync(hp, d_allowed, n, hipMemcpyDeviceToHost, P.hs2));
+        KETO_HIP(hipMemcpyAsync(hp + need - 8, any, 8, hipMemcpyDeviceToHost, P.hs2));
+        KETO_HIP(hipStreamSynchronize(P.hs2));
+        std::memcpy(allowed, hp, n);
+        unsigned long long has_err = 0;
+        std::memcpy(&has_err, hp + need - 8, 8);
+        if (has_err) {
+            KETO_HIP(hipMemcpyAsync(err, d_err, n * 4, hipMemcpyDeviceToHost, P.hs2));
+            KETO_HIP(hipStreamSynchronize(P.hs2));
+        } else {
+            std::memset(err, 0, n * 4);
+        }
     }
     st.run_s = secs(t0);
     if (flags & KETO_F_COUNT_WORK) {
@@ -1004,7 +1223,43 @@ void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8
     }
     snap.reset();
     trim_stream(P);
-    P.last = st;
+}
+}  // namespace
+
+// Batches in flight: while batch k is remapped, built and checked on this thread, the closure of
+// batch k+1 runs on a helper thread (its own stream; the collective, if any, is called from that
+// thread, one batch after another as on every rank).  One batch = the plain synchronous call.
+void partition_check_many(PartitionHandle *PH, uint32_t nb, const keto_query *const *q, const uint64_t *n,
+                          uint8_t *const *allowed, int32_t *const *err, uint32_t flags) {
+    Partition &P = *PH;
+    KETO_HIP(hipSetDevice(P.device));
+    if (!nb) return;
+    stage_closure(P, P.slots[0], q[0], n[0]);
+    for (uint32_t k = 0; k < nb; k++) {
+        std::exception_ptr ex;
+        std::thread next;
+        if (k + 1 < nb)
+            next = std::thread([&, k] {
+                try {
+                    stage_closure(P, P.slots[(k + 1) & 1], q[k + 1], n[k + 1]);
+                } catch (...) {
+                    ex = std::current_exception();
+                }
+            });
+        try {
+            stage_check(P, P.slots[k & 1], n[k], allowed[k], err[k], flags);
+        } catch (...) {
+            if (next.joinable()) next.join();
+            throw;
+        }
+        if (next.joinable()) next.join();
+        P.last = P.slots[k & 1].st;
+        if (ex) std::rethrow_exception(ex);
+    }
+}
+
+void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
+    partition_check_many(PH, 1, &q, &n, &allowed, &err, flags);
 }
 
 uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, uint64_t n) {
@@ -1014,17 +1269,23 @@ uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, ui
     st.batches = 1;
     auto t0 = std::chrono::steady_clock::now();
     DevBuf dr(std::max<uint64_t>(1, n) * sizeof(keto_subject_set)), keys(std::max<uint64_t>(1, n) * 8);
-    if (n) KETO_HIP(hipMemcpyAsync(dr.p, roots, n * sizeof(keto_subject_set), hipMemcpyHostToDevice, P.hs));
-    if (n) hipLaunchKernelGGL(k_root_keys, grid_for(n), dim3(BLK), 0, P.hs, dptr<keto_subject_set>(dr), n, dptr<uint64_t>(keys));
-    const uint64_t nt = closure(P, dptr<uint64_t>(keys), n, nullptr, 0, false, st);
+    uint64_t nt = 0;
+    {
+        ScratchStream on_hs(P.hs);  // (the closure's buffers are used on P.hs; the build's on the null stream)
+        if (n) KETO_HIP(hipMemcpyAsync(dr.p, roots, n * sizeof(keto_subject_set), hipMemcpyHostToDevice, P.hs));
+        if (n)
+            hipLaunchKernelGGL(k_root_keys, grid_for(n), dim3(BLK), 0, P.hs, dptr<keto_subject_set>(dr), n,
+                               dptr<uint64_t>(keys));
+        nt = closure(P, dptr<uint64_t>(keys), n, nullptr, 0, false, st);
+    }
     st.closure_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
-    remap_ids(P, nt, nullptr, dptr<keto_subject_set>(dr), n);
+    remap_ids(P, dptr<keto_tuple>(P.closure), nt, nullptr, dptr<keto_subject_set>(dr), n, P.hs, P.scratch);
     std::vector<keto_subject_set> lroots(n);
     if (n) KETO_HIP(hipMemcpy(lroots.data(), dr.p, n * sizeof(keto_subject_set), hipMemcpyDeviceToHost));
     std::vector<uint32_t> uniq(P.n_local);
     if (P.n_local) KETO_HIP(hipMemcpy(uniq.data(), P.uniq.p, P.n_local * 4, hipMemcpyDeviceToHost));
-    std::unique_ptr<Snapshot> snap(closure_snapshot(P, nt));
+    std::unique_ptr<Snapshot> snap(closure_snapshot(P, dptr<keto_tuple>(P.closure), nt));
     st.build_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
     P.xoffs.assign(n + 1, 0);

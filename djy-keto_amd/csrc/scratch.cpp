@@ -126,17 +126,26 @@ void *pool_acquire(int device, size_t bytes, size_t *got) {
 
 // ---- build scratch cache ----------------------------------------------------------------------
 // The builder's temporaries (DevBuf) come and go every build; hipFree of a large block unmaps it
-// (~0.3 ms each: 5 ms of a config-5 batch's closure build went to them).  Freed blocks stay in a
-// per-device cache instead (capped: KETO_SCRATCH_CAP_MB, default a sixteenth of the device) and
-// are handed out again best-fit within 2x.  A block may still be read by queued kernels when it
-// is returned, so the first reuse after any return synchronises the device once (as hipFree did).
+// (~0.3 ms each: 5 ms of a config-5 batch's closure build went to them) and synchronises the
+// whole device (so a pipelined partition batch's build would wait for the next batch's closure
+// kernels at every small free).  Freed blocks stay in a per-device cache instead (capped:
+// KETO_SCRATCH_CAP_MB, default a sixteenth of the device), handed out again best-fit within 2x.
+// A returned block may still be read by queued kernels: it carries an event recorded on the
+// stream the releasing thread works on (scratch_stream; the null stream by default), and its
+// next user waits for that event -- not for the whole device.
 namespace {
+struct CacheBlock {
+    void *p;
+    size_t bytes;
+    hipEvent_t ev;
+};
 struct ScratchCache {
     std::mutex mu;
-    std::vector<PoolBlock> free;
+    std::vector<CacheBlock> free;
+    std::vector<hipEvent_t> events;  // spare events
     size_t held = 0, cap = 0;
-    bool dirty = false;
 };
+thread_local hipStream_t tl_stream = nullptr;
 ScratchCache &scache(int device) {
     static ScratchCache caches[64];
     ScratchCache &C = caches[std::clamp(device, 0, 63)];
@@ -148,25 +157,32 @@ ScratchCache &scache(int device) {
     }
     return C;
 }
-constexpr size_t SCRATCH_MIN = (size_t)1 << 20;  // smaller blocks: plain hipMalloc / hipFree
 void scratch_trim(int device) {
     ScratchCache &C = scache(device);
     std::lock_guard<std::mutex> g(C.mu);
     if (C.free.empty()) return;
     (void)hipDeviceSynchronize();
-    for (auto &b : C.free) (void)hipFree(b.p);
+    for (auto &b : C.free) {
+        (void)hipFree(b.p);
+        C.events.push_back(b.ev);
+    }
     C.free.clear();
     C.held = 0;
-    C.dirty = false;
 }
 }  // namespace
+
+hipStream_t scratch_stream(hipStream_t s) {
+    const hipStream_t old = tl_stream;
+    tl_stream = s;
+    return old;
+}
 
 void *scratch_get(size_t bytes, size_t *got) {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (bytes >= SCRATCH_MIN) {
+    {
         ScratchCache &C = scache(dev);
-        std::lock_guard<std::mutex> g(C.mu);
+        std::unique_lock<std::mutex> g(C.mu);
         size_t best = SIZE_MAX, at = 0;
         for (size_t i = 0; i < C.free.size(); i++)
             if (C.free[i].bytes >= bytes && C.free[i].bytes <= 2 * bytes && C.free[i].bytes < best) {
@@ -174,15 +190,15 @@ void *scratch_get(size_t bytes, size_t *got) {
                 at = i;
             }
         if (best != SIZE_MAX) {
-            if (C.dirty) {
-                KETO_HIP(hipDeviceSynchronize());
-                C.dirty = false;
-            }
-            void *q = C.free[at].p;
+            const CacheBlock b = C.free[at];
             C.held -= best;
             C.free.erase(C.free.begin() + (ptrdiff_t)at);
+            g.unlock();
+            KETO_HIP(hipEventSynchronize(b.ev));  // its last reader's stream got past the release
+            g.lock();
+            C.events.push_back(b.ev);
             *got = best;
-            return q;
+            return b.p;
         }
     }
     void *q = nullptr;
@@ -199,15 +215,22 @@ void scratch_put(void *p, size_t bytes) {
     if (!p) return;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (bytes >= SCRATCH_MIN) {
-        ScratchCache &C = scache(dev);
-        std::lock_guard<std::mutex> g(C.mu);
-        if (C.held + bytes <= C.cap) {
-            C.free.push_back(PoolBlock{p, bytes});
+    ScratchCache &C = scache(dev);
+    std::lock_guard<std::mutex> g(C.mu);
+    if (C.held + bytes <= C.cap) {
+        hipEvent_t ev = nullptr;
+        if (!C.events.empty()) {
+            ev = C.events.back();
+            C.events.pop_back();
+        } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            ev = nullptr;
+        }
+        if (ev && hipEventRecord(ev, tl_stream) == hipSuccess) {
+            C.free.push_back(CacheBlock{p, bytes, ev});
             C.held += bytes;
-            C.dirty = true;
             return;
         }
+        if (ev) C.events.push_back(ev);
     }
     (void)hipFree(p);
 }

@@ -219,7 +219,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     auto tp = std::chrono::steady_clock::now();
     auto phase = [&](const char *what) {
         if (!verbose) return;
-        KETO_HIP(hipDeviceSynchronize());
+        KETO_HIP(hipStreamSynchronize(nullptr));
         auto now = std::chrono::steady_clock::now();
         fprintf(stderr, "[keto build] %-14s %.3f s\n", what, std::chrono::duration<double>(now - tp).count());
         tp = now;
@@ -547,7 +547,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.n_nodes = N;
     D.n_uuids = s.n_uuids;
     D.strict = s.strict;
-    KETO_HIP(hipDeviceSynchronize());
+    KETO_HIP(hipStreamSynchronize(nullptr));  // the build ran on the null stream; engines read it from theirs
     phase("finish");
     s.info.n_entities = ent_total;
     s.info.n_tuples = n;

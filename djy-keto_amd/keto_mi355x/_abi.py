@@ -146,6 +146,7 @@ SIGNATURES = {
     "keto_partition_create": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, _U32, _VP,
                                              ctypes.POINTER(Limits), ctypes.POINTER(_VP)]),
     "keto_partition_check": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP, _U32]),
+    "keto_partition_check_many": (ctypes.c_int, [_VP, _U32, _VP, _VP, _VP, _VP, _U32]),
     "keto_partition_expand": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),
     "keto_partition_expand_result": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP]),
     "keto_partition_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(PartitionStats)]),

@@ -150,6 +150,21 @@ class PartitionedEngine:
             self.last_work = {k: [self.last[k], 0, 0] for k in ("rows", "edges", "probes", "queries")}
         return allowed, err[:len(q)]
 
+    def check_batches(self, batches: list, count_work: bool = False):
+        """several batches in order, pipelined (keto_partition_check_many: batch k+1's closure
+        runs while batch k is built and checked) -> [(allowed, err)] per batch"""
+        qs = [np.ascontiguousarray(b, dtype=_abi.QUERY_DT) for b in batches]
+        outs = [(np.zeros(len(q), np.uint8), np.zeros(max(1, len(q)), np.int32)) for q in qs]
+        k = len(qs)
+        P = ctypes.c_void_p * max(1, k)
+        qp = P(*[q.ctypes.data if len(q) else None for q in qs])
+        ap = P(*[a.ctypes.data for a, _ in outs])
+        ep = P(*[e.ctypes.data for _, e in outs])
+        ns = (ctypes.c_uint64 * max(1, k))(*[len(q) for q in qs])
+        check(lib().keto_partition_check_many(self.handle, k, qp, ns, ap, ep, _abi.F_COUNT_WORK if count_work else 0))
+        self._stats()
+        return [(a, e[:len(q)]) for (a, e), q in zip(outs, qs)]
+
     def expand_batch(self, roots: np.ndarray):
         """roots: SUBJSET_DT (this rank's) -> (nodes TREE_DT, offsets u64[n+1], err i32[n])"""
         r = np.ascontiguousarray(roots, dtype=_abi.SUBJSET_DT)

@@ -366,6 +366,11 @@ int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tup
  * name one of the batch's subjects: no other subject-id tuple is ever read by these queries. */
 int keto_partition_check(keto_partition *p, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
                          int32_t *out_err, uint32_t flags);
+/* collective: n_batches batches in order, as keto_partition_check each, pipelined -- batch k+1's
+ * closure exchange runs (on a helper thread, which then calls the collective) while batch k is
+ * built and checked.  Every rank passes the same n_batches.  Stats: the last batch's. */
+int keto_partition_check_many(keto_partition *p, uint32_t n_batches, const keto_query *const *queries, const uint64_t *n,
+                              uint8_t *const *out_allowed, int32_t *const *out_err, uint32_t flags);
 /* collective: expands this rank's roots; *out_nodes_needed = nodes of all the trees.  Then
  * (local, no collective) keto_partition_expand_result copies them out, as keto_expand_batch. */
 int keto_partition_expand(keto_partition *p, const keto_subject_set *roots, uint64_t n, uint64_t *out_nodes_needed);

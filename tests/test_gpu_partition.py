@@ -57,11 +57,29 @@ def test_single_rank_partitioned_matches_oracle():
     dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=8)
     np.testing.assert_array_equal(err, oerr)
     np.testing.assert_array_equal(allowed, dec)
-    # a second batch on the same engine (workspace reuse)
+    # a second batch on the same engine (workspace reuse): its closure is enqueued level after
+    # level with no host round trip (closure_self); the same batch again on the synchronous levels
     q2 = synth.drive_queries(wl, 5000, seed=32)
     a2, e2 = eng.check_batch(q2)
-    d2, _, _ = orc.check_batch(queries_to_oracle(q2), threads=8)
+    ref2 = closure(wl.tuples, q2["ns"], q2["obj"], wl.max_depth + 1, subjects=q2["s_obj"][q2["subj_kind"] == 0])
+    assert eng.last["tuples"] == len(ref2)
+    levels2 = eng.last["levels"]
+    d2, oe2, _ = orc.check_batch(queries_to_oracle(q2), threads=8)
     np.testing.assert_array_equal(a2, d2)
+    os.environ["KETO_PART_SYNC_LEVELS"] = "1"
+    try:
+        a3, e3 = eng.check_batch(q2)
+    finally:
+        del os.environ["KETO_PART_SYNC_LEVELS"]
+    assert eng.last["tuples"] == len(ref2) and eng.last["levels"] == levels2
+    np.testing.assert_array_equal(a3, d2)
+    # pipelined batches (keto_partition_check_many): each batch's closure on the helper thread
+    # while the batch before it is built and checked; the same answers in the same order
+    many = eng.check_batches([q2, q, q2, q])
+    for (a, e), d, oe in zip(many, (d2, dec, d2, dec), (oe2, oerr, oe2, oerr)):
+        np.testing.assert_array_equal(a, d)
+        np.testing.assert_array_equal(e, oe)
+    assert eng.last["tuples"] == len(ref)
     roots = _roots(wl, np.random.default_rng(1), 256)
     nodes, offs, xerr = eng.expand_batch(roots)
     assert eng.last["tuples"] == len(closure(wl.tuples, roots["ns"], roots["obj"], wl.max_depth + 1))
@@ -109,8 +127,16 @@ def _worker(rank, world, port, out, device_buffers=False):
             on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), wl.max_depth)
             mine = nodes[int(offs[i]):int(offs[i + 1])]
             tree_mis += len(mine) != len(on) or not (mine["s_obj"] == on["sid"]).all()
+        # pipelined: the closures of batches 2 and 3 exchanged from the helper thread while the
+        # batch before them is checked (every rank passes the same number of batches)
+        q2 = synth.drive_queries(wl, 4096, seed=60 + rank)
+        d2, oe2, _ = orc.check_batch(queries_to_oracle(q2), threads=4)
+        many = eng.check_batches([q, q2, q])
+        pipe_mis = 0
+        for (a, e), d, oe in zip(many, (dec, d2, dec), (oerr, oe2, oerr)):
+            pipe_mis += int((a != d).sum() + (e != oe).sum())
         out[rank] = (int((allowed != dec).sum()), int((err != oerr).sum()), int(dec.sum()), st["bytes_sent"],
-                     tree_mis, int((xerr != 0).sum()))
+                     tree_mis, int((xerr != 0).sum()), pipe_mis)
         eng.close()
     finally:
         dist.destroy_process_group()
@@ -127,6 +153,6 @@ def test_two_rank_partitioned_matches_oracle(device_buffers):
         mp.spawn(_worker, args=(world, _free_port(), out, device_buffers), nprocs=world, join=True)
         res = dict(out)
     for r in range(world):
-        dmis, emis, n_allowed, sent, tree_mis, xerr = res[r]
-        assert dmis == 0 and emis == 0 and tree_mis == 0 and xerr == 0
+        dmis, emis, n_allowed, sent, tree_mis, xerr, pipe_mis = res[r]
+        assert dmis == 0 and emis == 0 and tree_mis == 0 and xerr == 0 and pipe_mis == 0
         assert n_allowed > 0 and sent > 0

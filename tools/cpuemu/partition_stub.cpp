@@ -8,6 +8,10 @@ struct PartitionHandle {};
 PartitionHandle *partition_create(const keto_snapshot_config *, const keto_tuple *, uint64_t, bool, const keto_collective *,
                                   const keto_limits *) { unavailable(); }
 void partition_check(PartitionHandle *, const keto_query *, uint64_t, uint8_t *, int32_t *, uint32_t) { unavailable(); }
+void partition_check_many(PartitionHandle *, uint32_t, const keto_query *const *, const uint64_t *, uint8_t *const *, int32_t *const *,
+                          uint32_t) {
+    unavailable();
+}
 uint64_t partition_expand(PartitionHandle *, const keto_subject_set *, uint64_t) { unavailable(); }
 void partition_expand_result(PartitionHandle *, keto_tree_node *, uint64_t, uint64_t *, int32_t *) { unavailable(); }
 void partition_stats(PartitionHandle *, keto_partition_stats *) { unavailable(); }

@@ -6,7 +6,7 @@ set -u
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out && export TMPDIR=/tmp
 O=gpurun_out/${1:-r03c5p} && rm -rf $O && mkdir -p $O
 S=${2:-10}
-ARGS="--workload c5 --scale $S --steps 4 --warmup 1 --no-cpu-baseline"
+ARGS="--workload c5 --scale $S --steps 10 --warmup 2 --no-cpu-baseline"
 [ -n "${SKIP_LINE:-}" ] || KETO_BUILD_VERBOSE=1 KETO_PART_VERBOSE=1 timeout -k 10 400 python3 -u bench.py $ARGS > $O/c5.log 2>&1 \
   || { echo "c5 bench failed"; tail -8 $O/c5.log; exit 1; }
 grep -E "keto (build|partition)" $O/c5.log | tail -45
