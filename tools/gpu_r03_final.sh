@@ -27,5 +27,6 @@ done
 python3 tools/pmc_split.py $O/pmc_split.json $O/pmc3 $O/pmc4 $O/pmc1 $O/pmc2 || echo "split failed (not fatal)"
 rm -rf $O/pmc1 $O/pmc2 $O/pmc3 $O/pmc4 $O/kt
 cp $O/r03_traffic_c4.json profiles/ 2>/dev/null  # (so the bench line below reports it)
+[ -n "${NO_BENCH:-}" ] && exit 0  # (the bench line in a call of its own: tools/gpu_r03_bench.sh)
 timeout -k 10 600 python3 -u bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -8 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | cut -c1-1500
