@@ -239,16 +239,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             P.gbase[t * GEN_STRIDE + k + 1] = gm.base[t] + (gm.pre[t + 1] - gm.pre[t]);
     // blocks without a goal of this generation leave before staging the tables: small batches
     // and the empty generations an asynchronous batch launches speculatively cost ~nothing
-#ifdef KETO_FR_XCD
-    // XCD-aware chunk order (experiment): the dispatcher places block b on XCD b % 8; stripes of
-    // KETO_FR_XCD consecutive chunks (siblings, one query's goals) go to one XCD's blocks, so a
-    // query's subject record and shared rows stay in one L2
-    const uint32_t nx = (gridDim.x % 8u == 0u) ? 8u : 1u, xcd = blockIdx.x % nx, per = gridDim.x / nx;
-    auto chunk_of = [&](uint32_t u) { return ((u / KETO_FR_XCD) * nx + xcd) * KETO_FR_XCD + u % KETO_FR_XCD; };
-    if (chunk_of(blockIdx.x / nx) * blockDim.x >= cnt) return;
-#else
     if (blockIdx.x * blockDim.x >= cnt) return;
-#endif
     const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
     // this wave's slice
     const uint32_t so = (blockIdx.x * ((blockDim.x + 63) >> 6) + (threadIdx.x >> 6)) % FR_SHARDS;
@@ -266,13 +257,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
     __shared__ uint4 rg_g[XBLOCK];
     __shared__ uint32_t rg_i[XBLOCK], rg_n[XBLOCK / 64][NB + 1];
 #endif
-#ifdef KETO_FR_XCD
-    for (uint32_t u = blockIdx.x / nx;; u += per) {
-        const uint32_t j0 = chunk_of(u) * blockDim.x;
-        if (j0 >= cnt) break;
-#else
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
-#endif
         const uint32_t j = j0 + threadIdx.x;
         // goals of queries routed meanwhile still run (rare); they can no longer spawn
         bool live = j < cnt;
