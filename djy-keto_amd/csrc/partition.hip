@@ -670,7 +670,11 @@ std::vector<uint64_t> exchange(Partition &P, const void *src, const std::vector<
 void reserve_closure(Partition &P, uint64_t keep, uint64_t n) {
     const size_t need = std::max<uint64_t>(1, n) * sizeof(keto_tuple);
     if (P.closure.p && P.closure.bytes >= need) return;
-    DevBuf b(std::max<size_t>(need * 2, 64u << 20));
+    // (KETO_PART_MIN_CLOSURE, tuples: a smaller floor than 64 MB, so tests reach the overflow path)
+    static const size_t floor_bytes = getenv("KETO_PART_MIN_CLOSURE")
+                                          ? std::max<size_t>(1, strtoull(getenv("KETO_PART_MIN_CLOSURE"), nullptr, 10)) * sizeof(keto_tuple)
+                                          : (size_t)64 << 20;
+    DevBuf b(std::max<size_t>(need * 2, floor_bytes));
     if (keep) KETO_HIP(hipMemcpyAsync(b.p, P.closure.p, keep * sizeof(keto_tuple), hipMemcpyDeviceToDevice, P.hs));
     P.closure = std::move(b);
 }

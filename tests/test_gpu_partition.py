@@ -44,6 +44,10 @@ def _oracle(wl):
 
 
 def test_single_rank_partitioned_matches_oracle():
+    # closure buffers sized by the batches alone (no 64 MB floor): a later, larger batch then
+    # outgrows the buffer its slot kept, and the one-rank closure falls back to the synchronous
+    # levels (read once per process, before its first partition batch)
+    os.environ["KETO_PART_MIN_CLOSURE"] = "1000"
     wl = _wl()
     q = synth.drive_queries(wl, 20_000, seed=31)
     q["max_depth"][:2000] = np.random.default_rng(0).integers(1, 8, 2000)
@@ -91,6 +95,26 @@ def test_single_rank_partitioned_matches_oracle():
         for f_p, f_o in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"),
                          ("s_rel", "srel"), ("n_children", "n_children")):
             np.testing.assert_array_equal(mine[f_p], on[f_o])
+    eng.close()
+
+
+def test_single_rank_closure_outgrows_its_buffer():
+    """a batch whose closure is over twice the largest its slot saw: the one-rank closure
+    (closure_self, no host round trip per level) overflows the buffer it was sized by, and the
+    batch's closure is redone on the synchronous levels, which grow it"""
+    os.environ["KETO_PART_MIN_CLOSURE"] = "1000"  # (no 64 MB floor; read once per process)
+    wl = _wl()
+    eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, wl.tuples,
+                                      max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    orc = _oracle(wl)
+    for n, seed in ((64, 41), (128, 42), (20_000, 43), (64, 44)):
+        q = synth.drive_queries(wl, n, seed=seed)
+        allowed, err = eng.check_batch(q)
+        ref = closure(wl.tuples, q["ns"], q["obj"], wl.max_depth + 1, subjects=q["s_obj"][q["subj_kind"] == 0])
+        assert eng.last["tuples"] == len(ref)
+        dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+        np.testing.assert_array_equal(allowed, dec)
+        np.testing.assert_array_equal(err, oerr)
     eng.close()
 
 
