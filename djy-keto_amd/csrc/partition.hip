@@ -111,9 +111,11 @@ __device__ __forceinline__ void block_append(const T (&v)[TILE_K], uint32_t mask
          t0 += (uint64_t)gridDim.x * blockDim.x * TILE_K)
 inline dim3 grid_tiles(uint64_t n) { return grid_for((n + TILE_K - 1) / TILE_K); }
 
+// sort key of a store tuple: its object key, then subject sets before subject ids (a run's
+// subject-set tuples are its first setn[run] entries)
 __global__ __launch_bounds__(BLK) void k_tuple_keys(const keto_tuple *t, uint64_t n, uint64_t *keys, uint32_t *idx) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
-        keys[i] = okey(t[i].ns, t[i].obj);
+        keys[i] = (okey(t[i].ns, t[i].obj) << 1) | (t[i].subj_kind == 1 ? 0u : 1u);
         idx[i] = (uint32_t)i;
     }
 }
@@ -149,11 +151,38 @@ __global__ __launch_bounds__(BLK) void k_gather_store(const keto_tuple *t, const
 }
 // run starts of the sorted keys: flag[i] = key[i] != key[i-1]
 __global__ __launch_bounds__(BLK) void k_run_flags(const uint64_t *k, uint64_t n, uint32_t *flag) {
-    for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+    for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || (k[i] >> 1) != (k[i - 1] >> 1)) ? 1u : 0u;
 }
 // compacted runs: run r starts at the i with flag[i] and exclusive-scan pos[i] == r
 __global__ __launch_bounds__(BLK) void k_run_starts(const uint64_t *k, const uint32_t *flag, const uint64_t *pos,
                                                      uint64_t n, uint64_t *ukeys, uint64_t *beg) {
+    for (uint64_t i = gid(); i < n; i += gstride())
+        if (flag[i]) {
+            ukeys[pos[i]] = k[i] >> 1;
+            beg[pos[i]] = i;
+        }
+}
+// subject-set tuples per run (they lead it): run r = inclusive scan of the run flags - 1
+__global__ __launch_bounds__(BLK) void k_set_counts(const uint2 *meta, const uint32_t *flag, const uint64_t *pos, uint64_t n,
+                                                    uint32_t *setn) {
+    for (uint64_t i = gid(); i < n; i += gstride())
+        if (meta[i].y >> 31) atomicAdd(&setn[pos[i] + flag[i] - 1], 1u);
+}
+// the subject index's input: (subject id, run << 32 | position) of every subject-id tuple, and
+// ~0 keys (sorted past the end) for subject-set tuples
+__global__ __launch_bounds__(BLK) void k_subject_pairs(const uint2 *meta, const uint32_t *flag, const uint64_t *pos, uint64_t n,
+                                                       uint32_t *skey, uint64_t *sval) {
+    for (uint64_t i = gid(); i < n; i += gstride()) {
+        const uint2 m = meta[i];
+        skey[i] = (m.y >> 31) ? 0xFFFFFFFFu : m.x;
+        sval[i] = ((pos[i] + flag[i] - 1) << 32) | i;
+    }
+}
+__global__ __launch_bounds__(BLK) void k_u32_run_flags(const uint32_t *k, uint64_t n, uint32_t *flag) {
+    for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+}
+__global__ __launch_bounds__(BLK) void k_u32_run_starts(const uint32_t *k, const uint32_t *flag, const uint64_t *pos, uint64_t n,
+                                                        uint64_t *ukeys, uint64_t *beg) {
     for (uint64_t i = gid(); i < n; i += gstride())
         if (flag[i]) {
             ukeys[pos[i]] = k[i];
@@ -256,6 +285,8 @@ struct Lookup {
     const uint32_t *subj_bits;    // 2^SUBJ_BITS-bit filter of the set: most subject-id tuples miss it
     uint32_t world;
     int filter;
+    const uint32_t *setn;         // subject-set tuples leading each run
+    int set_only;                 // walk only those (the subject-id tuples come from the subject pass)
 };
 __device__ __forceinline__ unsigned long long subj_key(uint32_t src, uint32_t sid) {
     return (((unsigned long long)src << 32) | sid) + 1ull;  // 0 = empty slot
@@ -285,18 +316,27 @@ __global__ __launch_bounds__(BLK) void k_subj_fill(const uint32_t *subj, const u
         }
     }
 }
-__device__ __forceinline__ bool run_of(const Lookup &L, uint64_t key, uint64_t &b, uint64_t &e) {
-    uint64_t h = mix64(key + 1) & L.index_mask;
+// a key's range in a k_index_fill table over runs (beg[run], beg[run + 1])
+__device__ __forceinline__ bool index_range(const uint4 *index, uint64_t mask, const uint64_t *beg, uint64_t key, uint64_t &b,
+                                            uint64_t &e, uint32_t &run) {
+    uint64_t h = mix64(key + 1) & mask;
     for (;;) {  // one 16-byte probe per step; the table is at most half full
-        const uint4 sl = L.index[h];
+        const uint4 sl = index[h];
         if (sl.z == NONE32) return false;
         if (sl.x == (uint32_t)key && sl.y == (uint32_t)(key >> 32)) {
-            b = L.beg[sl.z];
-            e = L.beg[sl.z + 1];
+            run = sl.z;
+            b = beg[sl.z];
+            e = beg[sl.z + 1];
             return true;
         }
-        h = (h + 1) & L.index_mask;
+        h = (h + 1) & mask;
     }
+}
+__device__ __forceinline__ bool run_of(const Lookup &L, uint64_t key, uint64_t &b, uint64_t &e) {
+    uint32_t r;
+    if (!index_range(L.index, L.index_mask, L.beg, key, b, e, r)) return false;
+    if (L.set_only) e = b + L.setn[r];
+    return true;
 }
 __device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
     uint32_t lo = 0, hi = L.world;  // last source whose offset <= i
@@ -445,6 +485,61 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, con
     }
 }
 
+// The subject index of a one-rank partition: every subject-id tuple, grouped by subject id
+// (runs over the sorted ids, looked up through a k_index_fill table); entry = run << 32 | position.
+struct SubjectIndex {
+    const uint64_t *beg;
+    const uint4 *index;
+    uint64_t mask;
+    const uint64_t *val;
+};
+__device__ __forceinline__ bool seen_has(const unsigned long long *table, uint64_t mask, uint64_t key) {
+    const unsigned long long k = key + 1ull;
+    uint64_t h = mix64(k) & mask;
+    for (;;) {  // at most half full: every probe sequence ends at an empty slot
+        const unsigned long long v = table[h];
+        if (v == k) return true;
+        if (v == 0ull) return false;
+        h = (h + 1) & mask;
+    }
+}
+// The one-rank Check closure's subject-id tuples, from the subject side: the reference reads a
+// subject-id tuple only through an EXISTS probe against the query's own subject (engine.go:167-208,
+// traverser.go:73-80, the OR shortcut), so the closure needs exactly the batch subjects' tuples
+// whose object it asked for -- each batch subject's index entries, kept when their run's key is
+// in the closure's seen set.  The same tuples the levels' filter keeps, found through ~6 entries
+// per subject instead of every subject-id tuple of every object asked for.
+__global__ __launch_bounds__(BLK) void k_subject_pass(Lookup L, SubjectIndex X, const uint32_t *subj, uint64_t n_subj,
+                                                       const unsigned long long *table, uint64_t tmask, keto_tuple *out,
+                                                       uint64_t cap, unsigned long long *total, unsigned long long *overflow) {
+    __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_wsum[BLK / 64 + 1];
+    for (uint64_t i0 = (uint64_t)blockIdx.x * BLK; i0 < n_subj; i0 += (uint64_t)gridDim.x * BLK) {
+        const uint64_t i = i0 + threadIdx.x;
+        uint64_t b = 0, e = 0;
+        uint32_t run = 0;
+        if (i < n_subj) index_range(X.index, X.mask, X.beg, subj[i], b, e, run);
+        uint32_t c = 0, km = 0;  // km: which of the first 32 entries are kept
+        for (uint64_t j = b; j < e; j++)
+            if (seen_has(table, tmask, L.ukeys[X.val[j] >> 32])) {
+                if (j - b < 32) km |= 1u << (j - b);
+                c++;
+            }
+        uint64_t o = block_reserve(c, total, &s_base, s_wsum);
+        for (uint64_t j = b; j < e && c; j++) {
+            const uint64_t v = X.val[j];
+            const uint64_t key = L.ukeys[v >> 32];
+            if (j - b < 32 ? !((km >> (j - b)) & 1u) : !seen_has(table, tmask, key)) continue;
+            if (o >= cap) {
+                atomicOr(overflow, 1ull);
+                break;
+            }
+            const uint64_t p = v & 0xFFFFFFFFull;
+            out[o++] = st_tuple(key, L.meta[p], L.shard[p]);
+        }
+    }
+}
+
 // next frontier: the subject-set objects of the tuples received
 __global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, const unsigned long long *range_dev,
                                                uint64_t *cand, unsigned long long *n_cand) {
@@ -558,6 +653,11 @@ struct Partition {
     // keys ukeys[m], beg[m+1]
     DevBuf meta, shard, ukeys, beg, index;
     uint64_t n = 0, m = 0, index_mask = 0;
+    DevBuf setn;  // subject-set tuples leading each run
+    // one rank: the subject index (k_subject_pass); sx_beg[ms + 1] over sx_val, sx_index by id
+    DevBuf sx_beg, sx_index, sx_val;
+    uint64_t sx_mask = 0;
+    bool have_sx = false;
     hipStream_t hs = nullptr;
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
@@ -697,7 +797,8 @@ void ensure_table(Partition &P, uint64_t add) {
 // synchronous path).  Buffers are sized for the worst case the buffer allows -- every candidate
 // is a batch key or the subject set of a gathered tuple -- and a closure that outgrows the
 // buffer returns UINT64_MAX (the caller reruns the batch's closure on the synchronous path).
-uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool filter, int levels, keto_partition_stats &st) {
+uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool filter, uint64_t n_subj, int levels,
+                      keto_partition_stats &st) {
     using ull = unsigned long long;
     const uint64_t cap = P.closure.bytes / sizeof(keto_tuple);
     P.n_seen = 0;
@@ -716,7 +817,8 @@ uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool 
     if (n_keys) KETO_HIP(hipMemcpyAsync(P.cand.p, keys, n_keys * 8, hipMemcpyDeviceToDevice, P.hs));
     Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
              dptr<uint2>(P.meta), dptr<uint4>(P.shard), dptr<uint64_t>(P.fresh), dptr<uint64_t>(P.req_off),
-             dptr<ull>(P.subj_set), P.subj_mask, dptr<uint32_t>(P.subj_bits), 1u, filter ? 1 : 0};
+             dptr<ull>(P.subj_set), P.subj_mask, dptr<uint32_t>(P.subj_bits), 1u, filter ? 1 : 0,
+             dptr<uint32_t>(P.setn), (filter && P.have_sx) ? 1 : 0};
     const dim3 G(std::max(1, num_cus(P.device)) * 8u);
     keto_tuple *cl = dptr<keto_tuple>(P.closure);
     for (int l = 0; l < levels; l++) {
@@ -728,6 +830,11 @@ uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool 
         hipLaunchKernelGGL(k_lookup_gather, G, dim3(BLK), 0, P.hs, L, 0, m, cl, cap, c, c + 1);
         hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, P.hs, c, m + 2, (ull)cap);
         hipLaunchKernelGGL(k_next, G, dim3(BLK), 0, P.hs, cl, 0, m + 1, dptr<uint64_t>(P.cand), m + 3);
+    }
+    if (L.set_only && n_subj) {  // the subject-id tuples, from the subject side
+        const SubjectIndex X{dptr<uint64_t>(P.sx_beg), dptr<uint4>(P.sx_index), P.sx_mask, dptr<uint64_t>(P.sx_val)};
+        hipLaunchKernelGGL(k_subject_pass, grid_for(n_subj), dim3(BLK), 0, P.hs, L, X, dptr<uint32_t>(P.subj), n_subj,
+                           dptr<ull>(P.table), P.table_mask, cl, cap, c, c + 1);
     }
     KETO_HIP(hipGetLastError());
     std::vector<ull> h(3 + 4 * (size_t)levels);
@@ -784,7 +891,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
 
     const int levels = P.limits.max_read_depth + 1;
     if (W == 1 && P.closure.p && !getenv("KETO_PART_SYNC_LEVELS")) {
-        const uint64_t got = closure_self(P, keys, n_keys, filter, levels, st);
+        const uint64_t got = closure_self(P, keys, n_keys, filter, filter ? soff[W] : 0, levels, st);
         if (got != UINT64_MAX) {
             st.tuples = got;
             return got;
@@ -999,6 +1106,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     P->cfg.namespaces_json = P->json.c_str();
     KETO_HIP(hipStreamCreateWithFlags(&P->hs, hipStreamNonBlocking));
     KETO_HIP(hipStreamCreateWithFlags(&P->hs2, hipStreamNonBlocking));
+    ScratchStream on_hs(P->hs);  // (the store is built on P->hs)
     P->verbose = getenv("KETO_PART_VERBOSE") != nullptr;
     P->trim = getenv("KETO_PART_TRIM") != nullptr;
     if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
@@ -1049,6 +1157,59 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
         hipLaunchKernelGGL(k_run_starts, grid_for(n), dim3(BLK), 0, Q.hs, kout, fl, fp, n, dptr<uint64_t>(Q.ukeys),
                            dptr<uint64_t>(Q.beg));
     KETO_HIP(hipMemcpyAsync(dptr<uint64_t>(Q.beg) + Q.m, &Q.n, 8, hipMemcpyHostToDevice, Q.hs));
+    Q.setn = DevBuf(std::max<uint64_t>(1, Q.m) * 4);
+    KETO_HIP(hipMemsetAsync(Q.setn.p, 0, std::max<uint64_t>(1, Q.m) * 4, Q.hs));
+    if (n) hipLaunchKernelGGL(k_set_counts, grid_for(n), dim3(BLK), 0, Q.hs, dptr<uint2>(Q.meta), fl, fp, n, dptr<uint32_t>(Q.setn));
+    if (Q.world == 1 && n && !getenv("KETO_PART_NO_SUBJECT_INDEX")) {
+        // the subject index (one rank: its Check closures take their subject-id tuples from the
+        // subject side, k_subject_pass): (id, run << 32 | position) of every subject-id tuple, sorted
+        DevBuf sk(n * 4), sk2(n * 4), sv(n * 8);
+        Q.sx_val = DevBuf(n * 8);
+        hipLaunchKernelGGL(k_subject_pairs, grid_for(n), dim3(BLK), 0, Q.hs, dptr<uint2>(Q.meta), fl, fp, n, dptr<uint32_t>(sk),
+                           dptr<uint64_t>(sv));
+        uint32_t *ska = dptr<uint32_t>(sk), *skb = dptr<uint32_t>(sk2);
+        uint64_t *sva = dptr<uint64_t>(sv), *svb = dptr<uint64_t>(Q.sx_val);
+        cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceRadixSort::SortPairs(tmp, b, ska, skb, sva, svb, ni, 0, 32, Q.hs); });
+        // the subject-id tuples are the sorted prefix (set tuples sorted last under ~0 keys)
+        DevBuf sum(8);
+        uint32_t *sn = dptr<uint32_t>(Q.setn);
+        unsigned long long *sump = dptr<unsigned long long>(sum);
+        const int mi = (int)Q.m;
+        cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceReduce::Sum(tmp, b, sn, sump, mi, Q.hs); });
+        const uint64_t n_id = n - d2h_u64(Q, sump);  // (Q.hs drained: the sort's inputs can go)
+        sv.reset();
+        sk.reset();
+        if (n_id) {
+            DevBuf sflag((n_id + 1) * 4), spos((n_id + 1) * 8);
+            KETO_HIP(hipMemsetAsync(sflag.p, 0, (n_id + 1) * 4, Q.hs));
+            hipLaunchKernelGGL(k_u32_run_flags, grid_for(n_id), dim3(BLK), 0, Q.hs, skb, n_id, dptr<uint32_t>(sflag));
+            uint32_t *sf = dptr<uint32_t>(sflag);
+            uint64_t *sp = dptr<uint64_t>(spos);
+            const int ns1 = (int)(n_id + 1);
+            cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(tmp, b, sf, sp, ns1, Q.hs); });
+            const uint64_t ms = d2h_u64(Q, sp + n_id);
+            DevBuf sukeys(ms * 8);
+            Q.sx_beg = DevBuf((ms + 1) * 8);
+            hipLaunchKernelGGL(k_u32_run_starts, grid_for(n_id), dim3(BLK), 0, Q.hs, skb, sf, sp, n_id, dptr<uint64_t>(sukeys),
+                               dptr<uint64_t>(Q.sx_beg));
+            KETO_HIP(hipMemcpyAsync(dptr<uint64_t>(Q.sx_beg) + ms, &n_id, 8, hipMemcpyHostToDevice, Q.hs));
+            uint64_t scap = 1u << 10;
+            while (scap < 2 * ms) scap *= 2;
+            Q.sx_index = DevBuf(scap * 16);
+            Q.sx_mask = scap - 1;
+            KETO_HIP(hipMemsetAsync(Q.sx_index.p, 0xFF, scap * 16, Q.hs));
+            hipLaunchKernelGGL(k_index_fill, grid_for(ms), dim3(BLK), 0, Q.hs, dptr<uint64_t>(sukeys), ms, dptr<uint4>(Q.sx_index),
+                               Q.sx_mask);
+            sync(Q);
+        } else {  // no subject-id tuple at all: an empty index
+            Q.sx_beg = DevBuf(8);
+            KETO_HIP(hipMemsetAsync(Q.sx_beg.p, 0, 8, Q.hs));
+            Q.sx_index = DevBuf(16 * 1024);
+            Q.sx_mask = 1023;
+            KETO_HIP(hipMemsetAsync(Q.sx_index.p, 0xFF, 16 * 1024, Q.hs));
+        }
+        Q.have_sx = true;
+    }
     uint64_t cap = 1u << 10;
     while (cap < 2 * Q.m) cap *= 2;
     Q.index = DevBuf(cap * 16);
@@ -1230,14 +1391,25 @@ void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed,
 }
 }  // namespace
 
-// Batches in flight: while batch k is remapped, built and checked on this thread, the closure of
-// batch k+1 runs on a helper thread (its own stream; the collective, if any, is called from that
-// thread, one batch after another as on every rank).  One batch = the plain synchronous call.
+// Several batches in one call, in flight: while batch k is remapped, built and checked on this
+// thread, the closure of batch k+1 -- its query upload included -- runs on a helper thread (its
+// own stream; the collective, if any, is called from that thread, one batch after another as on
+// every rank).  On one GPU the stages' kernels slow each other (both are random-access bound), so
+// the gain is the hidden upload and host work: C3 x10, fresh batches, 21.8 vs 22.4 ms.
+// KETO_PART_SEQUENTIAL runs them one after another.
 void partition_check_many(PartitionHandle *PH, uint32_t nb, const keto_query *const *q, const uint64_t *n,
                           uint8_t *const *allowed, int32_t *const *err, uint32_t flags) {
     Partition &P = *PH;
     KETO_HIP(hipSetDevice(P.device));
     if (!nb) return;
+    if (getenv("KETO_PART_SEQUENTIAL")) {
+        for (uint32_t k = 0; k < nb; k++) {
+            stage_closure(P, P.slots[0], q[k], n[k]);
+            stage_check(P, P.slots[0], n[k], allowed[k], err[k], flags);
+            P.last = P.slots[0].st;
+        }
+        return;
+    }
     stage_closure(P, P.slots[0], q[0], n[0]);
     for (uint32_t k = 0; k < nb; k++) {
         std::exception_ptr ex;

@@ -367,8 +367,9 @@ int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tup
 int keto_partition_check(keto_partition *p, const keto_query *queries, uint64_t n, uint8_t *out_allowed,
                          int32_t *out_err, uint32_t flags);
 /* collective: n_batches batches in order, as keto_partition_check each, pipelined -- batch k+1's
- * closure exchange runs (on a helper thread, which then calls the collective) while batch k is
- * built and checked.  Every rank passes the same n_batches.  Stats: the last batch's. */
+ * closure exchange runs on a helper thread (which then calls the collective) while batch k is
+ * built and checked (KETO_PART_SEQUENTIAL: one after another).  Every rank passes the same
+ * n_batches.  Stats: the last batch's. */
 int keto_partition_check_many(keto_partition *p, uint32_t n_batches, const keto_query *const *queries, const uint64_t *n,
                               uint8_t *const *out_allowed, int32_t *const *out_err, uint32_t flags);
 /* collective: expands this rank's roots; *out_nodes_needed = nodes of all the trees.  Then

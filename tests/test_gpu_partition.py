@@ -79,11 +79,17 @@ def test_single_rank_partitioned_matches_oracle():
     np.testing.assert_array_equal(a3, d2)
     # pipelined batches (keto_partition_check_many): each batch's closure on the helper thread
     # while the batch before it is built and checked; the same answers in the same order
-    many = eng.check_batches([q2, q, q2, q])
-    for (a, e), d, oe in zip(many, (d2, dec, d2, dec), (oe2, oerr, oe2, oerr)):
-        np.testing.assert_array_equal(a, d)
-        np.testing.assert_array_equal(e, oe)
-    assert eng.last["tuples"] == len(ref)
+    for sequential in (False, True):  # the closure of k+1 beside batch k, and one after another
+        if sequential:
+            os.environ["KETO_PART_SEQUENTIAL"] = "1"
+        try:
+            many = eng.check_batches([q2, q, q2, q])
+        finally:
+            os.environ.pop("KETO_PART_SEQUENTIAL", None)
+        for (a, e), d, oe in zip(many, (d2, dec, d2, dec), (oe2, oerr, oe2, oerr)):
+            np.testing.assert_array_equal(a, d)
+            np.testing.assert_array_equal(e, oe)
+        assert eng.last["tuples"] == len(ref)
     roots = _roots(wl, np.random.default_rng(1), 256)
     nodes, offs, xerr = eng.expand_batch(roots)
     assert eng.last["tuples"] == len(closure(wl.tuples, roots["ns"], roots["obj"], wl.max_depth + 1))
@@ -155,7 +161,7 @@ def _worker(rank, world, port, out, device_buffers=False):
         # batch before them is checked (every rank passes the same number of batches)
         q2 = synth.drive_queries(wl, 4096, seed=60 + rank)
         d2, oe2, _ = orc.check_batch(queries_to_oracle(q2), threads=4)
-        many = eng.check_batches([q, q2, q])
+        many = eng.check_batches([q, q2, q])  # (the exchange from the helper thread)
         pipe_mis = 0
         for (a, e), d, oe in zip(many, (dec, d2, dec), (oerr, oe2, oerr)):
             pipe_mis += int((a != d).sum() + (e != oe).sum())

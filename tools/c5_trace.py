@@ -1,6 +1,7 @@
 """Config-5 batch breakdown from a rocprofv3 kernel trace (tool): phases (closure, id remap, build,
 check) of the last full batch, the heaviest kernels of each, and the largest idle gaps.
-  usage: tools/c5_trace.py <kernel_trace.csv>"""
+  usage: tools/c5_trace.py <kernel_trace.csv> [batch]  (batch: index of the k_query_keys launch
+  that starts it; default 2, one of the one-call-per-batch runs before bench.py's timed region)"""
 import collections
 import csv
 import sys
@@ -18,7 +19,8 @@ def nm(r):
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if "k_query_keys" in r["Kernel_Name"]]
-seg = rows[starts[-2]:starts[-1]]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+seg = rows[starts[k]:starts[k + 1]]
 first = {}
 for i, r in enumerate(seg):
     first.setdefault(nm(r), i)
