@@ -1395,7 +1395,7 @@ void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed,
 // thread, the closure of batch k+1 -- its query upload included -- runs on a helper thread (its
 // own stream; the collective, if any, is called from that thread, one batch after another as on
 // every rank).  On one GPU the stages' kernels slow each other (both are random-access bound), so
-// the gain is the hidden upload and host work: C3 x10, fresh batches, 21.8 vs 22.4 ms.
+// the gain is the hidden upload and host work: C3 x10, fresh batches, ~2 % (21.1-21.4 vs 21.5-21.7 ms).
 // KETO_PART_SEQUENTIAL runs them one after another.
 void partition_check_many(PartitionHandle *PH, uint32_t nb, const keto_query *const *q, const uint64_t *n,
                           uint8_t *const *allowed, int32_t *const *err, uint32_t flags) {
