@@ -121,6 +121,10 @@ extern "C" {
 
 int keto_abi_version(void) { return KETO_ABI_VERSION; }
 
+int keto_shutdown(void) {
+    return guarded([&] { keto::pool_shutdown(); });
+}
+
 size_t keto_last_error(char *buf, size_t len) {
     if (buf && len) {
         size_t n = std::min(len - 1, g_err.size());

@@ -46,6 +46,7 @@ struct Snapshot {
     std::vector<std::shared_ptr<void>> owned;  // (parallel to allocs: a patched snapshot shares its base's unchanged arrays)
     keto_snapshot_info info{};
     uint64_t store_id = 0;     // the keto_store it was cut from (0: built directly)
+    uint64_t cfg_hash = 0;     // config_hash of the configuration it was compiled from (patches keep it)
     uint64_t probe_used = 0;   // probe-hash slots holding a key or a tombstone (patches keep the load bounded)
 
     // a device allocation of this snapshot (back to the pool with its last sharer)
@@ -59,6 +60,9 @@ struct Snapshot {
 
 Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
                          bool sched_weights = true);
+// 64-bit FNV-1a of everything a snapshot compiles from its configuration (name tables, AST JSON,
+// uuid space, strict mode; not the device): equal hashes = the same compiled tables
+uint64_t config_hash(const keto_snapshot_config *cfg);
 // snapshot.cpp: a built snapshot to a file and back (keto_snapshot_save / _load)
 void save_snapshot(const Snapshot &s, const char *path);
 Snapshot *load_snapshot(const char *path, int device);
@@ -222,6 +226,7 @@ void *pool_acquire(int device, size_t bytes, size_t *got);
 void pool_release(int device, void *p, size_t bytes);
 void pool_reserve(int device, const std::vector<size_t> &sizes);
 void pool_trim(int device);
+void pool_shutdown();  // keto_shutdown: every device's pool and scratch cache back to the runtime
 // builder temporaries (DevBuf): a per-device cache of freed blocks (scratch.cpp).  A block
 // returned by a thread is fenced by an event on that thread's stream (scratch_stream sets it;
 // returns the previous one), which its next user waits for.

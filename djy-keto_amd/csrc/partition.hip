@@ -1329,6 +1329,7 @@ void stage_closure(Partition &P, Partition::Slot &S, const keto_query *q, uint64
 // decisions out
 void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
     KETO_HIP(hipSetDevice(P.device));
+    ScratchStream on_hs2(P.hs2);  // (the remap's and the decisions' buffers are used on P.hs2)
     keto_partition_stats &st = S.st;
     auto t0 = std::chrono::steady_clock::now();
     keto_query *dq = dptr<keto_query>(S.bq);  // the batch, uploaded by batch_keys

@@ -254,32 +254,42 @@ __global__ __launch_bounds__(BLK) void k_put_edges(DevSnapshot s, uint4 *set_row
     r.w = r.y > r.x + 1 ? set_dst[r.x + 1] : NONE32;
     set_row[key[j]] = r;
 }
-// edges into a node whose set row became empty / non-empty: its parents are the reverse row of
-// the subject set (n_uuids + c); one block per such node
-__global__ __launch_bounds__(BLK) void k_fix_leaf(DevSnapshot s, uint4 *set_row, uint32_t *set_dst, const uint32_t *rev_off,
-                                                  const uint32_t *rev_nodes, const uint32_t *flip, uint32_t m) {
+// Edges into a node whose set row became empty / non-empty: its parents are the reverse row of
+// the subject set (n_uuids + c).  Two launches, one block per such node each:
+//   k_flip_leaf  sets / clears EDGE_LEAF on the set_dst words naming c -- each word names one
+//                child, so the blocks write disjoint words (a row listing c twice: the same
+//                value twice);
+//   k_fix_inline then rewrites the inline copies (set_row .z/.w) of every such parent from the
+//                final set_dst.  Two flipped siblings under one parent both rewrite its row, with
+//                the same words: the launch boundary orders them after every flip.  (One launch
+//                let a block copy a word another block was still changing.)
+__global__ __launch_bounds__(BLK) void k_flip_leaf(DevSnapshot s, const uint4 *set_row, uint32_t *set_dst,
+                                                   const uint32_t *rev_off, const uint32_t *rev_nodes, const uint32_t *flip,
+                                                   uint32_t m) {
     if (blockIdx.x >= m) return;
     const uint32_t c = flip[blockIdx.x];
     const bool leaf = set_row[c].x == set_row[c].y;
     const uint64_t v = (uint64_t)s.n_uuids + c;
     for (uint32_t r = rev_off[v] + threadIdx.x; r < rev_off[v + 1]; r += blockDim.x) {
-        const uint32_t p = rev_nodes[r];
-        uint4 row = set_row[p];
-        bool changed = false;
+        const uint4 row = set_row[rev_nodes[r]];
         for (uint32_t k = row.x; k < row.y; k++) {
             const uint32_t e = set_dst[k];
             if ((e & s.edge_mask) != c) continue;
-            const uint32_t ne = leaf ? (e | EDGE_LEAF) : (e & ~EDGE_LEAF);
-            if (ne != e) {
-                set_dst[k] = ne;
-                changed = true;
-            }
+            set_dst[k] = leaf ? (e | EDGE_LEAF) : (e & ~EDGE_LEAF);
         }
-        if (changed) {  // (one parent row may list c twice: every thread of p writes the same words)
-            row.z = row.y > row.x ? set_dst[row.x] : NONE32;
-            row.w = row.y > row.x + 1 ? set_dst[row.x + 1] : NONE32;
-            set_row[p] = row;
-        }
+    }
+}
+__global__ __launch_bounds__(BLK) void k_fix_inline(DevSnapshot s, uint4 *set_row, const uint32_t *set_dst,
+                                                    const uint32_t *rev_off, const uint32_t *rev_nodes, const uint32_t *flip,
+                                                    uint32_t m) {
+    if (blockIdx.x >= m) return;
+    const uint64_t v = (uint64_t)s.n_uuids + flip[blockIdx.x];
+    for (uint32_t r = rev_off[v] + threadIdx.x; r < rev_off[v + 1]; r += blockDim.x) {
+        const uint32_t p = rev_nodes[r];
+        uint4 row = set_row[p];
+        row.z = row.y > row.x ? set_dst[row.x] : NONE32;
+        row.w = row.y > row.x + 1 ? set_dst[row.x + 1] : NONE32;
+        set_row[p] = row;
     }
 }
 // does any node of a slot still hold a subject-set row: job {slot, first node, nodes, stride};
@@ -567,6 +577,7 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     s.info = B.info;
     s.info.device_bytes = 0;
     s.store_id = B.store_id;
+    s.cfg_hash = B.cfg_hash;
     s.probe_used = B.probe_used + ins_keys.size();
     DevSnapshot &X = s.dev;
     X = D;
@@ -649,7 +660,9 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
         if ((set_len[j] == 0) != (old_n[j].w == old_n[j].z)) flip.push_back(key_n[j]);
     if (D.edge_leaf && !flip.empty()) {
         DevBuf d_flip = up(flip);
-        hipLaunchKernelGGL(k_fix_leaf, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, X, set_row, set_dst, rev_off, rev_nodes,
+        hipLaunchKernelGGL(k_flip_leaf, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, X, set_row, set_dst, rev_off, rev_nodes,
+                           d_flip.u32(), (uint32_t)flip.size());
+        hipLaunchKernelGGL(k_fix_inline, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, X, set_row, set_dst, rev_off, rev_nodes,
                            d_flip.u32(), (uint32_t)flip.size());
         KETO_HIP(hipGetLastError());
     }

@@ -79,9 +79,12 @@ struct DevicePool {
     std::vector<PoolBlock> free;
     size_t held = 0, cap = 0;
 };
-DevicePool &pool(int device) {
+DevicePool &pool_slot(int device) {
     static DevicePool pools[64];
-    DevicePool &P = pools[std::clamp(device, 0, 63)];
+    return pools[std::clamp(device, 0, 63)];
+}
+DevicePool &pool(int device) {
+    DevicePool &P = pool_slot(device);
     if (!P.cap) {  // (KETO_POOL_CAP_MB: processes that share one device, e.g. test ranks, each hold less)
         size_t fr = 0, total = 0;
         const char *e = getenv("KETO_POOL_CAP_MB");
@@ -146,9 +149,12 @@ struct ScratchCache {
     size_t held = 0, cap = 0;
 };
 thread_local hipStream_t tl_stream = nullptr;
-ScratchCache &scache(int device) {
+ScratchCache &scache_slot(int device) {
     static ScratchCache caches[64];
-    ScratchCache &C = caches[std::clamp(device, 0, 63)];
+    return caches[std::clamp(device, 0, 63)];
+}
+ScratchCache &scache(int device) {
+    ScratchCache &C = scache_slot(device);
     if (!C.cap) {
         size_t fr = 0, total = 0;
         const char *e = getenv("KETO_SCRATCH_CAP_MB");
@@ -244,6 +250,23 @@ void pool_trim(int device) {
     for (auto &b : P.free) (void)hipFree(b.p);
     P.free.clear();
     P.held = 0;
+}
+
+// keto_shutdown: every cached block and spare event of every device this process touched goes
+// back to the runtime now, while it is certainly alive -- not left to the HIP runtime's own
+// teardown in exit(), which runs after the interpreter (and under rocprofv3 after its tool)
+// has begun to unwind.  The caches stay usable: a later call simply allocates again.
+void pool_shutdown() {
+    for (int d = 0; d < 64; d++) {
+        DevicePool &P = pool_slot(d);
+        ScratchCache &C = scache_slot(d);
+        if (!P.cap && !C.cap) continue;  // never used on this device
+        if (hipSetDevice(d) != hipSuccess) continue;
+        pool_trim(d);
+        std::lock_guard<std::mutex> g(C.mu);
+        for (hipEvent_t e : C.events) (void)hipEventDestroy(e);
+        C.events.clear();
+    }
 }
 
 void pool_release(int device, void *p, size_t bytes) {

@@ -144,6 +144,30 @@ uint32_t Snapshot::ns_of(uint32_t node) const {
     return lo;
 }
 
+uint64_t config_hash(const keto_snapshot_config *cfg) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    auto bytes = [&](const void *p, size_t n) {
+        for (size_t i = 0; i < n; i++) {
+            h ^= static_cast<const uint8_t *>(p)[i];
+            h *= 0x100000001b3ull;
+        }
+    };
+    auto str = [&](const char *s) {  // (length-prefixed: name boundaries matter)
+        const uint64_t n = s ? std::strlen(s) : 0;
+        bytes(&n, 8);
+        if (n) bytes(s, n);
+    };
+    bytes(&cfg->n_namespaces, 4);
+    for (uint32_t i = 0; i < cfg->n_namespaces; i++) str(cfg->namespace_names ? cfg->namespace_names[i] : nullptr);
+    bytes(&cfg->n_relations, 4);
+    for (uint32_t i = 0; i < cfg->n_relations; i++) str(cfg->relation_names ? cfg->relation_names[i] : nullptr);
+    bytes(&cfg->n_uuids, 4);
+    str(cfg->namespaces_json);
+    const int32_t strict = cfg->strict_mode != 0;
+    bytes(&strict, 4);
+    return h;
+}
+
 Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
                          bool sched_weights) {
     auto t0 = std::chrono::steady_clock::now();
@@ -161,6 +185,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     s.n_uuids = cfg->n_uuids;
     s.strict = cfg->strict_mode != 0;
     s.n_rel_caller = cfg->n_relations;
+    s.cfg_hash = config_hash(cfg);
     Compiler C{s, {}};
     for (uint32_t i = 0; i < s.n_ns; i++) s.ns_names.emplace_back(cfg->namespace_names && cfg->namespace_names[i] ? cfg->namespace_names[i] : "");
     for (uint32_t i = 0; i < cfg->n_relations; i++) {
@@ -732,7 +757,10 @@ Snapshot *load_snapshot(const char *path, int device) {
     try {
         for (size_t i = 0; i < bytes.size(); i++) {
             void *p = nullptr;
-            KETO_HIP(hipMalloc(&p, std::max<size_t>(16, bytes[i])));
+            // 16 zeroed bytes past the array, as DevBuf and the pool give a built snapshot: the
+            // kernels' 16-byte window loads may read past an array's last element
+            KETO_HIP(hipMalloc(&p, bytes[i] + 16));
+            KETO_HIP(hipMemset(static_cast<char *>(p) + bytes[i], 0, 16));
             const uint64_t keep = s.info.device_bytes;
             s.own(p, bytes[i]);
             s.info.device_bytes = keep;  // (the file's info already counts every array)

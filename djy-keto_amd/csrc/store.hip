@@ -150,58 +150,64 @@ void store_transact(TupleStore &st, const keto_tuple *ins, uint64_t n_ins, const
                     bool device_ptrs) {
     KETO_HIP(hipSetDevice(st.device));
     const hipMemcpyKind kind = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    {   // the change log entry of this version (a transaction larger than the log holds none: a
-        // snapshot across it is a full build)
-        TupleStore::Change c{st.version + 1, n_ins, n_del, build::DevBuf(sizeof(keto_tuple) * std::max<uint64_t>(1, n_ins + n_del))};
-        if (n_ins) KETO_HIP(hipMemcpy(c.rows.p, ins, n_ins * sizeof(keto_tuple), kind));
-        if (n_del) KETO_HIP(hipMemcpy(static_cast<keto_tuple *>(c.rows.p) + n_ins, del, n_del * sizeof(keto_tuple), kind));
-        st.log_rows += n_ins + n_del;
-        st.log.push_back(std::move(c));
-        while (!st.log.empty() && st.log_rows > TupleStore::LOG_MAX_ROWS) {
-            st.log_rows -= st.log.front().n_ins + st.log.front().n_del;
-            st.log.pop_front();
-        }
-    }
+    // the change log entry of this version, logged only once the transaction has been applied
+    // (next to version++): a transaction that throws part-way leaves neither an entry nor a new
+    // version.  (A transaction larger than the log holds none: a snapshot across it is a full build.)
+    TupleStore::Change c{st.version + 1, n_ins, n_del, build::DevBuf(sizeof(keto_tuple) * std::max<uint64_t>(1, n_ins + n_del))};
+    if (n_ins) KETO_HIP(hipMemcpy(c.rows.p, ins, n_ins * sizeof(keto_tuple), kind));
+    if (n_del) KETO_HIP(hipMemcpy(static_cast<keto_tuple *>(c.rows.p) + n_ins, del, n_del * sizeof(keto_tuple), kind));
+    const uint64_t n_before = st.n;
     if (n_ins) {  // WriteRelationTuples: appended rows, fresh shard_ids from the caller
         st.reserve(st.n + n_ins);
         KETO_HIP(hipMemcpy(st.rows() + st.n, ins, n_ins * sizeof(keto_tuple), kind));
-        st.n += n_ins;
     }
-    if (n_del && st.n) {  // DeleteRelationTuples over everything, the new rows included
+    // (the appended rows count only once the deletes below went through: st.n stays n_before
+    // until the end, so a throw leaves the store's content as it was)
+    const uint64_t n_all = n_before + n_ins;
+    uint64_t n_after = n_all;
+    if (n_del && n_all) {  // DeleteRelationTuples over everything, the new rows included
         build::DevBuf d(n_del * sizeof(keto_tuple));
         KETO_HIP(hipMemcpy(d.p, del, n_del * sizeof(keto_tuple), kind));
         uint64_t size = 64;
         while (size < 2 * n_del) size <<= 1;
-        build::DevBuf slots(size * 4), dead(st.n), cnt(3 * sizeof(unsigned long long));
+        build::DevBuf slots(size * 4), dead(n_all), cnt(3 * sizeof(unsigned long long));
         KETO_HIP(hipMemset(slots.p, 0, size * 4));
         KETO_HIP(hipMemset(cnt.p, 0, 3 * sizeof(unsigned long long)));
-        auto *c = static_cast<unsigned long long *>(cnt.p);
+        auto *cn = static_cast<unsigned long long *>(cnt.p);
         hipLaunchKernelGGL(k_del_insert, grid_for(n_del), dim3(BLK), 0, 0, static_cast<const keto_tuple *>(d.p), n_del,
                            slots.u32(), size - 1);
         KETO_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_mark, grid_for(st.n), dim3(BLK), 0, 0, st.rows(), st.n,
+        hipLaunchKernelGGL(k_mark, grid_for(n_all), dim3(BLK), 0, 0, st.rows(), n_all,
                            static_cast<const keto_tuple *>(d.p), slots.u32(), size - 1,
-                           static_cast<uint8_t *>(dead.p), c + 2);
+                           static_cast<uint8_t *>(dead.p), cn + 2);
         KETO_HIP(hipGetLastError());
         unsigned long long n_dead = 0;
-        KETO_HIP(hipMemcpy(&n_dead, c + 2, sizeof(n_dead), hipMemcpyDeviceToHost));
+        KETO_HIP(hipMemcpy(&n_dead, cn + 2, sizeof(n_dead), hipMemcpyDeviceToHost));
         if (n_dead) {
-            const uint64_t keep = st.n - n_dead;
+            const uint64_t keep = n_all - n_dead;
             build::DevBuf holes(n_dead * 8), movers(n_dead * 8);
-            hipLaunchKernelGGL(k_holes_movers, grid_for(st.n), dim3(BLK), 0, 0, static_cast<const uint8_t *>(dead.p),
-                               st.n, keep, static_cast<uint64_t *>(holes.p), static_cast<uint64_t *>(movers.p), c);
+            hipLaunchKernelGGL(k_holes_movers, grid_for(n_all), dim3(BLK), 0, 0, static_cast<const uint8_t *>(dead.p),
+                               n_all, keep, static_cast<uint64_t *>(holes.p), static_cast<uint64_t *>(movers.p), cn);
             KETO_HIP(hipGetLastError());
             unsigned long long m[2] = {0, 0};
-            KETO_HIP(hipMemcpy(m, c, sizeof(m), hipMemcpyDeviceToHost));
+            KETO_HIP(hipMemcpy(m, cn, sizeof(m), hipMemcpyDeviceToHost));
             if (m[0] != m[1]) throw Error(KETO_E_DEVICE, "compaction lists disagree");
             hipLaunchKernelGGL(k_move, grid_for(m[0]), dim3(BLK), 0, 0, st.rows(),
                                static_cast<const uint64_t *>(holes.p), static_cast<const uint64_t *>(movers.p), m[0]);
             KETO_HIP(hipGetLastError());
-            st.n = keep;
+            n_after = keep;
         }
     }
     KETO_HIP(hipDeviceSynchronize());
+    // applied: the new content, its version and its log entry together
+    st.n = n_after;
     st.version++;
+    st.log_rows += n_ins + n_del;
+    st.log.push_back(std::move(c));
+    while (!st.log.empty() && st.log_rows > TupleStore::LOG_MAX_ROWS) {
+        st.log_rows -= st.log.front().n_ins + st.log.front().n_del;
+        st.log.pop_front();
+    }
 }
 
 void store_free(TupleStore *st) { delete st; }
@@ -234,12 +240,16 @@ Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg) 
 
 Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const keto_snapshot_config *cfg, bool *patched) {
     if (!cfg || cfg->device != st.device) throw Error(KETO_E_INVALID, "config names another device");
-    if (base.store_id == st.id && base.device == st.device && base.info.version <= st.version) {
-        // the log must hold every version after the base's
+    // a patch reuses base's compiled namespaces, name tables and id space: only for the same
+    // configuration (a namespace reload, renamed relations or a larger uuid space build in full)
+    if (base.store_id == st.id && base.device == st.device && base.info.version <= st.version &&
+        base.cfg_hash == config_hash(cfg)) {
+        // the log must hold every version after the base's, each once, in order (the gather
+        // below takes exactly the entries this loop counts)
         uint64_t want = base.info.version + 1, n_rows = 0;
         bool covered = true;
         for (const auto &c : st.log)
-            if (c.version >= want) {
+            if (c.version > base.info.version) {
                 if (c.version != want) covered = false;
                 want++;
                 n_rows += c.n_ins + c.n_del;

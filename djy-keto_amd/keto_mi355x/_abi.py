@@ -1,8 +1,10 @@
 """ctypes declarations of include/keto_mi355x.h (the C ABI of libketo_mi355x.so)."""
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -85,7 +87,7 @@ class PartitionStats(ctypes.Structure):
 
 
 # keto_collective callbacks
-ABI_VERSION = 3  # include/keto_mi355x.h KETO_ABI_VERSION
+ABI_VERSION = 4  # include/keto_mi355x.h KETO_ABI_VERSION
 
 ALLTOALL_U64_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                    ctypes.POINTER(ctypes.c_uint64))
@@ -106,6 +108,7 @@ class NameTables(ctypes.Structure):
 _VP, _U32, _I32, _U64, _SZ = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
 SIGNATURES = {
     "keto_abi_version": (ctypes.c_int, []),
+    "keto_shutdown": (ctypes.c_int, []),
     "keto_last_error": (_SZ, [ctypes.c_char_p, _SZ]),
     "keto_snapshot_build": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, ctypes.POINTER(_VP)]),
     "keto_snapshot_build_device": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, ctypes.POINTER(_VP)]),
@@ -180,7 +183,39 @@ def lib():
         if L.keto_abi_version() != ABI_VERSION:
             raise RuntimeError("libketo_mi355x ABI version mismatch")
         _lib = L
+        atexit.register(_shutdown)
     return _lib
+
+
+# Objects owning library handles (streams, snapshots, ...).  At interpreter exit they are closed
+# -- dispatchers before the snapshots they serve, streams before snapshots -- and keto_shutdown
+# hands the library's cached device blocks and events back, all while the HIP runtime is still
+# fully alive: nothing of the library is left to the runtime's own teardown inside exit().
+_live = weakref.WeakSet()
+_CLOSE_ORDER = ("Dispatcher", "PartitionedEngine", "Stream", "Snapshot", "TupleStore", "DeviceBuffer", "PinnedArray")
+
+
+def track(obj):
+    _live.add(obj)
+    return obj
+
+
+def _close_rank(obj) -> int:
+    name = type(obj).__name__
+    return _CLOSE_ORDER.index(name) if name in _CLOSE_ORDER else len(_CLOSE_ORDER)
+
+
+def _shutdown():
+    if _lib is None:
+        return
+    for obj in sorted(list(_live), key=_close_rank):
+        fn = getattr(obj, "close", None) or getattr(obj, "free", None)
+        try:
+            if fn is not None:
+                fn()
+        except Exception:  # (exit path: keep closing the rest)
+            pass
+    _lib.keto_shutdown()
 
 
 def last_error() -> str:

@@ -91,6 +91,7 @@ class Snapshot:
         self.handle = h
         self.device = device
         self.ns_names, self.rel_names = list(ns_names), list(rel_names)
+        _abi.track(self)
 
     def info(self) -> dict:
         inf = _abi.SnapshotInfo()
@@ -109,6 +110,7 @@ class Snapshot:
         check(lib().keto_snapshot_load(str(path).encode(), device, ctypes.byref(h)))
         self.handle, self.device = h, device
         self.ns_names, self.rel_names = list(ns_names), list(rel_names)
+        _abi.track(self)
         return self
 
     def close(self):
@@ -129,6 +131,7 @@ class TupleStore:
         h = ctypes.c_void_p()
         check(lib().keto_store_create(device, t.ctypes.data if len(t) else None, len(t), 0, ctypes.byref(h)))
         self.handle, self.device = h, device
+        _abi.track(self)
 
     def transact(self, insert: np.ndarray | None = None, delete: np.ndarray | None = None):
         ins = np.ascontiguousarray(insert if insert is not None else np.zeros(0, _abi.TUPLE_DT), dtype=_abi.TUPLE_DT)
@@ -156,6 +159,7 @@ class Stream:
         check(lib().keto_stream_create(device, ctypes.byref(h)))
         self.handle = h
         self.device = device
+        _abi.track(self)
 
     def sync(self):
         check(lib().keto_stream_sync(self.handle))
@@ -208,6 +212,7 @@ class DeviceBuffer:
         p = ctypes.c_void_p()
         check(lib().keto_device_alloc(device, max(1, nbytes), ctypes.byref(p)))
         self.ptr, self.nbytes = p, nbytes
+        _abi.track(self)
 
     def upload(self, stream: Stream, arr: np.ndarray):
         arr = np.ascontiguousarray(arr)
@@ -239,6 +244,7 @@ class PinnedArray:
         self.ptr = p
         buf = (ctypes.c_uint8 * self.nbytes).from_address(p.value)
         self.array = np.frombuffer(buf, dtype=np.uint8, count=n * dtype.itemsize).view(dtype)
+        _abi.track(self)
 
     def free(self):
         if self.ptr:
@@ -365,6 +371,7 @@ class Dispatcher:
         check(lib().keto_dispatcher_create(snapshot.handle, ctypes.byref(cfg), ctypes.byref(h)))
         self.handle = h
         self.snapshot = snapshot
+        _abi.track(self)
 
     def check(self, queries: np.ndarray):
         q = np.ascontiguousarray(queries, dtype=_abi.QUERY_DT)

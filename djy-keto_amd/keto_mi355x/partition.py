@@ -129,6 +129,7 @@ class PartitionedEngine:
                                               ctypes.byref(h)))
         self.handle = h
         self.last = {}
+        _abi.track(self)
 
     def levels(self) -> int:
         return self.max_read_depth + 1

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 3
+#define KETO_ABI_VERSION 4
 
 /* status codes */
 #define KETO_OK 0
@@ -155,6 +155,13 @@ typedef struct keto_stream keto_stream;
 int keto_abi_version(void);
 /* copies the thread's last error message; returns its full length */
 size_t keto_last_error(char *buf, size_t len);
+/* Returns every device block and event the library caches between calls (its snapshot-array
+ * pool and builder scratch cache, on every device it used) to the HIP runtime.  Call it at
+ * process exit after freeing the library's objects, before the runtime's own teardown (a Go
+ * host: after the last keto_*_free, e.g. from the server's shutdown hook; the Python mirror
+ * registers it with atexit).  The library stays usable afterwards: the caches refill on
+ * demand.  No reference counterpart. */
+int keto_shutdown(void);
 
 int keto_snapshot_build(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n_tuples,
                         keto_snapshot **out);

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     lib = km.lib()
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.keto_abi_version() == 3
+    assert lib.keto_abi_version() == 4
 
 
 def test_record_layouts_match_header():
@@ -62,3 +62,33 @@ def test_no_cpu_fallback_without_gpu():
     t = np.zeros(1, dtype=km.TUPLE_DT)
     with pytest.raises(km.KetoError):
         km.Snapshot(cfg, t, ["g"], ["m"], 2)
+
+
+def test_exit_teardown_order():
+    """At interpreter exit (_abi._shutdown, registered with atexit when the library loads) the
+    live handle owners are closed dispatchers first, then partitions, streams, snapshots, stores
+    and raw buffers, and keto_shutdown returns the library's cached device blocks -- while the
+    HIP runtime is still alive (the round-3 exit SIGSEGV)."""
+    km.lib()
+    closed = []
+    objs = []
+    for name in ("PinnedArray", "Snapshot", "Dispatcher", "TupleStore", "Stream", "PartitionedEngine",
+                 "DeviceBuffer"):
+        meth = "free" if name in ("PinnedArray", "DeviceBuffer") else "close"
+        cls = type(name, (), {meth: (lambda self, n=name: closed.append(n))})
+        objs.append(_abi.track(cls()))
+    _abi._shutdown()
+    assert closed == ["Dispatcher", "PartitionedEngine", "Stream", "Snapshot", "TupleStore", "DeviceBuffer",
+                      "PinnedArray"]
+    assert km.lib().keto_shutdown() == 0  # idempotent, and harmless without a device
+
+
+def test_process_exit_is_clean():
+    """a process that loaded the library exits 0 through the atexit path"""
+    import subprocess
+    import sys
+    code = "import keto_mi355x as km; km.lib(); print('ok')"
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "djy-keto_amd"),
+                                                       os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr

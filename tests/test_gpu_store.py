@@ -238,3 +238,90 @@ def test_patch_falls_back_when_base_has_no_node():
     assert not o2.patched
     st.close()
     other.close()
+
+
+def _first_edges(rows):
+    """a row's tuples in shard order (traverser.go:88)"""
+    key = [bytes(r) for r in rows["shard_id"]]
+    return rows[np.argsort(np.array(key, dtype=object), kind="stable")]
+
+
+def test_patch_two_sibling_leaf_flips_under_one_parent():
+    """one transaction gives two leaf child groups -- the first two edges of an
+    untouched parent's row, i.e. both of its inline edge copies -- their first nested group.
+    Both flips rewrite the parent's inline words; the patched snapshot must still equal the full
+    build (EDGE_LEAF read through set_row .z/.w for rows of <= 2 edges) and the oracle"""
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=8)
+    t = wl.tuples
+    g_ns, mem = wl.ns_names.index("Group"), wl.rel_names.index("members")
+    nested = t[(t["ns"] == g_ns) & (t["rel"] == mem) & (t["subj_kind"] == 1)]
+    has_rows = set(nested["obj"].tolist())
+    parent, kids = None, None
+    for p in np.unique(nested["obj"]):
+        row = _first_edges(nested[nested["obj"] == p])
+        if len(row) >= 2 and row["s_obj"][0] not in has_rows and row["s_obj"][1] not in has_rows \
+                and row["s_obj"][0] != row["s_obj"][1]:
+            parent, kids = int(p), [int(row["s_obj"][0]), int(row["s_obj"][1])]
+            break
+    assert parent is not None, "no parent with two leaf children first in shard order"
+    st = km.TupleStore(t)
+    host = t.copy()
+    base = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    donor = int(nested["obj"][0])  # a group that has members of its own
+    ins = np.zeros(2, dtype=t.dtype)
+    ins["ns"], ins["obj"], ins["rel"] = g_ns, kids, mem
+    ins["subj_kind"], ins["s_ns"], ins["s_obj"], ins["s_rel"] = 1, g_ns, donor, mem
+    ins["shard_id"] = np.random.default_rng(1).integers(0, 256, (2, 16), dtype=np.uint8)
+    st.transact(ins, None)
+    host = transact(host, ins, ins[:0])
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=base)
+    assert snap.patched
+    full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    rng = np.random.default_rng(5)
+    q = synth.drive_queries(wl, 4096, seed=3)
+    # the parent's membership of every member of the donor group: through a flipped child only
+    members = t[(t["ns"] == g_ns) & (t["obj"] == donor) & (t["rel"] == mem) & (t["subj_kind"] == 0)]
+    k = min(len(members), 256)
+    q["ns"][:k], q["obj"][:k], q["rel"][:k] = g_ns, parent, mem
+    q["subj_kind"][:k], q["s_obj"][:k], q["s_ns"][:k], q["s_rel"][:k] = 0, members["s_obj"][:k], 0, 0
+    q["max_depth"][:k] = 0
+    roots = _roots(wl, rng, 64)
+    roots["ns"][0], roots["obj"][0], roots["rel"][0] = g_ns, parent, mem
+    allowed = _compare(wl, snap, full, q, roots)
+    assert allowed[:k].any()
+    w, _ = world_from_workload(wl)
+    orc = refsem.Oracle(w, host.view(refsem.TUPLE_DT).copy(), shard_bytes=True)
+    orc.set_limits(wl.max_depth, wl.max_width)
+    dec, _, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+    np.testing.assert_array_equal(allowed, dec)
+    st.close()
+
+
+def test_patch_with_changed_namespace_config_builds_in_full():
+    """a patch reuses its base's compiled rewrites only for the same configuration.
+    After a namespace reload (here: File/Folder `view` becomes `!banned` alone) the call builds in full
+    (patched = False) and answers with the new rewrites; with the new configuration on both sides
+    the next patch runs again"""
+    import copy
+    wl = synth.drive(depth=4, n_groups=300, n_users=1000, seed=5)
+    st = km.TupleStore(wl.tuples)
+    base = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    ns2 = copy.deepcopy(wl.namespaces)
+    for name in ("File", "Folder"):
+        for r in ns2[name]:
+            if r["name"] == "view" and r["rewrite"]["operator"] == "and":  # (File and Folder share one list)
+                r["rewrite"] = {"operator": "or", "children": [r["rewrite"]["children"][1]]}  # {!banned}
+    ins = wl.tuples[:1].copy()
+    ins["shard_id"][:, 0] ^= 0x5A
+    st.transact(ins, None)
+    nxt = km.Snapshot(ns2, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=base)
+    assert not nxt.patched
+    full = km.Snapshot(ns2, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    q = synth.drive_queries(wl, 4096, seed=2)
+    a_new = _compare(wl, nxt, full, q, _roots(wl, np.random.default_rng(0), 64))
+    a_old, _ = km.CheckEngine(base, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    assert (a_new != a_old).any()  # non-viewers are allowed now: the old rewrites were not kept
+    st.transact(ins, None)
+    again = km.Snapshot(ns2, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=nxt)
+    assert again.patched
+    st.close()
