@@ -1329,11 +1329,13 @@ void stage_closure(Partition &P, Partition::Slot &S, const keto_query *q, uint64
 // decisions out
 void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
     KETO_HIP(hipSetDevice(P.device));
-    ScratchStream on_hs2(P.hs2);  // (the remap's and the decisions' buffers are used on P.hs2)
     keto_partition_stats &st = S.st;
     auto t0 = std::chrono::steady_clock::now();
     keto_query *dq = dptr<keto_query>(S.bq);  // the batch, uploaded by batch_keys
-    remap_ids(P, dptr<keto_tuple>(S.closure), S.nt, dq, nullptr, n, P.hs2, P.scratch2);
+    {
+        ScratchStream on_hs2(P.hs2);  // (the remap's buffers are used on P.hs2; the build below runs on the null stream)
+        remap_ids(P, dptr<keto_tuple>(S.closure), S.nt, dq, nullptr, n, P.hs2, P.scratch2);
+    }
     std::unique_ptr<Snapshot> snap(closure_snapshot(P, dptr<keto_tuple>(S.closure), S.nt));
     st.build_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
