@@ -496,18 +496,18 @@ void *DevBuf::release() {
     return q;
 }
 
-void scan_excl(uint32_t *v, uint64_t n) {
+void scan_excl(uint32_t *v, uint64_t n, hipStream_t s) {
     const uint64_t nt = std::max<uint64_t>(1, (n + SCAN_TILE - 1) / SCAN_TILE);
     if (nt == 1) {
-        hipLaunchKernelGGL(k_tile_apply, dim3(1), dim3(BLK), 0, 0, v, n, nullptr, 1);
+        hipLaunchKernelGGL(k_tile_apply, dim3(1), dim3(BLK), 0, s, v, n, nullptr, 1);
         KETO_HIP(hipGetLastError());
         return;
     }
     DevBuf sums(4 * (nt + 1));
-    hipLaunchKernelGGL(k_tile_sum, dim3((uint32_t)nt), dim3(BLK), 0, 0, v, n, sums.u32(), nt);
+    hipLaunchKernelGGL(k_tile_sum, dim3((uint32_t)nt), dim3(BLK), 0, s, v, n, sums.u32(), nt);
     KETO_HIP(hipGetLastError());
-    scan_excl(sums.u32(), nt);
-    hipLaunchKernelGGL(k_tile_apply, dim3((uint32_t)nt), dim3(BLK), 0, 0, v, n, sums.u32(), nt);
+    scan_excl(sums.u32(), nt, s);
+    hipLaunchKernelGGL(k_tile_apply, dim3((uint32_t)nt), dim3(BLK), 0, s, v, n, sums.u32(), nt);
     KETO_HIP(hipGetLastError());
 }
 

@@ -537,6 +537,11 @@ int keto_partition_stats_get(keto_partition *p, keto_partition_stats *out) {
     return KETO_OK;
 }
 
+int keto_partition_levels_get(keto_partition *p, keto_partition_level *out, uint32_t cap, uint32_t *n) {
+    if (!p || !n || (cap && !out)) return fail(KETO_E_INVALID, "null argument");
+    return guarded([&] { keto::partition_levels(reinterpret_cast<keto::PartitionHandle *>(p), out, cap, n); });
+}
+
 int keto_partition_free(keto_partition *p) {
     return guarded([&] { keto::partition_free(reinterpret_cast<keto::PartitionHandle *>(p)); });
 }

@@ -84,7 +84,9 @@ struct DevBuf {
     void *release();
     uint32_t *u32() const { return static_cast<uint32_t *>(p); }
 };
-void scan_excl(uint32_t *v, uint64_t n);  // v[0..n) -> exclusive prefix sums, v[n] = total
+// v[0..n) -> exclusive prefix sums, v[n] = total, on stream s (temporaries fenced by the calling
+// thread's ScratchStream)
+void scan_excl(uint32_t *v, uint64_t n, hipStream_t s = nullptr);
 uint32_t read_u32(const uint32_t *d, uint64_t i);
 void validate(const keto_tuple *t, uint64_t n, uint32_t n_ns, uint32_t n_rel_caller, uint32_t n_uuids, uint32_t n_rel,
               uint32_t *used, unsigned long long *bad);
@@ -320,6 +322,20 @@ Snapshot *patch_snapshot(const Snapshot &base, const keto_tuple *store_rows, uin
 void store_free(TupleStore *st);
 void store_info(const TupleStore &st, uint64_t *n, uint64_t *version);
 
+// devprim.hip: stream-ordered primitives of the partition path (hand-written gfx950 kernels)
+namespace prim {
+// stable LSD radix sort of n pairs on the low `bits` bits of the keys, ping-ponging between
+// (k0, v0) and (k1, v1); true when the result ends in (k1, v1)
+bool sort_pairs(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t bits, hipStream_t s);
+bool sort_pairs(uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, uint64_t n, uint32_t bits, hipStream_t s);
+// the distinct values of sorted a[0..n) into out; returns their count (synchronises s)
+uint64_t unique_sorted(const uint32_t *a, uint64_t n, uint32_t *out, hipStream_t s);
+// flag[i] = a[i] != a[i-1] (flag[0] = 1), flag[n] = 0: n + 1 slots, ready for build::scan_excl
+void run_flags(const uint64_t *a, uint64_t n, uint32_t *flag, hipStream_t s);
+void run_flags(const uint32_t *a, uint64_t n, uint32_t *flag, hipStream_t s);
+void sum_u32(const uint32_t *v, uint64_t n, unsigned long long *out, hipStream_t s);  // *out = sum (device)
+}  // namespace prim
+
 // partition.hip: graphs partitioned by object over the ranks of a job (keto_partition_*)
 struct PartitionHandle;
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
@@ -330,6 +346,7 @@ void partition_check_many(PartitionHandle *p, uint32_t nb, const keto_query *con
 uint64_t partition_expand(PartitionHandle *p, const keto_subject_set *roots, uint64_t n);
 void partition_expand_result(PartitionHandle *p, keto_tree_node *nodes, uint64_t cap, uint64_t *offsets, int32_t *err);
 void partition_stats(PartitionHandle *p, keto_partition_stats *out);
+void partition_levels(PartitionHandle *p, keto_partition_level *out, uint32_t cap, uint32_t *n);
 void partition_free(PartitionHandle *p);
 
 }  // namespace keto

@@ -25,6 +25,9 @@
 //  2. the closure (in shard order after the build's own sort) becomes an ordinary device
 //     snapshot (build_snapshot, the replicated path's builder);
 //  3. the unmodified Check / Expand kernels run on it.
+// A job of one rank holds the whole graph: its partition is built once, at creation, into a
+// resident snapshot (the replicated path's), and every batch runs on it directly -- no closure,
+// no per-batch build (KETO_PART_CLOSURE=1 keeps the closure path, for tests of it on one GPU).
 // The closure holds every row the reference engine could read for these queries, so the
 // kernels take exactly the decisions (and build exactly the trees) they would on the whole
 // graph; exactness needs no distributed version of the sequential walk.
@@ -32,8 +35,6 @@
 // The collective is the caller's (keto_collective): a Go host passes its RCCL communicator's
 // all-to-all, the tests pass gloo.  coll == NULL runs one rank with no exchange.
 #include <hip/hip_runtime.h>
-
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -111,8 +112,7 @@ __device__ __forceinline__ void block_append(const T (&v)[TILE_K], uint32_t mask
          t0 += (uint64_t)gridDim.x * blockDim.x * TILE_K)
 inline dim3 grid_tiles(uint64_t n) { return grid_for((n + TILE_K - 1) / TILE_K); }
 
-// sort key of a store tuple: its object key, then subject sets before subject ids (a run's
-// subject-set tuples are its first setn[run] entries)
+// sort key of a store tuple: its object key, then subject sets before subject ids
 __global__ __launch_bounds__(BLK) void k_tuple_keys(const keto_tuple *t, uint64_t n, uint64_t *keys, uint32_t *idx) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
         keys[i] = (okey(t[i].ns, t[i].obj) << 1) | (t[i].subj_kind == 1 ? 0u : 1u);
@@ -154,38 +154,11 @@ __global__ __launch_bounds__(BLK) void k_run_flags(const uint64_t *k, uint64_t n
     for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || (k[i] >> 1) != (k[i - 1] >> 1)) ? 1u : 0u;
 }
 // compacted runs: run r starts at the i with flag[i] and exclusive-scan pos[i] == r
-__global__ __launch_bounds__(BLK) void k_run_starts(const uint64_t *k, const uint32_t *flag, const uint64_t *pos,
+__global__ __launch_bounds__(BLK) void k_run_starts(const uint64_t *k, const uint32_t *flag, const uint32_t *pos,
                                                      uint64_t n, uint64_t *ukeys, uint64_t *beg) {
     for (uint64_t i = gid(); i < n; i += gstride())
         if (flag[i]) {
             ukeys[pos[i]] = k[i] >> 1;
-            beg[pos[i]] = i;
-        }
-}
-// subject-set tuples per run (they lead it): run r = inclusive scan of the run flags - 1
-__global__ __launch_bounds__(BLK) void k_set_counts(const uint2 *meta, const uint32_t *flag, const uint64_t *pos, uint64_t n,
-                                                    uint32_t *setn) {
-    for (uint64_t i = gid(); i < n; i += gstride())
-        if (meta[i].y >> 31) atomicAdd(&setn[pos[i] + flag[i] - 1], 1u);
-}
-// the subject index's input: (subject id, run << 32 | position) of every subject-id tuple, and
-// ~0 keys (sorted past the end) for subject-set tuples
-__global__ __launch_bounds__(BLK) void k_subject_pairs(const uint2 *meta, const uint32_t *flag, const uint64_t *pos, uint64_t n,
-                                                       uint32_t *skey, uint64_t *sval) {
-    for (uint64_t i = gid(); i < n; i += gstride()) {
-        const uint2 m = meta[i];
-        skey[i] = (m.y >> 31) ? 0xFFFFFFFFu : m.x;
-        sval[i] = ((pos[i] + flag[i] - 1) << 32) | i;
-    }
-}
-__global__ __launch_bounds__(BLK) void k_u32_run_flags(const uint32_t *k, uint64_t n, uint32_t *flag) {
-    for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
-}
-__global__ __launch_bounds__(BLK) void k_u32_run_starts(const uint32_t *k, const uint32_t *flag, const uint64_t *pos, uint64_t n,
-                                                        uint64_t *ukeys, uint64_t *beg) {
-    for (uint64_t i = gid(); i < n; i += gstride())
-        if (flag[i]) {
-            ukeys[pos[i]] = k[i];
             beg[pos[i]] = i;
         }
 }
@@ -285,8 +258,6 @@ struct Lookup {
     const uint32_t *subj_bits;    // 2^SUBJ_BITS-bit filter of the set: most subject-id tuples miss it
     uint32_t world;
     int filter;
-    const uint32_t *setn;         // subject-set tuples leading each run
-    int set_only;                 // walk only those (the subject-id tuples come from the subject pass)
 };
 __device__ __forceinline__ unsigned long long subj_key(uint32_t src, uint32_t sid) {
     return (((unsigned long long)src << 32) | sid) + 1ull;  // 0 = empty slot
@@ -334,9 +305,7 @@ __device__ __forceinline__ bool index_range(const uint4 *index, uint64_t mask, c
 }
 __device__ __forceinline__ bool run_of(const Lookup &L, uint64_t key, uint64_t &b, uint64_t &e) {
     uint32_t r;
-    if (!index_range(L.index, L.index_mask, L.beg, key, b, e, r)) return false;
-    if (L.set_only) e = b + L.setn[r];
-    return true;
+    return index_range(L.index, L.index_mask, L.beg, key, b, e, r);
 }
 __device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
     uint32_t lo = 0, hi = L.world;  // last source whose offset <= i
@@ -360,9 +329,10 @@ __device__ __forceinline__ bool keep(const Lookup &L, uint2 m, uint32_t src) {
         h = (h + 1) & L.subj_mask;
     }
 }
-__global__ __launch_bounds__(BLK) void k_lookup_count(Lookup L, uint64_t n, uint64_t *cnt) {
+__global__ __launch_bounds__(BLK) void k_lookup_count(Lookup L, uint64_t n, uint32_t *cnt) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
-        uint64_t b, e, c = 0;
+        uint64_t b, e;
+        uint32_t c = 0;
         if (run_of(L, L.req[i], b, e)) {
             const uint32_t src = source_of(L, i);
             for (uint64_t j = b; j < e; j++) c += keep(L, L.meta[j], src) ? 1 : 0;
@@ -370,7 +340,7 @@ __global__ __launch_bounds__(BLK) void k_lookup_count(Lookup L, uint64_t n, uint
         cnt[i] = c;
     }
 }
-__global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const uint64_t *pos, keto_tuple *out) {
+__global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const uint32_t *pos, keto_tuple *out) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
         uint64_t b, e;
         if (!run_of(L, L.req[i], b, e)) continue;
@@ -485,61 +455,6 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, con
     }
 }
 
-// The subject index of a one-rank partition: every subject-id tuple, grouped by subject id
-// (runs over the sorted ids, looked up through a k_index_fill table); entry = run << 32 | position.
-struct SubjectIndex {
-    const uint64_t *beg;
-    const uint4 *index;
-    uint64_t mask;
-    const uint64_t *val;
-};
-__device__ __forceinline__ bool seen_has(const unsigned long long *table, uint64_t mask, uint64_t key) {
-    const unsigned long long k = key + 1ull;
-    uint64_t h = mix64(k) & mask;
-    for (;;) {  // at most half full: every probe sequence ends at an empty slot
-        const unsigned long long v = table[h];
-        if (v == k) return true;
-        if (v == 0ull) return false;
-        h = (h + 1) & mask;
-    }
-}
-// The one-rank Check closure's subject-id tuples, from the subject side: the reference reads a
-// subject-id tuple only through an EXISTS probe against the query's own subject (engine.go:167-208,
-// traverser.go:73-80, the OR shortcut), so the closure needs exactly the batch subjects' tuples
-// whose object it asked for -- each batch subject's index entries, kept when their run's key is
-// in the closure's seen set.  The same tuples the levels' filter keeps, found through ~6 entries
-// per subject instead of every subject-id tuple of every object asked for.
-__global__ __launch_bounds__(BLK) void k_subject_pass(Lookup L, SubjectIndex X, const uint32_t *subj, uint64_t n_subj,
-                                                       const unsigned long long *table, uint64_t tmask, keto_tuple *out,
-                                                       uint64_t cap, unsigned long long *total, unsigned long long *overflow) {
-    __shared__ unsigned long long s_base;
-    __shared__ uint32_t s_wsum[BLK / 64 + 1];
-    for (uint64_t i0 = (uint64_t)blockIdx.x * BLK; i0 < n_subj; i0 += (uint64_t)gridDim.x * BLK) {
-        const uint64_t i = i0 + threadIdx.x;
-        uint64_t b = 0, e = 0;
-        uint32_t run = 0;
-        if (i < n_subj) index_range(X.index, X.mask, X.beg, subj[i], b, e, run);
-        uint32_t c = 0, km = 0;  // km: which of the first 32 entries are kept
-        for (uint64_t j = b; j < e; j++)
-            if (seen_has(table, tmask, L.ukeys[X.val[j] >> 32])) {
-                if (j - b < 32) km |= 1u << (j - b);
-                c++;
-            }
-        uint64_t o = block_reserve(c, total, &s_base, s_wsum);
-        for (uint64_t j = b; j < e && c; j++) {
-            const uint64_t v = X.val[j];
-            const uint64_t key = L.ukeys[v >> 32];
-            if (j - b < 32 ? !((km >> (j - b)) & 1u) : !seen_has(table, tmask, key)) continue;
-            if (o >= cap) {
-                atomicOr(overflow, 1ull);
-                break;
-            }
-            const uint64_t p = v & 0xFFFFFFFFull;
-            out[o++] = st_tuple(key, L.meta[p], L.shard[p]);
-        }
-    }
-}
-
 // next frontier: the subject-set objects of the tuples received
 __global__ __launch_bounds__(BLK) void k_next(const keto_tuple *t, uint64_t n, const unsigned long long *range_dev,
                                                uint64_t *cand, unsigned long long *n_cand) {
@@ -600,16 +515,15 @@ __global__ __launch_bounds__(BLK) void k_ids_roots(const keto_subject_set *r, ui
         pos[base + i] = (uint32_t)(base + i);
     }
 }
-__global__ __launch_bounds__(BLK) void k_flags32(const uint32_t *k, uint64_t n, uint32_t *flag) {
-    for (uint64_t i = gid(); i < n; i += gstride()) flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
-}
-// sorted entry i: local id = (inclusive count of distinct ids up to i) - 1
-__global__ __launch_bounds__(BLK) void k_ids_assign(const uint32_t *sk, const uint32_t *spos, const uint32_t *flag,
-                                                     const uint32_t *incl, uint64_t n, uint32_t *lid, uint32_t *uniq) {
+// sorted entry i: local id = (distinct ids before it, the exclusive scan of the run flags)
+// + its own flag - 1
+__global__ __launch_bounds__(BLK) void k_ids_assign(const uint32_t *sk, const uint32_t *spos, const uint32_t *excl,
+                                                     uint64_t n, uint32_t *lid, uint32_t *uniq) {
     for (uint64_t i = gid(); i < n; i += gstride()) {
-        const uint32_t l = incl[i] - 1;
+        const bool head = i == 0 || sk[i] != sk[i - 1];
+        const uint32_t l = excl[i] + (head ? 1u : 0u) - 1u;
         lid[spos[i]] = l;
-        if (flag[i]) uniq[l] = sk[i];
+        if (head) uniq[l] = sk[i];
     }
 }
 __global__ __launch_bounds__(BLK) void k_apply_tuples(keto_tuple *t, uint64_t n, const uint32_t *lid) {
@@ -653,11 +567,9 @@ struct Partition {
     // keys ukeys[m], beg[m+1]
     DevBuf meta, shard, ukeys, beg, index;
     uint64_t n = 0, m = 0, index_mask = 0;
-    DevBuf setn;  // subject-set tuples leading each run
-    // one rank: the subject index (k_subject_pass); sx_beg[ms + 1] over sx_val, sx_index by id
-    DevBuf sx_beg, sx_index, sx_val;
-    uint64_t sx_mask = 0;
-    bool have_sx = false;
+    // a job of one rank: the whole graph as one resident snapshot, built at creation (null: the
+    // per-batch closure path)
+    std::unique_ptr<Snapshot> home;
     hipStream_t hs = nullptr;
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
@@ -665,26 +577,28 @@ struct Partition {
         closure, lctr;
     uint64_t subj_mask = 0;
     // compact id space of the last closure (remap_ids): local id -> global uuid id
-    DevBuf rm_ids, rm_pos, rm_ids2, rm_pos2, rm_flag, rm_rank, rm_lid, uniq, bout;
+    DevBuf rm_ids, rm_pos, rm_ids2, rm_pos2, rm_flag, rm_lid, uniq, bout;
     uint64_t n_local = 0;
     void *hpin = nullptr;  // pinned staging for a batch's decisions
     size_t hpin_bytes = 0;
     // batches in flight (partition_check_many): the closure of batch k+1 (stage 1: hs, the
-    // members above) runs while batch k is remapped, built and checked (stage 2: hs2, scratch2,
+    // members above) runs while batch k is remapped, built and checked (stage 2: hs2,
     // ctr2, the remap buffers, kstream); each batch's closure and queries live in its slot
     struct Slot {
         DevBuf closure, bq;
         uint64_t nt = 0;
         keto_partition_stats st{};
+        std::vector<keto_partition_level> levels;
     };
     Slot slots[2];
     hipStream_t hs2 = nullptr;
-    DevBuf scratch2, ctr2;
-    DevBuf bq, braw, bsorted, bkeys, bsubj, bsubj_src, bhist;  // per-batch inputs, reused
+    DevBuf ctr2;
+    DevBuf bq, braw, bsorted, braw_v, bsorted_v, bkeys, bsubj, bsubj_src, bhist;  // per-batch inputs, reused
     bool verbose = false;
     bool trim = false;  // KETO_PART_TRIM: the engine stream's scratch is released after every batch
     uint64_t table_mask = 0, n_seen = 0;
     keto_partition_stats last{};
+    std::vector<keto_partition_level> cur_levels, last_levels;  // the closure running / the last batch's
     // Expand results between keto_partition_expand and keto_partition_expand_result
     std::vector<keto_tree_node> xnodes;
     std::vector<uint64_t> xoffs;
@@ -698,18 +612,6 @@ struct Partition {
 };
 
 void sync(Partition &P) { KETO_HIP(hipStreamSynchronize(P.hs)); }
-
-template <class F>
-void cub_call(DevBuf &scratch, F &&f) {  // hipCUB two-phase call with a reused scratch buffer
-    size_t bytes = 0;
-    KETO_HIP(f(nullptr, bytes));
-    ensure(scratch, bytes);
-    KETO_HIP(f(scratch.p, bytes));
-}
-template <class F>
-void cub_call(Partition &P, F &&f) {
-    cub_call(P.scratch, std::forward<F>(f));
-}
 
 uint64_t d2h_u64(Partition &P, const void *d) {
     uint64_t v = 0;
@@ -817,8 +719,7 @@ uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool 
     if (n_keys) KETO_HIP(hipMemcpyAsync(P.cand.p, keys, n_keys * 8, hipMemcpyDeviceToDevice, P.hs));
     Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
              dptr<uint2>(P.meta), dptr<uint4>(P.shard), dptr<uint64_t>(P.fresh), dptr<uint64_t>(P.req_off),
-             dptr<ull>(P.subj_set), P.subj_mask, dptr<uint32_t>(P.subj_bits), 1u, filter ? 1 : 0,
-             dptr<uint32_t>(P.setn), (filter && P.have_sx) ? 1 : 0};
+             dptr<ull>(P.subj_set), P.subj_mask, dptr<uint32_t>(P.subj_bits), 1u, filter ? 1 : 0};
     const dim3 G(std::max(1, num_cus(P.device)) * 8u);
     keto_tuple *cl = dptr<keto_tuple>(P.closure);
     for (int l = 0; l < levels; l++) {
@@ -831,11 +732,6 @@ uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool 
         hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, P.hs, c, m + 2, (ull)cap);
         hipLaunchKernelGGL(k_next, G, dim3(BLK), 0, P.hs, cl, 0, m + 1, dptr<uint64_t>(P.cand), m + 3);
     }
-    if (L.set_only && n_subj) {  // the subject-id tuples, from the subject side
-        const SubjectIndex X{dptr<uint64_t>(P.sx_beg), dptr<uint4>(P.sx_index), P.sx_mask, dptr<uint64_t>(P.sx_val)};
-        hipLaunchKernelGGL(k_subject_pass, grid_for(n_subj), dim3(BLK), 0, P.hs, L, X, dptr<uint32_t>(P.subj), n_subj,
-                           dptr<ull>(P.table), P.table_mask, cl, cap, c, c + 1);
-    }
     KETO_HIP(hipGetLastError());
     std::vector<ull> h(3 + 4 * (size_t)levels);
     KETO_HIP(hipMemcpyAsync(h.data(), c, nb, hipMemcpyDeviceToHost, P.hs));
@@ -846,6 +742,7 @@ uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool 
         if (!nn) break;
         st.levels++;
         st.objects += nn;
+        P.cur_levels.push_back(keto_partition_level{nn, 0, h[3 + 4 * l + 2] - h[3 + 4 * l + 1], 0, 0.0});
     }
     if (P.verbose)
         fprintf(stderr, "[keto partition] one-rank closure: %llu tuples, %llu levels, %llu objects (no per-level sync)\n",
@@ -858,6 +755,7 @@ uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool 
 uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint32_t *subj, uint64_t n_subj,
                  bool filter, keto_partition_stats &st) {
     const uint32_t W = P.world;
+    P.cur_levels.clear();
     // every owner gets this rank's subject list once per batch
     std::vector<uint64_t> subj_cnt(W, filter ? n_subj : 0);
     DevBuf &subj_src = P.bsubj_src;
@@ -898,6 +796,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         }
         st.levels = 0;  // the buffer was too small: the synchronous levels below grow it
         st.objects = 0;
+        P.cur_levels.clear();
     }
     // seen set: fresh per batch
     P.n_seen = 0;
@@ -918,6 +817,14 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         ts = now;
     };
     for (int level = 0; level < levels; level++) {
+        const auto lv_t0 = std::chrono::steady_clock::now();
+        const uint64_t lv_b0 = st.bytes_sent;
+        uint64_t lv_req = 0, lv_new = 0;
+        auto end_level = [&](uint64_t n_got) {  // keto_partition_level of this level
+            P.cur_levels.push_back(keto_partition_level{
+                lv_new, lv_req, n_got, st.bytes_sent - lv_b0 - lv_req,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lv_t0).count()});
+        };
         if (P.verbose) {
             sync(P);
             fprintf(stderr, "[keto partition] level %d: %llu candidates, prev level %.3f ms\n", level,
@@ -936,6 +843,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         const uint64_t n_new = d2h_u64(P, c);
         mark(0);
         if (allreduce_max(P, n_new) == 0) break;
+        lv_new = n_new;
         st.levels++;
         st.objects += n_new;
         if (!P.seen.p || P.seen.bytes < (P.n_seen + n_new) * 8) {  // remembered for rehashing
@@ -970,6 +878,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                                    W, dptr<unsigned long long>(hist), dptr<uint64_t>(P.routed));
         }
         std::vector<uint64_t> from = exchange(P, P.routed.p, send, 8, P.req, st.bytes_sent);
+        lv_req = st.bytes_sent - lv_b0;
         mark(1);
         std::vector<uint64_t> roff(W + 1, 0);
         for (uint32_t r = 0; r < W; r++) roff[r + 1] = roff[r] + from[r];
@@ -1002,24 +911,24 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                 n_cand = d2h_u64(P, c);
                 mark(4);
                 total += n_got;
+                end_level(n_got);
                 continue;
             }
             // overflow: the level again with the two passes (the closure grows to fit)
         }
-        ensure(P.cnt, (n_req + 1) * 8);
-        ensure(P.pos, (n_req + 1) * 8);
-        KETO_HIP(hipMemsetAsync(P.cnt.p, 0, (n_req + 1) * 8, P.hs));
-        if (n_req) hipLaunchKernelGGL(k_lookup_count, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, dptr<uint64_t>(P.cnt));
-        uint64_t *cntp = dptr<uint64_t>(P.cnt), *posp = dptr<uint64_t>(P.pos);
-        const int nn = (int)(n_req + 1);
-        cub_call(P, [&](void *tmp, size_t &b) {
-            return hipcub::DeviceScan::ExclusiveSum(tmp, b, cntp, posp, nn, P.hs);
-        });
+        // counts, scanned in place into each request's first output position (u32: a level ships
+        // fewer than 2^32 tuples -- the compact id pass takes at most 2^31)
+        ensure(P.pos, (n_req + 1) * 4);
+        uint32_t *posp = dptr<uint32_t>(P.pos);
+        KETO_HIP(hipMemsetAsync(posp, 0, (n_req + 1) * 4, P.hs));
+        if (n_req) hipLaunchKernelGGL(k_lookup_count, grid_for(n_req), dim3(BLK), 0, P.hs, L, n_req, posp);
+        build::scan_excl(posp, n_req, P.hs);
         // tuples per source = pos at the source boundaries
-        std::vector<uint64_t> pb(W + 1, 0);
+        std::vector<uint32_t> pbv(W + 1, 0);
         for (uint32_t r = 0; r <= W; r++)
-            KETO_HIP(hipMemcpyAsync(&pb[r], posp + roff[r], 8, hipMemcpyDeviceToHost, P.hs));
+            KETO_HIP(hipMemcpyAsync(&pbv[r], posp + roff[r], 4, hipMemcpyDeviceToHost, P.hs));
         sync(P);
+        std::vector<uint64_t> pb(pbv.begin(), pbv.end());
         mark(2);
         const uint64_t n_out = pb[W];
         uint64_t n_got = 0;
@@ -1053,6 +962,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
         n_cand = d2h_u64(P, c);
         mark(4);
         total += n_got;
+        end_level(n_got);
     }
     sync(P);
     if (P.verbose)
@@ -1106,12 +1016,22 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     P->cfg.namespaces_json = P->json.c_str();
     KETO_HIP(hipStreamCreateWithFlags(&P->hs, hipStreamNonBlocking));
     KETO_HIP(hipStreamCreateWithFlags(&P->hs2, hipStreamNonBlocking));
-    ScratchStream on_hs(P->hs);  // (the store is built on P->hs)
     P->verbose = getenv("KETO_PART_VERBOSE") != nullptr;
     P->trim = getenv("KETO_PART_TRIM") != nullptr;
     if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
-    // the partition, grouped by object key (stable radix sort of (key, index), then a gather)
     P->n = n;
+    if (P->world == 1 && !getenv("KETO_PART_CLOSURE")) {
+        // one rank owns every object: its partition is the whole graph, built once into a
+        // resident snapshot (scheduling weights included, as a replica's) that every batch reads
+        auto t0 = std::chrono::steady_clock::now();
+        P->home.reset(build_snapshot(&P->cfg, tuples, n, device_ptrs));
+        if (P->verbose)
+            fprintf(stderr, "[keto partition] one rank: %llu tuples as a resident snapshot, %.2f s\n", (unsigned long long)n,
+                    secs(t0));
+        return P.release();
+    }
+    ScratchStream on_hs(P->hs);  // (the store is built on P->hs)
+    // the partition, grouped by object key (stable radix sort of (key, index), then a gather)
     DevBuf raw;
     const keto_tuple *src = tuples;
     if (!device_ptrs) {
@@ -1123,13 +1043,13 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     DevBuf k0(std::max<uint64_t>(1, n) * 8), k1(std::max<uint64_t>(1, n) * 8), i0(std::max<uint64_t>(1, n) * 4),
         i1(std::max<uint64_t>(1, n) * 4);
     if (n) hipLaunchKernelGGL(k_tuple_keys, grid_for(n), dim3(BLK), 0, Q.hs, src, n, dptr<uint64_t>(k0), dptr<uint32_t>(i0));
-    const int ni = (int)n;
-    uint64_t *kin = dptr<uint64_t>(k0), *kout = dptr<uint64_t>(k1);
-    uint32_t *vin = dptr<uint32_t>(i0), *vout = dptr<uint32_t>(i1);
-    if (n)
-        cub_call(Q, [&](void *tmp, size_t &b) {
-            return hipcub::DeviceRadixSort::SortPairs(tmp, b, kin, kout, vin, vout, ni, 0, 64, Q.hs);
-        });
+    // key = (ns << 32 | obj) << 1 | kind: 33 bits plus the namespace's
+    uint32_t ns_bits = 1;
+    while ((1u << ns_bits) < cfg->n_namespaces) ns_bits++;
+    const bool in1 = prim::sort_pairs(dptr<uint64_t>(k0), dptr<uint32_t>(i0), dptr<uint64_t>(k1), dptr<uint32_t>(i1), n,
+                                      33 + ns_bits, Q.hs);
+    const uint64_t *kout = in1 ? dptr<uint64_t>(k1) : dptr<uint64_t>(k0);
+    const uint32_t *vout = in1 ? dptr<uint32_t>(i1) : dptr<uint32_t>(i0);
     Q.meta = DevBuf(std::max<uint64_t>(1, n) * sizeof(uint2));
     Q.shard = DevBuf(std::max<uint64_t>(1, n) * sizeof(uint4));
     ensure(Q.ctr, 64);
@@ -1139,77 +1059,22 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
                            dptr<uint4>(Q.shard), dptr<unsigned long long>(Q.ctr));
     if (d2h_u64(Q, Q.ctr.p)) throw Error(KETO_E_INVALID, "partition tuple with a relation / namespace id past the store's fields");
     raw.reset();
-    k0 = DevBuf();  // (kout = k1 stays: the run boundaries below)
-    i0 = DevBuf();
-    i1 = DevBuf();
-    // runs: one entry per object key
-    DevBuf flag(std::max<uint64_t>(1, n + 1) * 4), fpos(std::max<uint64_t>(1, n + 1) * 8);
-    KETO_HIP(hipMemsetAsync(flag.p, 0, (n + 1) * 4, Q.hs));
-    if (n) hipLaunchKernelGGL(k_run_flags, grid_for(n), dim3(BLK), 0, Q.hs, kout, n, dptr<uint32_t>(flag));
-    uint32_t *fl = dptr<uint32_t>(flag);
-    uint64_t *fp = dptr<uint64_t>(fpos);
-    const int nf = (int)(n + 1);
-    cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(tmp, b, fl, fp, nf, Q.hs); });
-    Q.m = d2h_u64(Q, fp + n);
+    // runs: one entry per object key (run flags scanned in place into run positions)
+    DevBuf fpos(std::max<uint64_t>(1, n + 1) * 4), flag(std::max<uint64_t>(1, n + 1) * 4);
+    uint32_t *fl = dptr<uint32_t>(flag), *fp = dptr<uint32_t>(fpos);
+    if (n) hipLaunchKernelGGL(k_run_flags, grid_for(n), dim3(BLK), 0, Q.hs, kout, n, fl);
+    KETO_HIP(hipMemcpyAsync(fp, fl, n * 4, hipMemcpyDeviceToDevice, Q.hs));
+    build::scan_excl(fp, n, Q.hs);
+    uint32_t m32 = 0;
+    KETO_HIP(hipMemcpyAsync(&m32, fp + n, 4, hipMemcpyDeviceToHost, Q.hs));
+    sync(Q);
+    Q.m = n ? m32 : 0;
     Q.ukeys = DevBuf(std::max<uint64_t>(1, Q.m) * 8);
     Q.beg = DevBuf((Q.m + 1) * 8);
     if (n)
         hipLaunchKernelGGL(k_run_starts, grid_for(n), dim3(BLK), 0, Q.hs, kout, fl, fp, n, dptr<uint64_t>(Q.ukeys),
                            dptr<uint64_t>(Q.beg));
     KETO_HIP(hipMemcpyAsync(dptr<uint64_t>(Q.beg) + Q.m, &Q.n, 8, hipMemcpyHostToDevice, Q.hs));
-    Q.setn = DevBuf(std::max<uint64_t>(1, Q.m) * 4);
-    KETO_HIP(hipMemsetAsync(Q.setn.p, 0, std::max<uint64_t>(1, Q.m) * 4, Q.hs));
-    if (n) hipLaunchKernelGGL(k_set_counts, grid_for(n), dim3(BLK), 0, Q.hs, dptr<uint2>(Q.meta), fl, fp, n, dptr<uint32_t>(Q.setn));
-    if (Q.world == 1 && n && !getenv("KETO_PART_NO_SUBJECT_INDEX")) {
-        // the subject index (one rank: its Check closures take their subject-id tuples from the
-        // subject side, k_subject_pass): (id, run << 32 | position) of every subject-id tuple, sorted
-        DevBuf sk(n * 4), sk2(n * 4), sv(n * 8);
-        Q.sx_val = DevBuf(n * 8);
-        hipLaunchKernelGGL(k_subject_pairs, grid_for(n), dim3(BLK), 0, Q.hs, dptr<uint2>(Q.meta), fl, fp, n, dptr<uint32_t>(sk),
-                           dptr<uint64_t>(sv));
-        uint32_t *ska = dptr<uint32_t>(sk), *skb = dptr<uint32_t>(sk2);
-        uint64_t *sva = dptr<uint64_t>(sv), *svb = dptr<uint64_t>(Q.sx_val);
-        cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceRadixSort::SortPairs(tmp, b, ska, skb, sva, svb, ni, 0, 32, Q.hs); });
-        // the subject-id tuples are the sorted prefix (set tuples sorted last under ~0 keys)
-        DevBuf sum(8);
-        uint32_t *sn = dptr<uint32_t>(Q.setn);
-        unsigned long long *sump = dptr<unsigned long long>(sum);
-        const int mi = (int)Q.m;
-        cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceReduce::Sum(tmp, b, sn, sump, mi, Q.hs); });
-        const uint64_t n_id = n - d2h_u64(Q, sump);  // (Q.hs drained: the sort's inputs can go)
-        sv.reset();
-        sk.reset();
-        if (n_id) {
-            DevBuf sflag((n_id + 1) * 4), spos((n_id + 1) * 8);
-            KETO_HIP(hipMemsetAsync(sflag.p, 0, (n_id + 1) * 4, Q.hs));
-            hipLaunchKernelGGL(k_u32_run_flags, grid_for(n_id), dim3(BLK), 0, Q.hs, skb, n_id, dptr<uint32_t>(sflag));
-            uint32_t *sf = dptr<uint32_t>(sflag);
-            uint64_t *sp = dptr<uint64_t>(spos);
-            const int ns1 = (int)(n_id + 1);
-            cub_call(Q, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(tmp, b, sf, sp, ns1, Q.hs); });
-            const uint64_t ms = d2h_u64(Q, sp + n_id);
-            DevBuf sukeys(ms * 8);
-            Q.sx_beg = DevBuf((ms + 1) * 8);
-            hipLaunchKernelGGL(k_u32_run_starts, grid_for(n_id), dim3(BLK), 0, Q.hs, skb, sf, sp, n_id, dptr<uint64_t>(sukeys),
-                               dptr<uint64_t>(Q.sx_beg));
-            KETO_HIP(hipMemcpyAsync(dptr<uint64_t>(Q.sx_beg) + ms, &n_id, 8, hipMemcpyHostToDevice, Q.hs));
-            uint64_t scap = 1u << 10;
-            while (scap < 2 * ms) scap *= 2;
-            Q.sx_index = DevBuf(scap * 16);
-            Q.sx_mask = scap - 1;
-            KETO_HIP(hipMemsetAsync(Q.sx_index.p, 0xFF, scap * 16, Q.hs));
-            hipLaunchKernelGGL(k_index_fill, grid_for(ms), dim3(BLK), 0, Q.hs, dptr<uint64_t>(sukeys), ms, dptr<uint4>(Q.sx_index),
-                               Q.sx_mask);
-            sync(Q);
-        } else {  // no subject-id tuple at all: an empty index
-            Q.sx_beg = DevBuf(8);
-            KETO_HIP(hipMemsetAsync(Q.sx_beg.p, 0, 8, Q.hs));
-            Q.sx_index = DevBuf(16 * 1024);
-            Q.sx_mask = 1023;
-            KETO_HIP(hipMemsetAsync(Q.sx_index.p, 0xFF, 16 * 1024, Q.hs));
-        }
-        Q.have_sx = true;
-    }
     uint64_t cap = 1u << 10;
     while (cap < 2 * Q.m) cap *= 2;
     Q.index = DevBuf(cap * 16);
@@ -1218,6 +1083,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     if (Q.m)
         hipLaunchKernelGGL(k_index_fill, grid_for(Q.m), dim3(BLK), 0, Q.hs, dptr<uint64_t>(Q.ukeys), Q.m,
                            dptr<uint4>(Q.index), Q.index_mask);
+    KETO_HIP(hipGetLastError());
     sync(Q);
     return P.release();
 }
@@ -1231,6 +1097,8 @@ uint64_t batch_keys(Partition &P, const keto_query *q, uint64_t n, DevBuf &keys,
     ensure(keys, std::max<uint64_t>(1, n) * 8);
     ensure(raw, std::max<uint64_t>(1, n) * 4);
     ensure(sorted, std::max<uint64_t>(1, n) * 4);
+    ensure(P.braw_v, std::max<uint64_t>(1, n) * 4);
+    ensure(P.bsorted_v, std::max<uint64_t>(1, n) * 4);
     ensure(subj, std::max<uint64_t>(1, n) * 4 + 8);
     ensure(P.ctr, 64);
     unsigned long long *c = dptr<unsigned long long>(P.ctr);
@@ -1240,42 +1108,40 @@ uint64_t batch_keys(Partition &P, const keto_query *q, uint64_t n, DevBuf &keys,
                            dptr<uint32_t>(raw), c);
     const uint64_t ns = d2h_u64(P, c);
     if (!ns) return 0;
-    uint32_t *rin = dptr<uint32_t>(raw), *rout = dptr<uint32_t>(sorted), *uo = dptr<uint32_t>(subj);
-    unsigned long long *nu = c + 1;
-    const int nsi = (int)ns;
-    cub_call(P, [&](void *tmp, size_t &b) { return hipcub::DeviceRadixSort::SortKeys(tmp, b, rin, rout, nsi, 0, 32, P.hs); });
-    cub_call(P, [&](void *tmp, size_t &b) { return hipcub::DeviceSelect::Unique(tmp, b, rout, uo, nu, nsi, P.hs); });
-    return d2h_u64(P, nu);
+    // (the sort carries a payload it ignores: only the keys matter here)
+    const bool in1 = prim::sort_pairs(dptr<uint32_t>(raw), dptr<uint32_t>(P.braw_v), dptr<uint32_t>(sorted),
+                                      dptr<uint32_t>(P.bsorted_v), ns, 32, P.hs);
+    return prim::unique_sorted(in1 ? dptr<uint32_t>(sorted) : dptr<uint32_t>(raw), ns, dptr<uint32_t>(subj), P.hs);
 }
 
 // The closure's tuples plus the batch's queries (q, device) or Expand roots (r, device) over the
 // compact id space: rewritten in place, P.uniq[local] = global, P.n_local ids.
-void remap_ids(Partition &P, keto_tuple *t, uint64_t nt, keto_query *q, keto_subject_set *r, uint64_t n, hipStream_t hs,
-               DevBuf &scratch) {
+void remap_ids(Partition &P, keto_tuple *t, uint64_t nt, keto_query *q, keto_subject_set *r, uint64_t n, hipStream_t hs) {
     const uint64_t E = 2 * nt + (q ? 2 * n : n);
     if (E >= (1ull << 31)) throw Error(KETO_E_LIMIT, "closure too large for the compact id pass (2^31 ids)");
-    for (DevBuf *b : {&P.rm_ids, &P.rm_pos, &P.rm_ids2, &P.rm_pos2, &P.rm_flag, &P.rm_rank, &P.rm_lid, &P.uniq})
+    for (DevBuf *b : {&P.rm_ids, &P.rm_pos, &P.rm_ids2, &P.rm_pos2, &P.rm_lid, &P.uniq})
         ensure(*b, std::max<uint64_t>(1, E) * 4);
-    uint32_t *ids = dptr<uint32_t>(P.rm_ids), *pos = dptr<uint32_t>(P.rm_pos), *sk = dptr<uint32_t>(P.rm_ids2),
-             *sp = dptr<uint32_t>(P.rm_pos2), *fl = dptr<uint32_t>(P.rm_flag), *rk = dptr<uint32_t>(P.rm_rank),
-             *lid = dptr<uint32_t>(P.rm_lid);
+    ensure(P.rm_flag, (std::max<uint64_t>(1, E) + 1) * 4);
+    uint32_t *ids = dptr<uint32_t>(P.rm_ids), *pos = dptr<uint32_t>(P.rm_pos), *ids2 = dptr<uint32_t>(P.rm_ids2),
+             *pos2 = dptr<uint32_t>(P.rm_pos2), *fl = dptr<uint32_t>(P.rm_flag), *lid = dptr<uint32_t>(P.rm_lid);
     if (nt) hipLaunchKernelGGL(k_ids_tuples, grid_for(nt), dim3(BLK), 0, hs, t, nt, ids, pos);
     if (n && q) hipLaunchKernelGGL(k_ids_queries, grid_for(n), dim3(BLK), 0, hs, q, n, 2 * nt, ids, pos);
     if (n && r) hipLaunchKernelGGL(k_ids_roots, grid_for(n), dim3(BLK), 0, hs, r, n, 2 * nt, ids, pos);
     P.n_local = 0;
     if (E) {
-        const int ne = (int)E;
-        cub_call(scratch, [&](void *tmp, size_t &b) {
-            return hipcub::DeviceRadixSort::SortPairs(tmp, b, ids, sk, pos, sp, ne, 0, 32, hs);
-        });
-        hipLaunchKernelGGL(k_flags32, grid_for(E), dim3(BLK), 0, hs, sk, E, fl);
-        cub_call(scratch, [&](void *tmp, size_t &b) { return hipcub::DeviceScan::InclusiveSum(tmp, b, fl, rk, ne, hs); });
-        hipLaunchKernelGGL(k_ids_assign, grid_for(E), dim3(BLK), 0, hs, sk, sp, fl, rk, E, lid, dptr<uint32_t>(P.uniq));
+        uint32_t bits = 1;  // ids are < n_uuids: only their digits are sorted
+        while (bits < 32 && (1ull << bits) < (uint64_t)std::max<uint32_t>(2, P.cfg.n_uuids)) bits++;
+        const bool in1 = prim::sort_pairs(ids, pos, ids2, pos2, E, bits, hs);
+        const uint32_t *sk = in1 ? ids2 : ids, *sp = in1 ? pos2 : pos;
+        prim::run_flags(sk, E, fl, hs);
+        build::scan_excl(fl, E, hs);
+        hipLaunchKernelGGL(k_ids_assign, grid_for(E), dim3(BLK), 0, hs, sk, sp, fl, E, lid, dptr<uint32_t>(P.uniq));
         uint32_t m = 0;
-        KETO_HIP(hipMemcpyAsync(&m, rk + E - 1, 4, hipMemcpyDeviceToHost, hs));
+        KETO_HIP(hipMemcpyAsync(&m, fl + E, 4, hipMemcpyDeviceToHost, hs));
         if (nt) hipLaunchKernelGGL(k_apply_tuples, grid_for(nt), dim3(BLK), 0, hs, t, nt, lid);
         if (n && q) hipLaunchKernelGGL(k_apply_queries, grid_for(n), dim3(BLK), 0, hs, q, n, 2 * nt, lid);
         if (n && r) hipLaunchKernelGGL(k_apply_roots, grid_for(n), dim3(BLK), 0, hs, r, n, 2 * nt, lid);
+        KETO_HIP(hipGetLastError());
         KETO_HIP(hipStreamSynchronize(hs));
         P.n_local = m;
     }
@@ -1295,6 +1161,12 @@ Snapshot *closure_snapshot(Partition &P, const keto_tuple *t, uint64_t n_tuples)
     keto_snapshot_config cfg = P.cfg;
     cfg.n_uuids = (uint32_t)std::max<uint64_t>(1, P.n_local);
     return build_snapshot(&cfg, t, n_tuples, true, false);  // (one batch: no weights)
+}
+
+void throw_last(int rc) {
+    char buf[512];
+    keto_last_error(buf, sizeof buf);
+    throw Error(rc, buf);
 }
 }  // namespace
 
@@ -1316,6 +1188,7 @@ void stage_closure(Partition &P, Partition::Slot &S, const keto_query *q, uint64
             fprintf(stderr, "[keto partition] batch keys + %llu subjects: %.3f ms\n", (unsigned long long)n_subj, secs(t0) * 1e3);
         S.nt = closure(P, dptr<uint64_t>(keys), n, dptr<uint32_t>(subj), n_subj, true, S.st);
         S.st.closure_s = secs(t0);
+        S.levels = P.cur_levels;
     } catch (...) {
         std::swap(P.closure, S.closure);
         std::swap(P.bq, S.bq);
@@ -1334,7 +1207,7 @@ void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed,
     keto_query *dq = dptr<keto_query>(S.bq);  // the batch, uploaded by batch_keys
     {
         ScratchStream on_hs2(P.hs2);  // (the remap's buffers are used on P.hs2; the build below runs on the null stream)
-        remap_ids(P, dptr<keto_tuple>(S.closure), S.nt, dq, nullptr, n, P.hs2, P.scratch2);
+        remap_ids(P, dptr<keto_tuple>(S.closure), S.nt, dq, nullptr, n, P.hs2);
     }
     std::unique_ptr<Snapshot> snap(closure_snapshot(P, dptr<keto_tuple>(S.closure), S.nt));
     st.build_s = secs(t0);
@@ -1344,11 +1217,7 @@ void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed,
     int32_t *d_err = reinterpret_cast<int32_t *>(dptr<uint8_t>(P.bout) + (n + 255) / 256 * 256);
     const int rc = keto_check_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, dq, n, &P.limits, d_allowed,
                                     d_err, KETO_F_DEVICE_PTRS | (flags & (KETO_F_COUNT_WORK | KETO_F_ERR_DETAIL)));
-    if (rc != KETO_OK) {
-        char buf[512];
-        keto_last_error(buf, sizeof buf);
-        throw Error(rc, buf);
-    }
+    if (rc != KETO_OK) throw_last(rc);
     if (n) {
         // decisions through pinned staging; the error codes only when a query has one (a 4n-byte
         // pageable copy costs as much as the check kernels' tail)
@@ -1392,6 +1261,37 @@ void stage_check(Partition &P, Partition::Slot &S, uint64_t n, uint8_t *allowed,
     snap.reset();
     trim_stream(P);
 }
+
+// A job of one rank: the batches straight on the resident snapshot, enqueued one after another
+// on the engine stream (KETO_F_ASYNC: each batch's H2D / D2H on the stream's copy streams beside
+// its neighbours' kernels), one synchronisation at the end.  A counted batch runs synchronously.
+void home_check_many(Partition &P, uint32_t nb, const keto_query *const *q, const uint64_t *n, uint8_t *const *allowed,
+                     int32_t *const *err, uint32_t flags) {
+    auto t0 = std::chrono::steady_clock::now();
+    keto_snapshot *snap = reinterpret_cast<keto_snapshot *>(P.home.get());
+    const bool count = (flags & KETO_F_COUNT_WORK) != 0;
+    const uint32_t f = (flags & (KETO_F_COUNT_WORK | KETO_F_ERR_DETAIL)) | (count ? 0u : KETO_F_ASYNC);
+    for (uint32_t k = 0; k < nb; k++) {
+        const int rc = keto_check_batch(snap, P.kstream, q[k], n[k], &P.limits, allowed[k], err[k], f);
+        if (rc != KETO_OK) throw_last(rc);
+    }
+    const int rc = keto_stream_sync(P.kstream);
+    if (rc != KETO_OK) throw_last(rc);
+    keto_partition_stats st{};
+    st.batches = nb;
+    st.run_s = secs(t0) / std::max<uint32_t>(1, nb);
+    if (count) {
+        keto_work_counters wc{};
+        if (keto_stream_counters(P.kstream, &wc, 1) == KETO_OK) {
+            st.rows = wc.rows[0];
+            st.edges = wc.edges[0];
+            st.probes = wc.probes[0];
+            st.queries = wc.queries[0];
+        }
+    }
+    P.last = st;
+    P.last_levels.clear();
+}
 }  // namespace
 
 // Several batches in one call, in flight: while batch k is remapped, built and checked on this
@@ -1405,11 +1305,13 @@ void partition_check_many(PartitionHandle *PH, uint32_t nb, const keto_query *co
     Partition &P = *PH;
     KETO_HIP(hipSetDevice(P.device));
     if (!nb) return;
+    if (P.home) return home_check_many(P, nb, q, n, allowed, err, flags);
     if (getenv("KETO_PART_SEQUENTIAL")) {
         for (uint32_t k = 0; k < nb; k++) {
             stage_closure(P, P.slots[0], q[k], n[k]);
             stage_check(P, P.slots[0], n[k], allowed[k], err[k], flags);
             P.last = P.slots[0].st;
+            P.last_levels = P.slots[0].levels;
         }
         return;
     }
@@ -1433,6 +1335,7 @@ void partition_check_many(PartitionHandle *PH, uint32_t nb, const keto_query *co
         }
         if (next.joinable()) next.join();
         P.last = P.slots[k & 1].st;
+        P.last_levels = P.slots[k & 1].levels;
         if (ex) std::rethrow_exception(ex);
     }
 }
@@ -1441,25 +1344,51 @@ void partition_check(PartitionHandle *PH, const keto_query *q, uint64_t n, uint8
     partition_check_many(PH, 1, &q, &n, &allowed, &err, flags);
 }
 
+namespace {
+// keto_expand_batch into P.xnodes / xoffs / xerr (grown until the trees fit)
+void expand_into(Partition &P, keto_snapshot *snap, const keto_subject_set *roots, uint64_t n) {
+    P.xoffs.assign(n + 1, 0);
+    P.xerr.assign(std::max<uint64_t>(1, n), 0);
+    if (P.xnodes.empty()) P.xnodes.resize(1u << 16);
+    for (;;) {
+        const int rc = keto_expand_batch(snap, P.kstream, roots, n, &P.limits, P.xnodes.data(), P.xnodes.size(),
+                                         P.xoffs.data(), P.xerr.data());
+        if (rc == KETO_E_CAPACITY) {
+            P.xnodes.resize(P.xoffs[n]);
+            continue;
+        }
+        if (rc != KETO_OK) throw_last(rc);
+        break;
+    }
+}
+}  // namespace
+
 uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, uint64_t n) {
     Partition &P = *PH;
     KETO_HIP(hipSetDevice(P.device));
     keto_partition_stats st{};
     st.batches = 1;
     auto t0 = std::chrono::steady_clock::now();
+    if (P.home) {  // one rank: the resident snapshot
+        expand_into(P, reinterpret_cast<keto_snapshot *>(P.home.get()), roots, n);
+        st.run_s = secs(t0);
+        P.last = st;
+        P.last_levels.clear();
+        return P.xoffs[n];
+    }
     DevBuf dr(std::max<uint64_t>(1, n) * sizeof(keto_subject_set)), keys(std::max<uint64_t>(1, n) * 8);
     uint64_t nt = 0;
     {
-        ScratchStream on_hs(P.hs);  // (the closure's buffers are used on P.hs; the build's on the null stream)
+        ScratchStream on_hs(P.hs);  // (the closure's and the remap's buffers are used on P.hs)
         if (n) KETO_HIP(hipMemcpyAsync(dr.p, roots, n * sizeof(keto_subject_set), hipMemcpyHostToDevice, P.hs));
         if (n)
             hipLaunchKernelGGL(k_root_keys, grid_for(n), dim3(BLK), 0, P.hs, dptr<keto_subject_set>(dr), n,
                                dptr<uint64_t>(keys));
         nt = closure(P, dptr<uint64_t>(keys), n, nullptr, 0, false, st);
+        st.closure_s = secs(t0);
+        t0 = std::chrono::steady_clock::now();
+        remap_ids(P, dptr<keto_tuple>(P.closure), nt, nullptr, dptr<keto_subject_set>(dr), n, P.hs);
     }
-    st.closure_s = secs(t0);
-    t0 = std::chrono::steady_clock::now();
-    remap_ids(P, dptr<keto_tuple>(P.closure), nt, nullptr, dptr<keto_subject_set>(dr), n, P.hs, P.scratch);
     std::vector<keto_subject_set> lroots(n);
     if (n) KETO_HIP(hipMemcpy(lroots.data(), dr.p, n * sizeof(keto_subject_set), hipMemcpyDeviceToHost));
     std::vector<uint32_t> uniq(P.n_local);
@@ -1467,29 +1396,14 @@ uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, ui
     std::unique_ptr<Snapshot> snap(closure_snapshot(P, dptr<keto_tuple>(P.closure), nt));
     st.build_s = secs(t0);
     t0 = std::chrono::steady_clock::now();
-    P.xoffs.assign(n + 1, 0);
-    P.xerr.assign(std::max<uint64_t>(1, n), 0);
-    if (P.xnodes.empty()) P.xnodes.resize(1u << 16);
-    for (;;) {
-        const int rc = keto_expand_batch(reinterpret_cast<keto_snapshot *>(snap.get()), P.kstream, lroots.data(), n, &P.limits,
-                                         P.xnodes.data(), P.xnodes.size(), P.xoffs.data(), P.xerr.data());
-        if (rc == KETO_E_CAPACITY) {
-            P.xnodes.resize(P.xoffs[n]);
-            continue;
-        }
-        if (rc != KETO_OK) {
-            char buf[512];
-            keto_last_error(buf, sizeof buf);
-            throw Error(rc, buf);
-        }
-        break;
-    }
+    expand_into(P, reinterpret_cast<keto_snapshot *>(snap.get()), lroots.data(), n);
     for (uint64_t i = 0; i < P.xoffs[n]; i++)  // the trees' subject ids back to the global id space
         if (P.xnodes[i].s_obj < P.n_local) P.xnodes[i].s_obj = uniq[P.xnodes[i].s_obj];
     st.run_s = secs(t0);
     snap.reset();
     trim_stream(P);
     P.last = st;
+    P.last_levels = P.cur_levels;
     return P.xoffs[n];
 }
 
@@ -1505,6 +1419,11 @@ void partition_expand_result(PartitionHandle *PH, keto_tree_node *nodes, uint64_
 }
 
 void partition_stats(PartitionHandle *PH, keto_partition_stats *out) { *out = PH->last; }
+void partition_levels(PartitionHandle *PH, keto_partition_level *out, uint32_t cap, uint32_t *n) {
+    const auto &L = PH->last_levels;
+    *n = (uint32_t)L.size();
+    for (uint32_t i = 0; i < cap && i < L.size(); i++) out[i] = L[i];
+}
 void partition_free(PartitionHandle *PH) { delete PH; }
 
 }  // namespace keto

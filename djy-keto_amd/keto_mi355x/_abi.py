@@ -86,6 +86,11 @@ class PartitionStats(ctypes.Structure):
                 ("edges", ctypes.c_uint64), ("probes", ctypes.c_uint64), ("queries", ctypes.c_uint64)]
 
 
+class PartitionLevel(ctypes.Structure):
+    _fields_ = [("objects", ctypes.c_uint64), ("request_bytes", ctypes.c_uint64), ("tuples", ctypes.c_uint64),
+                ("tuple_bytes_sent", ctypes.c_uint64), ("ms", ctypes.c_double)]
+
+
 # keto_collective callbacks
 ABI_VERSION = 4  # include/keto_mi355x.h KETO_ABI_VERSION
 
@@ -153,6 +158,7 @@ SIGNATURES = {
     "keto_partition_expand": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),
     "keto_partition_expand_result": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP]),
     "keto_partition_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(PartitionStats)]),
+    "keto_partition_levels_get": (ctypes.c_int, [_VP, ctypes.POINTER(PartitionLevel), _U32, ctypes.POINTER(_U32)]),
     "keto_partition_free": (ctypes.c_int, [_VP]),
     "keto_trees_to_json": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
     "keto_trees_to_proto": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),

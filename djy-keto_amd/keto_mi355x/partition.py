@@ -139,6 +139,14 @@ class PartitionedEngine:
         check(lib().keto_partition_stats_get(self.handle, ctypes.byref(st)))
         self.last = {k: getattr(st, k) for k, _ in st._fields_}
 
+    def level_stats(self) -> list:
+        """the last batch's closure exchange level by level (keto_partition_levels_get)"""
+        n = ctypes.c_uint32()
+        check(lib().keto_partition_levels_get(self.handle, None, 0, ctypes.byref(n)))
+        arr = (_abi.PartitionLevel * max(1, n.value))()
+        check(lib().keto_partition_levels_get(self.handle, arr, n.value, ctypes.byref(n)))
+        return [{k: getattr(arr[i], k) for k, _ in _abi.PartitionLevel._fields_} for i in range(n.value)]
+
     def check_batch(self, queries: np.ndarray, count_work: bool = False):
         """queries: QUERY_DT (this rank's) -> (allowed u8[n], err i32[n])"""
         q = np.ascontiguousarray(queries, dtype=_abi.QUERY_DT)

@@ -336,8 +336,13 @@ static inline uint32_t keto_object_owner(uint32_t ns, uint32_t obj, uint32_t npa
  * snapshot and runs the Check / Expand kernels on it: the decisions and trees of the whole
  * graph.  There is no reference counterpart (Keto never partitions).
  *
- * The exchange goes through the caller's collective, host buffers only, every rank calling in
- * the same order (a Go host wraps its RCCL communicator; the tests wrap gloo): */
+ * A job of one rank (coll NULL or world 1) holds the whole graph: its partition is built once,
+ * at creation, into a resident snapshot and every batch runs on it -- no closure, no per-batch
+ * build.
+ *
+ * The exchange goes through the caller's collective, every rank calling in the same order (a Go
+ * host wraps its RCCL communicator; the tests wrap gloo): the host-buffer alltoallv always, and
+ * with alltoallv_device (optional, below) the library's device buffers on its stream: */
 typedef struct keto_collective {
     void *ctx;
     int32_t rank, world;
@@ -386,6 +391,16 @@ int keto_partition_expand_result(keto_partition *p, keto_tree_node *out_nodes, u
                                  int32_t *out_err);
 /* the last batch's closure and phase times */
 int keto_partition_stats_get(keto_partition *p, keto_partition_stats *out);
+/* The last batch's closure exchange level by level (a job of one rank over its resident snapshot
+ * has none): *n = the levels run; the first min(cap, *n) are copied to out. */
+typedef struct keto_partition_level {
+    uint64_t objects;          /* objects this rank asked for at this level (new to its seen set) */
+    uint64_t request_bytes;    /* object keys it sent to the other ranks */
+    uint64_t tuples;           /* tuples it received: its closure grows by these */
+    uint64_t tuple_bytes_sent; /* tuples it shipped to the other ranks (as an owner) */
+    double ms;                 /* the level's wall time on this rank (0 when the levels were enqueued at once) */
+} keto_partition_level;
+int keto_partition_levels_get(keto_partition *p, keto_partition_level *out, uint32_t cap, uint32_t *n);
 int keto_partition_free(keto_partition *p);
 
 /* pinned host memory (hipHostMalloc) for the query / output buffers of KETO_F_ASYNC batches */

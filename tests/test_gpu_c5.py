@@ -13,9 +13,15 @@ oracle's answers are the whole graph's (oracle/refsem.c, internal/check/engine.g
 
 Per rank: a 2^20-query batch whose first 1% asks request depths 1-4 (the truncation sub-batch,
 engine.go:82-84), run twice (determinism); an exact oracle sample of every truncation query
-plus 64Ki others; 32 Expand roots (256 over the job) against oracle trees, child order
-included (internal/expand/engine.go:54-124).
+plus 64Ki others; 512 Expand roots (4,096 over the job: BASELINE config 5's "batched Expand
+trees") against oracle trees, child order included (internal/expand/engine.go:54-124).
+
+Every rank's phase times (closure exchange, closure build, check / expand) and its closure
+exchange level by level (keto_partition_levels_get: objects asked, request bytes, tuples
+received, tuple bytes shipped, ms) go to gpurun_out/c5x40_phases.json (profiles/ keeps a copy
+per round).
 """
+import json
 import os
 import socket
 import sys
@@ -33,6 +39,7 @@ WORLD = 8
 SCALE = 40
 N = 1 << 20
 SAMPLE = 1 << 16
+ROOTS = 512  # Expand roots per rank
 
 
 def _free_port():
@@ -121,8 +128,12 @@ def _worker(rank, world, port, out):
         t0 = time.perf_counter()
         a1, e1 = eng.check_batch(q)
         st1 = dict(eng.last)
+        lv1 = eng.level_stats()
         _log(rank, f"batch 1: {time.perf_counter() - t0:.1f} s, closure {st1['tuples']} tuples / {st1['levels']} levels, {_free_gib()}")
+        t0 = time.perf_counter()
         a2, e2 = eng.check_batch(q)
+        wall2 = time.perf_counter() - t0
+        st2, lv2 = dict(eng.last), eng.level_stats()
         idx = _sample(70 + rank)
         qs = q[idx]
         rows = lambda k: synth.drive_object_tuples(wl, k)  # noqa: E731 -- the generator's rows, not the device's
@@ -134,8 +145,11 @@ def _worker(rank, world, port, out):
         dec, err, _ = orc.check_batch(qs.view(refsem.QUERY_DT), threads=2)
         _log(rank, f"oracle sample {len(idx)} over a host closure of {len(ct)} tuples: {time.perf_counter() - t0:.1f} s")
         orc.close()
-        roots = _roots(km, wl, 32, 90 + rank)
+        roots = _roots(km, wl, ROOTS, 90 + rank)
+        t0 = time.perf_counter()
         nodes, offs, xerr = eng.expand_batch(roots)
+        xwall = time.perf_counter() - t0
+        xst, xlv = dict(eng.last), eng.level_stats()
         ct2 = closure(rows, roots["ns"], roots["obj"], wl.max_depth + 1)
         orc2 = refsem.Oracle(w, ct2.view(refsem.TUPLE_DT), shard_bytes=True)
         orc2.set_limits(wl.max_depth, wl.max_width)
@@ -158,6 +172,13 @@ def _worker(rank, world, port, out):
             "rest_allowed": float(a1[trunc:].mean()),
             "sample": len(idx), "dec_mis": int((a1[idx] != dec).sum()), "err_mis": int((e1[idx] != err).sum()),
             "host_closure": len(ct), "tree_mis": tree_mis, "xerr": int((xerr != 0).sum()), "tree_nodes": n_nodes,
+            "phases": {"check_batch": {"queries": N, "wall_s": wall2, **{k: st2[k] for k in (
+                           "closure_s", "build_s", "run_s", "tuples", "objects", "levels", "bytes_sent")},
+                           "levels_detail": lv2},
+                       "check_batch_first": {k: st1[k] for k in ("closure_s", "build_s", "run_s", "tuples")},
+                       "expand_batch": {"roots": ROOTS, "wall_s": xwall, "tree_nodes": int(offs[-1]), **{k: xst[k] for k in (
+                           "closure_s", "build_s", "run_s", "tuples", "objects", "levels", "bytes_sent")},
+                           "levels_detail": xlv}},
         }
         eng.close()
     except BaseException:
@@ -174,6 +195,12 @@ def test_c5_x40_eight_ranks_matches_oracle():
         mp.spawn(_worker, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
         res = dict(out)
     assert sorted(res) == list(range(WORLD))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "c5x40_phases.json"), "w") as f:
+        json.dump({"what": "tests/test_gpu_c5.py: C3 x40 over 8 gloo ranks sharing one MI355X; per rank the second "
+                           "(warm) 2^20-query check batch and one 512-root Expand batch, phase times from "
+                           "keto_partition_stats_get, the closure exchange per level from keto_partition_levels_get",
+                   "ranks": {str(k): v["phases"] for k, v in sorted(res.items())}}, f, indent=1)
     total = res[0]["total"]
     assert total > 4_000_000_000  # configs[4]: C3 x40
     assert sum(r["n_part"] for r in res.values()) == total  # the partitions cover the graph once
@@ -183,7 +210,7 @@ def test_c5_x40_eight_ranks_matches_oracle():
         assert r["errors"] == 0, r
         assert r["dec_mis"] == 0 and r["err_mis"] == 0, r
         assert r["tree_mis"] == 0 and r["xerr"] == 0, r
-        assert r["tree_nodes"] > 32
+        assert r["tree_nodes"] > ROOTS
         assert 0.2 < r["allowed"] < 0.8
         assert r["trunc_allowed"] < r["rest_allowed"]  # the truncation sub-batch really truncates
         assert 0 < r["closure"] < total and r["bytes_sent"] > 0

@@ -43,7 +43,49 @@ def _oracle(wl):
     return orc
 
 
-def test_single_rank_partitioned_matches_oracle():
+@pytest.fixture
+def closure_path(monkeypatch):
+    """a one-rank job through the per-batch closure path (KETO_PART_CLOSURE: by default one rank
+    runs on its resident snapshot), to test the closure machinery on one GPU"""
+    monkeypatch.setenv("KETO_PART_CLOSURE", "1")
+
+
+def test_single_rank_resident_snapshot_matches_oracle():
+    """a job of one rank (no collective) holds the whole graph: its partition becomes one resident
+    snapshot at creation and every batch runs on it -- no closure, no per-batch build; the same
+    decisions, pipelined batches and Expand trees as the oracle over the whole graph"""
+    wl = _wl()
+    q = synth.drive_queries(wl, 20_000, seed=31)
+    q["max_depth"][:2000] = np.random.default_rng(0).integers(1, 8, 2000)
+    eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, wl.tuples,
+                                      max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    allowed, err = eng.check_batch(q, count_work=True)
+    assert eng.last["tuples"] == 0 and eng.last["levels"] == 0 and eng.level_stats() == []
+    assert eng.last["queries"] == len(q) and eng.last["rows"] > 0
+    orc = _oracle(wl)
+    dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+    np.testing.assert_array_equal(err, oerr)
+    np.testing.assert_array_equal(allowed, dec)
+    q2 = synth.drive_queries(wl, 5000, seed=32)
+    d2, oe2, _ = orc.check_batch(queries_to_oracle(q2), threads=8)
+    many = eng.check_batches([q2, q, q2, q, q2])
+    for (a, e), d, oe in zip(many, (d2, dec, d2, dec, d2), (oe2, oerr, oe2, oerr, oe2)):
+        np.testing.assert_array_equal(a, d)
+        np.testing.assert_array_equal(e, oe)
+    roots = _roots(wl, np.random.default_rng(1), 256)
+    nodes, offs, xerr = eng.expand_batch(roots)
+    assert (xerr == 0).all()
+    for i, r in enumerate(roots):
+        on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), wl.max_depth)
+        mine = nodes[int(offs[i]):int(offs[i + 1])]
+        assert len(mine) == len(on)
+        for f_p, f_o in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"),
+                         ("s_rel", "srel"), ("n_children", "n_children")):
+            np.testing.assert_array_equal(mine[f_p], on[f_o])
+    eng.close()
+
+
+def test_single_rank_partitioned_matches_oracle(closure_path):
     # closure buffers sized by the batches alone (no 64 MB floor): a later, larger batch then
     # outgrows the buffer its slot kept, and the one-rank closure falls back to the synchronous
     # levels (read once per process, before its first partition batch)
@@ -76,6 +118,9 @@ def test_single_rank_partitioned_matches_oracle():
     finally:
         del os.environ["KETO_PART_SYNC_LEVELS"]
     assert eng.last["tuples"] == len(ref2) and eng.last["levels"] == levels2
+    lv = eng.level_stats()  # the synchronous levels: per level, timed
+    assert len(lv) == levels2 and sum(x["tuples"] for x in lv) == len(ref2) and all(x["ms"] > 0 for x in lv)
+    assert sum(x["objects"] for x in lv) == eng.last["objects"]
     np.testing.assert_array_equal(a3, d2)
     # pipelined batches (keto_partition_check_many): each batch's closure on the helper thread
     # while the batch before it is built and checked; the same answers in the same order
@@ -104,7 +149,7 @@ def test_single_rank_partitioned_matches_oracle():
     eng.close()
 
 
-def test_single_rank_closure_outgrows_its_buffer():
+def test_single_rank_closure_outgrows_its_buffer(closure_path):
     """a batch whose closure is over twice the largest its slot saw: the one-rank closure
     (closure_self, no host round trip per level) overflows the buffer it was sized by, and the
     batch's closure is redone on the synchronous levels, which grow it"""
@@ -148,6 +193,9 @@ def _worker(rank, world, port, out, device_buffers=False):
         q = synth.drive_queries(wl, 8192, seed=40 + rank)
         allowed, err = eng.check_batch(q)
         st = dict(eng.last)
+        lv = eng.level_stats()  # per level: the bytes of both exchanges (the batch's subject list aside)
+        lv_bytes = sum(x["request_bytes"] + x["tuple_bytes_sent"] for x in lv)
+        lv_ok = len(lv) == st["levels"] and 0 < lv_bytes <= st["bytes_sent"] and sum(x["objects"] for x in lv) == st["objects"]
         orc = _oracle(wl)
         dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=4)
         roots = _roots(wl, np.random.default_rng(rank), 64)
@@ -166,7 +214,7 @@ def _worker(rank, world, port, out, device_buffers=False):
         for (a, e), d, oe in zip(many, (dec, d2, dec), (oerr, oe2, oerr)):
             pipe_mis += int((a != d).sum() + (e != oe).sum())
         out[rank] = (int((allowed != dec).sum()), int((err != oerr).sum()), int(dec.sum()), st["bytes_sent"],
-                     tree_mis, int((xerr != 0).sum()), pipe_mis)
+                     tree_mis, int((xerr != 0).sum()), pipe_mis, lv_ok)
         eng.close()
     finally:
         dist.destroy_process_group()
@@ -183,6 +231,6 @@ def test_two_rank_partitioned_matches_oracle(device_buffers):
         mp.spawn(_worker, args=(world, _free_port(), out, device_buffers), nprocs=world, join=True)
         res = dict(out)
     for r in range(world):
-        dmis, emis, n_allowed, sent, tree_mis, xerr, pipe_mis = res[r]
-        assert dmis == 0 and emis == 0 and tree_mis == 0 and xerr == 0 and pipe_mis == 0
+        dmis, emis, n_allowed, sent, tree_mis, xerr, pipe_mis, lv_ok = res[r]
+        assert dmis == 0 and emis == 0 and tree_mis == 0 and xerr == 0 and pipe_mis == 0 and lv_ok
         assert n_allowed > 0 and sent > 0

@@ -1,5 +1,6 @@
-// TEST/DEBUG TOOL ONLY: the CPU emulation build has no hipCUB, so keto_partition_* (csrc/partition.hip)
-// is not emulated; its entry points fail loudly here.
+// TEST/DEBUG TOOL ONLY: keto_partition_* (csrc/partition.hip, csrc/devprim.hip) is not emulated -- its
+// kernels are written for 256-thread blocks of 64-lane waves (ballot ranks, one digit per thread),
+// which the one-lane emulation cannot run; its entry points fail loudly here.
 #include "../../djy-keto_amd/csrc/engine.hpp"
 
 namespace keto {
@@ -15,5 +16,6 @@ void partition_check_many(PartitionHandle *, uint32_t, const keto_query *const *
 uint64_t partition_expand(PartitionHandle *, const keto_subject_set *, uint64_t) { unavailable(); }
 void partition_expand_result(PartitionHandle *, keto_tree_node *, uint64_t, uint64_t *, int32_t *) { unavailable(); }
 void partition_stats(PartitionHandle *, keto_partition_stats *) { unavailable(); }
+void partition_levels(PartitionHandle *, keto_partition_level *, uint32_t, uint32_t *) { unavailable(); }
 void partition_free(PartitionHandle *) {}
 }  // namespace keto
