@@ -287,18 +287,29 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
     r["obj"][h:] = rng.integers(0, wl.meta["folders_per_root"], n - h)
     xe = km.ExpandEngine(snap, stream, max_read_depth=wl.max_depth)
     nodes, offs, err = xe.build_trees(r)  # warm-up (sizes the output buffer)
+    # the API into pageable numpy memory, then into pinned memory (keto_host_alloc: the trees'
+    # one D2H runs as a straight DMA) -- what a Go shim gets with C.malloc vs keto_host_alloc
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        xe.build_trees(r)
+    dt_pageable = (time.perf_counter() - t0) / reps
+    pin = km.PinnedArray(int(offs[n]) * 5 // 4 + 64, km.TREE_DT)
+    xe.build_trees(r, out=pin)
     stream.counters(reset=True)
     stream.expand_time(reset=True)
     t0 = time.perf_counter()
     for _ in range(reps):
-        nodes, offs, err = xe.build_trees(r)
+        nodes, offs, err = xe.build_trees(r, out=pin)
     dt = (time.perf_counter() - t0) / reps
+    nodes = nodes.copy()
+    pin.free()
     c = stream.counters(reset=True)
     ms, nb = stream.expand_time(reset=True)
     kms = ms / max(1, nb)
     # algorithmic bytes: 8*rows + 4*edges + 12*out_nodes per batch
     xbytes = (8 * c["rows"] + 4 * c["edges"] + 12 * c["out_nodes"]) / reps
-    return {"roots_per_batch": n, "ms_per_batch": dt * 1e3, "trees_per_s": n / dt, "nodes_per_batch": int(offs[n]),
+    return {"roots_per_batch": n, "ms_per_batch": dt * 1e3, "ms_per_batch_pageable_out": dt_pageable * 1e3,
+            "trees_per_s": n / dt, "nodes_per_batch": int(offs[n]),
             "errors": int((err != 0).sum()), "max_read_depth": wl.max_depth,
             "traversal_kernel_ms": kms,
             "roofline": {"bound": "hbm", "achieved": xbytes / (kms * 1e-3) / 1e9 if kms else None, "peak": HBM_PEAK_GBS,
@@ -306,8 +317,9 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
                          "algorithmic_bytes_per_batch": xbytes,
                          "bytes_model": "8*rows + 4*edges + 12*out_nodes (SURVEY.md 8.1 (d))",
                          "kernel": "expand_wave (wave per root, one traversal) + fallback count pass if any"},
-            "note": "ms_per_batch: host roots in, trees out (API form, root order) incl. PCIe; roots: Group#members "
-                    "and Folder#viewers"}
+            "note": "ms_per_batch: host roots in, trees out into pinned host memory (API form, root order) incl. "
+                    "PCIe; ms_per_batch_pageable_out: the same into pageable memory; traversal_kernel_ms: HIP events "
+                    "around the traversal on the engine stream; roots: Group#members and Folder#viewers"}
 
 
 def store_probe(km, wl, q, n_ins: int = 600, n_del: int = 400):
@@ -480,6 +492,12 @@ def run_c5(args, rank, world, device, dist_on):
         dist.barrier()
     elapsed_local = time.perf_counter() - t_start
     pipe_vs_first = int((outs[0][0] != allowed).sum())
+    # every distinct timed batch again, counted (the DFS interpreter on the same closure / snapshot)
+    pipe_vs_dfs = 0
+    for b, (a, _) in zip(batches, outs):
+        a2, _ = eng.check_batch(b, count_work=True)
+        pipe_vs_dfs += int((a2 != a).sum())
+    levels_detail = eng.level_stats()
     value, elapsed, total = job_rate(elapsed_local, args.batch * args.steps, f"cuda:{device}" if dist_on else "cpu")
     ranks_ms = per_rank_ms(elapsed_local / args.steps * 1e3, f"cuda:{device}" if dist_on else "cpu")
     ms_step = elapsed_local / args.steps * 1e3
@@ -489,6 +507,9 @@ def run_c5(args, rank, world, device, dist_on):
     check_bytes = 8 * cw["rows"][0] + 4 * cw["edges"][0] + 8 * cw["probes"][0] + 17 * cw["queries"][0]
     step_bytes = check_bytes + 3 * 48 * closure_tuples
     achieved = step_bytes / (ms_step * 1e-3) / 1e9
+    resident = eng.last.get("levels", 0) == 0 and closure_tuples == 0
+    how = ("one rank: the partition is the whole graph, built once into a resident snapshot -- no closure, no "
+           "per-batch build" if resident else f"closure of max_read_depth+1 = {eng.levels()} levels per batch")
     out = {
         "metric": METRIC, "value": value, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "per_rank_ms_per_step": ranks_ms,
@@ -496,8 +517,7 @@ def run_c5(args, rank, world, device, dist_on):
         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (seeded Drive-style folder forest, BASELINE config 5; generated per partition)",
         "config": {"workload": f"C5 Drive-style x{args.scale}: {wl.meta['n_tuples']} tuples partitioned by "
-                               f"object over {world} rank(s), {args.batch} checks/batch/GPU, closure of "
-                               f"max_read_depth+1 = {eng.levels()} levels per batch",
+                               f"object over {world} rank(s), {args.batch} checks/batch/GPU, {how}",
                    "tuples": int(wl.meta["n_tuples"]), "batch_per_gpu": args.batch,
                    "parallelism": f"object partition x{world} (RCCL all-to-all closure exchange per level)"},
         "allowed_fraction": float(allowed.mean()),
@@ -507,14 +527,17 @@ def run_c5(args, rank, world, device, dist_on):
                              "check; phases_ms_per_step and sequential_ms_per_step: one batch (the counted one) again "
                              "and again, one call at a time (warm caches: not comparable with value)",
                      "sequential_ms_per_step": seq_ms, "distinct_batches": len(batches),
-                     "first_batch_vs_counted_mismatches": pipe_vs_first},
+                     "first_batch_vs_counted_mismatches": pipe_vs_first,
+                     "mismatches": pipe_vs_dfs,
+                     "mismatches_what": "every distinct timed batch vs a counted rerun of it (DFS interpreter)"},
         "closure": {"tuples": eng.last["tuples"], "objects": eng.last["objects"], "levels": eng.last["levels"],
                     "bytes_sent": eng.last["bytes_sent"],
-                    "partition_tuples": n_part},
+                    "partition_tuples": n_part, "levels_detail": levels_detail},
         "shared_gpu": bool(dist_on and shared),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "the whole step: closure exchange + closure build + check (one rank)",
+                     "kernel": ("the whole step: H2D + check path + D2H on the resident snapshot" if resident else
+                                "the whole step: closure exchange + closure build + check (one rank)"),
                      "algorithmic_bytes_per_step": int(step_bytes), "check_bytes": int(check_bytes),
                      "closure_tuples": int(closure_tuples),
                      "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (check) + 3*48*closure tuples"},
@@ -793,6 +816,14 @@ def main(argv=None):
     dq.upload(stream, qb[0].array)
     eng.check_batch_device(dq, len(q), da, de, sync=True)
     pipe_vs_resident = int((da.download(stream, np.zeros(len(q), np.uint8)) != pipe_allowed[0]).sum())
+    # every distinct timed batch against the DFS interpreter (a counted rerun of the same queries:
+    # the reference recursion in its canonical order, pinned to the oracle by the GPU suite)
+    pipe_vs_dfs = 0
+    for k in range(nb):
+        dq.upload(stream, qb[k].array)
+        eng.check_batch_device(dq, len(q), da, de, sync=True, count_work=True)
+        pipe_vs_dfs += int((da.download(stream, np.zeros(len(q), np.uint8)) != pipe_allowed[k]).sum())
+    stream.counters(reset=True)
     log(f"[rank {rank}] pipelined: {elapsed_local / args.steps * 1e3:.2f} ms/step "
         f"({time.perf_counter() - t_setup:.1f}s since start)")
     # p99 batch latency over >= 100 batches of 64Ki queries (one rank's stream)
@@ -859,6 +890,9 @@ def main(argv=None):
                      "distinct_batches": nb, "streams": "1 compute + 2 copy",
                      "kernel_ms_per_batch": [ks / max(1, kn) for ks, kn in pipe_kernel],
                      "first_batch_vs_device_resident_mismatches": pipe_vs_resident,
+                     "mismatches": pipe_vs_dfs,
+                     "mismatches_what": f"all {nb} distinct timed batches ({nb * args.batch} queries) vs the DFS "
+                                        "interpreter on a counted rerun of the same queries",
                      "allowed_fraction": float(np.mean([a.mean() for a in pipe_allowed]))},
         "device_resident": {"checks_per_s": resident_rate, "ms_per_step": resident_el / args.steps * 1e3,
                             "kernel_ms": kernel_ms,

@@ -56,6 +56,7 @@ Stream::~Stream() {
     if (frontier_block.host) (void)hipHostFree(frontier_block.host);
     if (xw.mem) (void)hipFree(xw.mem);
     if (xw.outbuf) (void)hipFree(xw.outbuf);
+    if (xw.hpin) (void)hipHostFree(xw.hpin);
     for (hipEvent_t e : xw.ev)
         if (e) (void)hipEventDestroy(e);
     if (lists) (void)hipFree(lists);

@@ -190,6 +190,8 @@ struct Stream {
         int32_t *err = nullptr;
         uint32_t *fb_list = nullptr;
         hipEvent_t ev[2] = {nullptr, nullptr};  // around the traversal (expand_wave + the fallback's count pass)
+        void *hpin = nullptr;                   // pinned read-back of the offsets, errors and stage top
+        size_t hpin_bytes = 0;
         double ms_sum = 0;
         uint64_t batches = 0;
     } xw;

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "device_common.hpp"
@@ -408,6 +409,51 @@ __global__ __launch_bounds__(256) void expand_place(const keto_tree_node *stage,
     }
 }
 
+// root-order offsets of the trees on the device: offsets[i + 1] = offsets[i] + (err[i] ? 0 :
+// sizes[i]) -- one block, chunks of XO_RUN * blockDim roots with a carried sum (a batch is a few
+// thousand roots), so the host reads offsets and errors back in one copy
+constexpr uint32_t XO_BLOCK = 1024, XO_RUN = 4;
+__global__ __launch_bounds__(XO_BLOCK) void expand_offsets(const unsigned long long *sizes, const int32_t *err, uint32_t n,
+                                                         unsigned long long *offsets) {
+    __shared__ unsigned long long wsum[XO_BLOCK / 64 + 1];
+    const uint32_t t = threadIdx.x, lane = __lane_id(), w = t >> 6, nw = (blockDim.x + 63) >> 6;
+    unsigned long long carry = 0;
+    if (t == 0) offsets[0] = 0;
+    for (uint32_t b = 0; b < n; b += blockDim.x * XO_RUN) {
+        unsigned long long x[XO_RUN], acc = 0;
+        const uint32_t i0 = b + t * XO_RUN;
+        for (uint32_t k = 0; k < XO_RUN; k++) {
+            const uint32_t i = i0 + k;
+            x[k] = (i < n && !err[i]) ? sizes[i] : 0ull;
+            acc += x[k];
+        }
+        unsigned long long v = acc;
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const unsigned long long y = __shfl_up(v, off);
+            if (lane >= off) v += y;
+        }
+        if (lane == 63 || t == blockDim.x - 1) wsum[w] = v;  // (the wave's last lane)
+        __syncthreads();
+        if (t == 0) {
+            unsigned long long s = 0;
+            for (uint32_t k = 0; k < nw; k++) {
+                const unsigned long long y = wsum[k];
+                wsum[k] = s;
+                s += y;
+            }
+            wsum[nw] = s;
+        }
+        __syncthreads();
+        unsigned long long o = carry + wsum[w] + v - acc;
+        for (uint32_t k = 0; k < XO_RUN; k++) {
+            o += x[k];
+            if (i0 + k < n) offsets[i0 + k + 1] = o;
+        }
+        carry += wsum[nw];
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
@@ -478,7 +524,7 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         while (nc < n) nc <<= 1;
         const uint64_t sc = std::max<uint64_t>(X.stage_cap, 1u << 22);
         const size_t bytes = xal(64) + xal(grid * XW_PRIV * sizeof(keto_tree_node)) + xal(sc * sizeof(keto_tree_node)) +
-                             3 * xal(nc * 8) + xal(nc * 4) + xal(nc * 4);
+                             2 * xal(nc * 8) + xal((nc + 1) * 8) + xal(nc * 4) + xal(nc * 4);
         KETO_HIP(hipMalloc(&X.mem, bytes));
         char *p = static_cast<char *>(X.mem);
         X.ctrl = reinterpret_cast<unsigned long long *>(p);
@@ -492,13 +538,22 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         X.soff = reinterpret_cast<unsigned long long *>(p);
         p += xal(nc * 8);
         X.offsets = reinterpret_cast<uint64_t *>(p);
-        p += xal(nc * 8);
+        p += xal((nc + 1) * 8);
         X.err = reinterpret_cast<int32_t *>(p);
         p += xal(nc * 4);
         X.fb_list = reinterpret_cast<uint32_t *>(p);
         X.grid = grid;
         X.stage_cap = sc;
         X.ncap = nc;
+    }
+    // pinned read-back: ctrl (stage top, fallback count), offsets[n + 1], errors[n]
+    const size_t hb = 64 + (n + 1) * 8 + n * 4;
+    if (X.hpin_bytes < hb) {
+        if (X.hpin) KETO_HIP(hipHostFree(X.hpin));
+        X.hpin = nullptr;
+        X.hpin_bytes = 0;
+        KETO_HIP(hipHostMalloc(&X.hpin, 2 * hb, 0));
+        X.hpin_bytes = 2 * hb;
     }
     KETO_HIP(hipMemsetAsync(X.ctrl, 0, 64, st.stream));
     // KETO_EXPAND_WAVE=0 (A/B, tests): every root through the lane kernel
@@ -533,35 +588,40 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
     } else {
         KETO_HIP(hipMemsetAsync(X.soff, 0xFF, n * 8, st.stream));
     }
-    unsigned long long h[3] = {0, 0, 0};
-    KETO_HIP(hipMemcpyAsync(h, X.ctrl, 24, hipMemcpyDeviceToHost, st.stream));
-    KETO_HIP(hipStreamSynchronize(st.stream));
-    const uint32_t nfb = wave ? (uint32_t)h[2] : (uint32_t)n;
+    // the roots past the wave kernel's LDS / staging space: the lane kernel counts them, reading
+    // their count from the device (no host round trip; with none its launches end at once)
     ExpandLaunch F{};
     F.roots = d_roots;
     F.n = n;
     F.max_depth = max_depth;
     F.sizes = reinterpret_cast<uint64_t *>(X.sizes);
-    F.offsets = X.offsets;
+    F.offsets = X.offsets;  // (root i's first node: offsets[i], read by the emit pass below)
     F.err = X.err;
     F.list = wave ? X.fb_list : nullptr;
     F.list_count = wave ? P.fb_count : nullptr;
-    F.nl = nfb;
-    if (nfb) {  // roots past the wave kernel's LDS / staging space: the lane kernel counts them
-        F.emit = false;
-        run_expand(s, st, F);
-    }
+    F.nl = n;
+    F.emit = false;
+    run_expand(s, st, F);
     KETO_HIP(hipEventRecord(X.ev[1], st.stream));
-    std::vector<unsigned long long> sizes(n);
-    KETO_HIP(hipMemcpyAsync(sizes.data(), X.sizes, n * 8, hipMemcpyDeviceToHost, st.stream));
-    KETO_HIP(hipMemcpyAsync(out_err, X.err, n * 4, hipMemcpyDeviceToHost, st.stream));
+    hipLaunchKernelGGL(expand_offsets, dim3(1), dim3(XO_BLOCK), 0, st.stream, X.sizes, X.err, (uint32_t)n,
+                       reinterpret_cast<unsigned long long *>(X.offsets));
+    KETO_HIP(hipGetLastError());
+    char *hp = static_cast<char *>(X.hpin);
+    unsigned long long *h = reinterpret_cast<unsigned long long *>(hp);
+    uint64_t *hoff = reinterpret_cast<uint64_t *>(hp + 64);
+    int32_t *herr = reinterpret_cast<int32_t *>(hp + 64 + (n + 1) * 8);
+    KETO_HIP(hipMemcpyAsync(h, X.ctrl, 24, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipMemcpyAsync(hoff, X.offsets, (n + 1) * 8, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipMemcpyAsync(herr, X.err, n * 4, hipMemcpyDeviceToHost, st.stream));
     KETO_HIP(hipStreamSynchronize(st.stream));
     float ms = 0;
     if (hipEventElapsedTime(&ms, X.ev[0], X.ev[1]) == hipSuccess) {
         X.ms_sum += ms;
         X.batches++;
     }
-    for (uint64_t i = 0; i < n; i++) out_offsets[i + 1] = out_offsets[i] + (out_err[i] ? 0 : sizes[i]);
+    std::memcpy(out_offsets, hoff, (n + 1) * 8);
+    std::memcpy(out_err, herr, n * 4);
+    const uint32_t nfb = wave ? (uint32_t)h[2] : (uint32_t)n;
     const uint64_t total = out_offsets[n];
     if (h[0] > X.stage_cap / 2) X.stage_cap = std::max<uint64_t>(X.stage_cap, 2 * h[0]), X.ncap = 0;  // (regrown next batch)
     if (total > out_cap || (total && !out_nodes)) return false;
@@ -573,15 +633,16 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         KETO_HIP(hipMalloc(&X.outbuf, total * sizeof(keto_tree_node)));
         X.out_cap = total;
     }
-    KETO_HIP(hipMemcpyAsync(X.offsets, out_offsets, n * 8, hipMemcpyHostToDevice, st.stream));
     hipLaunchKernelGGL(expand_place, dim3((uint32_t)std::min<uint64_t>(n, cus * 16)), dim3(256), 0, st.stream, X.stage, X.soff,
                        X.sizes, X.offsets, (uint32_t)n, X.outbuf);
     KETO_HIP(hipGetLastError());
     if (nfb) {
         F.emit = true;
+        F.nl = nfb;
         F.out = X.outbuf;
         run_expand(s, st, F);
     }
+    // one copy of the trees in root order (caller memory from keto_host_alloc: straight DMA)
     KETO_HIP(hipMemcpyAsync(out_nodes, X.outbuf, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st.stream));
     KETO_HIP(hipStreamSynchronize(st.stream));
     return true;

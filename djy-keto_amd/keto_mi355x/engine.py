@@ -321,15 +321,20 @@ class ExpandEngine:
         self.limits = _abi.Limits(max_read_depth, 100)
         self._cap = 0  # output nodes the last batch needed: sizes the next one (no count-pass retry)
 
-    def build_trees(self, roots: np.ndarray):
-        """roots: SUBJSET_DT array -> (nodes TREE_DT, offsets uint64[n+1], err int32[n])."""
+    def build_trees(self, roots: np.ndarray, out: "PinnedArray | None" = None):
+        """roots: SUBJSET_DT array -> (nodes TREE_DT, offsets uint64[n+1], err int32[n]).
+        out: a PinnedArray of TREE_DT (keto_host_alloc) the trees are copied into -- one DMA
+        instead of a staged pageable copy -- while it holds them."""
         r = np.ascontiguousarray(roots, dtype=_abi.SUBJSET_DT)
         n = len(r)
         offs = np.zeros(n + 1, dtype=np.uint64)
         err = np.zeros(max(1, n), dtype=np.int32)
         cap = max(64, 16 * n, self._cap)
         while True:
-            nodes = np.empty(cap, dtype=_abi.TREE_DT)  # filled by the library up to offs[n]
+            if out is not None and len(out.array) >= cap:
+                nodes, cap = out.array, len(out.array)
+            else:
+                nodes = np.empty(cap, dtype=_abi.TREE_DT)  # filled by the library up to offs[n]
             rc = lib().keto_expand_batch(self.snapshot.handle, self.stream.handle, r.ctypes.data, n,
                                          ctypes.byref(self.limits), nodes.ctypes.data, cap, offs.ctypes.data,
                                          err.ctypes.data)

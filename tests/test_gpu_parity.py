@@ -458,3 +458,41 @@ def test_expand_drive_trees_wave_and_fallback(stream, mode):
                          ("s_rel", "srel"), ("n_children", "n_children")):
             np.testing.assert_array_equal(mine[f_p], on[f_o])
     assert big > 10  # the mixed batch really sends trees to the fallback
+
+
+C1_OBJECTS = ["/cats", "/cats/1.mp4", "/cats/2.mp4"]
+C1_RELATIONS = ["owner", "view"]
+C1_SUBJECTS = ["cat lady", "*", "nobody"]
+
+
+def c1_queries(n: int = 10_000, seed: int = 42) -> list:
+    """BASELINE configs[0] as SURVEY.md 8.1 (d) configures it: n seed-42 uniform draws over the
+    18 combinations {/cats, /cats/1.mp4, /cats/2.mp4} x {owner, view} x {cat lady, *, nobody}"""
+    combos = [(o, r, s) for o in C1_OBJECTS for r in C1_RELATIONS for s in C1_SUBJECTS]
+    pick = np.random.default_rng(seed).integers(0, len(combos), n)
+    return [f"videos:{combos[i][0]}#{combos[i][1]}@{combos[i][2]}" for i in pick]
+
+
+def test_c1_cat_videos_as_configured(stream):
+    """configs[0]: the cat-videos example's 7 tuples (contrib/cat-videos-example/relation-tuples/
+    *.json, namespace `videos` without relation config, keto.yml), 10,000 seed-42 Checks over all
+    18 combinations in one batch: every decision equal to the oracle's, and every combination's
+    answer equal to the hand-derived fixture answers where it has one"""
+    fx = load("cat_videos")
+    w = refsem.World(namespaces=fx["namespaces"], max_depth=5, max_width=100)
+    t = w.tuple_array(fx["tuples"])
+    strs = c1_queries()
+    q = w.query_array([(s, 0) for s in strs])
+    assert len(set(strs)) == 18  # every combination is asked
+    snap = product_snapshot(w, t)
+    allowed, err = km.CheckEngine(snap, stream, max_read_depth=5, max_read_width=100).check_batch(queries_to_product(q))
+    orc = refsem.Oracle(w, t)
+    dec, oerr, _ = _oracle_decisions(orc, q, 5, 100)
+    np.testing.assert_array_equal(err, oerr)
+    np.testing.assert_array_equal(allowed, dec)
+    known = {c["query"]: c["allowed"] for c in fx["checks"] if c.get("depth", 0) == 0}
+    by_combo = {s: bool(a) for s, a in zip(strs, allowed)}
+    for s, a in known.items():
+        if s in by_combo:
+            assert by_combo[s] == a, s
+    assert 0 < allowed.mean() < 1

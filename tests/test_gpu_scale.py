@@ -84,9 +84,28 @@ def _check_config(wl, orc, seed):
     # the truncation sub-batch really truncates: shallower requests allow less
     trunc = a1[: N // 100].mean()
     assert trunc < a1[N // 100:].mean()
+    # Expand on the replicated snapshot at full size: 512 roots, every tree exact against the
+    # oracle's (internal/expand/engine.go:54-124), child order included
+    roots = _roots(wl, 512, seed + 100)
+    nodes, offs, xerr = km.ExpandEngine(snap, st, max_read_depth=wl.max_depth).build_trees(roots)
+    _check_trees(orc, wl, roots, nodes, offs, xerr)
     st.close()
     snap.close()
     return a1
+
+
+def _check_trees(orc, wl, roots, nodes, offs, xerr):
+    assert (xerr == 0).all()
+    n_nodes = 0
+    for i, r in enumerate(roots):
+        on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), wl.max_depth)
+        mine = nodes[int(offs[i]):int(offs[i + 1])]
+        assert len(mine) == len(on)
+        n_nodes += len(on)
+        for f_p, f_o in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"),
+                         ("s_rel", "srel"), ("n_children", "n_children")):
+            np.testing.assert_array_equal(mine[f_p], on[f_o])
+    assert n_nodes > len(roots)
 
 
 def test_c3_drive_100m_tuples():
@@ -128,10 +147,13 @@ def _roots(wl, n, seed):
     return r
 
 
-def test_c5_partitioned_one_rank(c4):
+def test_c5_partitioned_one_rank(c4, monkeypatch):
     """C5's data path on C4's graph: the partitioned engine (closure exchange, per-batch
-    device snapshot, unmodified kernels) on one rank, Check + 256 Expand roots."""
+    device snapshot, unmodified kernels) on one rank, Check + 256 Expand roots.  (A job of one
+    rank runs on a resident snapshot by default; KETO_PART_CLOSURE keeps the closure path, the
+    one every rank of a multi-rank job runs.)"""
     from keto_mi355x import partition
+    monkeypatch.setenv("KETO_PART_CLOSURE", "1")
     wl, orc = c4
     t0 = time.perf_counter()
     eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, wl.tuples,
@@ -150,15 +172,5 @@ def test_c5_partitioned_one_rank(c4):
     np.testing.assert_array_equal(a[idx], dec)
     roots = _roots(wl, 256, 26)
     nodes, offs, xerr = eng.expand_batch(roots)
-    assert (xerr == 0).all()
-    n_nodes = 0
-    for i, r in enumerate(roots):
-        on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), wl.max_depth)
-        mine = nodes[int(offs[i]):int(offs[i + 1])]
-        assert len(mine) == len(on)
-        n_nodes += len(on)
-        for f_p, f_o in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"),
-                         ("s_rel", "srel"), ("n_children", "n_children")):
-            np.testing.assert_array_equal(mine[f_p], on[f_o])
-    assert n_nodes > 256
+    _check_trees(orc, wl, roots, nodes, offs, xerr)
     eng.close()
