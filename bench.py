@@ -675,6 +675,13 @@ def main(argv=None):
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # CPU: launcher + rank protocol only
     argv = sys.argv[1:] if argv is None else list(argv)
     args = ap.parse_args(argv)
+    if os.environ.get("KETO_BENCH_MAPS"):  # diagnostics: the process's mappings at exit (map a crash's PCs)
+        import atexit
+
+        def dump_maps(path=os.environ["KETO_BENCH_MAPS"]):
+            with open("/proc/self/maps") as f, open(path, "w") as o:
+                o.write(f.read())
+        atexit.register(dump_maps)
 
     # --gpus N decides the job size: without torchrun's environment this process launches the N
     # ranks itself (before anything initialises HIP); under torchrun the world must be N
