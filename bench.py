@@ -480,13 +480,18 @@ def run_c5(args, rank, world, device, dist_on):
         for k in phases:
             phases[k] += eng.last[k]
     seq_ms = (time.perf_counter() - t_seq) / n_seq * 1e3
-    # the timed region: K fresh seeded batches through one keto_partition_check_many call
-    batches = [q] + [synth.drive_queries(wl, args.batch, seed=shard_seed(11 + 1000 * s, rank)) for s in range(1, args.steps)]
+    # the timed region: K fresh seeded batches through one keto_partition_check_many call, in
+    # pinned host memory as the C4 line's (keto_host_alloc: straight DMA for the one-rank path)
+    pin_q = [km.PinnedArray(args.batch, km.QUERY_DT) for _ in range(args.steps)]
+    pin_o = [(km.PinnedArray(args.batch, np.uint8), km.PinnedArray(args.batch, np.int32)) for _ in range(args.steps)]
+    for s_, pq in enumerate(pin_q):
+        pq.array[:] = q if s_ == 0 else synth.drive_queries(wl, args.batch, seed=shard_seed(11 + 1000 * s_, rank))
+    batches = [pq.array for pq in pin_q]
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    outs = eng.check_batches(batches)
+    outs = eng.check_batches(batches, outs=[(a.array, e.array) for a, e in pin_o])
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -522,10 +527,14 @@ def run_c5(args, rank, world, device, dist_on):
                    "parallelism": f"object partition x{world} (RCCL all-to-all closure exchange per level)"},
         "allowed_fraction": float(allowed.mean()),
         "phases_ms_per_step": {k: v / n_seq * 1e3 for k, v in phases.items()},
-        "pipeline": {"what": "value: the K timed fresh batches in one keto_partition_check_many call -- batch k+1's "
-                             "closure (its query upload included) on a helper thread beside batch k's remap, build and "
-                             "check; phases_ms_per_step and sequential_ms_per_step: one batch (the counted one) again "
-                             "and again, one call at a time (warm caches: not comparable with value)",
+        "pipeline": {"what": ("value: the K timed fresh batches (pinned host memory) in one keto_partition_check_many "
+                              "call -- " + ("one rank: each batch's H2D + check path + D2H enqueued on the engine stream "
+                                            "(KETO_F_ASYNC, two copy streams), one synchronisation at the end"
+                                            if resident else
+                                            "batch k+1's closure (its query upload included) on a helper thread beside "
+                                            "batch k's remap, build and check") +
+                              "; phases_ms_per_step and sequential_ms_per_step: one batch (the counted one) again and "
+                              "again, one call at a time (warm caches: not comparable with value)"),
                      "sequential_ms_per_step": seq_ms, "distinct_batches": len(batches),
                      "first_batch_vs_counted_mismatches": pipe_vs_first,
                      "mismatches": pipe_vs_dfs,

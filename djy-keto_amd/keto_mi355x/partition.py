@@ -159,11 +159,14 @@ class PartitionedEngine:
             self.last_work = {k: [self.last[k], 0, 0] for k in ("rows", "edges", "probes", "queries")}
         return allowed, err[:len(q)]
 
-    def check_batches(self, batches: list, count_work: bool = False):
+    def check_batches(self, batches: list, count_work: bool = False, outs: list | None = None):
         """several batches in order, pipelined (keto_partition_check_many: batch k+1's closure
-        runs while batch k is built and checked) -> [(allowed, err)] per batch"""
+        runs while batch k is built and checked) -> [(allowed, err)] per batch.  outs: optional
+        [(allowed u8[n], err i32[n])] to write into (e.g. pinned arrays, keto_host_alloc: the
+        one-rank path's copies then run as straight DMA, as keto_check_batch's do)."""
         qs = [np.ascontiguousarray(b, dtype=_abi.QUERY_DT) for b in batches]
-        outs = [(np.zeros(len(q), np.uint8), np.zeros(max(1, len(q)), np.int32)) for q in qs]
+        if outs is None:
+            outs = [(np.zeros(len(q), np.uint8), np.zeros(max(1, len(q)), np.int32)) for q in qs]
         k = len(qs)
         P = ctypes.c_void_p * max(1, k)
         qp = P(*[q.ctypes.data if len(q) else None for q in qs])
