@@ -67,6 +67,7 @@ struct FrontierParams {
     uint32_t gen;
     uint32_t gen_cap;            // generations this batch may run (MAX_GEN; asynchronous batches: the speculated count)
     uint32_t *qrouted;           // [n / 32] one bit per query position: routed to the DFS interpreter (L2-resident)
+    uint32_t *any_routed;        // != 0 once some query of the batch was routed (cleared with ctrl)
     uint32_t budget;
     unsigned long long *dkeys;   // decisive (scope, visited key) pairs of the batch (epoch-tagged)
     uint32_t *dcnt;              // their occurrences, counted by fr_repeat
@@ -151,6 +152,7 @@ __device__ __forceinline__ uint32_t dbit(unsigned long long key) {
 // a 4-byte word per query that every goal fetched as a random line from HBM.
 __device__ __forceinline__ void route(const FrontierParams &P, uint32_t pos) {
     atomicOr(&P.qrouted[pos >> 5], 1u << (pos & 31u));
+    if (!*P.any_routed) atomicOr(P.any_routed, 1u);  // (rare: one word, written once per batch in practice)
 }
 __device__ __forceinline__ bool routed(const FrontierParams &P, uint32_t pos) { return (P.qrouted[pos >> 5] >> (pos & 31u)) & 1u; }
 
@@ -259,7 +261,15 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
 #endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
-        // goals of queries routed meanwhile still run (rare); they can no longer spawn
+        // goals of queries routed meanwhile still run (rare); they can no longer spawn.  A goal
+        // reads its query's routed bit only once some query of the batch was routed: one word per
+        // block step instead of a load per goal (routing is best-effort pruning here -- the
+        // decision at generation 0 reads the bits themselves)
+#ifndef KETO_NO_RFLAG  // (A/B builds: every goal reads its bit)
+        const bool any_routed = *static_cast<volatile const uint32_t *>(P.any_routed) != 0u;
+#else
+        const bool any_routed = true;
+#endif
         bool live = j < cnt;
         uint32_t i = live ? gen_goal(P, gm, j) : 0u;
         uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
 #endif
         const uint32_t node = g.x, pos = g.y, w = g.z, scope = g.w;
         const uint32_t d = w & GD_MAX, kind = (w >> 12) & 7u, op = w >> 16;
-        const bool qr = live && routed(P, pos);
+        const bool qr = live && any_routed && routed(P, pos);
         // The loads the goal kinds start from, issued together: the row an ES / TTU reads, and
         // the subject's membership record (IA direct check, ES lookahead, OR shortcut).
         uint32_t rnode = NONE32;
@@ -606,6 +616,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     P.gbase = gbase;
     P.gcount = gcount;
     P.qrouted = f.qrouted;
+    P.any_routed = fb_count + 1;
     P.budget = L.budget;
     P.dkeys = f.dkeys;
     P.dcnt = f.dcnt;

@@ -95,6 +95,7 @@ inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p += v; r
 inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) { auto o = *p; *p += v; return o; }
 inline unsigned long long atomicOr(unsigned long long *p, unsigned long long v) { auto o = *p; *p |= v; return o; }
 inline uint32_t atomicOr(uint32_t *p, uint32_t v) { uint32_t o = *p; *p |= v; return o; }
+inline unsigned long long atomicAnd(unsigned long long *p, unsigned long long v) { auto o = *p; *p &= v; return o; }
 inline unsigned long long atomicMin(unsigned long long *p, unsigned long long v) { auto o = *p; *p = std::min(o, v); return o; }
 inline unsigned long long atomicMax(unsigned long long *p, unsigned long long v) { auto o = *p; *p = std::max(o, v); return o; }
 inline uint32_t atomicCAS(uint32_t *p, uint32_t c, uint32_t v) {
