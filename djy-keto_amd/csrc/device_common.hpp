@@ -36,7 +36,14 @@ __device__ __forceinline__ uint32_t ent_lookup(const DevSnapshot &s, uint32_t ns
     const uint4 b = s.ent_rank[ck >> 6];
     const uint64_t m = (uint64_t)b.x | ((uint64_t)b.y << 32);
     const uint32_t j = (uint32_t)(ck & 63);
-    if (!((m >> j) & 1ull)) return NONE32;
+    if (!((m >> j) & 1ull)) {
+        if (!s.ext) return NONE32;
+        for (uint32_t h = (uint32_t)mix64((((uint64_t)ns << 32) | obj) + 1) & s.ext_mask;; h = (h + 1) & s.ext_mask) {
+            const uint4 x = s.ext[h];  // (at most half full: every walk ends at an empty slot)
+            if (x.z == NONE32) return NONE32;
+            if (x.x == obj && x.y == ns) return x.z;
+        }
+    }
     return b.z + (uint32_t)__popcll(m & ((1ull << j) - 1ull));
 }
 

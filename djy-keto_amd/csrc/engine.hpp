@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -25,6 +26,18 @@ struct Error : std::runtime_error {
         if (_e != hipSuccess)                                                                       \
             throw ::keto::Error(KETO_E_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
     } while (0)
+
+// Room a store snapshot keeps for objects created after it (keto_store_snapshot_patch): spare
+// entities in every namespace, between its real entities and its phantom, handed out once across
+// every snapshot patched from it (the family shares this record: no spare is given twice)
+struct Spares {
+    std::mutex mu;
+    std::vector<uint32_t> first, count, used;  // per namespace
+};
+struct BuildOpts {
+    uint32_t uuid_capacity = 0;  // id space (>= cfg n_uuids): ids past the caller's are unknown until written
+    bool spares = false;         // spare entities per namespace (n_real / 16 + 256)
+};
 
 // Host mirror of the snapshot + its device buffers.
 struct Snapshot {
@@ -48,6 +61,8 @@ struct Snapshot {
     uint64_t store_id = 0;     // the keto_store it was cut from (0: built directly)
     uint64_t cfg_hash = 0;     // config_hash of the configuration it was compiled from (patches keep it)
     uint64_t probe_used = 0;   // probe-hash slots holding a key or a tombstone (patches keep the load bounded)
+    std::shared_ptr<Spares> spares;  // (store snapshots: room for new objects)
+    std::vector<uint4> ext;          // {obj, ns, entity, 0} of the objects placed on spares (dev.ext's entries)
 
     // a device allocation of this snapshot (back to the pool with its last sharer)
     void own(void *p, size_t bytes);
@@ -59,9 +74,9 @@ struct Snapshot {
 };
 
 Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
-                         bool sched_weights = true);
+                         bool sched_weights = true, const BuildOpts *opts = nullptr);
 // 64-bit FNV-1a of everything a snapshot compiles from its configuration (name tables, AST JSON,
-// uuid space, strict mode; not the device): equal hashes = the same compiled tables
+// strict mode; not the device, not n_uuids): equal hashes = the same compiled tables
 uint64_t config_hash(const keto_snapshot_config *cfg);
 // snapshot.cpp: a built snapshot to a file and back (keto_snapshot_save / _load)
 void save_snapshot(const Snapshot &s, const char *path);

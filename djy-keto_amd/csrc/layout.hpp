@@ -106,6 +106,10 @@ struct DevSnapshot {
     // {set bits lo, hi, entity of the block's first set bit, 0}; an unset bit = no entity
     const uint4 *ent_rank;
     uint64_t ent_stride;
+    // objects a patched store snapshot created (keto_store_snapshot_patch): open addressing over
+    // {obj, ns, entity, 0}, entity NONE32 = empty; consulted when the rank table has no entity
+    const uint4 *ext;
+    uint32_t ext_mask;
     // membership probe hash for "heavy" subjects (reverse row longer than probe_k):
     // 16-byte buckets of two keys ((subject_idx<<32)|node)+1, linear probing over buckets
     const uint4 *probe;

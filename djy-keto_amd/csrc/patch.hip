@@ -344,6 +344,12 @@ __global__ __launch_bounds__(BLK) void k_probe_apply(unsigned long long *probe, 
     }
 }
 
+// ent_obj of the spare entities new objects were placed on
+__global__ __launch_bounds__(BLK) void k_ent_obj_set(uint32_t *ent_obj, const uint2 *set, uint32_t m) {
+    const uint64_t i = gid();
+    if (i < m) ent_obj[set[i].x] = set[i].y;
+}
+
 struct Touched {  // a touched row or subject, keyed for the scan
     uint4 key;
     uint32_t idx;  // node / subject index
@@ -372,12 +378,100 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     // ---- 1. place the touched tuples in the base's node space -----------------------------------
     std::vector<keto_tuple> ht(n_touched);
     std::vector<uint4> pl(n_touched);
-    if (n_touched) {
+    DevSnapshot Dp = D;  // the base's view, plus the objects this patch creates (step 0 below)
+    std::vector<uint4> ext = B.ext;
+    void *ext_dev = nullptr;  // a new ext table (owned by the new snapshot once it exists)
+    std::vector<uint2> ent_set;  // {spare entity, obj}
+    auto place_all = [&] {
         DevBuf d_pl(sizeof(uint4) * n_touched);
-        KETO_HIP(hipMemcpy(ht.data(), touched, sizeof(keto_tuple) * n_touched, hipMemcpyDeviceToHost));
-        hipLaunchKernelGGL(k_place, grid_for(n_touched), dim3(BLK), 0, 0, D, touched, n_touched, static_cast<uint4 *>(d_pl.p));
+        hipLaunchKernelGGL(k_place, grid_for(n_touched), dim3(BLK), 0, 0, Dp, touched, n_touched, static_cast<uint4 *>(d_pl.p));
         KETO_HIP(hipGetLastError());
         KETO_HIP(hipMemcpy(pl.data(), d_pl.p, sizeof(uint4) * n_touched, hipMemcpyDeviceToHost));
+    };
+    if (n_touched) {
+        KETO_HIP(hipMemcpy(ht.data(), touched, sizeof(keto_tuple) * n_touched, hipMemcpyDeviceToHost));
+        place_all();
+    }
+    // ---- 0. objects the inserts create: the reference writes a row for any object
+    // (relationtuples.go:104-126); an (ns, obj) -- row object or subject-set object -- that has no
+    // entity in the base but a slot for the relation and an id inside the base's id space goes on
+    // one of the namespace's spare entities (a store snapshot keeps them: BuildOpts), entered in
+    // the ext table ent_lookup consults.  A namespace whose visited keys alias across namespaces
+    // (relinfo bit 20) or that ran out of spares builds in full.
+    std::vector<std::pair<uint32_t, uint32_t>> fresh_objs;  // (ns, obj)
+    if (B.spares) {
+        auto needs_entity = [&](uint32_t ns, uint32_t obj, uint32_t rel) {
+            if (ns >= B.n_ns || rel >= B.n_rel || obj >= B.n_uuids) return false;
+            return nr_slot(B.nsrel[(size_t)ns * B.n_rel + rel]) != NO_SLOT;
+        };
+        for (uint64_t i = 0; i < n_touched; i++) {
+            if (!is_ins[i]) continue;
+            const keto_tuple &t = ht[i];
+            if (pl[i].x == NONE32 && needs_entity(t.ns, t.obj, t.rel)) fresh_objs.emplace_back(t.ns, t.obj);
+            if (t.subj_kind == 1 && pl[i].y == NONE32 && needs_entity(t.s_ns, t.s_obj, t.s_rel))
+                fresh_objs.emplace_back(t.s_ns, t.s_obj);
+        }
+        std::sort(fresh_objs.begin(), fresh_objs.end());
+        fresh_objs.erase(std::unique(fresh_objs.begin(), fresh_objs.end()), fresh_objs.end());
+        // (an object the row object check flagged may have an entity after all -- the tuple failed on
+        // its subject; those are filtered by the device lookup below)
+    }
+    if (!fresh_objs.empty()) {
+        std::vector<uint4> probe(fresh_objs.size());
+        {   // which of them really lack an entity (ent_lookup, ext included)
+            std::vector<keto_tuple> q(fresh_objs.size());
+            for (size_t k = 0; k < fresh_objs.size(); k++) {
+                q[k] = keto_tuple{};
+                q[k].ns = fresh_objs[k].first;
+                q[k].obj = fresh_objs[k].second;
+                uint32_t rel = 0;  // any relation with a slot in ns
+                while (rel < B.n_rel && nr_slot(B.nsrel[(size_t)q[k].ns * B.n_rel + rel]) == NO_SLOT) rel++;
+                q[k].rel = rel;
+                q[k].subj_kind = 0;
+            }
+            DevBuf dq(sizeof(keto_tuple) * q.size()), dp(sizeof(uint4) * q.size());
+            KETO_HIP(hipMemcpy(dq.p, q.data(), sizeof(keto_tuple) * q.size(), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(k_place, grid_for(q.size()), dim3(BLK), 0, 0, Dp, static_cast<const keto_tuple *>(dq.p), q.size(),
+                               static_cast<uint4 *>(dp.p));
+            KETO_HIP(hipGetLastError());
+            KETO_HIP(hipMemcpy(probe.data(), dp.p, sizeof(uint4) * q.size(), hipMemcpyDeviceToHost));
+        }
+        std::lock_guard<std::mutex> g(B.spares->mu);
+        for (size_t k = 0; k < fresh_objs.size(); k++) {
+            if (probe[k].x != NONE32) continue;  // it has an entity
+            const uint32_t ns = fresh_objs[k].first, obj = fresh_objs[k].second;
+            for (uint32_t sl = 0; sl < B.ns[ns].n_slots; sl++)
+                if ((B.relinfo[B.ns[ns].slot_base + sl] >> 20) & 1u) return nullptr;  // aliased visited keys
+            if (B.spares->used[ns] >= B.spares->count[ns]) return nullptr;  // out of spares
+            const uint32_t e = B.spares->first[ns] + B.spares->used[ns]++;
+            ext.push_back(make_uint4(obj, ns, e, 0));
+            ent_set.push_back(make_uint2(e, obj));
+        }
+    }
+    std::unique_ptr<void, void (*)(void *)> ext_guard(nullptr, [](void *p) { (void)hipFree(p); });
+    if (!ent_set.empty()) {
+        // the ext table of the new snapshot: every object placed on a spare so far in this family line
+        uint32_t size = 64;
+        while (size < 2 * ext.size()) size <<= 1;
+        std::vector<uint4> tab(size, make_uint4(0, 0, NONE32, 0));
+        for (const uint4 &x : ext) {
+            uint32_t h = (uint32_t)mix64((((uint64_t)x.y << 32) | x.x) + 1) & (size - 1);
+            while (tab[h].z != NONE32) h = (h + 1) & (size - 1);
+            tab[h] = x;
+        }
+        KETO_HIP(hipMalloc(&ext_dev, 16ull * size));
+        ext_guard.reset(ext_dev);
+        KETO_HIP(hipMemcpy(ext_dev, tab.data(), 16ull * size, hipMemcpyHostToDevice));
+        Dp.ext = static_cast<const uint4 *>(ext_dev);
+        Dp.ext_mask = size - 1;
+        // the spares' uuid ids for Expand output: words of the shared ent_obj no snapshot of the
+        // family reads before this one (a spare is handed out once)
+        DevBuf d_set(sizeof(uint2) * ent_set.size());
+        KETO_HIP(hipMemcpy(d_set.p, ent_set.data(), sizeof(uint2) * ent_set.size(), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_ent_obj_set, grid_for(ent_set.size()), dim3(BLK), 0, 0, const_cast<uint32_t *>(D.ent_obj),
+                           static_cast<const uint2 *>(d_set.p), (uint32_t)ent_set.size());
+        KETO_HIP(hipGetLastError());
+        place_all();
     }
     std::unordered_map<uint32_t, size_t> node_at, subj_at;  // node / subject index -> position in the sorted lists
     std::vector<Touched> tn, ts;
@@ -453,7 +547,7 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
                 out.resize(c[w]);
                 if (!c[w]) continue;
                 DevBuf mb(sizeof(Match) * c[w]);
-                hipLaunchKernelGGL(k_matches, grid_for(c[w]), dim3(BLK), 0, 0, D, rows, w ? sl.u32() : rl.u32(), c[w],
+                hipLaunchKernelGGL(k_matches, grid_for(c[w]), dim3(BLK), 0, 0, Dp, rows, w ? sl.u32() : rl.u32(), c[w],
                                    static_cast<Match *>(mb.p));
                 KETO_HIP(hipGetLastError());
                 KETO_HIP(hipMemcpy(out.data(), mb.p, sizeof(Match) * c[w], hipMemcpyDeviceToHost));
@@ -589,12 +683,19 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     s.store_id = B.store_id;
     s.cfg_hash = B.cfg_hash;
     s.probe_used = B.probe_used + ins_keys.size();
+    s.spares = B.spares;
+    s.ext = ext;
     DevSnapshot &X = s.dev;
-    X = D;
+    X = Dp;  // (the base's arrays, its ext table or this patch's)
     for (const void *p : {(const void *)D.weight, (const void *)D.ent_obj, (const void *)D.slot_rel, (const void *)D.vkey,
                           (const void *)D.ns, (const void *)D.nsrel, (const void *)D.ops, (const void *)D.op_children,
                           (const void *)D.op_items, (const void *)D.or_items, (const void *)D.ent_rank})
         s.share(B, p);
+    if (ext_dev) {
+        s.own(ext_guard.release(), 16ull * ((uint64_t)Dp.ext_mask + 1));
+    } else if (D.ext) {
+        s.share(B, D.ext);
+    }
     auto fresh = [&](size_t bytes) -> void * { return s.alloc((bytes + 31) / 16 * 16); };
     // size change per touched row, cumulative
     std::vector<long long> cum_all(m), cum_set(m), cum_rev(ms);

@@ -161,15 +161,14 @@ uint64_t config_hash(const keto_snapshot_config *cfg) {
     for (uint32_t i = 0; i < cfg->n_namespaces; i++) str(cfg->namespace_names ? cfg->namespace_names[i] : nullptr);
     bytes(&cfg->n_relations, 4);
     for (uint32_t i = 0; i < cfg->n_relations; i++) str(cfg->relation_names ? cfg->relation_names[i] : nullptr);
-    bytes(&cfg->n_uuids, 4);
-    str(cfg->namespaces_json);
+    str(cfg->namespaces_json);  // (not n_uuids: a patch takes a larger one up to its base's id capacity)
     const int32_t strict = cfg->strict_mode != 0;
     bytes(&strict, 4);
     return h;
 }
 
 Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
-                         bool sched_weights) {
+                         bool sched_weights, const BuildOpts *opts) {
     auto t0 = std::chrono::steady_clock::now();
     if (!cfg) throw Error(KETO_E_INVALID, "null config");
     if (n && !tuples) throw Error(KETO_E_INVALID, "null tuples");
@@ -182,7 +181,8 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     Snapshot &s = *S;
     s.device = cfg->device;
     s.n_ns = cfg->n_namespaces;
-    s.n_uuids = cfg->n_uuids;
+    s.n_uuids = std::max(cfg->n_uuids, opts ? opts->uuid_capacity : 0u);
+    if (s.n_uuids >= 0x80000000u) throw Error(KETO_E_LIMIT, "n_uuids must be < 2^31");
     s.strict = cfg->strict_mode != 0;
     s.n_rel_caller = cfg->n_relations;
     s.cfg_hash = config_hash(cfg);
@@ -365,11 +365,23 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     for (uint32_t ns = 0; ns <= s.n_ns; ns++) rank0[ns] = build::read_u32(d_rank.u32(), ns * bpn);
     uint64_t ent_total = 0, node_total = 0;
     std::vector<uint32_t> ent_base(s.n_ns);
+    if (opts && opts->spares) {
+        s.spares = std::make_shared<Spares>();
+        s.spares->first.resize(s.n_ns);
+        s.spares->count.resize(s.n_ns);
+        s.spares->used.assign(s.n_ns, 0);
+    }
     for (uint32_t ns = 0; ns < s.n_ns; ns++) {
         n_real[ns] = rank0[ns + 1] - rank0[ns];
         s.ns[ns].ent_base = ent_base[ns] = (uint32_t)ent_total;
         s.ns[ns].node_base = (uint32_t)node_total;
-        uint64_t ne = (uint64_t)n_real[ns] + 1;  // + phantom
+        // real entities, then the spares a store snapshot keeps for new objects, then the phantom
+        const uint32_t spare = s.spares && s.ns[ns].n_slots ? n_real[ns] / 16 + 256 : 0;
+        if (s.spares) {
+            s.spares->first[ns] = ent_base[ns] + n_real[ns];
+            s.spares->count[ns] = spare;
+        }
+        uint64_t ne = (uint64_t)n_real[ns] + spare + 1;  // + phantom
         ent_total += ne;
         node_total += ne * s.ns[ns].n_slots;
         if (node_total >= VIRT_BIT || ent_total >= VIRT_BIT) throw Error(KETO_E_LIMIT, "node space exceeds 2^31");
@@ -671,6 +683,7 @@ void dev_ptrs(DevSnapshot &D, F &&f) {
     f(reinterpret_cast<const void *&>(D.or_items));
     f(reinterpret_cast<const void *&>(D.ent_rank));
     f(reinterpret_cast<const void *&>(D.set_bits));
+    f(reinterpret_cast<const void *&>(D.ext));
     f(reinterpret_cast<const void *&>(D.probe));
 }
 constexpr size_t STAGE = 64u << 20;  // device <-> file through a pinned buffer of this size
@@ -757,7 +770,7 @@ Snapshot *load_snapshot(const char *path, int device) {
     std::vector<size_t> bytes;
     F.get_v(idx);
     F.get_v(bytes);
-    if (idx.size() != 20) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+    if (idx.size() != 21) throw Error(KETO_E_INVALID, "snapshot file corrupt");
     void *stage = nullptr;
     KETO_HIP(hipHostMalloc(&stage, STAGE, 0));
     try {

@@ -231,7 +231,13 @@ static void reserve_next_patch(const Snapshot &s) {
 
 Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg) {
     if (!cfg || cfg->device != st.device) throw Error(KETO_E_INVALID, "config names another device");
-    Snapshot *s = build_snapshot(cfg, st.rows(), st.n, true);
+    // room for what later transactions create, so their patches need no full build: an id space
+    // past the caller's (ids not yet written are unknown objects and subjects, as before) and
+    // spare entities in every namespace (patch.hip places new objects on them)
+    BuildOpts o;
+    o.uuid_capacity = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, (uint64_t)cfg->n_uuids + cfg->n_uuids / 16 + 65536);
+    o.spares = true;
+    Snapshot *s = build_snapshot(cfg, st.rows(), st.n, true, true, &o);
     s->info.version = st.version;
     s->store_id = st.id;
     reserve_next_patch(*s);
@@ -243,7 +249,7 @@ Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const
     // a patch reuses base's compiled namespaces, name tables and id space: only for the same
     // configuration (a namespace reload, renamed relations or a larger uuid space build in full)
     if (base.store_id == st.id && base.device == st.device && base.info.version <= st.version &&
-        base.cfg_hash == config_hash(cfg)) {
+        base.cfg_hash == config_hash(cfg) && cfg->n_uuids <= base.n_uuids) {
         // the log must hold every version after the base's, each once, in order (the gather
         // below takes exactly the entries this loop counts)
         uint64_t want = base.info.version + 1, n_rows = 0;

@@ -219,9 +219,9 @@ def test_patched_snapshots_equal_full_builds():
 
 
 def test_patch_falls_back_when_base_has_no_node():
-    """a transaction naming an object the base snapshot has never seen cannot be patched in: the
-    full build runs (patched = False) and the result is still the store's content; a snapshot of
-    another store is never patched"""
+    """a transaction creating more objects than the base snapshot kept spare entities for (half
+    the graph at once) cannot be patched in: the full build runs (patched = False) and the result
+    is still the store's content; a snapshot of another store is never patched"""
     wl = synth.drive(depth=4, n_groups=300, n_users=1000, seed=5)
     st = km.TupleStore(wl.tuples[: len(wl.tuples) // 2])
     snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
@@ -324,4 +324,87 @@ def test_patch_with_changed_namespace_config_builds_in_full():
     st.transact(ins, None)
     again = km.Snapshot(ns2, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=nxt)
     assert again.patched
+    st.close()
+
+
+def _new_files(wl, rng, ids, parents_of, acl_per_file=9):
+    """rows creating File objects `ids`: a parent tuple each (File:f#parents@Folder:p#, the
+    generator's shape) and acl_per_file ACL rows (viewers / editors / owners: users, 30 %
+    Group#members sets)"""
+    f_ns, fo_ns, g_ns = wl.ns_names.index("File"), wl.ns_names.index("Folder"), wl.ns_names.index("Group")
+    par, mem, empty = wl.rel_names.index("parents"), wl.rel_names.index("members"), wl.rel_names.index("")
+    acl = [wl.rel_names.index(r) for r in ("viewers", "editors", "owners")]
+    n = len(ids)
+    rows = np.zeros(n * (1 + acl_per_file), dtype=wl.tuples.dtype)
+    rows["ns"] = f_ns
+    rows["obj"] = np.repeat(ids, 1 + acl_per_file)
+    head = np.arange(n) * (1 + acl_per_file)
+    rows["rel"][head], rows["subj_kind"][head] = par, 1
+    rows["s_ns"][head], rows["s_obj"][head], rows["s_rel"][head] = fo_ns, parents_of, empty
+    rest = np.setdiff1d(np.arange(len(rows)), head)
+    rows["rel"][rest] = rng.choice(acl, len(rest))
+    grp = rng.random(len(rest)) < 0.3
+    rows["subj_kind"][rest[grp]], rows["s_ns"][rest[grp]], rows["s_rel"][rest[grp]] = 1, g_ns, mem
+    rows["s_obj"][rest[grp]] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], grp.sum())
+    rows["s_obj"][rest[~grp]] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], (~grp).sum())
+    rows["shard_id"] = rng.integers(0, 256, (len(rows), 16), dtype=np.uint8)
+    return rows
+
+
+def test_patch_creates_objects():
+    """verdict r3: the reference's insert creates rows for any object (persistence/sql/
+    relationtuples.go:104-126, 277-287).  A transaction of 1,000 rows creating 100 new files (a
+    parent tuple + 9 ACL rows each, ids past the base's) is patched in -- the new objects go on
+    the base's spare entities -- and then a second one creating a new folder and files under it
+    (a new subject-set object): every Check (goal counts too) and Expand tree equals a full build
+    of the same version, and the oracle agrees; the new files' answers are not the phantom's"""
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=8)
+    rng = np.random.default_rng(11)
+    st = km.TupleStore(wl.tuples)
+    host = wl.tuples.copy()
+    base = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    w, _ = world_from_workload(wl)
+    folders = rng.integers(0, wl.meta["n_folders"], 100)
+    n_uuids = wl.n_uuids
+    new_ids = n_uuids + np.arange(100)
+    ins = _new_files(wl, rng, new_ids, folders)
+    assert len(ins) == 1000
+    snaps = [base]
+    for step in range(2):
+        if step == 1:  # a new folder (under an existing one) and 20 files in it
+            fo_ns = wl.ns_names.index("Folder")
+            new_folder = n_uuids
+            files = n_uuids + 1 + np.arange(20)
+            ins = _new_files(wl, rng, files, np.full(20, new_folder))
+            up = ins[:1].copy()
+            up["ns"], up["obj"], up["s_obj"] = fo_ns, new_folder, int(folders[0])
+            ins = np.concatenate([up, ins])
+            new_ids = np.concatenate([[new_folder], files])
+        n_uuids = int(new_ids.max()) + 1
+        st.transact(ins, None)
+        host = transact(host, ins, ins[:0])
+        snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids, store=st, base=snaps[-1])
+        assert snap.patched, f"step {step}: the full build ran"
+        full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids, store=st)
+        q = synth.drive_queries(wl, 8192, seed=20 + step)
+        k = 4096  # view / edit of the new objects for random users (ids past the workload's included)
+        f_ns = wl.ns_names.index("File") if step == 0 else np.where(np.arange(k) % 21 == 0, wl.ns_names.index("Folder"),
+                                                                        wl.ns_names.index("File"))
+        q["ns"][:k] = f_ns
+        q["obj"][:k] = rng.choice(new_ids, k)
+        q["rel"][:k] = rng.choice([wl.rel_names.index("view"), wl.rel_names.index("edit")], k)
+        q["subj_kind"][:k], q["s_ns"][:k], q["s_rel"][:k] = 0, 0, 0
+        q["s_obj"][:k] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], k)
+        q["max_depth"][:k] = 0
+        roots = _roots(wl, rng, 64)
+        roots["ns"][:32], roots["obj"][:32] = wl.ns_names.index("File"), rng.choice(new_ids, 32)
+        roots["rel"][:32] = wl.rel_names.index("viewers")
+        allowed = _compare(wl, snap, full, q, roots)
+        assert allowed[:k].any()  # the new files are found, not the phantom
+        orc = refsem.Oracle(w, host.view(refsem.TUPLE_DT).copy(), shard_bytes=True)
+        orc.set_limits(wl.max_depth, wl.max_width)
+        dec, err, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+        np.testing.assert_array_equal(allowed, dec)
+        full.close()
+        snaps.append(snap)
     st.close()

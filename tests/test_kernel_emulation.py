@@ -95,4 +95,4 @@ def test_patched_snapshots_exact_under_emulation(tmp_path):
                         os.path.join(ROOT, "tests", "test_gpu_store.py"), "-k", "patch"],
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "4 passed" in r.stdout
+    assert "5 passed" in r.stdout
