@@ -462,14 +462,6 @@ __global__ __launch_bounds__(BLK) void k_alias_mark(uint32_t *set_dst, uint64_t 
     if (i < n && vkey[set_dst[i]] != set_dst[i]) set_dst[i] |= EDGE_ALIAS;
 }
 
-// bit i of the bitmap: node i's set row is non-empty (a wave ORs its 64 bits into one word)
-__global__ __launch_bounds__(BLK) void k_set_bits(const uint4 *set_row, uint64_t n, unsigned long long *bits) {
-    for (uint64_t i = gid(); i - __lane_id() < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const bool live = i < n;
-        const bool b = live && set_row[i].x != set_row[i].y;
-        run_atomic_or(bits, i >> 6, b ? (1ull << (i & 63)) : 0ull, live);
-    }
-}
 __global__ __launch_bounds__(BLK) void k_leaf_mark(uint32_t *set_dst, uint64_t n, const uint4 *set_row) {
     const uint64_t i = gid();
     if (i >= n) return;
@@ -677,12 +669,6 @@ void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32
 void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag,
                  uint32_t n_slots) {
     if (n) hipLaunchKernelGGL(k_slot_idrows, grid_cap(n, FLAG_GRID), dim3(BLK), 0, 0, t, n, slot_of, n_rel, ns, flag, n_slots);
-    KETO_HIP(hipGetLastError());
-}
-
-void set_bits(const uint4 *set_row, uint64_t n_rows, unsigned long long *bits) {
-    KETO_HIP(hipMemset(bits, 0, 8 * (n_rows / 64 + 1)));
-    if (n_rows) hipLaunchKernelGGL(k_set_bits, grid_cap(n_rows, 1u << 16), dim3(BLK), 0, 0, set_row, n_rows, bits);
     KETO_HIP(hipGetLastError());
 }
 

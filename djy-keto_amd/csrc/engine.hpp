@@ -130,8 +130,6 @@ struct RowsOut {
 void rows(const RowsIn &in, RowsOut &out);
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows);
 void leaf_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows);
-// bits[n_rows / 64 + 1] (zeroed here): bit i = set_row[i] non-empty (DevSnapshot::set_bits)
-void set_bits(const uint4 *set_row, uint64_t n_rows, unsigned long long *bits);
 // flag[global slot] |= 1 where a row of the slot holds a subject set (flag zeroed by the caller)
 void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag, uint32_t n_slots);
 void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag,

@@ -243,6 +243,14 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
     // and the empty generations an asynchronous batch launches speculatively cost ~nothing
     if (blockIdx.x * blockDim.x >= cnt) return;
     const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
+    // A goal reads its query's routed bit only once some query of the batch was routed (by an
+    // earlier generation, or this one so far): one word per block instead of a load per goal.
+    // Routing is best-effort pruning here -- the decision at generation 0 reads the bits themselves.
+#ifndef KETO_NO_RFLAG  // (A/B builds: every goal reads its bit)
+    const bool any_routed = *P.any_routed != 0u;
+#else
+    const bool any_routed = true;
+#endif
     // this wave's slice
     const uint32_t so = (blockIdx.x * ((blockDim.x + 63) >> 6) + (threadIdx.x >> 6)) % FR_SHARDS;
     const uint32_t nbase = so * P.scap + gm.base[so] + (gm.pre[so + 1] - gm.pre[so]), send = (so + 1) * P.scap;
@@ -261,15 +269,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
 #endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
-        // goals of queries routed meanwhile still run (rare); they can no longer spawn.  A goal
-        // reads its query's routed bit only once some query of the batch was routed: one word per
-        // block step instead of a load per goal (routing is best-effort pruning here -- the
-        // decision at generation 0 reads the bits themselves)
-#ifndef KETO_NO_RFLAG  // (A/B builds: every goal reads its bit)
-        const bool any_routed = *static_cast<volatile const uint32_t *>(P.any_routed) != 0u;
-#else
-        const bool any_routed = true;
-#endif
+        // goals of queries routed meanwhile still run (rare); they can no longer spawn
         bool live = j < cnt;
         uint32_t i = live ? gen_goal(P, gm, j) : 0u;
         uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);

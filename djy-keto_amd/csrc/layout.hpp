@@ -83,10 +83,6 @@ struct DevSnapshot {
     const uint32_t *set_dst;   // node | EDGE_ALIAS | EDGE_LEAF, shard order within a row
     uint32_t edge_mask;        // node bits of a set_dst entry (and of set_row's inline edges)
     uint32_t edge_leaf;        // set_dst entries carry EDGE_LEAF
-    // [n_nodes / 64 + 1] bit c = node c's subject-set row is non-empty: a rewrite's candidates
-    // (the sibling slots of one entity, adjacent bits of one word) are decided without their
-    // 16-byte set_row loads (null: read set_row)
-    const unsigned long long *set_bits;
     const uint32_t *weight;    // [n_nodes] capped path count below a node (longest-first scheduling)
     const uint32_t *ent_obj;   // [n_entities] entity -> uuid id (NONE32 for phantoms): Expand output
     const uint32_t *slot_rel;  // [total slots] global slot -> relation name id: Expand output

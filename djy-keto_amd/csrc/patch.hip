@@ -310,16 +310,6 @@ __global__ __launch_bounds__(BLK) void k_slot_any(const uint4 *set_row, const ui
         }
     }
 }
-// the set-row bitmap's bits of the nodes whose set row flipped: set / cleared from the new rows
-__global__ __launch_bounds__(BLK) void k_bits_fix(const uint4 *set_row, unsigned long long *bits, const uint32_t *flip,
-                                                  uint32_t m) {
-    const uint64_t i = gid();
-    if (i >= m) return;
-    const uint32_t c = flip[i];
-    const unsigned long long b = 1ull << (c & 63u);
-    if (set_row[c].x != set_row[c].y) atomicOr(&bits[c >> 6], b);
-    else atomicAnd(&bits[c >> 6], ~b);
-}
 // probe keys: inserts into empty slots (or found present), removals to tombstones
 __global__ __launch_bounds__(BLK) void k_probe_apply(unsigned long long *probe, uint64_t bmask, const unsigned long long *keys,
                                                      uint32_t n_ins, uint32_t n_del) {
@@ -776,21 +766,6 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
         hipLaunchKernelGGL(k_fix_inline, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, X, set_row, set_dst, rev_off, rev_nodes,
                            d_flip.u32(), (uint32_t)flip.size());
         KETO_HIP(hipGetLastError());
-    }
-    // the set-row bitmap: the base's, with the flipped nodes' bits (shared when nothing flipped)
-    X.set_bits = D.set_bits;
-    if (D.set_bits) {
-        if (flip.empty()) {
-            s.share(B, D.set_bits);
-        } else {
-            auto *sb = static_cast<unsigned long long *>(fresh(8ull * ((uint64_t)N / 64 + 1)));
-            KETO_HIP(hipMemcpyAsync(sb, D.set_bits, 8ull * ((uint64_t)N / 64 + 1), hipMemcpyDeviceToDevice, 0));
-            DevBuf d_flip = up(flip);
-            hipLaunchKernelGGL(k_bits_fix, grid_for(flip.size()), dim3(BLK), 0, 0, set_row, sb, d_flip.u32(),
-                               (uint32_t)flip.size());
-            KETO_HIP(hipGetLastError());
-            X.set_bits = sb;
-        }
     }
     phase("leaf");
     // probe hash: a copy with the heavy subjects' key changes

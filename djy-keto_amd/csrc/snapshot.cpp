@@ -509,11 +509,6 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         D.edge_mask = ~(EDGE_ALIAS | EDGE_LEAF);
         D.edge_leaf = 1;
     }
-    {   // the set-row bitmap (a rewrite's candidates decided without their set_row loads)
-        auto *sb = static_cast<unsigned long long *>(dalloc(8 * ((uint64_t)N / 64 + 1)));
-        build::set_bits(ro.set_row, N, sb);
-        D.set_bits = sb;
-    }
     // slots whose rows can hold subject sets: an expand-subject of any other slot finds none
     if (total_slots) {
         DevBuf flag(4ull * total_slots);
@@ -682,7 +677,6 @@ void dev_ptrs(DevSnapshot &D, F &&f) {
     f(reinterpret_cast<const void *&>(D.op_items));
     f(reinterpret_cast<const void *&>(D.or_items));
     f(reinterpret_cast<const void *&>(D.ent_rank));
-    f(reinterpret_cast<const void *&>(D.set_bits));
     f(reinterpret_cast<const void *&>(D.ext));
     f(reinterpret_cast<const void *&>(D.probe));
 }
@@ -770,7 +764,7 @@ Snapshot *load_snapshot(const char *path, int device) {
     std::vector<size_t> bytes;
     F.get_v(idx);
     F.get_v(bytes);
-    if (idx.size() != 21) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+    if (idx.size() != 20) throw Error(KETO_E_INVALID, "snapshot file corrupt");
     void *stage = nullptr;
     KETO_HIP(hipHostMalloc(&stage, STAGE, 0));
     try {
