@@ -273,6 +273,11 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         bool live = j < cnt;
         uint32_t i = live ? gen_goal(P, gm, j) : 0u;
         uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
+        // (the goal this thread loaded, and where the regroup put it: its gfn / gvs record is
+        // written back by this thread, in generation order, from the slot's results)
+        const bool own_live = live;
+        const uint32_t own_i = i;
+        uint32_t own_slot = threadIdx.x;
 #ifndef KETO_FR_NOREGROUP
         {   // Block regroup: the block's goals ordered by class -- expand-subjects, rewrites, the
             // rest, then dead lanes; batch order within a class -- so that a wave runs one class's
@@ -301,6 +306,7 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
                 }
             rg_g[slot] = g;
             rg_i[slot] = i;
+            own_slot = slot;
             __syncthreads();
             g = rg_g[threadIdx.x];
             i = rg_i[threadIdx.x];
@@ -355,10 +361,27 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             nc = 0;
             val = M_NOT;
         }
+#if !defined(KETO_FR_NOREGROUP) && !defined(KETO_FR_OLDGFN)  // (KETO_FR_OLDGFN: A/B builds)
+        // the goal records go out in generation order: the regrouped lane leaves them in its LDS
+        // slot (rg_g: this lane alone read it since the regroup), the thread that loaded the goal
+        // writes them -- consecutive goals from consecutive lanes, whole lines per wave instead of
+        // one scattered 8 B + 4 B write per goal (those were most of the kernel's write requests)
+        if (live) rg_g[threadIdx.x] = make_uint4(cb, nc | (rop << 24) | (chain ? GFN_CHAIN : 0u), val, 0);
+        __syncthreads();
+        if (own_live) {
+            const uint4 r = rg_g[own_slot];
+            P.gfn[own_i] = make_uint2(r.x, r.y);
+            reinterpret_cast<uint32_t *>(P.gvs)[2 * (size_t)own_i] = r.z;
+        }
+#else
+        (void)own_live;
+        (void)own_i;
+        (void)own_slot;
         if (live) {
             P.gfn[i] = make_uint2(cb, nc | (rop << 24) | (chain ? GFN_CHAIN : 0u));
             reinterpret_cast<uint32_t *>(P.gvs)[2 * (size_t)i] = val;
         }
+#endif
         // ---- occurrences: an ES goal's kept children, goals and leaves alike, are the keys it
         // adds to its scope (CheckAndAddVisited, engine.go:157-160): one run of its wave's slice
         const uint32_t nocc = (live && kind == G_ES && (nc || xrel)) ? pat + (chain ? 1u : 0u) : 0u;
