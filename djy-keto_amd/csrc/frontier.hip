@@ -266,6 +266,9 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
     constexpr uint32_t NB = KETO_FR_RG_BUCKETS;  // goal classes; dead lanes are one more
     __shared__ uint4 rg_g[XBLOCK];
     __shared__ uint32_t rg_i[XBLOCK], rg_n[XBLOCK / 64][NB + 1];
+#ifndef KETO_FR_LATE_SUBJ
+    __shared__ uint4 rg_s[XBLOCK];
+#endif
 #endif
     for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
         const uint32_t j = j0 + threadIdx.x;
@@ -278,6 +281,12 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         const bool own_live = live;
         const uint32_t own_i = i;
         uint32_t own_slot = threadIdx.x;
+#if !defined(KETO_FR_NOREGROUP) && !defined(KETO_FR_LATE_SUBJ)
+        // the query subject's membership record, loaded in generation order -- neighbouring goals
+        // mostly belong to one query (a parent's children are contiguous), so a wave's loads fall
+        // on few records and coalesce -- and carried through the regroup in LDS
+        uint4 srec = live ? P.start[2 * (size_t)g.y + 1] : make_uint4(0, 0, 0, 0);
+#endif
 #ifndef KETO_FR_NOREGROUP
         {   // Block regroup: the block's goals ordered by class -- expand-subjects, rewrites, the
             // rest, then dead lanes; batch order within a class -- so that a wave runs one class's
@@ -306,10 +315,16 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
                 }
             rg_g[slot] = g;
             rg_i[slot] = i;
+#ifndef KETO_FR_LATE_SUBJ
+            rg_s[slot] = srec;
+#endif
             own_slot = slot;
             __syncthreads();
             g = rg_g[threadIdx.x];
             i = rg_i[threadIdx.x];
+#ifndef KETO_FR_LATE_SUBJ
+            srec = rg_s[threadIdx.x];
+#endif
             live = threadIdx.x < n_live;
         }
 #endif
@@ -325,7 +340,11 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             if (!(ts & VIRT_BIT)) rnode = ts;
         }
         const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
+#if !defined(KETO_FR_NOREGROUP) && !defined(KETO_FR_LATE_SUBJ)
+        const Subject q = live ? subject_of(srec) : Subject{0, false, make_uint4(0, 0, 0, 0)};
+#else
         const Subject q = live ? load_subject(P, pos) : Subject{0, false, make_uint4(0, 0, 0, 0)};
+#endif
         FR_MARK(0);
         // ---- phase A: decide, or count the children -------------------------------------------
         const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W);
