@@ -322,6 +322,11 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
                     "around the traversal on the engine stream; roots: Group#members and Folder#viewers"}
 
 
+def synth_new_files(wl, ids, parents, rng):
+    from keto_mi355x import synth
+    return synth.drive_new_files(wl, ids, parents, rng)
+
+
 def store_probe(km, wl, q, n_ins: int = 600, n_del: int = 400):
     """Incremental snapshots at the workload's size: the graph in a
     device tuple store (keto_store_*), a TransactRelationTuples of n_ins + n_del rows (new ACL rows
@@ -353,20 +358,52 @@ def store_probe(km, wl, q, n_ins: int = 600, n_del: int = 400):
     was_patched = patched.patched
     base.close()
     res = [km.CheckEngine(patched, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)]
-    pi = patched.info()
-    patched.close()  # (device memory: the full build of the same version comes next)
+    # a second transaction creates objects (verdict r3: Keto's most common write is a new file):
+    # 100 new files, a parent tuple + 9 ACL rows each, ids past the graph's -- patched onto the
+    # previous version's spare entities
+    n_new = 100
+    new_ids = wl.n_uuids + np.arange(n_new)
+    ins2 = synth_new_files(wl, new_ids, rng.integers(0, wl.meta["n_folders"], n_new), rng)
+    n_uuids2 = wl.n_uuids + n_new
+    st.transact(ins2, None)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict, store=st)
+    patched2 = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids2, strict=wl.strict, store=st,
+                           base=patched)
+    patch2_ms = (time.perf_counter() - t0) * 1e3
+    q2 = q.copy()
+    k = min(len(q2), 1 << 16)  # view / edit of the new files by random users
+    q2["ns"][:k], q2["obj"][:k] = wl.ns_names.index("File"), rng.choice(new_ids, k)
+    q2["rel"][:k] = rng.choice([wl.rel_names.index("view"), wl.rel_names.index("edit")], k)
+    q2["subj_kind"][:k], q2["s_ns"][:k], q2["s_rel"][:k], q2["max_depth"][:k] = 0, 0, 0, 0
+    q2["s_obj"][:k] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], k)
+    res2 = [km.CheckEngine(patched2, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q2)]
+    new_objs = {"transaction_rows": int(len(ins2)), "new_files": n_new, "patched": patched2.patched,
+                "patch_ms": patch2_ms, "new_file_checks_allowed": float(res2[0][0][:k].mean())}
+    pi = patched.info()
+    patched.close()  # (device memory: the full builds of the same versions come next)
+    patched2.close()
+    t0 = time.perf_counter()
+    full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids2, strict=wl.strict, store=st)
     full_ms = (time.perf_counter() - t0) * 1e3
+    res2.append(km.CheckEngine(full, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q2))
+    new_objs["checks_vs_full_build"] = {"n": int(len(q2)), "mismatches": int((res2[0][0] != res2[1][0]).sum()
+                                                                           + (res2[0][1] != res2[1][1]).sum())}
+    # version 1 against a full build of it: the store without the second transaction's rows
+    st.transact(None, ins2)
+    full.close()
+    full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids2, strict=wl.strict, store=st)
     res.append(km.CheckEngine(full, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q))
     fi = full.info()
     out = {"transaction_rows": n_ins + n_del, "patched": was_patched, "patch_ms": patch_ms, "full_build_ms": full_ms,
+           "new_objects": new_objs,
            "transact_ms": transact_ms, "store_load_s": load_s, "version": int(pi["version"]),
            "n_tuples_equal": pi["n_tuples"] == fi["n_tuples"],
            "checks_vs_full_build": {"n": int(len(q)), "mismatches": int((res[0][0] != res[1][0]).sum()
                                                                          + (res[0][1] != res[1][1]).sum())},
            "what": "keto_store_transact of the rows, then keto_store_snapshot_patch of the previous snapshot "
-                   "(host API call to a usable snapshot); full_build_ms: keto_store_snapshot of the same version"}
+                   "(host API call to a usable snapshot); full_build_ms: keto_store_snapshot of the same version; "
+                   "new_objects: a second transaction creating 100 files, patched onto the first patch"}
     full.close()
     st.close()
     torch.cuda.empty_cache()

@@ -327,30 +327,6 @@ def test_patch_with_changed_namespace_config_builds_in_full():
     st.close()
 
 
-def _new_files(wl, rng, ids, parents_of, acl_per_file=9):
-    """rows creating File objects `ids`: a parent tuple each (File:f#parents@Folder:p#, the
-    generator's shape) and acl_per_file ACL rows (viewers / editors / owners: users, 30 %
-    Group#members sets)"""
-    f_ns, fo_ns, g_ns = wl.ns_names.index("File"), wl.ns_names.index("Folder"), wl.ns_names.index("Group")
-    par, mem, empty = wl.rel_names.index("parents"), wl.rel_names.index("members"), wl.rel_names.index("")
-    acl = [wl.rel_names.index(r) for r in ("viewers", "editors", "owners")]
-    n = len(ids)
-    rows = np.zeros(n * (1 + acl_per_file), dtype=wl.tuples.dtype)
-    rows["ns"] = f_ns
-    rows["obj"] = np.repeat(ids, 1 + acl_per_file)
-    head = np.arange(n) * (1 + acl_per_file)
-    rows["rel"][head], rows["subj_kind"][head] = par, 1
-    rows["s_ns"][head], rows["s_obj"][head], rows["s_rel"][head] = fo_ns, parents_of, empty
-    rest = np.setdiff1d(np.arange(len(rows)), head)
-    rows["rel"][rest] = rng.choice(acl, len(rest))
-    grp = rng.random(len(rest)) < 0.3
-    rows["subj_kind"][rest[grp]], rows["s_ns"][rest[grp]], rows["s_rel"][rest[grp]] = 1, g_ns, mem
-    rows["s_obj"][rest[grp]] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], grp.sum())
-    rows["s_obj"][rest[~grp]] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], (~grp).sum())
-    rows["shard_id"] = rng.integers(0, 256, (len(rows), 16), dtype=np.uint8)
-    return rows
-
-
 def test_patch_creates_objects():
     """verdict r3: the reference's insert creates rows for any object (persistence/sql/
     relationtuples.go:104-126, 277-287).  A transaction of 1,000 rows creating 100 new files (a
@@ -367,7 +343,7 @@ def test_patch_creates_objects():
     folders = rng.integers(0, wl.meta["n_folders"], 100)
     n_uuids = wl.n_uuids
     new_ids = n_uuids + np.arange(100)
-    ins = _new_files(wl, rng, new_ids, folders)
+    ins = synth.drive_new_files(wl, new_ids, folders, rng)
     assert len(ins) == 1000
     snaps = [base]
     for step in range(2):
@@ -375,7 +351,7 @@ def test_patch_creates_objects():
             fo_ns = wl.ns_names.index("Folder")
             new_folder = n_uuids
             files = n_uuids + 1 + np.arange(20)
-            ins = _new_files(wl, rng, files, np.full(20, new_folder))
+            ins = synth.drive_new_files(wl, files, np.full(20, new_folder), rng)
             up = ins[:1].copy()
             up["ns"], up["obj"], up["s_obj"] = fo_ns, new_folder, int(folders[0])
             ins = np.concatenate([up, ins])
