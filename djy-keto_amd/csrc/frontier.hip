@@ -194,13 +194,17 @@ __device__ __forceinline__ uint32_t gen_goal(const FrontierParams &P, const GenM
 struct GlobalSink {
     const FrontierParams &P;
     __device__ __forceinline__ void spawn(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope) const {
+        LP(LP_WGOAL, &P.g0[c]);
         P.g0[c] = make_uint4(node, pos, word, scope);
     }
     __device__ __forceinline__ void spawn_es(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope,
                                              uint32_t) const {
         spawn(c, node, pos, word, scope);
     }
-    __device__ __forceinline__ void occ(uint32_t o, uint32_t scope, uint32_t key) const { P.occ[o] = make_uint2(scope, key); }
+    __device__ __forceinline__ void occ(uint32_t o, uint32_t scope, uint32_t key) const {
+        LP(LP_WOCC, &P.occ[o]);
+        P.occ[o] = make_uint2(scope, key);
+    }
 };
 // generation 0: query position i in slice i / chunk
 __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
@@ -275,6 +279,9 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         // goals of queries routed meanwhile still run (rare); they can no longer spawn
         bool live = j < cnt;
         uint32_t i = live ? gen_goal(P, gm, j) : 0u;
+#ifdef KETO_FR_LOADPROF
+        if (live) LP(LP_G0, &P.g0[i]);
+#endif
         uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
         // (the goal this thread loaded, and where the regroup put it: its gfn / gvs record is
         // written back by this thread, in generation order, from the slot's results)
@@ -285,6 +292,9 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         // the query subject's membership record, loaded in generation order -- neighbouring goals
         // mostly belong to one query (a parent's children are contiguous), so a wave's loads fall
         // on few records and coalesce -- and carried through the regroup in LDS
+#ifdef KETO_FR_LOADPROF
+        if (live) LP(LP_SUBJ, &P.start[2 * (size_t)g.y + 1]);
+#endif
         uint4 srec = live ? P.start[2 * (size_t)g.y + 1] : make_uint4(0, 0, 0, 0);
 #endif
 #ifndef KETO_FR_NOREGROUP
@@ -339,6 +349,10 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             const uint32_t ts = t_sibling(T, node, t_node_info(T, node), T.ops[op].rel_computed & 0xFFFFu);
             if (!(ts & VIRT_BIT)) rnode = ts;
         }
+#ifdef KETO_FR_LOADPROF
+        if (rnode != NONE32) LP(LP_ROW, &s.set_row[rnode]);
+        if (live && any_routed) LP(LP_ROUTED, &P.qrouted[pos >> 5]);
+#endif
         const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
 #if !defined(KETO_FR_NOREGROUP) && !defined(KETO_FR_LATE_SUBJ)
         const Subject q = live ? subject_of(srec) : Subject{0, false, make_uint4(0, 0, 0, 0)};
@@ -388,6 +402,8 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
         if (live) rg_g[threadIdx.x] = make_uint4(cb, nc | (rop << 24) | (chain ? GFN_CHAIN : 0u), val, 0);
         __syncthreads();
         if (own_live) {
+            LP(LP_WFN, &P.gfn[own_i]);
+            LP(LP_WFN, &P.gvs[own_i]);
             const uint4 r = rg_g[own_slot];
             P.gfn[own_i] = make_uint2(r.x, r.y);
             reinterpret_cast<uint32_t *>(P.gvs)[2 * (size_t)own_i] = r.z;
@@ -659,6 +675,12 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     P.gcount = gcount;
     P.qrouted = f.qrouted;
     P.any_routed = fb_count + 1;
+#ifdef KETO_FR_LOADPROF
+    {
+        unsigned long long *lc = st.counters;
+        KETO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(lp_counts), &lc, sizeof(lc)));
+    }
+#endif
     P.budget = L.budget;
     P.dkeys = f.dkeys;
     P.dcnt = f.dcnt;
