@@ -913,6 +913,16 @@ def main(argv=None):
     log(f"[rank {rank}] expand + serving probes done ({time.perf_counter() - t_setup:.1f}s since start)")
     store = None
     if rank == 0 and world == 1 and not args.no_store_probe and args.workload in ("c3", "c4"):
+        # the probe is a deployment's write path: the store, its served snapshot and the next one.
+        # The bench's own snapshot, streams and buffers are not part of it and are released first
+        # (in a deployment the served snapshot is the store's own)
+        if os.environ.get("KETO_BENCH_STORE_KEEP") is None:
+            for b_ in (dq, da, de, dql):
+                b_.free()
+            for s_ in strs:
+                s_.close()
+            snap.close()
+            torch.cuda.empty_cache()
         store = store_probe(km, wl, q)
         log(f"[rank {rank}] store probe: patch {store['patch_ms']:.1f} ms (patched {store['patched']}), full build "
             f"{store['full_build_ms']:.0f} ms ({time.perf_counter() - t_setup:.1f}s since start)")

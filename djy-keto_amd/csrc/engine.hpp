@@ -198,13 +198,15 @@ struct Stream {
     struct {
         void *mem = nullptr, *roots_mem = nullptr;
         uint64_t grid = 0, stage_cap = 0, ncap = 0;
-        keto_tree_node *priv = nullptr, *stage = nullptr, *outbuf = nullptr;
+        uint2 *priv = nullptr, *stage = nullptr;  // walk records {subject key, n_children | union} (expand.hip)
+        keto_tree_node *outbuf = nullptr;
         uint64_t out_cap = 0;
         unsigned long long *sizes = nullptr, *soff = nullptr, *ctrl = nullptr;
         uint64_t *offsets = nullptr;
         int32_t *err = nullptr;
         uint32_t *fb_list = nullptr;
-        hipEvent_t ev[2] = {nullptr, nullptr};  // around the traversal (expand_wave + the fallback's count pass)
+        // around the traversal (expand_wave + the fallback's count pass) and the placement in API form
+        hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
         void *hpin = nullptr;                   // pinned read-back of the offsets, errors and stage top
         size_t hpin_bytes = 0;
         double ms_sum = 0;

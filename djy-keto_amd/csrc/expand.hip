@@ -224,8 +224,8 @@ struct ExpandWaveParams {
     uint32_t n;
     int32_t max_depth;
     uint32_t priv_cap;              // <= XW_PRIV (tests lower it: KETO_XW_PRIV, mixed wave / fallback batches)
-    keto_tree_node *priv;           // [grid][XW_PRIV]: the tree being walked
-    keto_tree_node *stage;          // finished trees, in completion order
+    uint2 *priv;                    // [grid][XW_PRIV]: the tree being walked, as walk records (below)
+    uint2 *stage;                   // finished trees, in completion order
     unsigned long long stage_cap;
     unsigned long long *stage_top;
     unsigned long long *sizes, *soff;  // [n]: nodes of each tree, its offset in `stage` (NONE: fallback)
@@ -235,13 +235,22 @@ struct ExpandWaveParams {
     unsigned long long *counters;   // rows, edges, -, out nodes
 };
 
+// A walk record is what the DFS decides about a node: {subject key, n_children | XR_UNION}.  The
+// API form (namespace, object uuid, relation name: two more dependent loads per node) is made by
+// expand_place, in parallel over the batch, off the walk's serial chain of row loads.
+constexpr uint32_t XR_UNION = 1u << 31;
+
+__device__ __forceinline__ uint2 walk_rec(uint32_t skey, bool un, uint32_t nch) {
+    return make_uint2(skey, un ? (nch | XR_UNION) : 0u);
+}
+
 // one root per wavefront: see the file comment
 __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
     __shared__ uint32_t vis[XW_VIS];
     __shared__ uint4 stk[XW_STACK];
     const DevSnapshot &s = P.s;
     const uint32_t lane = threadIdx.x;
-    keto_tree_node *priv = P.priv + (size_t)blockIdx.x * XW_PRIV;
+    uint2 *priv = P.priv + (size_t)blockIdx.x * XW_PRIV;
     unsigned long long c_rows = 0, c_edges = 0, c_out = 0;
     for (;;) {
         uint32_t q = 0;
@@ -287,8 +296,9 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
             visit(key);  // the root is visited (:69-72)
             const uint32_t b = s.all_off[root], e = s.all_off[root + 1];
             rows++;
-            if (b != e) {  // no tuples on the first page -> nil (:97-99)
-                if (lane == 0) priv[0] = api_node(s, d <= 1 ? 4u : 1u, SKEY_SET | root, d <= 1 ? 0u : e - b);  // :101-104
+            if (b != e && e - b >= XR_UNION) fail = true;  // (a row past 2^31 tuples: the fallback)
+            if (b != e && !fail) {  // no tuples on the first page -> nil (:97-99)
+                if (lane == 0) priv[0] = walk_rec(SKEY_SET | root, d > 1, e - b);  // :101-104
                 cnt = 1;
                 uint4 top = make_uint4(b, e, (uint32_t)d, 0);
                 while (d > 1 && !fail) {
@@ -303,8 +313,7 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
                     const uint32_t sk = in ? s.all_subj[top.x + lane] : 0u;
                     const bool set = in && (sk & SKEY_SET);
                     uint32_t ck = 0, cb = 0, ce = 0;
-                    keto_tree_node nd{};
-                    if (in) nd = api_node(s, 4, sk, 0);
+                    const uint2 nd = walk_rec(sk, false, 0);
                     if (set) {
                         const uint32_t c = sk & ~SKEY_SET;
                         ck = c;
@@ -334,20 +343,17 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
                         const uint32_t ckj = __shfl(ck, j), cbj = __shfl(cb, j), cej = __shfl(ce, j);
                         edges++;
                         pos = j + 1;
-                        keto_tree_node leaf = nd;  // (lane j's record)
                         bool expand = false;
                         if (!visit(ckj)) {  // a revisit is nil -> a leaf (:112-117)
                             if (fail) break;
                             rows++;
                             expand = cbj != cej && top.z - 1 > 1;
-                        }
-                        if (lane == j) {
-                            if (expand) {
-                                leaf.type = 1;
-                                leaf.n_children = cej - cbj;
+                            if (expand && cej - cbj >= XR_UNION) {
+                                fail = true;
+                                break;
                             }
-                            if (cnt < P.priv_cap) priv[cnt] = leaf;
                         }
+                        if (lane == j && cnt < P.priv_cap) priv[cnt] = walk_rec(nd.x, expand, cej - cbj);
                         if (++cnt > P.priv_cap) {
                             fail = true;
                             break;
@@ -397,15 +403,20 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
     }
 }
 
-// trees from the stage into their root-order positions of the output
-__global__ __launch_bounds__(256) void expand_place(const keto_tree_node *stage, const unsigned long long *soff,
+// trees from the stage into their root-order positions of the output, each walk record made into
+// its API form on the way (Mapper.ToTree, uuid_mapping.go:356-385)
+__global__ __launch_bounds__(256) void expand_place(DevSnapshot s, const uint2 *stage, const unsigned long long *soff,
                                                     const unsigned long long *sizes, const uint64_t *offsets, uint32_t n,
                                                     keto_tree_node *out) {
     for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
         const unsigned long long so = soff[q];
         if (so == ~0ull) continue;  // a fallback root: expand_kernel's emit pass writes it
         const unsigned long long c = sizes[q];
-        for (unsigned long long i = threadIdx.x; i < c; i += blockDim.x) out[offsets[q] + i] = stage[so + i];
+        for (unsigned long long i = threadIdx.x; i < c; i += blockDim.x) {
+            const uint2 r = stage[so + i];
+            const bool un = (r.y & XR_UNION) != 0u;
+            out[offsets[q] + i] = api_node(s, un ? 1u : 4u, r.x, un ? r.y & ~XR_UNION : 0u);
+        }
     }
 }
 
@@ -516,23 +527,29 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
     if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
     auto &X = st.xw;
     const uint32_t cus = (uint32_t)num_cus(s.device);
-    const uint64_t grid = (uint64_t)cus * 8;  // 8 one-wave blocks per CU (a few KB of LDS each)
-    if (!X.mem || X.ncap < n) {
+    // one-wave blocks of 9 KB LDS each, KETO_XW_BPC per CU (default 8).  C4, 4,096 roots: 8 per CU
+    // (two roots after another per wave) 0.67 ms, 16 per CU (every root at once) 0.73 ms
+    static const uint64_t bpc = [] {
+        const char *e = getenv("KETO_XW_BPC");
+        return e ? (uint64_t)std::max(1, std::min(atoi(e), 17)) : 8ull;
+    }();
+    const uint64_t grid = (uint64_t)cus * bpc;
+    if (!X.mem || X.ncap < n || X.grid < grid) {
         if (X.mem) KETO_HIP(hipFree(X.mem));
         X.mem = nullptr;
         uint64_t nc = 1;
         while (nc < n) nc <<= 1;
         const uint64_t sc = std::max<uint64_t>(X.stage_cap, 1u << 22);
-        const size_t bytes = xal(64) + xal(grid * XW_PRIV * sizeof(keto_tree_node)) + xal(sc * sizeof(keto_tree_node)) +
+        const size_t bytes = xal(64) + xal(grid * XW_PRIV * sizeof(uint2)) + xal(sc * sizeof(uint2)) +
                              2 * xal(nc * 8) + xal((nc + 1) * 8) + xal(nc * 4) + xal(nc * 4);
         KETO_HIP(hipMalloc(&X.mem, bytes));
         char *p = static_cast<char *>(X.mem);
         X.ctrl = reinterpret_cast<unsigned long long *>(p);
         p += xal(64);
-        X.priv = reinterpret_cast<keto_tree_node *>(p);
-        p += xal(grid * XW_PRIV * sizeof(keto_tree_node));
-        X.stage = reinterpret_cast<keto_tree_node *>(p);
-        p += xal(sc * sizeof(keto_tree_node));
+        X.priv = reinterpret_cast<uint2 *>(p);
+        p += xal(grid * XW_PRIV * sizeof(uint2));
+        X.stage = reinterpret_cast<uint2 *>(p);
+        p += xal(sc * sizeof(uint2));
         X.sizes = reinterpret_cast<unsigned long long *>(p);
         p += xal(nc * 8);
         X.soff = reinterpret_cast<unsigned long long *>(p);
@@ -578,8 +595,7 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
     P.err = X.err;
     P.counters = st.counters;
     if (!X.ev[0]) {
-        KETO_HIP(hipEventCreate(&X.ev[0]));
-        KETO_HIP(hipEventCreate(&X.ev[1]));
+        for (hipEvent_t &e : X.ev) KETO_HIP(hipEventCreate(&e));
     }
     KETO_HIP(hipEventRecord(X.ev[0], st.stream));
     if (wave) {
@@ -615,17 +631,26 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
     KETO_HIP(hipMemcpyAsync(herr, X.err, n * 4, hipMemcpyDeviceToHost, st.stream));
     KETO_HIP(hipStreamSynchronize(st.stream));
     float ms = 0;
-    if (hipEventElapsedTime(&ms, X.ev[0], X.ev[1]) == hipSuccess) {
-        X.ms_sum += ms;
-        X.batches++;
-    }
+    const bool timed = hipEventElapsedTime(&ms, X.ev[0], X.ev[1]) == hipSuccess;
     std::memcpy(out_offsets, hoff, (n + 1) * 8);
     std::memcpy(out_err, herr, n * 4);
     const uint32_t nfb = wave ? (uint32_t)h[2] : (uint32_t)n;
     const uint64_t total = out_offsets[n];
     if (h[0] > X.stage_cap / 2) X.stage_cap = std::max<uint64_t>(X.stage_cap, 2 * h[0]), X.ncap = 0;  // (regrown next batch)
-    if (total > out_cap || (total && !out_nodes)) return false;
-    if (total == 0) return true;
+    auto account = [&](float extra) {  // traversal time: the walk, plus the records' API form
+        if (timed) {
+            X.ms_sum += ms + extra;
+            X.batches++;
+        }
+    };
+    if (total > out_cap || (total && !out_nodes)) {
+        account(0.f);
+        return false;
+    }
+    if (total == 0) {
+        account(0.f);
+        return true;
+    }
     if (X.out_cap < total) {
         if (X.outbuf) KETO_HIP(hipFree(X.outbuf));
         X.outbuf = nullptr;
@@ -633,8 +658,9 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         KETO_HIP(hipMalloc(&X.outbuf, total * sizeof(keto_tree_node)));
         X.out_cap = total;
     }
-    hipLaunchKernelGGL(expand_place, dim3((uint32_t)std::min<uint64_t>(n, cus * 16)), dim3(256), 0, st.stream, X.stage, X.soff,
-                       X.sizes, X.offsets, (uint32_t)n, X.outbuf);
+    KETO_HIP(hipEventRecord(X.ev[2], st.stream));
+    hipLaunchKernelGGL(expand_place, dim3((uint32_t)std::min<uint64_t>(n, cus * 16)), dim3(256), 0, st.stream, s.dev, X.stage,
+                       X.soff, X.sizes, X.offsets, (uint32_t)n, X.outbuf);
     KETO_HIP(hipGetLastError());
     if (nfb) {
         F.emit = true;
@@ -642,9 +668,12 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         F.out = X.outbuf;
         run_expand(s, st, F);
     }
+    KETO_HIP(hipEventRecord(X.ev[3], st.stream));
     // one copy of the trees in root order (caller memory from keto_host_alloc: straight DMA)
     KETO_HIP(hipMemcpyAsync(out_nodes, X.outbuf, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st.stream));
     KETO_HIP(hipStreamSynchronize(st.stream));
+    float ms2 = 0;
+    account(hipEventElapsedTime(&ms2, X.ev[2], X.ev[3]) == hipSuccess ? ms2 : 0.f);
     return true;
 }
 
