@@ -205,8 +205,7 @@ struct Stream {
         uint64_t *offsets = nullptr;
         int32_t *err = nullptr;
         uint32_t *fb_list = nullptr;
-        // around the traversal (expand_wave + the fallback's count pass) and the placement in API form
-        hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+        hipEvent_t ev[2] = {nullptr, nullptr};  // around the traversal (expand_wave + the fallback's count pass)
         void *hpin = nullptr;                   // pinned read-back of the offsets, errors and stage top
         size_t hpin_bytes = 0;
         double ms_sum = 0;

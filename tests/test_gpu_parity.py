@@ -416,11 +416,13 @@ def test_regrouped_interpreter_drive(stream, regroup_forced):
     assert c["per_tier"]["queries"][0] > 0
 
 
+@pytest.mark.parametrize("output", ["pageable", "pinned"])
 @pytest.mark.parametrize("mode", ["wave", "mixed", "lane"])
-def test_expand_drive_trees_wave_and_fallback(stream, mode):
+def test_expand_drive_trees_wave_and_fallback(stream, mode, output):
     """Expand on a Drive world: the wave-per-root kernel (every root), a batch where trees larger
     than a lowered staging capacity fall back to the lane kernel (both paths in one batch, placed
-    in root order), and the lane kernel alone -- exact trees, child order included, vs the oracle"""
+    in root order), and the lane kernel alone -- exact trees, child order included, vs the oracle;
+    into pageable output (staged copy) and pinned output (keto_host_alloc: one DMA)"""
     from keto_mi355x import synth
     wl = synth.drive(depth=5, n_groups=400, members_per_group=6, n_users=3000, seed=13)
     w, t = world_from_workload(wl)
@@ -439,7 +441,10 @@ def test_expand_drive_trees_wave_and_fallback(stream, mode):
     old = {k: os.environ.get(k) for k in ("KETO_XW_PRIV", "KETO_EXPAND_WAVE")}
     os.environ.update(env)
     try:
-        nodes, offs, err = km.ExpandEngine(snap, stream, max_read_depth=6).build_trees(roots)
+        pin = km.PinnedArray(1 << 16, km.TREE_DT) if output == "pinned" else None
+        nodes, offs, err = km.ExpandEngine(snap, stream, max_read_depth=6).build_trees(roots, out=pin)
+        if pin is not None:
+            assert int(offs[-1]) <= len(pin.array) and nodes.ctypes.data == pin.array.ctypes.data
     finally:
         for k, v in old.items():
             if v is None:
@@ -458,6 +463,41 @@ def test_expand_drive_trees_wave_and_fallback(stream, mode):
                          ("s_rel", "srel"), ("n_children", "n_children")):
             np.testing.assert_array_equal(mine[f_p], on[f_o])
     assert big > 10  # the mixed batch really sends trees to the fallback
+
+
+def test_expand_pinned_output_capacity(stream):
+    """keto_expand_batch into pinned output one node too small: KETO_E_CAPACITY with the size
+    needed in offsets[n] and nothing written (the total is checked before the copy); then the
+    exact capacity: the trees equal those of a pageable-output call"""
+    import ctypes
+    from keto_mi355x import _abi, synth
+    wl = synth.drive(depth=4, n_groups=200, members_per_group=5, n_users=1000, seed=5)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    eng = km.ExpandEngine(snap, stream, max_read_depth=5)
+    n = 64
+    rng = np.random.default_rng(1)
+    roots = np.zeros(n, dtype=km.SUBJSET_DT)
+    roots["ns"], roots["rel"] = wl.ns_names.index("Group"), wl.rel_names.index("members")
+    roots["obj"] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], n)
+    ref, ref_offs, ref_err = eng.build_trees(roots)
+    total = int(ref_offs[-1])
+    assert total > n
+    for cap in (total - 1, total):
+        pin = km.PinnedArray(cap, km.TREE_DT)
+        pin.array.view(np.uint8)[:] = 0xAB
+        offs = np.zeros(n + 1, np.uint64)
+        err = np.zeros(n, np.int32)
+        rc = _abi.lib().keto_expand_batch(snap.handle, stream.handle, roots.ctypes.data, n, ctypes.byref(eng.limits),
+                                          pin.array.ctypes.data, cap, offs.ctypes.data, err.ctypes.data)
+        np.testing.assert_array_equal(offs, ref_offs)
+        if cap < total:
+            assert rc == _abi.KETO_E_CAPACITY
+            assert (pin.array.view(np.uint8) == 0xAB).all()
+        else:
+            assert rc == 0
+            np.testing.assert_array_equal(err, ref_err)
+            assert pin.array.tobytes() == ref.tobytes()
+        pin.free()
 
 
 C1_OBJECTS = ["/cats", "/cats/1.mp4", "/cats/2.mp4"]
