@@ -1,14 +1,14 @@
 #!/bin/bash
-# Kernel + memory-copy traces of the pipelined `value` runs (tool): C5 x10 one rank, C4, C2 --
-# where a pipelined step's time goes beside its kernels.  Each step bounded; a failure ends the run.
+# Kernel traces of the pipelined `value` runs (tool): C2 and C4 -- the async batches' kernels and
+# the gaps between them, beside the device-resident batches of the same run.  (--memory-copy-trace
+# is left out: with it rocprofv3's own teardown faults at exit and no trace is written)
 set -u
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp
 O=gpurun_out/${1:-r04t} && rm -rf $O && mkdir -p $O
 P="--no-cpu-baseline --serve-clients 0 --latency-iters 0 --no-store-probe"
-timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace -d $O/c5 -o kt --output-format csv \
-  -- python3 bench.py --workload c5 --scale 10 --steps 20 --warmup 2 --no-cpu-baseline > $O/c5.log 2>&1 || { echo c5 failed; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace -d $O/c4 -o kt --output-format csv \
-  -- python3 bench.py --steps 10 $P > $O/c4.log 2>&1 || { echo c4 failed; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace -d $O/c2 -o kt --output-format csv \
-  -- python3 bench.py --workload c2 --steps 10 $P > $O/c2.log 2>&1 || { echo c2 failed; exit 1; }
-find $O -name "*.csv" | xargs ls -la
+for w in c2 c4; do
+  timeout -k 10 400 rocprofv3 --kernel-trace -d $O/$w -o kt --output-format csv -- python3 bench.py --workload $w --steps 10 $P > $O/$w.log 2>&1 \
+    || { echo "$w failed"; tail -3 $O/$w.log; exit 1; }
+  cp $(find $O/$w -name "*kernel_trace.csv" | head -1) $O/${w}_kernel_trace.csv && rm -rf $O/$w
+done
+ls -la $O
