@@ -124,6 +124,11 @@ template <bool COUNT, bool LDS_TABLES>
 __global__ __launch_bounds__(256) void check_kernel(CheckParams P) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const DevSnapshot &s = P.s;
+#ifndef KETO_DFS_OLD
+    // an empty device list (the frontier routed nothing, or no query outgrew the previous tier):
+    // the whole block leaves before staging the tables (the value is the same for every thread)
+    if (P.qlist && *P.qlist_count == 0) return;
+#endif
     const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
     const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long *vis = P.vis + (size_t)gl * P.vcap;
@@ -405,7 +410,7 @@ __global__ __launch_bounds__(RG) void check_kernel_rg(CheckParams P) {
 // The DFS interpreter over the resolved batch, or over the `nl` positions of the device list
 // `list` (queries the frontier engine routed here).  Tier 0's kernel is timed when `timed`.
 static void run_dfs(const Snapshot &s, Stream &st, const CheckLaunch &L, const uint32_t *list, const uint32_t *list_count,
-                    uint64_t nl, bool timed) {
+                    uint64_t nl, bool timed, bool count_on_device = false) {
     constexpr uint32_t BLOCK = 256;
     const uint32_t cus = (uint32_t)num_cus(s.device);
     // Queries that outgrow a tier's scratch go to the next (lanes, visited slots per lane,
@@ -481,6 +486,13 @@ static void run_dfs(const Snapshot &s, Stream &st, const CheckLaunch &L, const u
             // sets the step time (and so a small batch's latency).
             const uint64_t waves = lanes / 64;
             P.live_lanes = (uint32_t)std::min<uint64_t>(64, (nl + waves - 1) / waves);
+#ifndef KETO_DFS_OLD
+            // queries routed by an asynchronous frontier pass: their number is on the device and is
+            // few (C2: ~5 per 2^20, C4: 0), so each gets a wave of its own, as a synchronous pass's
+            // few routed queries do -- in one shared wave their divergent steps serialise (C2: up
+            // to 0.7 ms per batch instead of 0.15)
+            if (count_on_device) P.live_lanes = 1;
+#endif
             const uint64_t need = (nl + P.live_lanes - 1) / P.live_lanes * 64;
             lanes = (uint32_t)std::min<uint64_t>(lanes, (need + BLOCK - 1) / BLOCK * BLOCK);
         } else {
@@ -547,7 +559,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
         const uint32_t *fc = gen ? st.frontier.fb_count : st.frontier_block.fb_count;
         // asynchronous: the interpreter is sized for the whole pass and reads the routed count on
         // the device (its lanes find an empty list and leave)
-        if (routed) run_dfs(s, st, L, fl, fc, routed == FR_ROUTED_ON_DEVICE ? Lp.n : routed, false);
+        if (routed) run_dfs(s, st, L, fl, fc, routed == FR_ROUTED_ON_DEVICE ? Lp.n : routed, false, routed == FR_ROUTED_ON_DEVICE);
     }
     st.mark_end();
 }
