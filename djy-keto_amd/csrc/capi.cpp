@@ -51,6 +51,8 @@ Stream::~Stream() {
     if (expand_scratch.mem) (void)hipFree(expand_scratch.mem);
     if (frontier.mem) (void)hipFree(frontier.mem);
     if (frontier.host_ctrl) (void)hipHostFree(frontier.host_ctrl);
+    if (frontier.host_gens) (void)hipHostFree(frontier.host_gens);
+    if (frontier.gens_ev) (void)hipEventDestroy(frontier.gens_ev);
     if (frontier_block.mem) (void)hipFree(frontier_block.mem);
     if (frontier_block.fb_list) (void)hipFree(frontier_block.fb_list);
     if (frontier_block.host) (void)hipHostFree(frontier_block.host);

@@ -167,6 +167,12 @@ struct FrontierScratch {
     uint2 *occ = nullptr;
     uint32_t *host_ctrl = nullptr;  // pinned
     uint32_t last_gens = 0, last_goals = 0, last_routed = 0;
+    // asynchronous passes: each one's generation count goes to pinned host memory at its end
+    // (fr_gens_used + a 4-byte copy), and a later pass adopts it as its speculation depth once the
+    // copy has landed -- a stream that only ever runs asynchronous batches learns its depth too
+    uint32_t *host_gens = nullptr;  // pinned
+    hipEvent_t gens_ev = nullptr;
+    bool gens_pending = false;
     uint32_t epoch = 1;  // scope-table epoch of the next batch (frontier.hip TAB_EPOCHS)
     keto_frontier_stats stats{};
 };

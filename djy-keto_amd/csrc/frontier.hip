@@ -648,6 +648,27 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     f.dcap = dcap;
     f.ocap = ocap;
     if (!f.host_ctrl) KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&f.host_ctrl), FR_CTRL_BYTES, 0));
+    if (!f.host_gens) KETO_HIP(hipHostMalloc(reinterpret_cast<void **>(&f.host_gens), 64, 0));
+    if (!f.gens_ev) KETO_HIP(hipEventCreateWithFlags(&f.gens_ev, hipEventDisableTiming));
+}
+
+// An asynchronous pass's generation count, as the synchronous path computes it on the host:
+// the first generation whose goals (summed over the slices, each clamped to its slice) are none;
+// G when all G launched generations spawned (its deeper queries were routed).
+static_assert(FR_SHARDS == 64, "fr_gens_used: one lane per slice in one wave");
+__global__ __launch_bounds__(64) void fr_gens_used(const uint32_t *gbase, const uint32_t *gcount, uint32_t scap, uint32_t G,
+                                                    uint32_t *out) {
+    const uint32_t sh = threadIdx.x;  // one lane per slice (FR_SHARDS = 64)
+    uint32_t gens = G;
+    for (uint32_t g = 0; g <= G && g < GEN_STRIDE; g++) {
+        const uint32_t b = gbase[sh * GEN_STRIDE + g], c = gcount[sh * GEN_STRIDE + g];
+        const uint32_t t = std::min(c, scap - std::min(b, scap));
+        if (!__ballot(t != 0)) {
+            gens = g;
+            break;
+        }
+    }
+    if (sh == 0) *out = gens;
 }
 
 uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint64_t pos_base) {
@@ -722,6 +743,10 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
 #define KETO_FR_RGRID 4
 #endif
         // (a stream with no history speculates 24; every empty generation still costs two launches)
+        if (f.gens_pending && hipEventQuery(f.gens_ev) == hipSuccess) {  // an earlier async pass's depth
+            f.last_gens = *f.host_gens;
+            f.gens_pending = false;
+        }
         const uint32_t G = std::min<uint32_t>(MAX_GEN, f.last_gens ? f.last_gens + KETO_FR_SPEC_MARGIN : 24);
         P.gen_cap = G;
         for (uint32_t k = 0; k < G; k++) {
@@ -738,6 +763,13 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
             }
             hipLaunchKernelGGL(fr_reduce, dim3(cus * KETO_FR_RGRID), eb, 0, st.stream, P);
             KETO_HIP(hipGetLastError());
+        }
+        if (!f.gens_pending) {  // this pass's depth, for a later one (one read-back in flight at a time)
+            hipLaunchKernelGGL(fr_gens_used, dim3(1), dim3(FR_SHARDS), 0, st.stream, gbase, gcount, P.scap, G, fb_count + 3);
+            KETO_HIP(hipGetLastError());
+            KETO_HIP(hipMemcpyAsync(f.host_gens, fb_count + 3, 4, hipMemcpyDeviceToHost, st.stream));
+            KETO_HIP(hipEventRecord(f.gens_ev, st.stream));
+            f.gens_pending = true;
         }
         if (++f.epoch > TAB_EPOCHS) {
             KETO_HIP(hipMemsetAsync(f.dkeys, 0, f.dcap * 12, st.stream));
