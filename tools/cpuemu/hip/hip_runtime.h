@@ -78,6 +78,7 @@ inline hipError_t hipEventRecord(hipEvent_t e, hipStream_t) {
     return hipSuccess;
 }
 inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipEventQuery(hipEvent_t) { return hipSuccess; }  // (the emulation runs every launch at once)
 inline hipError_t hipEventElapsedTime(float *ms, hipEvent_t a, hipEvent_t b) { *ms = float(*(double *)b - *(double *)a); return hipSuccess; }
 template <class K>
 inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int *n, K, int, size_t) { *n = 2; return hipSuccess; }
