@@ -477,10 +477,9 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
         uint32_t sub = nc;  // goals below this one (the budget's count)
         if (nc) {
             uint32_t res = NONE32;
-            for (uint32_t c = fn.x; c < fn.x + nc; c++) {  // every child's count; the fold up to its result
-                const uint2 v = P.gvs[c];
+            auto fold = [&](const uint2 v) {  // every child's count; the fold up to its result
                 sub += v.y;
-                if (res != NONE32) continue;
+                if (res != NONE32) return;
                 const uint32_t cv = v.x;
                 if (rop == R_FIRST || rop == R_FIRST_AND) {  // first Err / IsMember
                     if (decisive(cv)) res = cv;
@@ -490,7 +489,21 @@ __global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
                     const uint32_t m = cv & 3u;
                     res = m == M_IS ? ((cv & ~3u) | M_NOT) : (m == M_NOT ? ((cv & ~3u) | M_IS) : cv);
                 }
+            };
+#ifdef KETO_FR_RED_SERIAL
+            for (uint32_t c = fn.x; c < fn.x + nc; c++) fold(P.gvs[c]);
+#else
+            // the children's records four at a time, their loads issued together
+            const uint32_t ce = fn.x + nc;
+            for (uint32_t c0 = fn.x; c0 < ce; c0 += 4) {
+                uint2 v[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) v[u] = c0 + u < ce ? P.gvs[c0 + u] : make_uint2(0, 0);
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++)
+                    if (c0 + u < ce) fold(v[u]);
             }
+#endif
             if (res == NONE32) res = val != NONE32 ? val : (rop == R_AND ? M_IS : M_NOT);
             if (rop == R_FIRST_AND) res = and_map(res);  // an AND over its merged OR
             val = res;
