@@ -1310,10 +1310,52 @@ static void u_fold(res r, int spawned, int is_or, res *out, int *have, int *stop
  * the first decisive of its own items (NotMember if none), so the concatenation decides the same
  * group; it only contributes when its rest depth d-1 > 0 (rewrites.go:39-42).  No goal is
  * spawned for the nested OR itself. */
+static int u_and_merge(uctx *u, uint32_t ns, uint32_t obj, int ai, int d);
+static int u_flatten_off = -1; /* RS_NO_FLATTEN=1: the spine off (the engine built without it) */
+
+/* The spine (csrc/frontier_goal.inc "spine"): the last item of an OR's walk is a
+ * tuple-to-userset whose row holds exactly one subject set, and that parent's check would be a
+ * RW goal spawned in its IA's place (u_sub) whose rewrite is an OR, or an AND that u_and_merge
+ * takes.  Then the parent's items run in this goal, in place of that RW goal: they are the
+ * walk's own tail.  A nested group's result only matters when decisive (first decisive in add
+ * order), and an and_merge keeps a decisive result decisive (IsMember stays, an error stays), so
+ * the flat walk picks the same first decisive result; only an error's membership bit can differ,
+ * which no output reads.  Returns the inner OR's index and sets *dn (its rest depth), else -1. */
+static int u_spine(uctx *u, const key7 *t, int computed, int d, int *dn) {
+    const rs_db *db = u->c->db;
+    if (u_flatten_off < 0) {
+        const char *e = getenv("RS_NO_FLATTEN");
+        u_flatten_off = e && e[0] == '1';
+    }
+    if (u_flatten_off || d <= 0) return -1;
+    int err;
+    const int ri = ast_relation_for(db, t->sns, computed, &err);
+    if (err || ri < 0 || db->rels[ri].rewrite < 0) return -1;
+    /* u_sub's "RW goal in the IA's place" path: no direct check and no expand-subject */
+    const int can_ss_rw = !db->strict || db->rels[ri].has_ss_type;
+    const int direct = !db->strict && d - 1 > 0 && exists(u->c, t->sns, t->sid, computed);
+    const int es = can_ss_rw && d - 1 > 0 && has_set_rows(db, t->sns, computed);
+    if (direct || es) return -1;
+    const int rw = db->rels[ri].rewrite;
+    const rs_ast *a = &db->ast[rw];
+    if (a->type != RS_REWRITE) return -1;
+    if (a->op == RS_OP_OR) {
+        *dn = d;
+        return rw;
+    }
+    const int orc = u_and_merge(u, t->sns, t->sid, rw, d);
+    if (orc < 0) return -1;
+    *dn = d - 1;
+    return orc;
+}
+
 static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen, res *out,
-                       int *have, int *stop) {
+                       int *have, int *stop, int last) {
     const rs_db *db = u->c->db;
     const rs_ast *a = &db->ast[ai];
+    int lastnc = -1; /* the last non-CSS child: the walk's last item when `last` */
+    for (int k = 0; k < a->child_count; k++)
+        if (db->ast[db->children[a->child_begin + k]].type != RS_CSS) lastnc = k;
     int has_css = 0, found = 0;
     for (int k = 0; k < a->child_count; k++) {
         const rs_ast *ch = &db->ast[db->children[a->child_begin + k]];
@@ -1342,7 +1384,7 @@ static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32
         const rs_ast *ch = &db->ast[ci];
         if (ch->type == RS_CSS) continue;
         if (ch->type == RS_REWRITE && ch->op == RS_OP_OR) { /* restDepth-1 (:118) */
-            if (d - 1 > 0) u_or_items(u, ns, obj, ci, d - 1, scope, gen, out, have, stop);
+            if (d - 1 > 0) u_or_items(u, ns, obj, ci, d - 1, scope, gen, out, have, stop, last && k == lastnc);
             if (u->routed) return;
             continue;
         }
@@ -1353,6 +1395,21 @@ static void u_or_items(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32
             if (d - 1 <= 0) continue;
             size_t lo, hi;
             node_rows(db, ns, obj, ch->rel, &lo, &hi);
+            if (last && k == lastnc) {
+                const key7 *one = NULL;
+                int n1 = 0;
+                for (size_t i = lo; i < hi; i++)
+                    if (ROW(db, i)->kind == 1) {
+                        one = ROW(db, i);
+                        n1++;
+                    }
+                int dn = 0;
+                const int inner = n1 == 1 ? u_spine(u, one, ch->computed, d - 1, &dn) : -1;
+                if (inner >= 0) { /* the parent's items: this walk's tail (no goal for its RW) */
+                    u_or_items(u, one->sns, one->sid, inner, dn, scope, gen, out, have, stop, 1);
+                    continue;
+                }
+            }
             for (size_t i = lo; i < hi && !*stop; i++) {
                 const key7 *t = ROW(db, i);
                 if (t->kind != 1) continue;
@@ -1413,14 +1470,14 @@ static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scop
     int stop = 0; /* a leaf decided it: later children are never spawned */
     const int orc = u_and_merge(u, ns, obj, ai, d);
     if (orc >= 0) {
-        u_or_items(u, ns, obj, orc, d - 1, scope, gen, &out, &have, &stop);
+        u_or_items(u, ns, obj, orc, d - 1, scope, gen, &out, &have, &stop, 1);
         if (u->routed) return R_NOT;
         res x = have ? out : R_NOT;
         if (x.err || x.m != RS_IS_MEMBER) x.m = RS_NOT_MEMBER;
         return x;
     }
     if (a->op == RS_OP_OR) {
-        u_or_items(u, ns, obj, ai, d, scope, gen, &out, &have, &stop);
+        u_or_items(u, ns, obj, ai, d, scope, gen, &out, &have, &stop, 1);
         if (u->routed) return R_NOT;
         return have ? out : R_NOT;
     }
