@@ -222,10 +222,12 @@ __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
 }
 
 // One generation: every goal decides what it can and spawns its children into the next.
-// Registers: 6 waves per SIMD (80 VGPRs) measured faster than the unconstrained 5 (93 VGPRs):
-// Drive profiling batch 10.3 vs 10.9 ms; a count / emit split at 6 + 8 waves was slower (12.7 ms).
+// Registers: 5 waves per SIMD (96 VGPRs).  Since the spine (frontier_goal.inc) the goal code
+// holds more state; C4: 5 waves with phase B reloading the rewrite candidates' rows (no stash)
+// 3.41 ms vs 6 waves with the stash 3.45 ms, 4 waves 3.59 ms (profiles/r04_waves_ab.txt).  (Round
+// 2, before the spine: 6 waves 10.3 vs 5 waves 10.9 ms on the Drive profiling batch.)
 #ifndef KETO_FR_WAVES
-#define KETO_FR_WAVES 6
+#define KETO_FR_WAVES 5
 #endif
 #ifndef KETO_FR_BLOCK
 #define KETO_FR_BLOCK 256
