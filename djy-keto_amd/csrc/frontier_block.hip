@@ -157,8 +157,10 @@ __device__ __forceinline__ void add_dec(const BlockParams &P, Chunk &C, uint32_t
     else route_slot(C, occ_at(P, C, o).x >> SCOPE_BITS);
 }
 
+// 5 waves per SIMD (96 VGPRs): with the spine's state, 6 waves spilled 41 VGPRs; C4 p99 of 64Ki
+// batches 0.566 / 0.562 vs 0.583 / 0.586 ms at 6 (profiles/r04_waves_ab.txt)
 #ifndef KETO_FRB_WAVES
-#define KETO_FRB_WAVES 6
+#define KETO_FRB_WAVES 5
 #endif
 
 template <bool LDS_TABLES>
