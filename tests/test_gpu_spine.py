@@ -109,3 +109,38 @@ def test_spine_worlds_match_oracle(seed, max_width):
         snap.close()
     finally:
         stream.close()
+
+
+def test_async_speculation_learns_depth_and_routes_deeper(monkeypatch):
+    """The generation engine's asynchronous batches speculate last-depth + 2 generations, the depth
+    learned from the device after earlier batches (frontier.hip fr_gens_used).  A stream that ran
+    shallow batches (request depths 1-2) then gets a deep one (the whole spine world at depth 16):
+    what lies past the speculated generations is routed and the DFS interpreter answers it -- the
+    decisions are the oracle's either way"""
+    monkeypatch.setenv("KETO_FR_ENGINE", "gen")  # (small batches would run the block engine)
+    w, t, q = spine_world(5, 10)
+    orc = refsem.Oracle(w, t)
+    orc.set_limits(w.max_depth, w.max_width)
+    shallow = q.copy()
+    shallow["depth"] = 2
+    deep = q.copy()
+    deep["depth"] = 16
+    stream = km.Stream(0)
+    try:
+        snap = product_snapshot(w, t)
+        eng = km.CheckEngine(snap, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+        for batch in (shallow, shallow, shallow, deep, deep):
+            dec, err, _ = orc.check_batch(batch, threads=4)
+            qa = km.PinnedArray(len(batch), km.QUERY_DT)
+            qa.array[:] = queries_to_product(batch)
+            out = (km.PinnedArray(len(batch), np.uint8), km.PinnedArray(len(batch), np.int32))
+            eng.check_batch_async(qa.array, out[0].array, out[1].array)
+            stream.sync()
+            np.testing.assert_array_equal(out[1].array, err)
+            np.testing.assert_array_equal(out[0].array, dec)
+            for a in (qa, *out):
+                a.free()
+        assert stream.frontier_stats()["async_batches"] == 5
+        snap.close()
+    finally:
+        stream.close()
