@@ -38,8 +38,10 @@ constexpr uint32_t PG_LOG2 = 12, PG = 1u << PG_LOG2;  // goals per page
 constexpr uint32_t MAX_PAGES = 64;             // a chunk's goal indices: < 2^18 (BQ x 2 x budget fits)
 constexpr uint32_t OPG_LOG2 = 12, OPG = 1u << OPG_LOG2;  // occurrences per page
 constexpr uint32_t MAX_OPAGES = 64;
-constexpr uint32_t DEC_CAP = 128;              // decisive ES keys per chunk (more: the query is routed)
+constexpr uint32_t DEC_CAP = 128;              // decisive ES keys counted per pass of the repeat check
 constexpr uint32_t SCOPE_BITS = 18;            // occurrence entry x = scope | chunk slot << SCOPE_BITS
+constexpr uint32_t DEC_BIT = 0x80000000u;      // ... | DEC_BIT: a decisive occurrence, not yet counted
+static_assert((((BQ - 1) << SCOPE_BITS) | ((1u << SCOPE_BITS) - 1)) < DEC_BIT, "occurrence entry bits");
 constexpr uint32_t NB = 3;                     // regroup classes (ES, RW, the rest) + dead lanes
 
 // one page of a chunk's goals (structure of arrays, 36 B per goal)
@@ -74,7 +76,7 @@ struct Chunk {  // LDS state of the workgroup's current chunk
     uint32_t gs[MAX_GEN + 2];
     uint32_t pt[MAX_PAGES], opt[MAX_OPAGES];
     uint32_t npages, nopages, gnext, onext, ndec, pool_out, nq, chunk, gens;
-    uint32_t dec[DEC_CAP], dcnt[DEC_CAP];
+    uint32_t dcnt[DEC_CAP];
     uint2 dkey[DEC_CAP];
 };
 
@@ -149,12 +151,11 @@ __device__ __forceinline__ uint32_t fold(const BlockParams &P, const Chunk &C, u
     return res;
 }
 
-// a decisive occurrence: into the chunk's decisive list (full: the query is routed)
+// a decisive occurrence: marked in place (each goal marks its own entries); C.ndec says some are
 __device__ __forceinline__ void add_dec(const BlockParams &P, Chunk &C, uint32_t o) {
     if (o == NONE32 || o >= C.nopages * OPG) return;
-    const uint32_t d = atomicAdd(&C.ndec, 1u);
-    if (d < DEC_CAP) C.dec[d] = o;
-    else route_slot(C, occ_at(P, C, o).x >> SCOPE_BITS);
+    occ_at(P, C, o).x |= DEC_BIT;
+    C.ndec = 1;
 }
 
 // 5 waves per SIMD (96 VGPRs): with the spine's state, 6 waves spilled 41 VGPRs; C4 p99 of 64Ki
@@ -339,23 +340,37 @@ __global__ __launch_bounds__(BB, KETO_FRB_WAVES) void fr_block(BlockParams P) {
             __syncthreads();
         }
         // ---- repeats: a decisive key that its scope received more than once routes the query ---------
-        const uint32_t ndec = std::min(C.ndec, DEC_CAP);
-        if (ndec) {
-            for (uint32_t d = tid; d < ndec; d += NT) {
-                C.dkey[d] = occ_at(P, C, C.dec[d]);
-                C.dcnt[d] = 0;
-            }
-            __syncthreads();
+        // (in passes of up to DEC_CAP marked keys: any number of decisive occurrences is counted)
+        if (C.ndec) {
             const uint32_t no = std::min(C.onext, C.nopages * OPG);
-            for (uint32_t o = tid; o < no; o += NT) {
-                const uint2 e = occ_at(P, C, o);
-                if (e.x == NONE32) continue;
-                for (uint32_t d = 0; d < ndec; d++)
-                    if (C.dkey[d].x == e.x && C.dkey[d].y == e.y) atomicAdd(&C.dcnt[d], 1u);
+            for (;;) {
+                __syncthreads();
+                if (tid == 0) C.ndec = 0;
+                __syncthreads();
+                for (uint32_t o = tid; o < no; o += NT) {  // take up to DEC_CAP marked entries, unmarking them
+                    const uint2 e = occ_at(P, C, o);
+                    if (e.x == NONE32 || !(e.x & DEC_BIT)) continue;
+                    const uint32_t d = atomicAdd(&C.ndec, 1u);
+                    if (d >= DEC_CAP) continue;
+                    C.dkey[d] = make_uint2(e.x & ~DEC_BIT, e.y);
+                    C.dcnt[d] = 0;
+                    occ_at(P, C, o).x = e.x & ~DEC_BIT;
+                }
+                __syncthreads();
+                const uint32_t nd = C.ndec, ndec = std::min(nd, DEC_CAP);
+                if (nd == 0) break;
+                for (uint32_t o = tid; o < no; o += NT) {
+                    const uint2 e = occ_at(P, C, o);
+                    if (e.x == NONE32) continue;
+                    const uint32_t x = e.x & ~DEC_BIT;
+                    for (uint32_t d = 0; d < ndec; d++)
+                        if (C.dkey[d].x == x && C.dkey[d].y == e.y) atomicAdd(&C.dcnt[d], 1u);
+                }
+                __syncthreads();
+                for (uint32_t d = tid; d < ndec; d += NT)
+                    if (C.dcnt[d] >= 2) route_slot(C, C.dkey[d].x >> SCOPE_BITS);
+                if (nd <= DEC_CAP) break;
             }
-            __syncthreads();
-            for (uint32_t d = tid; d < ndec; d += NT)
-                if (C.dcnt[d] >= 2) route_slot(C, C.dkey[d].x >> SCOPE_BITS);
             __syncthreads();
         }
         // ---- generation 0: the decisions ----------------------------------------------------------

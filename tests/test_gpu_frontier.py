@@ -53,9 +53,11 @@ def _frontier_batch(stream, eng, q):
     return allowed, err, stream.frontier_stats(reset=True)
 
 
+# (552, 591, 1269: worlds with more than 128 decisive expand-subject children in one chunk of the
+# block engine, which once routed the queries past that count -- tools/parity_sweep.py found them)
 @pytest.mark.parametrize("rewrites", [True, False])
 @pytest.mark.parametrize("b", [1024, 6])
-@pytest.mark.parametrize("seed", list(range(60)))
+@pytest.mark.parametrize("seed", list(range(60)) + [552, 591, 1269])
 def test_random_worlds_frontier_vs_oracle(budget, seed, b, rewrites):
     stream = budget(b)
     w, t, q, _ = random_world(seed, rewrites=rewrites)
