@@ -1,6 +1,7 @@
 #!/bin/bash
 # Block-engine repeat check without a decisive-key cap (tool): the frontier / parity / spine GPU
-# tests, then the random-world sweep (tools/parity_sweep.py) over the seeds that found the cap.
+# tests, then the random-world sweep (tools/parity_sweep.py) over the seeds that found the cap,
+# with the generation engine forced over 1,000 more, and 300 spine worlds x 3 width limits.
 set -u
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp
 O=gpurun_out/${1:-r04dec} && rm -rf $O && mkdir -p $O
@@ -9,4 +10,6 @@ rc=$?; tail -1 $O/tests.log; [ $rc -ne 0 ] && { grep -E "Error|assert|FAIL" $O/t
 timeout -k 10 500 python3 -u tools/parity_sweep.py --seeds 60:2060 > $O/auto.log 2>&1
 rc=$?; tail -1 $O/auto.log | cut -c1-600; [ $rc -ne 0 ] && exit $rc
 KETO_FR_ENGINE=gen timeout -k 10 400 python3 -u tools/parity_sweep.py --seeds 2060:3060 > $O/gen.log 2>&1
-rc=$?; tail -1 $O/gen.log | cut -c1-600; exit $rc
+rc=$?; tail -1 $O/gen.log | cut -c1-600; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 -u tools/parity_sweep.py --kind spine --seeds 100:400 > $O/spine.log 2>&1
+rc=$?; tail -1 $O/spine.log | cut -c1-600; exit $rc
