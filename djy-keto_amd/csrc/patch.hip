@@ -769,8 +769,13 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     }
     phase("leaf");
     // probe hash: a copy with the heavy subjects' key changes
-    void *probe = fresh(16ull * ((uint64_t)D.probe_mask + 1));
+    // (exactly the base's size, no tail pad -- a probe never reads past its last bucket -- so the
+    // pool's block of an earlier version of the family fits it: a fresh 16 GB block at C4 is
+    // cleared by the driver at first touch, 0.2-0.7 s)
+    void *probe = s.alloc(16ull * ((uint64_t)D.probe_mask + 1));
+    phase("probe-get");
     KETO_HIP(hipMemcpyAsync(probe, D.probe, 16ull * ((uint64_t)D.probe_mask + 1), hipMemcpyDeviceToDevice, 0));
+    phase("probe-copy");
     if (!ins_keys.empty() || !del_keys.empty()) {
         std::vector<unsigned long long> keys(ins_keys);
         keys.insert(keys.end(), del_keys.begin(), del_keys.end());

@@ -1,4 +1,5 @@
 // Device scratch management shared by the check and expand launchers.
+#include <cstdio>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -116,6 +117,12 @@ void *pool_acquire(int device, size_t bytes, size_t *got) {
         std::lock_guard<std::mutex> g(P.mu);
         void *q = nullptr;
         if (take(P, bytes, &q, got)) return q;
+        static const bool verbose = getenv("KETO_PATCH_VERBOSE") != nullptr;
+        if (verbose) {  // (where a patch's time goes: a miss is a fresh, driver-cleared allocation)
+            fprintf(stderr, "[keto pool] miss: %zu bytes; %zu held in", bytes, P.held);
+            for (const PoolBlock &b : P.free) fprintf(stderr, " %zu", b.bytes);
+            fprintf(stderr, "\n");
+        }
     }
     void *q = nullptr;
     if (hipMalloc(&q, bytes) != hipSuccess) {  // out of memory: hand the pool back and try again
