@@ -17,7 +17,8 @@
 // interpreter then takes the routed queries (their count stays on the device).
 //
 // Semantics are frontier_goal.inc's phase A / phase B, shared with frontier.hip; the goal
-// counts, generation counts and routed queries equal the restatement's (rs_check_u) exactly.
+// counts, generation counts and routed queries equal the restatement's (rs_check_u) exactly as
+// long as the goal and occurrence page pools last (a chunk that outgrows them routes its queries).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
