@@ -159,6 +159,7 @@ struct FrontierScratch {
     uint64_t cap = 0, ncap = 0, dcap = 0, ocap = 0;  // goals, queries, decisive-key slots, occurrences per slice
     uint32_t *ctrl = nullptr;              // [gbase | gcount | fallback count]
     uint32_t *qrouted = nullptr, *fb_list = nullptr, *fb_count = nullptr;  // qrouted: a bit per query
+    uint32_t *qspawn = nullptr;  // per query: goals spawned from generation KETO_FR_CAP_GEN on
     uint4 *g0 = nullptr;
     uint2 *gfn = nullptr;
     uint2 *gvs = nullptr;  // {value, goals below} per goal

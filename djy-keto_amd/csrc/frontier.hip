@@ -67,6 +67,7 @@ struct FrontierParams {
     uint32_t gen;
     uint32_t gen_cap;            // generations this batch may run (MAX_GEN; asynchronous batches: the speculated count)
     uint32_t *qrouted;           // [n / 32] one bit per query position: routed to the DFS interpreter (L2-resident)
+    uint32_t *qspawn;            // [n] goals a query spawned from generation KETO_FR_CAP_GEN on (a lower bound)
     uint32_t *any_routed;        // != 0 once some query of the batch was routed (cleared with ctrl)
     uint32_t budget;
     unsigned long long *dkeys;   // decisive (scope, visited key) pairs of the batch (epoch-tagged)
@@ -219,6 +220,7 @@ __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
     const uint32_t d = r0.z & 0xFFFFu;
     P.g0[(i / chunk) * P.scap + i % chunk] = make_uint4(r0.x, i, gword(G_IA, d), NONE32);
     if (d > GD_MAX) route(P, i);  // (the bits were cleared before the launch)
+    P.qspawn[i] = 0;
 }
 
 // One generation: every goal decides what it can and spawns its children into the next.
@@ -228,6 +230,9 @@ __global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
 // 2, before the spine: 6 waves 10.3 vs 5 waves 10.9 ms on the Drive profiling batch.)
 #ifndef KETO_FR_WAVES
 #define KETO_FR_WAVES 5
+#endif
+#ifndef KETO_FR_CAP_GEN
+#define KETO_FR_CAP_GEN 8
 #endif
 #ifndef KETO_FR_BLOCK
 #define KETO_FR_BLOCK 256
@@ -383,6 +388,17 @@ __global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParam
             route(P, pos);
             nc = 0;
         }
+#ifndef KETO_FR_NOSPAWNCAP  // (A/B builds only)
+        // A query past its budget is routed at generation 0 anyway (fr_reduce's subtree count);
+        // from generation KETO_FR_CAP_GEN on its spawns are also counted as they happen, and one
+        // whose count alone passes the budget stops here: a runaway query would otherwise keep
+        // spawning until MAX_GEN and fill its arena slice, routing its neighbours with it.  (The
+        // count is a lower bound of the subtree count, so the routed set is unchanged.)
+        if (nc && k >= KETO_FR_CAP_GEN && 1u + atomicAdd(&P.qspawn[pos], nc) + nc > P.budget) {
+            route(P, pos);
+            nc = 0;
+        }
+#endif
         FR_MARK(2);
         // ---- allocation: one atomic per wave, on the wave's slice counter -------------------------
         uint32_t wtot = 0;
@@ -640,6 +656,7 @@ void ensure_frontier(FrontierScratch &f, uint64_t n) {
     f.occ_count = f.fb_count + 4;
     p += ctrl;
     f.qrouted = reinterpret_cast<uint32_t *>(p);
+    f.qspawn = f.qrouted + ncap;  // (the bits take ncap / 32 words of the first ncap)
     f.fb_list = f.qrouted + 2 * ncap;
     p += al256(ncap * 12);
     f.g0 = reinterpret_cast<uint4 *>(p);
@@ -710,6 +727,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     P.gbase = gbase;
     P.gcount = gcount;
     P.qrouted = f.qrouted;
+    P.qspawn = f.qspawn;
     P.any_routed = fb_count + 1;
 #ifdef KETO_FR_LOADPROF
     {
