@@ -260,6 +260,7 @@ void pool_shutdown();  // keto_shutdown: every device's pool and scratch cache b
 void *scratch_get(size_t bytes, size_t *got);
 void scratch_put(void *p, size_t bytes);
 hipStream_t scratch_stream(hipStream_t s);
+void scratch_forget_stream(hipStream_t s);  // call before destroying a stream scratch_stream named
 struct ScratchStream {  // the calling thread's DevBufs live on stream s for this scope
     hipStream_t old;
     explicit ScratchStream(hipStream_t s) : old(scratch_stream(s)) {}

@@ -606,6 +606,8 @@ struct Partition {
     ~Partition() {
         if (hpin) (void)hipHostFree(hpin);
         if (kstream) keto_stream_destroy(kstream);
+        scratch_forget_stream(hs);
+        scratch_forget_stream(hs2);
         if (hs) (void)hipStreamDestroy(hs);
         if (hs2) (void)hipStreamDestroy(hs2);
     }

@@ -147,7 +147,8 @@ namespace {
 struct CacheBlock {
     void *p;
     size_t bytes;
-    hipEvent_t ev;
+    hipEvent_t ev;   // nullptr: nothing to wait for
+    hipStream_t st;  // the stream ev was recorded on
 };
 struct ScratchCache {
     std::mutex mu;
@@ -177,7 +178,7 @@ void scratch_trim(int device) {
     (void)hipDeviceSynchronize();
     for (auto &b : C.free) {
         (void)hipFree(b.p);
-        C.events.push_back(b.ev);
+        if (b.ev) C.events.push_back(b.ev);
     }
     C.free.clear();
     C.held = 0;
@@ -207,9 +208,9 @@ void *scratch_get(size_t bytes, size_t *got) {
             C.held -= best;
             C.free.erase(C.free.begin() + (ptrdiff_t)at);
             g.unlock();
-            KETO_HIP(hipEventSynchronize(b.ev));  // its last reader's stream got past the release
+            if (b.ev) KETO_HIP(hipEventSynchronize(b.ev));  // its last reader's stream got past the release
             g.lock();
-            C.events.push_back(b.ev);
+            if (b.ev) C.events.push_back(b.ev);
             *got = best;
             return b.p;
         }
@@ -239,13 +240,32 @@ void scratch_put(void *p, size_t bytes) {
             ev = nullptr;
         }
         if (ev && hipEventRecord(ev, tl_stream) == hipSuccess) {
-            C.free.push_back(CacheBlock{p, bytes, ev});
+            C.free.push_back(CacheBlock{p, bytes, ev, tl_stream});
             C.held += bytes;
             return;
         }
         if (ev) C.events.push_back(ev);
     }
     (void)hipFree(p);
+}
+
+// Before stream s is destroyed: the cached blocks whose event was recorded on s wait for it now
+// and drop the event (an event whose stream is gone must not be waited on: the runtime then
+// reads the dead stream's state -- seen as "operation not permitted on an event last recorded
+// in a capturing stream" in a later build).
+void scratch_forget_stream(hipStream_t s) {
+    if (!s) return;
+    for (int d = 0; d < 64; d++) {
+        ScratchCache &C = scache_slot(d);
+        if (!C.cap) continue;
+        std::lock_guard<std::mutex> g(C.mu);
+        for (auto &b : C.free)
+            if (b.ev && b.st == s) {
+                (void)hipEventSynchronize(b.ev);
+                C.events.push_back(b.ev);
+                b.ev = nullptr;
+            }
+    }
 }
 
 void pool_trim(int device) {
