@@ -462,6 +462,22 @@ __global__ __launch_bounds__(BLK) void k_alias_mark(uint32_t *set_dst, uint64_t 
     if (i < n && vkey[set_dst[i]] != set_dst[i]) set_dst[i] |= EDGE_ALIAS;
 }
 
+__global__ __launch_bounds__(BLK) void k_remote_mark(uint32_t *set_dst, uint64_t n, const NsDev *ns, uint32_t n_ns,
+                                                    const uint32_t *ent_obj, uint32_t rank, uint32_t world) {
+    const uint64_t i = gid();
+    if (i >= n) return;
+    const uint32_t c = set_dst[i] & ~(EDGE_ALIAS | EDGE_REMOTE);
+    uint32_t lo = 0, hi = n_ns;  // last namespace whose node_base <= c
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (ns[m].node_base <= c) lo = m;
+        else hi = m;
+    }
+    const NsDev nd = ns[lo];
+    const uint32_t obj = ent_obj[nd.ent_base + (c - nd.node_base) / nd.n_slots];
+    const uint64_t h = ((((uint64_t)lo) << 32) | obj) * 0x9E3779B97F4A7C15ull;  // keto_object_owner
+    if ((uint32_t)((h >> 32) % world) != rank) set_dst[i] |= EDGE_REMOTE;
+}
 __global__ __launch_bounds__(BLK) void k_leaf_mark(uint32_t *set_dst, uint64_t n, const uint4 *set_row) {
     const uint64_t i = gid();
     if (i >= n) return;
@@ -621,18 +637,20 @@ void rows(const RowsIn &in, RowsOut &out) {
         hipLaunchKernelGGL(k_set_row, grid_for(N), dim3(BLK), 0, 0, set_cnt.u32(), N, out.set_dst.u32(), out.set_row);
         KETO_HIP(hipGetLastError());
         // scheduling weights: capped path counts relaxed to a fixed point (<= WEIGHT_ROUNDS)
-        DevBuf w2(4 * (N + 1)), changed(4);
-        hipLaunchKernelGGL(k_fill32, grid_for(N), dim3(BLK), 0, 0, out.weight, N, 1u);
-        uint32_t *w = out.weight, *nw = w2.u32();
-        for (uint32_t round = 0; in.weights && round < WEIGHT_ROUNDS; round++) {
-            KETO_HIP(hipMemset(changed.p, 0, 4));
-            hipLaunchKernelGGL(k_weight, grid_for(N), dim3(BLK), 0, 0, set_cnt.u32(), out.set_dst.u32(), N, w, nw,
-                               changed.u32());
-            KETO_HIP(hipGetLastError());
-            std::swap(w, nw);
-            if (!read_u32(changed.u32(), 0)) break;
+        if (out.weight) {
+            DevBuf w2(4 * (N + 1)), changed(4);
+            hipLaunchKernelGGL(k_fill32, grid_for(N), dim3(BLK), 0, 0, out.weight, N, 1u);
+            uint32_t *w = out.weight, *nw = w2.u32();
+            for (uint32_t round = 0; in.weights && round < WEIGHT_ROUNDS; round++) {
+                KETO_HIP(hipMemset(changed.p, 0, 4));
+                hipLaunchKernelGGL(k_weight, grid_for(N), dim3(BLK), 0, 0, set_cnt.u32(), out.set_dst.u32(), N, w, nw,
+                                   changed.u32());
+                KETO_HIP(hipGetLastError());
+                std::swap(w, nw);
+                if (!read_u32(changed.u32(), 0)) break;
+            }
+            if (w != out.weight) KETO_HIP(hipMemcpy(out.weight, w, 4 * N, hipMemcpyDeviceToDevice));
         }
-        if (w != out.weight) KETO_HIP(hipMemcpy(out.weight, w, 4 * N, hipMemcpyDeviceToDevice));
     }
     row_idx.reset();
     step("rows+weights");
@@ -676,6 +694,14 @@ void leaf_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows) {
     if (n) hipLaunchKernelGGL(k_leaf_mark, grid_for(n), dim3(BLK), 0, 0, set_dst, n, set_row);
     hipLaunchKernelGGL(k_row_inline, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, set_dst);  // inline copies too
     KETO_HIP(hipGetLastError());
+}
+
+void remote_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns,
+                 const uint32_t *ent_obj, uint32_t rank, uint32_t world) {
+    if (n) hipLaunchKernelGGL(k_remote_mark, grid_for(n), dim3(BLK), 0, 0, set_dst, n, ns, n_ns, ent_obj, rank, world);
+    hipLaunchKernelGGL(k_row_inline, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, set_dst);  // inline copies too
+    KETO_HIP(hipGetLastError());
+    KETO_HIP(hipStreamSynchronize(nullptr));
 }
 
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows) {

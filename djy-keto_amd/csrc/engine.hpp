@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -37,6 +38,11 @@ struct Spares {
 struct BuildOpts {
     uint32_t uuid_capacity = 0;  // id space (>= cfg n_uuids): ids past the caller's are unknown until written
     bool spares = false;         // spare entities per namespace (n_real / 16 + 256)
+    // A partitioned graph's snapshots (frontier_dist.hip) share one node arithmetic: the (ns, rel)
+    // pairs the job's tuples use are agreed on (OR over the ranks) before slots are laid out
+    std::function<void(std::vector<uint8_t> &used)> agree_used;
+    bool no_leaf = false;     // no EDGE_LEAF marks (the bit is such a snapshot's EDGE_REMOTE)
+    bool no_weights = false;  // no scheduling-weight array at all (DevSnapshot::weight null)
 };
 
 // Host mirror of the snapshot + its device buffers.
@@ -130,6 +136,10 @@ struct RowsOut {
 void rows(const RowsIn &in, RowsOut &out);
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows);
 void leaf_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows);
+// EDGE_REMOTE on every edge into a node whose object `rank` does not own (keto_object_owner over
+// `world`); the inline copies in set_row follow
+void remote_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns,
+                 const uint32_t *ent_obj, uint32_t rank, uint32_t world);
 // flag[global slot] |= 1 where a row of the slot holds a subject set (flag zeroed by the caller)
 void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag, uint32_t n_slots);
 void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag,

@@ -44,563 +44,7 @@ namespace keto {
 namespace {
 
 #include "frontier_goal.inc"
-
-// The arena is cut into FR_SHARDS slices of `scap` goals; a block spawns into slice
-// blockIdx % FR_SHARDS, so the allocation counters of a generation are FR_SHARDS addresses,
-// not one (a single counter serialises every block's atomic: ~60M/s).  A generation is the
-// union of one contiguous range per slice; slices stack their generations.
-constexpr uint32_t FR_SHARDS = 64;
-constexpr uint32_t GEN_STRIDE = MAX_GEN + 2;
-// ctrl: gbase[FR_SHARDS][GEN_STRIDE] | gcount[FR_SHARDS][GEN_STRIDE] | fallback count (+3) |
-// occurrence counts[FR_SHARDS]
-constexpr size_t FR_CTRL_BYTES = (2 * FR_SHARDS * GEN_STRIDE + 4 + FR_SHARDS) * 4;
-
-struct FrontierParams {
-    DevSnapshot s;
-    const uint4 *start;  // resolve records: 2 per query position (resolve.hip)
-    uint32_t n;
-    uint4 *g0;
-    uint2 *gfn;
-    uint2 *gvs;                  // {value, goals below (fr_reduce): the root's is the query's count}
-    uint32_t cap, scap;          // arena goals, goals per slice
-    uint32_t *gbase, *gcount;    // [FR_SHARDS][GEN_STRIDE]: slice-local base and count per generation
-    uint32_t gen;
-    uint32_t gen_cap;            // generations this batch may run (MAX_GEN; asynchronous batches: the speculated count)
-    uint32_t *qrouted;           // [n / 32] one bit per query position: routed to the DFS interpreter (L2-resident)
-    uint32_t *qspawn;            // [n] goals a query spawned from generation KETO_FR_CAP_GEN on (a lower bound)
-    uint32_t *any_routed;        // != 0 once some query of the batch was routed (cleared with ctrl)
-    uint32_t budget;
-    unsigned long long *dkeys;   // decisive (scope, visited key) pairs of the batch (epoch-tagged)
-    uint32_t *dcnt;              // their occurrences, counted by fr_repeat
-    uint32_t *dbits;             // 2^DBITS_LOG2-bit filter of the decisive keys (L2-resident)
-    uint32_t dmask, epoch;
-    uint2 *occ;                  // every ES child's {scope, visited key}: FR_SHARDS slices of ocap
-    uint32_t *occ_count;         // [FR_SHARDS] entries per slice
-    uint32_t ocap;
-    uint32_t max_width;
-    uint8_t *out_allowed;
-    int32_t *out_err;
-    uint32_t err_detail;
-    uint32_t *fb_list, *fb_count;  // routed positions (+ pos_base: batch positions), for the DFS interpreter
-    uint32_t pos_base;             // this pass's first batch position (batches of > FR_MAX_BATCH run in passes)
-    unsigned long long *prof;      // KETO_FR_PROF builds: wave-cycles per phase of fr_expand
-};
-
-// Profiling builds (-DKETO_FR_PROF, tools/ab_build.sh): shader clock between phase marks
-#ifdef KETO_FR_PROF
-#define FR_MARK(n)                                                     \
-    do {                                                               \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
-        pacc[n] += t_ - pt;                                            \
-        pt = t_;                                                       \
-    } while (0)
-#else
-#define FR_MARK(n) ((void)0)
-#endif
-
-__device__ __forceinline__ Subject load_subject(const FrontierParams &P, uint32_t pos) {
-    return subject_of(P.start[2 * (size_t)pos + 1]);  // one load
-}
-// Decisive-key table: keys carry the batch's epoch (1..TAB_EPOCHS) in bits 61-63 (scope < 2^29:
-// a goal index), so the table is cleared once every TAB_EPOCHS batches instead of after each one:
-// a slot holding 0 or another epoch's key is free.  Within a batch a slot only ever goes from
-// free to a key of the batch, so a lookup may stop at the first free slot.
-constexpr uint32_t TAB_EPOCHS = 7;
-constexpr int TAB_PROBES = 256;  // a longer walk than this routes the query (crowded)
-__device__ __forceinline__ unsigned long long tab_key(uint32_t ep, uint32_t scope, uint32_t vk) {
-    return ((unsigned long long)ep << 61) | ((unsigned long long)scope << 32) | vk;
-}
-__device__ __forceinline__ bool tab_free(unsigned long long k, uint32_t ep) { return (uint32_t)(k >> 61) != ep; }
-// insert `key` starting at slot h whose current content is `old` (the caller's first CAS of 0 ->
-// key returned it); the slot where the key lives, -1 when the table is crowded.  *rep: the key
-// was already there.
-__device__ __forceinline__ int64_t tab_insert(unsigned long long *tk, uint32_t mask, uint32_t ep, unsigned long long key,
-                                              uint32_t h, unsigned long long old, bool *rep) {
-    *rep = false;
-    for (int probe = 0; probe < TAB_PROBES;) {
-        if (old == 0ull) return h;  // the CAS of 0 -> key that produced `old` inserted it
-        if (old == key) {
-            *rep = true;
-            return h;
-        }
-        if (tab_free(old, ep)) {  // a stale key: replace it
-            const unsigned long long r = atomicCAS(&tk[h], old, key);
-            if (r == old) return h;
-            old = r;  // another lane wrote a key of this batch here: look at it again
-            continue;
-        }
-        h = (h + 1) & mask;
-        probe++;
-        old = atomicCAS(&tk[h], 0ull, key);
-    }
-    return -1;
-}
-
-__device__ __forceinline__ uint32_t tab_hash(unsigned long long key, uint32_t mask) {
-    return (uint32_t)mix64(key & ((1ull << 61) - 1ull)) & mask;  // the epoch does not move a key
-}
-// The decisive keys' bit filter: fr_repeat looks up the table only for occurrences whose bit is
-// set.  64 KB: every fr_repeat block holds it in LDS.  Decisive ES children are rare (Drive: ~3
-// per 1000 queries), so nearly every occurrence is dismissed without a global access.
-constexpr uint32_t DBITS_LOG2 = 19;
-constexpr uint32_t REPEAT_BLOCK = 1024;
-__device__ __forceinline__ uint32_t dbit(unsigned long long key) {
-    return (uint32_t)(mix64(key & ((1ull << 61) - 1ull)) >> 40) & ((1u << DBITS_LOG2) - 1u);
-}
-
-// a routed query: its bit (every later goal of it stops spawning; generation 0 hands it over).
-// One bit per query keeps the flags every goal reads in L2 (128 KB per 2^20 queries) instead of
-// a 4-byte word per query that every goal fetched as a random line from HBM.
-__device__ __forceinline__ void route(const FrontierParams &P, uint32_t pos) {
-    atomicOr(&P.qrouted[pos >> 5], 1u << (pos & 31u));
-    if (!*P.any_routed) atomicOr(P.any_routed, 1u);  // (rare: one word, written once per batch in practice)
-}
-__device__ __forceinline__ bool routed(const FrontierParams &P, uint32_t pos) { return (P.qrouted[pos >> 5] >> (pos & 31u)) & 1u; }
-
-__device__ __forceinline__ void spawn(const FrontierParams &P, uint32_t c, uint32_t node, uint32_t pos, uint32_t word,
-                                      uint32_t scope) {
-    P.g0[c] = make_uint4(node, pos, word, scope);
-}
-
-
-// a generation's slices: exclusive prefix of their counts and their slice-local bases (LDS)
-struct GenMap {
-    uint32_t pre[FR_SHARDS + 1], base[FR_SHARDS];
-};
-__device__ __forceinline__ void load_gen(const FrontierParams &P, uint32_t k, GenMap &m) {
-    for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x) {
-        const uint32_t b = P.gbase[t * GEN_STRIDE + k];
-        m.base[t] = b;
-        m.pre[t + 1] = std::min(P.gcount[t * GEN_STRIDE + k], P.scap - std::min(b, P.scap));
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        m.pre[0] = 0;
-        for (uint32_t t = 0; t < FR_SHARDS; t++) m.pre[t + 1] += m.pre[t];
-    }
-    __syncthreads();
-}
-// the j-th goal of the generation (j < pre[FR_SHARDS]) -> arena index
-__device__ __forceinline__ uint32_t gen_goal(const FrontierParams &P, const GenMap &m, uint32_t j) {
-    uint32_t lo = 0, hi = FR_SHARDS;  // last slice with pre[t] <= j
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (m.pre[mid] <= j) lo = mid;
-        else hi = mid;
-    }
-    return lo * P.scap + m.base[lo] + (j - m.pre[lo]);
-}
-
-// the generation engine's sink: goal records into the arena, occurrences into the sliced list
-struct GlobalSink {
-    const FrontierParams &P;
-    __device__ __forceinline__ void spawn(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope) const {
-        LP(LP_WGOAL, &P.g0[c]);
-        P.g0[c] = make_uint4(node, pos, word, scope);
-    }
-    __device__ __forceinline__ void spawn_es(uint32_t c, uint32_t node, uint32_t pos, uint32_t word, uint32_t scope,
-                                             uint32_t) const {
-        spawn(c, node, pos, word, scope);
-    }
-    __device__ __forceinline__ void occ(uint32_t o, uint32_t scope, uint32_t key) const {
-        LP(LP_WOCC, &P.occ[o]);
-        P.occ[o] = make_uint2(scope, key);
-    }
-};
-// generation 0: query position i in slice i / chunk
-__global__ __launch_bounds__(256) void fr_init(FrontierParams P) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t chunk = (P.n + FR_SHARDS - 1) / FR_SHARDS;
-    if (i < FR_SHARDS) {
-        P.gbase[i * GEN_STRIDE] = 0;
-        P.gcount[i * GEN_STRIDE] = std::min(chunk, P.n - std::min(P.n, i * chunk));
-    }
-    if (i >= P.n) return;
-    const uint4 r0 = P.start[2 * (size_t)i];
-    const uint32_t d = r0.z & 0xFFFFu;
-    P.g0[(i / chunk) * P.scap + i % chunk] = make_uint4(r0.x, i, gword(G_IA, d), NONE32);
-    if (d > GD_MAX) route(P, i);  // (the bits were cleared before the launch)
-    P.qspawn[i] = 0;
-}
-
-// One generation: every goal decides what it can and spawns its children into the next.
-// Registers: 5 waves per SIMD (96 VGPRs).  Since the spine (frontier_goal.inc) the goal code
-// holds more state; C4: 5 waves with phase B reloading the rewrite candidates' rows (no stash)
-// 3.41 ms vs 6 waves with the stash 3.45 ms, 4 waves 3.59 ms (profiles/r04_waves_ab.txt).  (Round
-// 2, before the spine: 6 waves 10.3 vs 5 waves 10.9 ms on the Drive profiling batch.)
-#ifndef KETO_FR_WAVES
-#define KETO_FR_WAVES 5
-#endif
-#ifndef KETO_FR_CAP_GEN
-#define KETO_FR_CAP_GEN 8
-#endif
-#ifndef KETO_FR_BLOCK
-#define KETO_FR_BLOCK 256
-#endif
-constexpr uint32_t XBLOCK = KETO_FR_BLOCK;  // fr_expand's block: the regroup window
-template <bool LDS_TABLES>
-__global__ __launch_bounds__(XBLOCK, KETO_FR_WAVES) void fr_expand(FrontierParams P) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    const DevSnapshot &s = P.s;
-    __shared__ GenMap gm;
-    const uint32_t k = P.gen;
-    load_gen(P, k, gm);
-    const uint32_t cnt = gm.pre[FR_SHARDS];
-    // the next generation in each slice starts where this one ends
-    if (blockIdx.x == 0)
-        for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x)
-            P.gbase[t * GEN_STRIDE + k + 1] = gm.base[t] + (gm.pre[t + 1] - gm.pre[t]);
-    // blocks without a goal of this generation leave before staging the tables: small batches
-    // and the empty generations an asynchronous batch launches speculatively cost ~nothing
-    if (blockIdx.x * blockDim.x >= cnt) return;
-    const Tables T = LDS_TABLES ? stage_tables(s, lds) : global_tables(s);
-    // A goal reads its query's routed bit only once some query of the batch was routed (by an
-    // earlier generation, or this one so far): one word per block instead of a load per goal.
-    // Routing is best-effort pruning here -- the decision at generation 0 reads the bits themselves.
-#ifndef KETO_NO_RFLAG  // (A/B builds: every goal reads its bit)
-    const bool any_routed = *P.any_routed != 0u;
-#else
-    const bool any_routed = true;
-#endif
-    // this wave's slice
-    const uint32_t so = (blockIdx.x * ((blockDim.x + 63) >> 6) + (threadIdx.x >> 6)) % FR_SHARDS;
-    const uint32_t nbase = so * P.scap + gm.base[so] + (gm.pre[so + 1] - gm.pre[so]), send = (so + 1) * P.scap;
-    const bool last = k + 1 >= P.gen_cap;
-    const uint32_t W = P.max_width;
-#ifdef KETO_FR_PROF
-    unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
-#endif
-#ifndef KETO_FR_RG_BUCKETS
-#define KETO_FR_RG_BUCKETS 3
-#endif
-#ifndef KETO_FR_NOREGROUP
-    constexpr uint32_t NB = KETO_FR_RG_BUCKETS;  // goal classes; dead lanes are one more
-    __shared__ uint4 rg_g[XBLOCK];
-    __shared__ uint32_t rg_i[XBLOCK], rg_n[XBLOCK / 64][NB + 1];
-#ifndef KETO_FR_LATE_SUBJ
-    __shared__ uint4 rg_s[XBLOCK];
-#endif
-#endif
-    for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
-        const uint32_t j = j0 + threadIdx.x;
-        // goals of queries routed meanwhile still run (rare); they can no longer spawn
-        bool live = j < cnt;
-        uint32_t i = live ? gen_goal(P, gm, j) : 0u;
-#ifdef KETO_FR_LOADPROF
-        if (live) LP(LP_G0, &P.g0[i]);
-#endif
-        uint4 g = live ? P.g0[i] : make_uint4(0, 0, 0, 0);
-        // (the goal this thread loaded, and where the regroup put it: its gfn / gvs record is
-        // written back by this thread, in generation order, from the slot's results)
-        const bool own_live = live;
-        const uint32_t own_i = i;
-        uint32_t own_slot = threadIdx.x;
-#if !defined(KETO_FR_NOREGROUP) && !defined(KETO_FR_LATE_SUBJ)
-        // the query subject's membership record, loaded in generation order -- neighbouring goals
-        // mostly belong to one query (a parent's children are contiguous), so a wave's loads fall
-        // on few records and coalesce -- and carried through the regroup in LDS
-#ifdef KETO_FR_LOADPROF
-        if (live) LP(LP_SUBJ, &P.start[2 * (size_t)g.y + 1]);
-#endif
-        uint4 srec = live ? P.start[2 * (size_t)g.y + 1] : make_uint4(0, 0, 0, 0);
-#endif
-#ifndef KETO_FR_NOREGROUP
-        {   // Block regroup: the block's goals ordered by class -- expand-subjects, rewrites, the
-            // rest, then dead lanes; batch order within a class -- so that a wave runs one class's
-            // code instead of several under divergence.
-            const uint32_t wv = threadIdx.x >> 6, ln = __lane_id(), nw = (blockDim.x + 63) >> 6;
-            uint32_t cls = NB;
-            if (live) {
-                const uint32_t kd = (g.z >> 12) & 7u;
-                if (kd == G_ES) cls = 0;
-                else if (NB > 2 && kd == G_RW) cls = 1;  // (an AND over one OR runs the OR's code: and_merge)
-                else cls = NB - 1;
-            }
-            uint32_t rank = 0;
-            for (uint32_t c = 0; c <= NB; c++) {
-                const unsigned long long b = __ballot(cls == c);
-                if (c == cls) rank = (uint32_t)__popcll(b & ((1ull << ln) - 1ull));
-                if (ln == 0) rg_n[wv][c] = (uint32_t)__popcll(b);
-            }
-            __syncthreads();
-            uint32_t slot = rank, n_live = 0;
-            for (uint32_t c = 0; c <= NB; c++)
-                for (uint32_t t = 0; t < nw; t++) {
-                    const uint32_t m = rg_n[t][c];
-                    if (c < cls || (c == cls && t < wv)) slot += m;
-                    if (c < NB) n_live += m;
-                }
-            rg_g[slot] = g;
-            rg_i[slot] = i;
-#ifndef KETO_FR_LATE_SUBJ
-            rg_s[slot] = srec;
-#endif
-            own_slot = slot;
-            __syncthreads();
-            g = rg_g[threadIdx.x];
-            i = rg_i[threadIdx.x];
-#ifndef KETO_FR_LATE_SUBJ
-            srec = rg_s[threadIdx.x];
-#endif
-            live = threadIdx.x < n_live;
-        }
-#endif
-        const uint32_t node = g.x, pos = g.y, w = g.z, scope = g.w;
-        const uint32_t d = w & GD_MAX, kind = (w >> 12) & 7u, op = w >> 16;
-        const bool qr = live && any_routed && routed(P, pos);
-        // The loads the goal kinds start from, issued together: the row an ES / TTU reads, and
-        // the subject's membership record (IA direct check, ES lookahead, OR shortcut).
-        uint32_t rnode = NONE32;
-        if (live && kind == G_ES && !(node & VIRT_BIT)) rnode = node;
-        if (live && kind == G_TTU && d > 1) {
-            const uint32_t ts = t_sibling(T, node, t_node_info(T, node), T.ops[op].rel_computed & 0xFFFFu);
-            if (!(ts & VIRT_BIT)) rnode = ts;
-        }
-#ifdef KETO_FR_LOADPROF
-        if (rnode != NONE32) LP(LP_ROW, &s.set_row[rnode]);
-        if (live && any_routed) LP(LP_ROUTED, &P.qrouted[pos >> 5]);
-#endif
-        const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
-#if !defined(KETO_FR_NOREGROUP) && !defined(KETO_FR_LATE_SUBJ)
-        const Subject q = live ? subject_of(srec) : Subject{0, false, make_uint4(0, 0, 0, 0)};
-#else
-        const Subject q = live ? load_subject(P, pos) : Subject{0, false, make_uint4(0, 0, 0, 0)};
-#endif
-        FR_MARK(0);
-        // ---- phase A: decide, or count the children -------------------------------------------
-        const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W);
-        uint32_t nc = pa.nc, val = pa.val;
-        const uint32_t rop = pa.rop, pat = pa.pat, sc = pa.sc, xrel = pa.xrel;
-        const bool chain = pa.chain;
-        (void)sc;
-        if (nc > NC_MAX) {  // a row too long for the record: the DFS interpreter takes the query
-            route(P, pos);
-            nc = 0;
-        }
-        FR_MARK(1);
-        // ---- budget and generation cap.  A query's goal count is its root's subtree count, summed
-        // bottom-up by fr_reduce (gvs.y) without atomics, and compared with the budget at
-        // generation 0; here a routed query (its bit set by route) stops spawning, as does
-        // a goal with more children than the budget or at the last generation.  A query past its
-        // budget spawns on meanwhile (bounded by MAX_GEN and its arena slice) -----------------------
-        const uint32_t lane = __lane_id();
-        if (nc && (qr || nc > P.budget || last)) {
-            route(P, pos);
-            nc = 0;
-        }
-#ifndef KETO_FR_NOSPAWNCAP  // (A/B builds only)
-        // A query past its budget is routed at generation 0 anyway (fr_reduce's subtree count);
-        // from generation KETO_FR_CAP_GEN on its spawns are also counted as they happen, and one
-        // whose count alone passes the budget stops here: a runaway query would otherwise keep
-        // spawning until MAX_GEN and fill its arena slice, routing its neighbours with it.  (The
-        // count is a lower bound of the subtree count, so the routed set is unchanged.)
-        if (nc && k >= KETO_FR_CAP_GEN && 1u + atomicAdd(&P.qspawn[pos], nc) + nc > P.budget) {
-            route(P, pos);
-            nc = 0;
-        }
-#endif
-        FR_MARK(2);
-        // ---- allocation: one atomic per wave, on the wave's slice counter -------------------------
-        uint32_t wtot = 0;
-        const uint32_t off = wave_excl(nc, wtot);
-        uint32_t wbase = 0;
-        if (lane == 0 && wtot) wbase = atomicAdd(&P.gcount[so * GEN_STRIDE + k + 1], wtot);
-        const uint32_t cb = nbase + __shfl(wbase, 0) + off;
-        if (nc && (uint64_t)cb + nc > send) {  // slice full: route; fill the allocated slots that exist
-            route(P, pos);
-            for (uint32_t c = cb; c < send && c < cb + nc; c++) spawn(P, c, 0, pos, gword(G_DEAD, 0), NONE32);
-            nc = 0;
-            val = M_NOT;
-        }
-#if !defined(KETO_FR_NOREGROUP) && !defined(KETO_FR_OLDGFN)  // (KETO_FR_OLDGFN: A/B builds)
-        // the goal records go out in generation order: the regrouped lane leaves them in its LDS
-        // slot (rg_g: this lane alone read it since the regroup), the thread that loaded the goal
-        // writes them -- consecutive goals from consecutive lanes, whole lines per wave instead of
-        // one scattered 8 B + 4 B write per goal (those were most of the kernel's write requests)
-        if (live) rg_g[threadIdx.x] = make_uint4(cb, nc | (rop << 24) | (chain ? GFN_CHAIN : 0u), val, 0);
-        __syncthreads();
-        if (own_live) {
-            LP(LP_WFN, &P.gfn[own_i]);
-            LP(LP_WFN, &P.gvs[own_i]);
-            const uint4 r = rg_g[own_slot];
-            P.gfn[own_i] = make_uint2(r.x, r.y);
-            reinterpret_cast<uint32_t *>(P.gvs)[2 * (size_t)own_i] = r.z;
-        }
-#else
-        (void)own_live;
-        (void)own_i;
-        (void)own_slot;
-        if (live) {
-            P.gfn[i] = make_uint2(cb, nc | (rop << 24) | (chain ? GFN_CHAIN : 0u));
-            reinterpret_cast<uint32_t *>(P.gvs)[2 * (size_t)i] = val;
-        }
-#endif
-        // ---- occurrences: an ES goal's kept children, goals and leaves alike, are the keys it
-        // adds to its scope (CheckAndAddVisited, engine.go:157-160): one run of its wave's slice
-        const uint32_t nocc = (live && kind == G_ES && (nc || xrel)) ? pat + (chain ? 1u : 0u) : 0u;
-        uint32_t otot = 0;
-        const uint32_t ooff = wave_excl(nocc, otot);
-        uint32_t obase = 0;
-        if (lane == 0 && otot) obase = atomicAdd(&P.occ_count[so], otot);
-        uint32_t oc = __shfl(obase, 0) + ooff;
-        const bool occ_ok = (uint64_t)oc + nocc <= P.ocap;
-        if (nocc && !occ_ok) {  // list full: the DFS interpreter takes the query; the allocated slots
-            route(P, pos);      // that exist are cleared, so fr_repeat never counts an older batch's pair
-            for (uint32_t e = oc; e < P.ocap && e < oc + nocc; e++) P.occ[(size_t)so * P.ocap + e] = make_uint2(NONE32, 0);
-        }
-        oc += so * P.ocap;
-        FR_MARK(3);
-        // ---- phase B: write the children (the same walk as phase A) -------------------------------
-        if (nc || (kind == G_ES && xrel)) {
-            GlobalSink gs{P};
-            PhaseA pb = pa;
-            pb.nc = nc;
-            phase_b(s, T, q, node, pos, w, scope, row, pb, cb, oc, occ_ok, gs);
-        }
-        FR_MARK(4);
-    }
-#ifdef KETO_FR_PROF
-    if (__lane_id() == 0)
-        for (int n = 0; n < 7; n++) atomicAdd(&P.prof[n], pacc[n]);
-#endif
-}
-
-// a decisive occurrence of (scope, key): into the decisive table and its bit filter
-__device__ __forceinline__ void dec_insert(const FrontierParams &P, uint32_t scope, uint32_t vk, uint32_t pos) {
-    const unsigned long long key = tab_key(P.epoch, scope, vk);
-    const uint32_t h = tab_hash(key, P.dmask);
-    bool rep = false;
-    const int64_t at = tab_insert(P.dkeys, P.dmask, P.epoch, key, h, atomicCAS(&P.dkeys[h], 0ull, key), &rep);
-    if (at < 0) route(P, pos);  // crowded: the DFS interpreter takes the query
-    else if (!rep) P.dcnt[at] = 0;
-    const uint32_t b = dbit(key);
-    atomicOr(&P.dbits[b >> 5], 1u << (b & 31u));
-}
-
-// One generation, bottom-up: each goal reduces its children in add order (checkgroup H0,
-// binop.go, rewrites.go:183-199); a decisive occurrence of a repeated scope key routes the
-// query; generation 0 writes the decisions.  Every goal of the generation was expanded in
-// this batch, so its children range is always this batch's.
-__global__ __launch_bounds__(256) void fr_reduce(FrontierParams P) {
-    const DevSnapshot &s = P.s;
-    const uint32_t k = P.gen;
-    __shared__ GenMap gm;
-    load_gen(P, k, gm);
-    const uint32_t cnt = gm.pre[FR_SHARDS];
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
-        const uint32_t i = gen_goal(P, gm, j);
-        const uint2 fn = P.gfn[i];
-        uint32_t val = reinterpret_cast<const uint32_t *>(P.gvs)[2 * (size_t)i];
-        const uint32_t nc = fn.y & NC_MAX, rop = (fn.y >> 24) & 3u;
-        uint32_t sub = nc;  // goals below this one (the budget's count)
-        if (nc) {
-            uint32_t res = NONE32;
-            auto fold = [&](const uint2 v) {  // every child's count; the fold up to its result
-                sub += v.y;
-                if (res != NONE32) return;
-                const uint32_t cv = v.x;
-                if (rop == R_FIRST || rop == R_FIRST_AND) {  // first Err / IsMember
-                    if (decisive(cv)) res = cv;
-                } else if (rop == R_AND) {  // AND: the first non-member, keeping its error
-                    if ((cv >> 8) != 0 || (cv & 3u) != M_IS) res = (cv & ~3u) | M_NOT;
-                } else {  // NOT swaps IsMember / NotMember, keeps Unknown and the error
-                    const uint32_t m = cv & 3u;
-                    res = m == M_IS ? ((cv & ~3u) | M_NOT) : (m == M_NOT ? ((cv & ~3u) | M_IS) : cv);
-                }
-            };
-#ifdef KETO_FR_RED_SERIAL
-            for (uint32_t c = fn.x; c < fn.x + nc; c++) fold(P.gvs[c]);
-#else
-            // the children's records four at a time, their loads issued together
-            const uint32_t ce = fn.x + nc;
-            for (uint32_t c0 = fn.x; c0 < ce; c0 += 4) {
-                uint2 v[4];
-#pragma unroll
-                for (uint32_t u = 0; u < 4; u++) v[u] = c0 + u < ce ? P.gvs[c0 + u] : make_uint2(0, 0);
-#pragma unroll
-                for (uint32_t u = 0; u < 4; u++)
-                    if (c0 + u < ce) fold(v[u]);
-            }
-#endif
-            if (res == NONE32) res = val != NONE32 ? val : (rop == R_AND ? M_IS : M_NOT);
-            if (rop == R_FIRST_AND) res = and_map(res);  // an AND over its merged OR
-            val = res;
-        }
-        P.gvs[i] = make_uint2(val, sub);
-        if (k > 0 && decisive(val)) {  // a decisive ES child: its key goes into the decisive table
-            const uint4 g = P.g0[i];
-            if ((((g.z >> 12) & 7u) == G_IA || ((g.z >> 12) & 7u) == G_ES) && (g.z & GF_ESCHILD))  // (RW / TTU / INV hold an op there)
-                dec_insert(P, g.w, (g.z & GF_ALIAS) ? s.vkey[g.x] : g.x, g.y);
-            if (fn.y & GFN_CHAIN) {  // the child whose expand-subject it ran is decisive too
-                const uint32_t rawc = s.set_row[g.x].z, cc = rawc & s.edge_mask;
-                dec_insert(P, g.w == NONE32 ? i : g.w, (rawc & EDGE_ALIAS) ? s.vkey[cc] : cc, g.y);
-            }
-        }
-        if (k == 0) {  // generation 0: one goal per query position
-            const uint32_t pos = P.g0[i].y;
-            if (routed(P, pos) || 1u + sub > P.budget) {
-                P.fb_list[atomicAdd(P.fb_count, 1u)] = P.pos_base + pos;
-                continue;
-            }
-            const uint32_t q = P.start[2 * (size_t)pos].w;
-            const uint32_t err = val >> 8;
-            P.out_allowed[q] = (err == 0 && (val & 3u) == M_IS) ? 1 : 0;
-            P.out_err[q] = (int32_t)(P.err_detail ? err : err & 0xFFu);
-        }
-    }
-}
-
-// After every generation above 0 is reduced: each occurrence of a decisive key counts itself;
-// a second occurrence routes the query (the scope's first goal holds its position).
-__global__ __launch_bounds__(REPEAT_BLOCK) void fr_repeat(FrontierParams P) {
-    __shared__ uint32_t pre[FR_SHARDS + 1];
-    __shared__ uint4 bits[(1u << DBITS_LOG2) / 128];
-    for (uint32_t t = threadIdx.x; t < (1u << DBITS_LOG2) / 128; t += blockDim.x) bits[t] = reinterpret_cast<const uint4 *>(P.dbits)[t];
-    for (uint32_t t = threadIdx.x; t < FR_SHARDS; t += blockDim.x) pre[t + 1] = std::min(P.occ_count[t], P.ocap);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        pre[0] = 0;
-        for (uint32_t t = 0; t < FR_SHARDS; t++) pre[t + 1] += pre[t];
-    }
-    __syncthreads();
-    const uint32_t total = pre[FR_SHARDS];
-    constexpr uint32_t U = 4;  // occurrences in flight per lane (the loop is latency-bound)
-    const uint32_t G = gridDim.x * blockDim.x;
-    for (uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x; j0 < total; j0 += U * G) {
-        uint2 o[U];
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const uint32_t j = j0 + u * G;
-            o[u] = make_uint2(NONE32, 0);
-            if (j < total) {
-                uint32_t lo = 0, hi = FR_SHARDS;  // last slice with pre[t] <= j
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (pre[mid] <= j) lo = mid;
-                    else hi = mid;
-                }
-                o[u] = P.occ[(size_t)lo * P.ocap + (j - pre[lo])];
-            }
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            if (o[u].x == NONE32) continue;
-            const unsigned long long key = tab_key(P.epoch, o[u].x, o[u].y);
-            const uint32_t b = dbit(key);
-            if (!((reinterpret_cast<const uint32_t *>(bits)[b >> 5] >> (b & 31u)) & 1u)) continue;  // not a decisive key
-            uint32_t h = tab_hash(key, P.dmask);
-            for (int probe = 0; probe < TAB_PROBES; probe++) {
-                const unsigned long long kk = P.dkeys[h];
-                if (kk == key) {
-                    if (atomicAdd(&P.dcnt[h], 1u) >= 1u) route(P, P.g0[o[u].x].y);
-                    break;
-                }
-                if (tab_free(kk, P.epoch)) break;
-                h = (h + 1) & P.dmask;
-            }
-        }
-    }
-}
+#include "frontier_kernels.inc"
 
 }  // namespace
 
@@ -759,7 +203,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     // a persistent grid: exactly the blocks that fit at once (a block waiting for a free slot would
     // run only after a resident one finished its whole share)
     int per_cu = 0;
-    const void *kx = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true>) : reinterpret_cast<const void *>(&fr_expand<false>);
+    const void *kx = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true, false>) : reinterpret_cast<const void *>(&fr_expand<false, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kx, XBLOCK, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
     const dim3 eg(cus * (uint32_t)std::min(per_cu, (int)(2048 / XBLOCK))), xb(XBLOCK), eb(BLOCK);
     if (L.async) {
@@ -784,8 +228,8 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
         P.gen_cap = G;
         for (uint32_t k = 0; k < G; k++) {
             P.gen = k;
-            if (lds_tables) hipLaunchKernelGGL(fr_expand<true>, eg, xb, lds, st.stream, P);
-            else hipLaunchKernelGGL(fr_expand<false>, eg, xb, 0, st.stream, P);
+            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false>), eg, xb, lds, st.stream, P);
+            else hipLaunchKernelGGL((fr_expand<false, false>), eg, xb, 0, st.stream, P);
             KETO_HIP(hipGetLastError());
         }
         for (int32_t g = (int32_t)G - 1; g >= 0; g--) {
@@ -794,7 +238,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
                 hipLaunchKernelGGL(fr_repeat, dim3(cus * 2), dim3(REPEAT_BLOCK), 0, st.stream, P);
                 KETO_HIP(hipGetLastError());
             }
-            hipLaunchKernelGGL(fr_reduce, dim3(cus * KETO_FR_RGRID), eb, 0, st.stream, P);
+            hipLaunchKernelGGL(fr_reduce<false>, dim3(cus * KETO_FR_RGRID), eb, 0, st.stream, P);
             KETO_HIP(hipGetLastError());
         }
         if (!f.gens_pending) {  // this pass's depth, for a later one (one read-back in flight at a time)
@@ -822,8 +266,8 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
         const uint32_t kend = std::min(k + (k == 0 ? std::max(CHUNK, f.last_gens + 1) : CHUNK), MAX_GEN);
         for (; k < kend; k++) {
             P.gen = k;
-            if (lds_tables) hipLaunchKernelGGL(fr_expand<true>, eg, xb, lds, st.stream, P);
-            else hipLaunchKernelGGL(fr_expand<false>, eg, xb, 0, st.stream, P);
+            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false>), eg, xb, lds, st.stream, P);
+            else hipLaunchKernelGGL((fr_expand<false, false>), eg, xb, 0, st.stream, P);
             KETO_HIP(hipGetLastError());
         }
         KETO_HIP(hipMemcpyAsync(hc, f.ctrl, 2 * FR_SHARDS * GEN_STRIDE * 4, hipMemcpyDeviceToHost, st.stream));
@@ -852,7 +296,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
             KETO_HIP(hipGetLastError());
         }
         const dim3 rg((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tot[g] + BLOCK - 1) / BLOCK, cus * 16)));
-        hipLaunchKernelGGL(fr_reduce, rg, eb, 0, st.stream, P);
+        hipLaunchKernelGGL(fr_reduce<false>, rg, eb, 0, st.stream, P);
         KETO_HIP(hipGetLastError());
     }
     if (++f.epoch > TAB_EPOCHS) {  // every TAB_EPOCHS batches: clear the table

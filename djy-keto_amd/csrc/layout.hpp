@@ -23,6 +23,9 @@ constexpr uint32_t EDGE_ALIAS = 0x80000000u; // set_dst entry: visited key != no
 // subject-set tuple, so its expand-subject finds nothing -- an ES child the frontier engine
 // decides at spawn instead of spawning a goal that reads an empty row
 constexpr uint32_t EDGE_LEAF = 0x40000000u;
+// set_dst entry of a partitioned graph's snapshot (frontier_dist.hip; these snapshots carry no
+// EDGE_LEAF): the child node belongs to an object another rank owns -- its rows are there
+constexpr uint32_t EDGE_REMOTE = 0x40000000u;
 constexpr uint32_t SKEY_SET = 0x80000000u;   // all-row entry: subject set (else subject id)
 constexpr uint32_t NO_SLOT = 0xFFFFu;
 constexpr uint32_t NO_OP = 0xFFFFu;
@@ -87,6 +90,7 @@ struct DevSnapshot {
     const uint32_t *ent_obj;   // [n_entities] entity -> uuid id (NONE32 for phantoms): Expand output
     const uint32_t *slot_rel;  // [total slots] global slot -> relation name id: Expand output
     const uint32_t *vkey;      // [n_nodes] visited representative (only read for aliased nodes)
+    const uint32_t *vclass;    // [total slots] partitioned graphs: visited class of a slot (frontier_goal.inc gkey)
     const uint32_t *all_off;   // [n_nodes+1]  every tuple of a node, shard order (Expand)
     const uint32_t *all_subj;  // subject id, or SKEY_SET|node
     const uint32_t *rev_off;   // [n_uuids + n_nodes + 1]  subject -> sorted nodes containing it

@@ -48,6 +48,7 @@
 #include <vector>
 
 #include "device_common.hpp"
+#include "frontier_dist.hpp"
 
 namespace keto {
 namespace {
@@ -258,6 +259,11 @@ struct Lookup {
     const uint32_t *subj_bits;    // 2^SUBJ_BITS-bit filter of the set: most subject-id tuples miss it
     uint32_t world;
     int filter;
+    // a job over resident partitions (frontier_dist.hip): the rows of the rank's own snapshot stand
+    // for the store -- an object's tuples are its nodes' Expand rows (all_off / all_subj: one
+    // contiguous range per entity, slot after slot, each in shard order)
+    bool use_snap = false;
+    DevSnapshot S{};
 };
 __device__ __forceinline__ unsigned long long subj_key(uint32_t src, uint32_t sid) {
     return (((unsigned long long)src << 32) | sid) + 1ull;  // 0 = empty slot
@@ -304,8 +310,66 @@ __device__ __forceinline__ bool index_range(const uint4 *index, uint64_t mask, c
     }
 }
 __device__ __forceinline__ bool run_of(const Lookup &L, uint64_t key, uint64_t &b, uint64_t &e) {
+    if (L.use_snap) {
+        const uint32_t ns = (uint32_t)(key >> 32), en = ent_lookup(L.S, ns, (uint32_t)key);
+        if (en == NONE32) return false;
+        const NsDev nd = L.S.ns[ns];
+        const uint32_t node0 = nd.node_base + (en - nd.ent_base) * nd.n_slots;
+        b = L.S.all_off[node0];
+        e = L.S.all_off[node0 + nd.n_slots];
+        return true;
+    }
     uint32_t r;
     return index_range(L.index, L.index_mask, L.beg, key, b, e, r);
+}
+// the store record at position j: {subject, kind bit 31} (st_meta's fields the filter reads)
+__device__ __forceinline__ uint2 meta_at(const Lookup &L, uint64_t j) {
+    if (L.use_snap) {
+        const uint32_t sub = L.S.all_subj[j];
+        return make_uint2(sub & ~SKEY_SET, (sub & SKEY_SET) ? 1u << 31 : 0u);
+    }
+    return L.meta[j];
+}
+// the tuple at position j of key's run.  Resident snapshots: its node is the slot whose all-row
+// holds j, and its shard_id the position in that row (big-endian), which is all the closure
+// snapshot's sort by shard_id needs to rebuild every row in order
+__device__ __forceinline__ keto_tuple tuple_at(const Lookup &L, uint64_t key, uint64_t j) {
+    if (!L.use_snap) return st_tuple(key, L.meta[j], L.shard[j]);
+    const DevSnapshot &S = L.S;
+    const uint32_t ns = (uint32_t)(key >> 32), obj = (uint32_t)key;
+    const NsDev nd = S.ns[ns];
+    const uint32_t node0 = nd.node_base + (ent_lookup(S, ns, obj) - nd.ent_base) * nd.n_slots;
+    uint32_t k = 0;
+    while (k + 1 < nd.n_slots && S.all_off[node0 + k + 1] <= j) k++;
+    keto_tuple t;
+    t.ns = ns;
+    t.obj = obj;
+    t.rel = S.slot_rel[nd.slot_base + k];
+    t.reserved = 0;
+    const uint32_t sub = S.all_subj[j];
+    if (sub & SKEY_SET) {
+        const uint32_t c = sub & ~SKEY_SET;
+        uint32_t lo = 0, hi = S.n_ns;  // last namespace whose node_base <= c
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (S.ns[m].node_base <= c) lo = m;
+            else hi = m;
+        }
+        const NsDev n2 = S.ns[lo];
+        t.subj_kind = 1;
+        t.s_ns = lo;
+        t.s_obj = S.ent_obj[n2.ent_base + (c - n2.node_base) / n2.n_slots];
+        t.s_rel = S.slot_rel[n2.slot_base + (c - n2.node_base) % n2.n_slots];
+    } else {
+        t.subj_kind = 0;
+        t.s_obj = sub;
+        t.s_ns = 0;
+        t.s_rel = 0;
+    }
+    const uint32_t p = (uint32_t)(j - S.all_off[node0 + k]);  // shard_id bytes 0-3 = p, big-endian
+    *reinterpret_cast<uint4 *>(t.shard_id) =
+        make_uint4(((p >> 24) & 0xFFu) | (((p >> 16) & 0xFFu) << 8) | (((p >> 8) & 0xFFu) << 16) | ((p & 0xFFu) << 24), 0, 0, 0);
+    return t;
 }
 __device__ __forceinline__ uint32_t source_of(const Lookup &L, uint64_t i) {
     uint32_t lo = 0, hi = L.world;  // last source whose offset <= i
@@ -335,7 +399,7 @@ __global__ __launch_bounds__(BLK) void k_lookup_count(Lookup L, uint64_t n, uint
         uint32_t c = 0;
         if (run_of(L, L.req[i], b, e)) {
             const uint32_t src = source_of(L, i);
-            for (uint64_t j = b; j < e; j++) c += keep(L, L.meta[j], src) ? 1 : 0;
+            for (uint64_t j = b; j < e; j++) c += keep(L, meta_at(L, j), src) ? 1 : 0;
         }
         cnt[i] = c;
     }
@@ -346,10 +410,8 @@ __global__ __launch_bounds__(BLK) void k_lookup_fill(Lookup L, uint64_t n, const
         if (!run_of(L, L.req[i], b, e)) continue;
         const uint32_t src = source_of(L, i);
         uint64_t o = pos[i];
-        for (uint64_t j = b; j < e; j++) {
-            const uint2 m = L.meta[j];
-            if (keep(L, m, src)) out[o++] = st_tuple(L.req[i], m, L.shard[j]);
-        }
+        for (uint64_t j = b; j < e; j++)
+            if (keep(L, meta_at(L, j), src)) out[o++] = tuple_at(L, L.req[i], j);
     }
 }
 // Block exclusive scan of one u32 per thread (wave scans + the waves' sums); *tot = the sum.
@@ -419,7 +481,7 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, con
                         if (s_off[mid] <= x) lo = mid;
                         else hi = mid;
                     }
-                    kp = keep(L, L.meta[s_b[lo] + (x - s_off[lo])], 0);
+                    kp = keep(L, meta_at(L, s_b[lo] + (x - s_off[lo])), 0);
                 }
                 const unsigned long long m = __ballot(kp);
                 const uint32_t lane = __lane_id();
@@ -448,7 +510,7 @@ __global__ __launch_bounds__(BLK) void k_lookup_gather(Lookup L, uint64_t n, con
                     else hi = mid;
                 }
                 const uint64_t j = s_b[lo] + (x - s_off[lo]);
-                out[pos] = st_tuple(s_key[lo], L.meta[j], L.shard[j]);
+                out[pos] = tuple_at(L, s_key[lo], j);
             }
             __syncthreads();
         }
@@ -570,6 +632,11 @@ struct Partition {
     // a job of one rank: the whole graph as one resident snapshot, built at creation (null: the
     // per-batch closure path)
     std::unique_ptr<Snapshot> home;
+    // a job of several ranks: this rank's partition as a resident snapshot and the distributed
+    // frontier engine over it (frontier_dist.hip); the closure path answers its routed queries and
+    // Expand, reading that snapshot's rows (no separate store)
+    DistEngine *dist = nullptr;
+    DistStats dstats{};
     hipStream_t hs = nullptr;
     keto_stream *kstream = nullptr;
     // per-batch workspace (grown on demand, reused)
@@ -604,6 +671,7 @@ struct Partition {
     std::vector<uint64_t> xoffs;
     std::vector<int32_t> xerr;
     ~Partition() {
+        if (dist) dist_free(dist);
         if (hpin) (void)hipHostFree(hpin);
         if (kstream) keto_stream_destroy(kstream);
         scratch_forget_stream(hs);
@@ -614,6 +682,13 @@ struct Partition {
 };
 
 void sync(Partition &P) { KETO_HIP(hipStreamSynchronize(P.hs)); }
+
+// the closure's owner-side reads from the resident partition (a job of several ranks)
+void snap_source(Partition &P, Lookup &L) {
+    if (!P.dist) return;
+    L.use_snap = true;
+    L.S = dist_snapshot(*P.dist).dev;
+}
 
 uint64_t d2h_u64(Partition &P, const void *d) {
     uint64_t v = 0;
@@ -722,6 +797,7 @@ uint64_t closure_self(Partition &P, const uint64_t *keys, uint64_t n_keys, bool 
     Lookup L{dptr<uint64_t>(P.ukeys), dptr<uint64_t>(P.beg), P.m, dptr<uint4>(P.index), P.index_mask,
              dptr<uint2>(P.meta), dptr<uint4>(P.shard), dptr<uint64_t>(P.fresh), dptr<uint64_t>(P.req_off),
              dptr<ull>(P.subj_set), P.subj_mask, dptr<uint32_t>(P.subj_bits), 1u, filter ? 1 : 0};
+    snap_source(P, L);
     const dim3 G(std::max(1, num_cus(P.device)) * 8u);
     keto_tuple *cl = dptr<keto_tuple>(P.closure);
     for (int l = 0; l < levels; l++) {
@@ -892,6 +968,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
                  dptr<uint2>(P.meta), dptr<uint4>(P.shard),
                  dptr<uint64_t>(P.req), dptr<uint64_t>(P.req_off), dptr<unsigned long long>(P.subj_set), P.subj_mask,
                  dptr<uint32_t>(P.subj_bits), W, filter ? 1 : 0};
+        snap_source(P, L);
         if (W == 1 && P.closure.p) {  // one rank: a single gathering pass into the closure (k_lookup_gather)
             const uint64_t cap = P.closure.bytes / sizeof(keto_tuple) - total;
             unsigned long long *g = dptr<unsigned long long>(P.ctr) + 2;  // [2] total, [3] overflow
@@ -1022,6 +1099,15 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     P->trim = getenv("KETO_PART_TRIM") != nullptr;
     if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
     P->n = n;
+    if (P->world > 1 && !getenv("KETO_PART_CLOSURE")) {
+        // several ranks: the partition resident, the distributed frontier over it
+        auto t0 = std::chrono::steady_clock::now();
+        P->dist = dist_create(&P->cfg, tuples, n, device_ptrs, P->coll, P->limits);
+        if (P->verbose)
+            fprintf(stderr, "[keto partition] rank %u: %llu tuples as a resident partition, %.2f s\n", P->rank,
+                    (unsigned long long)n, secs(t0));
+        return P.release();
+    }
     if (P->world == 1 && !getenv("KETO_PART_CLOSURE")) {
         // one rank owns every object: its partition is the whole graph, built once into a
         // resident snapshot (scheduling weights included, as a replica's) that every batch reads
@@ -1294,6 +1380,64 @@ void home_check_many(Partition &P, uint32_t nb, const keto_query *const *q, cons
     P.last = st;
     P.last_levels.clear();
 }
+
+// A job of several ranks: each batch through the distributed frontier over the resident
+// partitions (frontier_dist.hip), then the queries it routed -- when any rank has some -- through
+// the per-batch closure, every rank taking part with its own (possibly none).  A counted batch
+// (KETO_F_COUNT_WORK: the DFS interpreter's work counters) runs on the closure path whole.
+void dist_check_many(Partition &P, uint32_t nb, const keto_query *const *q, const uint64_t *n, uint8_t *const *allowed,
+                     int32_t *const *err, uint32_t flags) {
+    const bool count = (flags & KETO_F_COUNT_WORK) != 0;
+    for (uint32_t k = 0; k < nb; k++) {
+        auto t0 = std::chrono::steady_clock::now();
+        keto_partition_stats st{};
+        st.batches = 1;
+        std::vector<uint32_t> routed;
+        if (count) {
+            routed.resize(n[k]);
+            for (uint64_t i = 0; i < n[k]; i++) routed[i] = (uint32_t)i;
+            P.last_levels.clear();
+        } else {
+            DistStats ds{};
+            dist_check(*P.dist, q[k], n[k], allowed[k], err[k], (flags & KETO_F_ERR_DETAIL) != 0, routed, ds);
+            P.dstats = ds;
+            st.generations = ds.generations;
+            st.goals = ds.goals;
+            st.routed = ds.routed;
+            st.exchange_bytes = ds.bytes_exchanged;
+            st.device_s = ds.device_s;
+            st.exchange_s = ds.exchange_s;
+            P.last_levels = dist_levels(*P.dist);
+        }
+        const uint64_t nr = routed.size();
+        if (allreduce_max(P, nr) > 0) {
+            std::vector<keto_query> sub(std::max<uint64_t>(1, nr));
+            for (uint64_t i = 0; i < nr; i++) sub[i] = q[k][routed[i]];
+            std::vector<uint8_t> a(std::max<uint64_t>(1, nr));
+            std::vector<int32_t> e(std::max<uint64_t>(1, nr));
+            Partition::Slot &S = P.slots[0];
+            stage_closure(P, S, sub.data(), nr);
+            stage_check(P, S, nr, a.data(), e.data(), flags);
+            for (uint64_t i = 0; i < nr; i++) {
+                allowed[k][routed[i]] = a[i];
+                err[k][routed[i]] = e[i];
+            }
+            st.levels = S.st.levels;
+            st.objects = S.st.objects;
+            st.tuples = S.st.tuples;
+            st.bytes_sent = S.st.bytes_sent;
+            st.closure_s = S.st.closure_s;
+            st.build_s = S.st.build_s;
+            st.rows = S.st.rows;
+            st.edges = S.st.edges;
+            st.probes = S.st.probes;
+            st.queries = S.st.queries;
+            if (count) P.last_levels = S.levels;
+        }
+        st.run_s = secs(t0);
+        P.last = st;
+    }
+}
 }  // namespace
 
 // Several batches in one call, in flight: while batch k is remapped, built and checked on this
@@ -1307,6 +1451,7 @@ void partition_check_many(PartitionHandle *PH, uint32_t nb, const keto_query *co
     Partition &P = *PH;
     KETO_HIP(hipSetDevice(P.device));
     if (!nb) return;
+    if (P.dist) return dist_check_many(P, nb, q, n, allowed, err, flags);
     if (P.home) return home_check_many(P, nb, q, n, allowed, err, flags);
     if (getenv("KETO_PART_SEQUENTIAL")) {
         for (uint32_t k = 0; k < nb; k++) {

@@ -292,6 +292,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         KETO_HIP(hipMemcpy(u.data(), d_used.p, 4 * NR, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < NR; i++) used[i] = u[i] != 0;
     }
+    if (opts && opts->agree_used) opts->agree_used(used);
     phase("validate");
 
     // ---- relation slots + status (namespace.ASTRelationFor, definitions.go:37-62) -------
@@ -419,7 +420,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     ro.all_subj = static_cast<uint32_t *>(dalloc(4 * n));
     ro.rev_nodes = static_cast<uint32_t *>(dalloc(4 * n));
     ro.set_row = static_cast<uint4 *>(dalloc(16 * (uint64_t)N));
-    ro.weight = static_cast<uint32_t *>(dalloc(4 * (uint64_t)N));
+    ro.weight = (opts && opts->no_weights) ? nullptr : static_cast<uint32_t *>(dalloc(4 * (uint64_t)N));
     std::vector<uint32_t> idrows(total_slots, 0);  // slots holding a subject-id tuple (RI_IDROWS)
     {
         DevBuf d_slot(4 * NR);
@@ -504,7 +505,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     // 30 bits, so only snapshots of fewer than 2^30 nodes carry the flag
     D.edge_mask = ~EDGE_ALIAS;
     D.edge_leaf = 0;
-    if (N < (1ull << 30) && ro.n_set) {
+    if (N < (1ull << 30) && ro.n_set && !(opts && opts->no_leaf)) {
         build::leaf_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, ro.set_row, N);
         D.edge_mask = ~(EDGE_ALIAS | EDGE_LEAF);
         D.edge_leaf = 1;
@@ -794,6 +795,7 @@ Snapshot *load_snapshot(const char *path, int device) {
         if (i >= (int64_t)s.allocs.size()) throw Error(KETO_E_INVALID, "snapshot file corrupt");
         p = i < 0 ? nullptr : s.allocs[(size_t)i];
     });
+    s.dev.vclass = nullptr;  // (partitioned graphs' snapshots are never saved)
     s.probe_used = (uint64_t)s.dev.probe_mask + 1;  // (not in the file: assume the build's bound, half the slots)
     s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return S.release();

@@ -83,7 +83,9 @@ class PartitionStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("levels", ctypes.c_uint64), ("objects", ctypes.c_uint64),
                 ("tuples", ctypes.c_uint64), ("bytes_sent", ctypes.c_uint64), ("closure_s", ctypes.c_double),
                 ("build_s", ctypes.c_double), ("run_s", ctypes.c_double), ("rows", ctypes.c_uint64),
-                ("edges", ctypes.c_uint64), ("probes", ctypes.c_uint64), ("queries", ctypes.c_uint64)]
+                ("edges", ctypes.c_uint64), ("probes", ctypes.c_uint64), ("queries", ctypes.c_uint64),
+                ("generations", ctypes.c_uint64), ("goals", ctypes.c_uint64), ("routed", ctypes.c_uint64),
+                ("exchange_bytes", ctypes.c_uint64), ("device_s", ctypes.c_double), ("exchange_s", ctypes.c_double)]
 
 
 class PartitionLevel(ctypes.Structure):
@@ -92,7 +94,7 @@ class PartitionLevel(ctypes.Structure):
 
 
 # keto_collective callbacks
-ABI_VERSION = 4  # include/keto_mi355x.h KETO_ABI_VERSION
+ABI_VERSION = 5  # include/keto_mi355x.h KETO_ABI_VERSION
 
 ALLTOALL_U64_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                    ctypes.POINTER(ctypes.c_uint64))

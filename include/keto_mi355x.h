@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 4
+#define KETO_ABI_VERSION 5
 
 /* status codes */
 #define KETO_OK 0
@@ -330,11 +330,18 @@ static inline uint32_t keto_object_owner(uint32_t ns, uint32_t obj, uint32_t npa
 }
 
 /* Graphs larger than one GPU: the job's ranks each hold the tuples they own
- * (keto_object_owner) and evaluate their own queries together.  Per batch the library runs a
- * level-synchronous closure exchange (object requests to their owners, their tuples back, one
- * all-to-all pair per depth level, max_read_depth + 1 levels), builds the closure into a device
- * snapshot and runs the Check / Expand kernels on it: the decisions and trees of the whole
- * graph.  There is no reference counterpart (Keto never partitions).
+ * (keto_object_owner) and evaluate their own queries together.  There is no reference
+ * counterpart (Keto never partitions); the decisions and trees are the whole graph's.
+ *
+ * A job of several ranks builds each rank's partition once, at creation, into a resident
+ * snapshot (node arithmetic and relation flags agreed over the job).  A Check batch runs the
+ * frontier engine on every rank at once: goals whose node another rank owns go to it as 32-byte
+ * records, one all-to-all per generation, and their values come back, one all-to-all per
+ * generation bottom-up.  The few queries whose answer could depend on
+ * visited-set pruning (or that outgrow the goal budget) are routed to the closure path below, as
+ * are Expand batches: a level-synchronous closure exchange (object requests to their owners,
+ * their tuples back, max_read_depth + 1 levels), built into a device snapshot on which the
+ * Check / Expand kernels run.  KETO_PART_CLOSURE=1 sends every batch down the closure path.
  *
  * A job of one rank (coll NULL or world 1) holds the whole graph: its partition is built once,
  * at creation, into a resident snapshot and every batch runs on it -- no closure, no per-batch
@@ -363,10 +370,18 @@ typedef struct keto_collective {
                             const uint64_t *recv_bytes, void *stream);
 } keto_collective;
 typedef struct keto_partition_stats {
+    /* the per-batch closure (a job of one rank on the closure path, Expand, and the queries the
+     * distributed frontier routes): its levels, objects, tuples and bytes, and phase times */
     uint64_t batches, levels, objects, tuples, bytes_sent;
     double closure_s, build_s, run_s;
     /* a KETO_F_COUNT_WORK batch: the check kernels' work counters (keto_work_counters, tier 0) */
     uint64_t rows, edges, probes, queries;
+    /* ABI 5, a job of several ranks over resident partitions (the distributed frontier): its
+     * generations and goals on this rank, the queries it routed to the closure path, the goal
+     * records and decisions this rank sent to the other ranks (bytes), its time on the device
+     * (the generations' kernels, HIP events) and inside the collective */
+    uint64_t generations, goals, routed, exchange_bytes;
+    double device_s, exchange_s;
 } keto_partition_stats;
 typedef struct keto_partition keto_partition;
 /* tuples: this rank's partition (host, or device memory of cfg->device with
@@ -391,14 +406,18 @@ int keto_partition_expand_result(keto_partition *p, keto_tree_node *out_nodes, u
                                  int32_t *out_err);
 /* the last batch's closure and phase times */
 int keto_partition_stats_get(keto_partition *p, keto_partition_stats *out);
-/* The last batch's closure exchange level by level (a job of one rank over its resident snapshot
- * has none): *n = the levels run; the first min(cap, *n) are copied to out. */
+/* The last batch's exchange level by level (a job of one rank over its resident snapshot has
+ * none): *n = the levels run; the first min(cap, *n) are copied to out.  Closure path: one level
+ * per closure level.  Distributed frontier (several ranks): one level per generation, with the
+ * fields as commented in brackets. */
 typedef struct keto_partition_level {
-    uint64_t objects;          /* objects this rank asked for at this level (new to its seen set) */
-    uint64_t request_bytes;    /* object keys it sent to the other ranks */
-    uint64_t tuples;           /* tuples it received: its closure grows by these */
-    uint64_t tuple_bytes_sent; /* tuples it shipped to the other ranks (as an owner) */
-    double ms;                 /* the level's wall time on this rank (0 when the levels were enqueued at once) */
+    uint64_t objects;          /* objects this rank asked for at this level (new to its seen set)
+                                  [the generation's goals on this rank] */
+    uint64_t request_bytes;    /* object keys it sent to the other ranks [goal records it sent to them] */
+    uint64_t tuples;           /* tuples it received: its closure grows by these [goal records it received] */
+    uint64_t tuple_bytes_sent; /* tuples it shipped to the other ranks (as an owner) [values it returned to them] */
+    double ms;                 /* the level's wall time on this rank (0 when the levels were enqueued at once)
+                                  [device time of the generation's kernels, both passes: no collective wait] */
 } keto_partition_level;
 int keto_partition_levels_get(keto_partition *p, keto_partition_level *out, uint32_t cap, uint32_t *n);
 int keto_partition_free(keto_partition *p);

@@ -1,0 +1,130 @@
+"""The distributed frontier (djy-keto_amd/csrc/frontier_dist.hip: a graph partitioned by object,
+each rank's partition resident, the goals that cross to another rank's objects exchanged once per
+generation and their values returned bottom-up) on the CPU, no GPU: the kernel SOURCES built for
+the host by tools/cpuemu (one lane at a time), on 2 and 3 gloo ranks, each holding only the tuples
+keto_object_owner gives it.
+
+Every query the engine decides itself must equal the oracle over the whole graph
+(oracle/refsem.c; internal/check/engine.go:65-266): random worlds with every rewrite kind,
+undeclared relations, cycles, depth and width truncation and strict mode (tests/randworld.py),
+and a small Drive forest.  The queries it routes to the closure path (visited-set repeats across
+ranks, the goal budget) come back flagged here (err -1: the closure path is GPU-only, its answers
+are tests/test_gpu_partition.py's); they must stay a small share."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EMU = os.path.join(ROOT, "tools", "cpuemu")
+
+
+@pytest.fixture(scope="module")
+def emu_lib(tmp_path_factory):
+    d = tmp_path_factory.mktemp("emu")
+    lib = d / "libketo_emu_dist.so"
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-s", "-j", jobs, "-C", EMU, f"OBJDIR={d / 'obj'}", f"LIB={lib}", "OPT=-O1"], check=True,
+                   timeout=900)
+    return str(lib)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, lib, case, seeds, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KETO_MI355X_ALLOW_OVERRIDE="tools",
+                      KETO_MI355X_LIB_OVERRIDE=lib)
+    for p in (ROOT, os.path.join(ROOT, "djy-keto_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import json
+
+        import refsem
+        from keto_mi355x import partition, synth
+        from product_helpers import queries_to_oracle, queries_to_product, tuples_to_product, world_from_workload
+        from randworld import random_world
+        from torch_collective import TorchCollective
+
+        coll = TorchCollective()
+        res = []
+        for seed in seeds:
+            if case == "random":
+                w, t, q_rs, _ = random_world(seed)
+                tup = tuples_to_product(t)
+                q = queries_to_product(q_rs)
+                ns_cfg, ns_names, rel_names = json.dumps(w.namespaces), w.ns_names.names, w.rel_names.names
+                n_uuids, strict, depth, width = max(1, len(w.uuids.names)), w.strict, w.max_depth, w.max_width
+                orc = refsem.Oracle(w, t)
+                orc.set_limits(depth, width)
+                oq = q_rs
+            else:
+                wl = synth.drive(depth=4, fanout=3, acl_per_node=6, n_groups=200, members_per_group=6, n_users=600,
+                                 seed=seed)
+                tup = wl.tuples
+                q = synth.drive_queries(wl, 3000, seed=seed + 7)
+                ns_cfg, ns_names, rel_names = wl.namespaces, wl.ns_names, wl.rel_names
+                n_uuids, strict, depth, width = wl.n_uuids, wl.strict, wl.max_depth, wl.max_width
+                w, _ = world_from_workload(wl, with_tuples=False)
+                orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
+                orc.set_limits(depth, width)
+                oq = queries_to_oracle(q)
+            own = partition.object_owner(tup["ns"], tup["obj"], world) == rank
+            eng = partition.PartitionedEngine(ns_cfg, ns_names, rel_names, n_uuids, tup[own], strict=strict,
+                                              max_read_depth=depth, max_read_width=width, collective=coll)
+            allowed, err = eng.check_batch(q)  # every rank checks the whole batch: each root at its owner
+            st = dict(eng.last)
+            lv = eng.level_stats()
+            dec, oerr, _ = orc.check_batch(oq, threads=1)
+            ok = err != -1
+            res.append(dict(seed=seed, n=len(q), routed=int((~ok).sum()), st_routed=int(st["routed"]),
+                            dmis=int((allowed[ok] != dec[ok]).sum()), emis=int((err[ok] != oerr[ok]).sum()),
+                            gens=int(st["generations"]), levels=len(lv), sent=int(st["exchange_bytes"]),
+                            allowed=int(allowed[ok].sum())))
+            orc.close()
+            eng.close()
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(lib, world, case, seeds):
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker, args=(world, _free_port(), lib, case, seeds, out), nprocs=world, join=True)
+        return dict(out)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_random_worlds_match_oracle(emu_lib, world):
+    res = _run(emu_lib, world, "random", list(range(300, 330)))
+    total = routed = 0
+    for r in range(world):
+        for x in res[r]:
+            assert x["dmis"] == 0 and x["emis"] == 0, (r, x)
+            assert x["routed"] == x["st_routed"] and x["levels"] == x["gens"], (r, x)
+            total += x["n"]
+            routed += x["routed"]
+    assert routed < 0.25 * total, (routed, total)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_small_drive_matches_oracle(emu_lib, world):
+    res = _run(emu_lib, world, "drive", [5])
+    for r in range(world):
+        for x in res[r]:
+            assert x["dmis"] == 0 and x["emis"] == 0, (r, x)
+            assert x["routed"] < 0.02 * x["n"], (r, x)
+            assert x["sent"] > 0 and x["gens"] > 3 and x["allowed"] > 0, (r, x)

@@ -177,11 +177,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out, device_buffers=False):
+def _worker(rank, world, port, out, device_buffers=False, mode="dist"):
     for p in (ROOT, os.path.join(ROOT, "djy-keto_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if mode == "closure":
+        os.environ["KETO_PART_CLOSURE"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from torch_collective import TorchCollective
@@ -195,7 +197,11 @@ def _worker(rank, world, port, out, device_buffers=False):
         st = dict(eng.last)
         lv = eng.level_stats()  # per level: the bytes of both exchanges (the batch's subject list aside)
         lv_bytes = sum(x["request_bytes"] + x["tuple_bytes_sent"] for x in lv)
-        lv_ok = len(lv) == st["levels"] and 0 < lv_bytes <= st["bytes_sent"] and sum(x["objects"] for x in lv) == st["objects"]
+        if mode == "closure":
+            lv_ok = len(lv) == st["levels"] and 0 < lv_bytes <= st["bytes_sent"] and sum(x["objects"] for x in lv) == st["objects"]
+        else:  # the distributed frontier: one level per generation, goal records out and values back
+            lv_ok = len(lv) == st["generations"] and lv_bytes == st["exchange_bytes"] > 0 and \
+                sum(x["objects"] for x in lv) == st["goals"] and (st["build_s"] == 0 or st["routed"] > 0)
         orc = _oracle(wl)
         dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=4)
         roots = _roots(wl, np.random.default_rng(rank), 64)
@@ -213,22 +219,27 @@ def _worker(rank, world, port, out, device_buffers=False):
         pipe_mis = 0
         for (a, e), d, oe in zip(many, (dec, d2, dec), (oerr, oe2, oerr)):
             pipe_mis += int((a != d).sum() + (e != oe).sum())
-        out[rank] = (int((allowed != dec).sum()), int((err != oerr).sum()), int(dec.sum()), st["bytes_sent"],
-                     tree_mis, int((xerr != 0).sum()), pipe_mis, lv_ok)
+        out[rank] = (int((allowed != dec).sum()), int((err != oerr).sum()), int(dec.sum()),
+                     st["bytes_sent"] if mode == "closure" else st["exchange_bytes"], tree_mis, int((xerr != 0).sum()),
+                     pipe_mis, lv_ok)
         eng.close()
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["dist", "closure"])
 @pytest.mark.parametrize("device_buffers", [False, True])
-def test_two_rank_partitioned_matches_oracle(device_buffers):
+def test_two_rank_partitioned_matches_oracle(device_buffers, mode):
     """two ranks sharing the GPU: the exchange over host copies (keto_collective.alltoallv), and
     over the library's device buffers on its stream (alltoallv_device; gloo stages on the
-    adapter's side, RCCL would move the bytes GPU to GPU)"""
+    adapter's side, RCCL would move the bytes GPU to GPU).  mode "dist": resident partitions and
+    the distributed frontier (frontier_dist.hip), its routed queries and Expand through the
+    closure over those partitions' rows; "closure": every batch through the per-batch closure
+    over a separate store (KETO_PART_CLOSURE)."""
     world = 2
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(world, _free_port(), out, device_buffers), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), out, device_buffers, mode), nprocs=world, join=True)
         res = dict(out)
     for r in range(world):
         dmis, emis, n_allowed, sent, tree_mis, xerr, pipe_mis, lv_ok = res[r]

@@ -1,21 +1,62 @@
-// TEST/DEBUG TOOL ONLY: keto_partition_* (csrc/partition.hip, csrc/devprim.hip) is not emulated -- its
-// kernels are written for 256-thread blocks of 64-lane waves (ballot ranks, one digit per thread),
-// which the one-lane emulation cannot run; its entry points fail loudly here.
+// TEST/DEBUG TOOL ONLY: keto_partition_* in the CPU emulation.  The closure path (csrc/partition.hip,
+// csrc/devprim.hip) is not emulated -- its kernels are written for 256-thread blocks of 64-lane
+// waves (ballot ranks, one digit per thread), which the one-lane emulation cannot run.  A job of
+// several ranks runs the distributed frontier (csrc/frontier_dist.hip) as the library does; the
+// queries it routes to the closure path come back with out_err = -1 here, so a test can compare
+// every other decision with the oracle.  Every other entry point fails loudly.
+#include <memory>
+#include <vector>
+
 #include "../../djy-keto_amd/csrc/engine.hpp"
+#include "../../djy-keto_amd/csrc/frontier_dist.hpp"
 
 namespace keto {
-struct PartitionHandle {};
-[[noreturn]] static void unavailable() { throw Error(KETO_E_DEVICE, "keto_partition_* is not part of the CPU emulation"); }
-PartitionHandle *partition_create(const keto_snapshot_config *, const keto_tuple *, uint64_t, bool, const keto_collective *,
-                                  const keto_limits *) { unavailable(); }
-void partition_check(PartitionHandle *, const keto_query *, uint64_t, uint8_t *, int32_t *, uint32_t) { unavailable(); }
-void partition_check_many(PartitionHandle *, uint32_t, const keto_query *const *, const uint64_t *, uint8_t *const *, int32_t *const *,
-                          uint32_t) {
-    unavailable();
+struct PartitionHandle {
+    DistEngine *dist = nullptr;
+    keto_partition_stats last{};
+    std::vector<keto_partition_level> levels;
+    ~PartitionHandle() {
+        if (dist) dist_free(dist);
+    }
+};
+[[noreturn]] static void unavailable() { throw Error(KETO_E_DEVICE, "the closure path of keto_partition_* is not part of the CPU emulation"); }
+PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_ptrs,
+                                  const keto_collective *coll, const keto_limits *limits) {
+    if (!coll || coll->world < 2) unavailable();
+    auto P = std::make_unique<PartitionHandle>();
+    keto_limits lim = limits ? *limits : keto_limits{5, 100};
+    P->dist = dist_create(cfg, tuples, n, device_ptrs, *coll, lim);
+    return P.release();
+}
+void partition_check_many(PartitionHandle *P, uint32_t nb, const keto_query *const *q, const uint64_t *n, uint8_t *const *allowed,
+                          int32_t *const *err, uint32_t flags) {
+    if (flags & KETO_F_COUNT_WORK) unavailable();
+    for (uint32_t k = 0; k < nb; k++) {
+        std::vector<uint32_t> routed;
+        DistStats ds{};
+        dist_check(*P->dist, q[k], n[k], allowed[k], err[k], (flags & KETO_F_ERR_DETAIL) != 0, routed, ds);
+        for (uint32_t i : routed) err[k][i] = -1;
+        P->last = keto_partition_stats{};
+        P->last.batches = 1;
+        P->last.generations = ds.generations;
+        P->last.goals = ds.goals;
+        P->last.routed = ds.routed;
+        P->last.exchange_bytes = ds.bytes_exchanged;
+        P->last.device_s = ds.device_s;
+        P->last.exchange_s = ds.exchange_s;
+        P->last.run_s = ds.wall_s;
+        P->levels = dist_levels(*P->dist);
+    }
+}
+void partition_check(PartitionHandle *P, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
+    partition_check_many(P, 1, &q, &n, &allowed, &err, flags);
 }
 uint64_t partition_expand(PartitionHandle *, const keto_subject_set *, uint64_t) { unavailable(); }
 void partition_expand_result(PartitionHandle *, keto_tree_node *, uint64_t, uint64_t *, int32_t *) { unavailable(); }
-void partition_stats(PartitionHandle *, keto_partition_stats *) { unavailable(); }
-void partition_levels(PartitionHandle *, keto_partition_level *, uint32_t, uint32_t *) { unavailable(); }
-void partition_free(PartitionHandle *) {}
+void partition_stats(PartitionHandle *P, keto_partition_stats *out) { *out = P->last; }
+void partition_levels(PartitionHandle *P, keto_partition_level *out, uint32_t cap, uint32_t *n) {
+    *n = (uint32_t)P->levels.size();
+    for (uint32_t i = 0; i < cap && i < P->levels.size(); i++) out[i] = P->levels[i];
+}
+void partition_free(PartitionHandle *P) { delete P; }
 }  // namespace keto
