@@ -159,10 +159,12 @@ def sql_baseline(orc, wl, q, max_depth, max_width, cores, per_core=512):
                       f"read (loaded untimed)"}, dec
 
 
-def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0, gpu_allowed=None):
+def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0, gpu_allowed=None, pipe=None, pipe_per_batch=4096):
     """The oracle (C restatement of the reference, oracle/refsem.c) on the host cores, on a
     bounded sample of the same batch over the same graph -- reported beside the GPU, never
-    the target.  The oracle indexes the engine's tuple records in place (no copy)."""
+    the target.  The oracle indexes the engine's tuple records in place (no copy).  pipe: the
+    timed pipelined batches [(queries, gpu decisions)]: a strided sample of each is checked by the
+    same oracle (cpu_baseline.pipe)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refsem
 
@@ -192,6 +194,20 @@ def cpu_baseline(wl, queries, max_depth, max_width, budget_s=12.0, gpu_allowed=N
         t0 = time.perf_counter()
         sched = schedule_report(orc, q, gpu_allowed, max(1 << 12, min(n, 1 << 16)), cores)
         log(f"schedule report ({sched['n']} queries): {time.perf_counter() - t0:.1f}s")
+    cpu_baseline.pipe = None
+    if pipe:
+        t0 = time.perf_counter()
+        mis = n_chk = 0
+        for qk, ak in pipe:
+            idx = np.arange(0, len(qk), max(1, len(qk) // pipe_per_batch))
+            d_, _, _ = orc.check_batch(np.ascontiguousarray(qk[idx]).view(refsem.QUERY_DT), threads=cores)
+            mis += int((d_ != ak[idx]).sum())
+            n_chk += len(idx)
+        cpu_baseline.pipe = {"n": n_chk, "batches": len(pipe), "mismatches": mis,
+                             "what": f"a strided sample (every {max(1, len(pipe[0][0]) // pipe_per_batch)}th query) of "
+                                     "each timed pipelined batch, decided by oracle/refsem.c over the whole graph",
+                             "seconds": time.perf_counter() - t0}
+        log(f"pipelined batches vs the oracle: {n_chk} queries, {mis} mismatches ({time.perf_counter() - t0:.1f}s)")
     sql = None
     try:
         t0 = time.perf_counter()
@@ -1002,8 +1018,12 @@ def main(argv=None):
         out["frontier"] = {"goals_per_batch": fr["goals"] / fr["batches"], "generations_max": fr["max_generations"],
                            "routed_fraction": fr["routed"] / max(1, fr["queries"]), "budget": 1024}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sched, cb, dec = cpu_baseline(wl, q, wl.max_depth, wl.max_width, args.cpu_budget, gpu_allowed=allowed)
+        sched, cb, dec = cpu_baseline(wl, q, wl.max_depth, wl.max_width, args.cpu_budget, gpu_allowed=allowed,
+                                      pipe=[(qb[k].array, pipe_allowed[k]) for k in range(nb)])
         out["cpu_baseline"] = cb
+        if cpu_baseline.pipe is not None:
+            out["pipeline"]["oracle_mismatches"] = cpu_baseline.pipe["mismatches"]
+            out["pipeline"]["oracle_sample"] = cpu_baseline.pipe
         out["cpu_baseline_sql_mode"] = getattr(cpu_baseline, "sql", None)
         ns = len(dec)
         out["cpu_parity_sample"] = {"n": ns, "mismatches": int((dec != allowed[:ns]).sum())}

@@ -64,9 +64,12 @@ Stream::~Stream() {
     if (lists) (void)hipFree(lists);
     if (qbuf) (void)hipFree(qbuf);
     if (obuf) (void)hipFree(obuf);
+    // every stream this object destroys first retires the scratch-cache events recorded on it
+    // (scratch_forget_stream: a later scratch_get must never wait on a dead stream's event)
     for (hipStream_t c : {h2d, d2h})
         if (c) {
             (void)hipStreamSynchronize(c);
+            scratch_forget_stream(c);
             (void)hipStreamDestroy(c);
         }
     for (Slot &sl : slot) {
@@ -80,7 +83,10 @@ Stream::~Stream() {
         if (ev_a[i]) (void)hipEventDestroy(ev_a[i]);
         if (ev_b[i]) (void)hipEventDestroy(ev_b[i]);
     }
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream) {
+        scratch_forget_stream(stream);
+        (void)hipStreamDestroy(stream);
+    }
 }
 
 void Stream::mark_begin() {

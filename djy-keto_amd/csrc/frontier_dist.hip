@@ -316,6 +316,9 @@ __global__ __launch_bounds__(DBLK) void k_decide(const uint2 *hv, uint32_t n, co
 struct Grow {
     void *p = nullptr;
     size_t cap = 0;
+    Grow() = default;
+    Grow(const Grow &) = delete;
+    Grow &operator=(const Grow &) = delete;
     ~Grow() {
         if (p) (void)hipFree(p);
     }
@@ -494,6 +497,34 @@ DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuple
 }
 
 void dist_free(DistEngine *E) { delete E; }
+DistView dist_view(DistEngine &E) { return DistView{E.device, E.rank, E.world, &E.coll, E.hs, E.snap.get(), E.limits}; }
+std::vector<uint64_t> dist_alltoall(const DistView &V, const std::vector<uint64_t> &send, double &wait_s) {
+    std::vector<uint64_t> recv(V.world, 0);
+    const auto t0 = std::chrono::steady_clock::now();
+    dcoll_check(V.coll->alltoall_u64(V.coll->ctx, send.data(), recv.data()), "alltoall_u64");
+    wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return recv;
+}
+void dist_alltoallv(const DistView &V, const void *src, const std::vector<uint64_t> &sb, void *dst,
+                    const std::vector<uint64_t> &rb, double &wait_s) {
+    uint64_t ns = 0, nr = 0;
+    for (uint32_t r = 0; r < V.world; r++) {
+        ns += sb[r];
+        nr += rb[r];
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    if (V.coll->alltoallv_device) {
+        dcoll_check(V.coll->alltoallv_device(V.coll->ctx, src, sb.data(), dst, rb.data(), V.hs), "alltoallv_device");
+    } else {
+        std::vector<uint8_t> hsend(std::max<uint64_t>(1, ns)), hrecv(std::max<uint64_t>(1, nr));
+        if (ns) KETO_HIP(hipMemcpyAsync(hsend.data(), src, ns, hipMemcpyDeviceToHost, V.hs));
+        KETO_HIP(hipStreamSynchronize(V.hs));
+        dcoll_check(V.coll->alltoallv(V.coll->ctx, hsend.data(), sb.data(), hrecv.data(), rb.data()), "alltoallv");
+        if (nr) KETO_HIP(hipMemcpyAsync(dst, hrecv.data(), nr, hipMemcpyHostToDevice, V.hs));
+        KETO_HIP(hipStreamSynchronize(V.hs));
+    }
+    wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
 const Snapshot &dist_snapshot(const DistEngine &E) { return *E.snap; }
 std::vector<keto_partition_level> dist_levels(const DistEngine &E) {
     std::vector<keto_partition_level> v;

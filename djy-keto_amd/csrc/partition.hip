@@ -1361,7 +1361,14 @@ void home_check_many(Partition &P, uint32_t nb, const keto_query *const *q, cons
     const uint32_t f = (flags & (KETO_F_COUNT_WORK | KETO_F_ERR_DETAIL)) | (count ? 0u : KETO_F_ASYNC);
     for (uint32_t k = 0; k < nb; k++) {
         const int rc = keto_check_batch(snap, P.kstream, q[k], n[k], &P.limits, allowed[k], err[k], f);
-        if (rc != KETO_OK) throw_last(rc);
+        if (rc != KETO_OK) {
+            // batches 0..k-1 are still queued with the caller's buffers (their H2D reads and D2H
+            // writes): they finish before the error goes back and the caller may free them
+            char msg[512];
+            keto_last_error(msg, sizeof msg);
+            (void)keto_stream_sync(P.kstream);
+            throw Error(rc, msg);
+        }
     }
     const int rc = keto_stream_sync(P.kstream);
     if (rc != KETO_OK) throw_last(rc);
@@ -1521,6 +1528,20 @@ uint64_t partition_expand(PartitionHandle *PH, const keto_subject_set *roots, ui
         st.run_s = secs(t0);
         P.last = st;
         P.last_levels.clear();
+        return P.xoffs[n];
+    }
+    if (P.dist && !getenv("KETO_PART_XCLOSURE")) {  // several ranks: rows fetched from the resident partitions, walked here
+        DistExpandStats xs;
+        dist_expand(*P.dist, roots, n, P.xnodes, P.xoffs, P.xerr, xs);
+        st.levels = xs.levels;
+        st.objects = xs.rows;
+        st.tuples = xs.entries;
+        st.bytes_sent = xs.bytes_sent;
+        st.closure_s = xs.fetch_s;
+        st.run_s = secs(t0);
+        st.exchange_s = xs.exchange_s;
+        P.last = st;
+        P.last_levels = xs.per_level;
         return P.xoffs[n];
     }
     DevBuf dr(std::max<uint64_t>(1, n) * sizeof(keto_subject_set)), keys(std::max<uint64_t>(1, n) * 8);

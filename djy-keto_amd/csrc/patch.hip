@@ -370,6 +370,19 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     std::vector<uint4> pl(n_touched);
     DevSnapshot Dp = D;  // the base's view, plus the objects this patch creates (step 0 below)
     std::vector<uint4> ext = B.ext;
+    // spares this patch takes go back if it then falls back to the full build (or throws), as
+    // long as no later patch of the family took spares since
+    struct Taken {
+        std::shared_ptr<Spares> spares;
+        std::vector<uint32_t> from, to;
+        bool keep = false;
+        ~Taken() {
+            if (keep || !spares) return;
+            std::lock_guard<std::mutex> g(spares->mu);
+            for (size_t ns = 0; ns < from.size(); ns++)
+                if (spares->used[ns] == to[ns]) spares->used[ns] = from[ns];
+        }
+    } taken;
     void *ext_dev = nullptr;  // a new ext table (owned by the new snapshot once it exists)
     std::vector<uint2> ent_set;  // {spare entity, obj}
     auto place_all = [&] {
@@ -427,15 +440,29 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
             KETO_HIP(hipMemcpy(probe.data(), dp.p, sizeof(uint4) * q.size(), hipMemcpyDeviceToHost));
         }
         std::lock_guard<std::mutex> g(B.spares->mu);
+        // every new object's namespace is checked first -- aliased visited keys, room -- so a
+        // patch that falls back to the full build takes no spare (they are the family's)
+        std::vector<uint32_t> want(B.n_ns, 0);
         for (size_t k = 0; k < fresh_objs.size(); k++) {
             if (probe[k].x != NONE32) continue;  // it has an entity
-            const uint32_t ns = fresh_objs[k].first, obj = fresh_objs[k].second;
+            const uint32_t ns = fresh_objs[k].first;
             for (uint32_t sl = 0; sl < B.ns[ns].n_slots; sl++)
                 if ((B.relinfo[B.ns[ns].slot_base + sl] >> 20) & 1u) return nullptr;  // aliased visited keys
-            if (B.spares->used[ns] >= B.spares->count[ns]) return nullptr;  // out of spares
+            if (B.spares->used[ns] + ++want[ns] > B.spares->count[ns]) return nullptr;  // out of spares
+        }
+        for (size_t k = 0; k < fresh_objs.size(); k++) {
+            if (probe[k].x != NONE32) continue;
+            const uint32_t ns = fresh_objs[k].first, obj = fresh_objs[k].second;
             const uint32_t e = B.spares->first[ns] + B.spares->used[ns]++;
             ext.push_back(make_uint4(obj, ns, e, 0));
             ent_set.push_back(make_uint2(e, obj));
+        }
+        taken.spares = B.spares;
+        taken.from.assign(B.n_ns, 0);
+        taken.to.assign(B.n_ns, 0);
+        for (uint32_t ns = 0; ns < B.n_ns; ns++) {
+            taken.to[ns] = B.spares->used[ns];
+            taken.from[ns] = taken.to[ns] - want[ns];
         }
     }
     std::unique_ptr<void, void (*)(void *)> ext_guard(nullptr, [](void *p) { (void)hipFree(p); });
@@ -846,6 +873,7 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
                         "probe +%zu -%zu keys, %.2f ms\n", (unsigned long long)n_touched, m, ms,
                 (unsigned long long)(rmatch.size() + smatch.size()), flip.size(), ins_keys.size(), del_keys.size(),
                 s.info.build_seconds * 1e3);
+    taken.keep = true;
     return S.release();
 }
 

@@ -207,9 +207,10 @@ void *scratch_get(size_t bytes, size_t *got) {
             const CacheBlock b = C.free[at];
             C.held -= best;
             C.free.erase(C.free.begin() + (ptrdiff_t)at);
-            g.unlock();
-            if (b.ev) KETO_HIP(hipEventSynchronize(b.ev));  // its last reader's stream got past the release
-            g.lock();
+            // its last reader's stream got past the release -- waited for under the lock, so a
+            // stream being destroyed (scratch_forget_stream takes the lock first) is either still
+            // alive here or has already retired this event
+            if (b.ev) KETO_HIP(hipEventSynchronize(b.ev));
             if (b.ev) C.events.push_back(b.ev);
             *got = best;
             return b.p;
@@ -284,6 +285,8 @@ void pool_trim(int device) {
 // teardown in exit(), which runs after the interpreter (and under rocprofv3 after its tool)
 // has begun to unwind.  The caches stay usable: a later call simply allocates again.
 void pool_shutdown() {
+    int cur = 0;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;  // (restored: the caller's thread stays on its device)
     for (int d = 0; d < 64; d++) {
         DevicePool &P = pool_slot(d);
         ScratchCache &C = scache_slot(d);
@@ -294,6 +297,7 @@ void pool_shutdown() {
         for (hipEvent_t e : C.events) (void)hipEventDestroy(e);
         C.events.clear();
     }
+    if (have_cur) (void)hipSetDevice(cur);
 }
 
 void pool_release(int device, void *p, size_t bytes) {

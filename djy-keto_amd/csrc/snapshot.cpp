@@ -366,7 +366,22 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     for (uint32_t ns = 0; ns <= s.n_ns; ns++) rank0[ns] = build::read_u32(d_rank.u32(), ns * bpn);
     uint64_t ent_total = 0, node_total = 0;
     std::vector<uint32_t> ent_base(s.n_ns);
-    if (opts && opts->spares) {
+    bool with_spares = opts && opts->spares;
+    if (with_spares) {
+        // the room a store snapshot keeps for new objects must not cost the snapshot its format:
+        // past 2^30 nodes the edges lose EDGE_LEAF (a speed drop), past 2^31 the build fails --
+        // without the spares, patches that create objects fall back to the full build instead
+        uint64_t with = 0, without = 0;
+        for (uint32_t ns = 0; ns < s.n_ns; ns++) {
+            const uint64_t real = rank0[ns + 1] - rank0[ns], sl = s.ns[ns].n_slots;
+            without += (real + 1) * sl;
+            with += (real + (sl ? real / 16 + 256 : 0) + 1) * sl;
+        }
+        if ((with >= (1ull << 30) && without < (1ull << 30)) || with >= VIRT_BIT ||
+            (uint64_t)s.n_uuids + with + 1 >= (1ull << 32))
+            with_spares = false;
+    }
+    if (with_spares) {
         s.spares = std::make_shared<Spares>();
         s.spares->first.resize(s.n_ns);
         s.spares->count.resize(s.n_ns);
@@ -377,7 +392,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         s.ns[ns].ent_base = ent_base[ns] = (uint32_t)ent_total;
         s.ns[ns].node_base = (uint32_t)node_total;
         // real entities, then the spares a store snapshot keeps for new objects, then the phantom
-        const uint32_t spare = s.spares && s.ns[ns].n_slots ? n_real[ns] / 16 + 256 : 0;
+        const uint32_t spare = with_spares && s.ns[ns].n_slots ? n_real[ns] / 16 + 256 : 0;
         if (s.spares) {
             s.spares->first[ns] = ent_base[ns] + n_real[ns];
             s.spares->count[ns] = spare;

@@ -54,6 +54,7 @@ def _worker(rank, world, port, lib, case, seeds, out):
 
         import refsem
         from keto_mi355x import partition, synth
+        import keto_mi355x as km
         from product_helpers import queries_to_oracle, queries_to_product, tuples_to_product, world_from_workload
         from randworld import random_world
         from torch_collective import TorchCollective
@@ -62,7 +63,9 @@ def _worker(rank, world, port, lib, case, seeds, out):
         res = []
         for seed in seeds:
             if case == "random":
-                w, t, q_rs, _ = random_world(seed)
+                w, t, q_rs, expands = random_world(seed)
+                roots = np.array([(w.ns_names.ids[a], w.uuids.ids[b], w.rel_names.ids[r], d) for a, b, r, d in expands],
+                                 dtype=km.SUBJSET_DT)
                 tup = tuples_to_product(t)
                 q = queries_to_product(q_rs)
                 ns_cfg, ns_names, rel_names = json.dumps(w.namespaces), w.ns_names.names, w.rel_names.names
@@ -81,6 +84,12 @@ def _worker(rank, world, port, lib, case, seeds, out):
                 orc = refsem.Oracle(w, wl.tuples.view(refsem.TUPLE_DT), shard_bytes=True)
                 orc.set_limits(depth, width)
                 oq = queries_to_oracle(q)
+                rng = np.random.default_rng(seed + rank)
+                roots = np.zeros(24, dtype=km.SUBJSET_DT)
+                roots["ns"][:12], roots["rel"][:12] = wl.ns_names.index("Group"), wl.rel_names.index("members")
+                roots["obj"][:12] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], 12)
+                roots["ns"][12:], roots["rel"][12:] = wl.ns_names.index("Folder"), wl.rel_names.index("viewers")
+                roots["obj"][12:] = rng.integers(0, wl.meta["folders_per_root"], 12)
             own = partition.object_owner(tup["ns"], tup["obj"], world) == rank
             eng = partition.PartitionedEngine(ns_cfg, ns_names, rel_names, n_uuids, tup[own], strict=strict,
                                               max_read_depth=depth, max_read_width=width, collective=coll)
@@ -89,10 +98,23 @@ def _worker(rank, world, port, lib, case, seeds, out):
             lv = eng.level_stats()
             dec, oerr, _ = orc.check_batch(oq, threads=1)
             ok = err != -1
+            # Expand: rows fetched from their owners, walked here (csrc/expand_dist.hip): exact trees
+            nodes, offs, xerr = eng.expand_batch(roots)
+            xst = dict(eng.last)
+            tree_mis = 0
+            for i, r in enumerate(roots):
+                on, _ = orc.expand(1, int(r["obj"]), int(r["ns"]), int(r["rel"]), int(r["max_depth"]))
+                mine = nodes[int(offs[i]):int(offs[i + 1])]
+                same = len(mine) == len(on)
+                for a, b in (("type", "type"), ("subj_kind", "kind"), ("s_obj", "sid"), ("s_ns", "sns"), ("s_rel", "srel"),
+                             ("n_children", "n_children")):
+                    same = same and np.array_equal(mine[a], on[b])
+                tree_mis += 0 if same else 1
             res.append(dict(seed=seed, n=len(q), routed=int((~ok).sum()), st_routed=int(st["routed"]),
                             dmis=int((allowed[ok] != dec[ok]).sum()), emis=int((err[ok] != oerr[ok]).sum()),
                             gens=int(st["generations"]), levels=len(lv), sent=int(st["exchange_bytes"]),
-                            allowed=int(allowed[ok].sum())))
+                            allowed=int(allowed[ok].sum()), tree_mis=int(tree_mis), xerr=int((xerr != 0).sum()),
+                            tree_nodes=int(offs[-1]), x_levels=int(xst["levels"])))
             orc.close()
             eng.close()
         out[rank] = res
@@ -114,6 +136,7 @@ def test_random_worlds_match_oracle(emu_lib, world):
     for r in range(world):
         for x in res[r]:
             assert x["dmis"] == 0 and x["emis"] == 0, (r, x)
+            assert x["tree_mis"] == 0 and x["xerr"] == 0, (r, x)
             assert x["routed"] == x["st_routed"] and x["levels"] == x["gens"], (r, x)
             total += x["n"]
             routed += x["routed"]
@@ -126,5 +149,18 @@ def test_small_drive_matches_oracle(emu_lib, world):
     for r in range(world):
         for x in res[r]:
             assert x["dmis"] == 0 and x["emis"] == 0, (r, x)
+            assert x["tree_mis"] == 0 and x["xerr"] == 0 and x["tree_nodes"] > 24 and x["x_levels"] > 1, (r, x)
             assert x["routed"] < 0.02 * x["n"], (r, x)
             assert x["sent"] > 0 and x["gens"] > 3 and x["allowed"] > 0, (r, x)
+
+
+def test_scratch_cache_never_waits_on_a_dead_stream(emu_lib):
+    """keto_stream_destroy retires the scratch-cache events recorded on its streams (compute, H2D,
+    D2H) before destroying them: a builder temporary released on each, then taken again after the
+    stream object is gone, must not be fenced by its dead stream's event (the round-4 end-of-suite
+    failure: hipEventSynchronize on an event of a destroyed stream).  tools/cpuemu models stream
+    liveness; tools/cpuemu/emu_probe.cpp is the probe (it fails with KETO_E_DEVICE without the
+    retirement)."""
+    import ctypes
+    lib = ctypes.CDLL(emu_lib)
+    assert lib.keto_emu_scratch_dead_stream_probe() == 0

@@ -65,21 +65,44 @@ inline hipError_t hipMemcpyToSymbol(void *sym, const void *s, size_t n, size_t o
 inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t) { std::memcpy(d, s, n); return hipSuccess; }
 inline hipError_t hipMemset(void *d, int v, size_t n) { std::memset(d, v, n); return hipSuccess; }
 inline hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t) { std::memset(d, v, n); return hipSuccess; }
-inline hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) { *s = (void *)1; return hipSuccess; }
+// Streams are objects that remember being destroyed (never freed: an event recorded on one may
+// outlive it), and waiting on an event whose stream is gone fails -- as the runtime refuses it
+// ("operation not permitted on an event last recorded in a capturing stream"), so the library's
+// scratch-cache discipline (scratch_forget_stream) is checked on the CPU.
+struct EmuStream {
+    bool alive = true;
+};
+struct EmuEvent {
+    double t = 0;
+    EmuStream *st = nullptr;
+};
+inline hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) { *s = new EmuStream(); return hipSuccess; }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
-inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
-inline hipError_t hipEventCreate(hipEvent_t *e) { *e = new double(0); return hipSuccess; }
-#define hipEventDisableTiming 2u
-inline hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) { return hipEventCreate(e); }
-inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
-inline hipError_t hipEventDestroy(hipEvent_t e) { delete (double *)e; return hipSuccess; }
-inline hipError_t hipEventRecord(hipEvent_t e, hipStream_t) {
-    *(double *)e = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+inline hipError_t hipStreamDestroy(hipStream_t s) {
+    if (s) static_cast<EmuStream *>(s)->alive = false;
     return hipSuccess;
 }
-inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
-inline hipError_t hipEventQuery(hipEvent_t) { return hipSuccess; }  // (the emulation runs every launch at once)
-inline hipError_t hipEventElapsedTime(float *ms, hipEvent_t a, hipEvent_t b) { *ms = float(*(double *)b - *(double *)a); return hipSuccess; }
+inline hipError_t hipEventCreate(hipEvent_t *e) { *e = new EmuEvent(); return hipSuccess; }
+#define hipEventDisableTiming 2u
+inline hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) { return hipEventCreate(e); }
+inline hipError_t hipEventDestroy(hipEvent_t e) { delete static_cast<EmuEvent *>(e); return hipSuccess; }
+inline hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
+    auto *v = static_cast<EmuEvent *>(e);
+    v->t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    v->st = static_cast<EmuStream *>(s);
+    return hipSuccess;
+}
+inline hipError_t emu_event_live(hipEvent_t e) {
+    const auto *v = static_cast<const EmuEvent *>(e);
+    return (v && v->st && !v->st->alive) ? 1 : hipSuccess;
+}
+inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t e, unsigned) { return emu_event_live(e); }
+inline hipError_t hipEventSynchronize(hipEvent_t e) { return emu_event_live(e); }
+inline hipError_t hipEventQuery(hipEvent_t e) { return emu_event_live(e); }  // (the emulation runs every launch at once)
+inline hipError_t hipEventElapsedTime(float *ms, hipEvent_t a, hipEvent_t b) {
+    *ms = float(static_cast<EmuEvent *>(b)->t - static_cast<EmuEvent *>(a)->t);
+    return hipSuccess;
+}
 template <class K>
 inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int *n, K, int, size_t) { *n = 2; return hipSuccess; }
 

@@ -4,6 +4,7 @@
 // several ranks runs the distributed frontier (csrc/frontier_dist.hip) as the library does; the
 // queries it routes to the closure path come back with out_err = -1 here, so a test can compare
 // every other decision with the oracle.  Every other entry point fails loudly.
+#include <algorithm>
 #include <memory>
 #include <vector>
 
@@ -15,6 +16,9 @@ struct PartitionHandle {
     DistEngine *dist = nullptr;
     keto_partition_stats last{};
     std::vector<keto_partition_level> levels;
+    std::vector<keto_tree_node> xnodes;
+    std::vector<uint64_t> xoffs;
+    std::vector<int32_t> xerr;
     ~PartitionHandle() {
         if (dist) dist_free(dist);
     }
@@ -51,8 +55,25 @@ void partition_check_many(PartitionHandle *P, uint32_t nb, const keto_query *con
 void partition_check(PartitionHandle *P, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
     partition_check_many(P, 1, &q, &n, &allowed, &err, flags);
 }
-uint64_t partition_expand(PartitionHandle *, const keto_subject_set *, uint64_t) { unavailable(); }
-void partition_expand_result(PartitionHandle *, keto_tree_node *, uint64_t, uint64_t *, int32_t *) { unavailable(); }
+uint64_t partition_expand(PartitionHandle *P, const keto_subject_set *roots, uint64_t n) {
+    DistExpandStats xs;
+    dist_expand(*P->dist, roots, n, P->xnodes, P->xoffs, P->xerr, xs);
+    P->last = keto_partition_stats{};
+    P->last.batches = 1;
+    P->last.levels = xs.levels;
+    P->last.objects = xs.rows;
+    P->last.tuples = xs.entries;
+    P->last.bytes_sent = xs.bytes_sent;
+    P->levels = xs.per_level;
+    return P->xoffs[n];
+}
+void partition_expand_result(PartitionHandle *P, keto_tree_node *nodes, uint64_t cap, uint64_t *offsets, int32_t *err) {
+    const uint64_t n = P->xoffs.empty() ? 0 : P->xoffs.size() - 1, total = n ? P->xoffs[n] : 0;
+    if (total > cap) throw Error(KETO_E_CAPACITY, "expand output");
+    std::copy(P->xoffs.begin(), P->xoffs.end(), offsets);
+    std::copy(P->xerr.begin(), P->xerr.begin() + n, err);
+    std::copy(P->xnodes.begin(), P->xnodes.begin() + total, nodes);
+}
 void partition_stats(PartitionHandle *P, keto_partition_stats *out) { *out = P->last; }
 void partition_levels(PartitionHandle *P, keto_partition_level *out, uint32_t cap, uint32_t *n) {
     *n = (uint32_t)P->levels.size();
