@@ -479,11 +479,14 @@ def c5_cpu_baseline(wl, q, budget_s: float):
 
 
 def run_c5(args, rank, world, device, dist_on):
-    """configs[4]: a graph partitioned by object over the ranks (keto_partition_*, csrc/partition.hip).
-    One step = one batch of this rank's Checks: closure exchange (all-to-all per BFS level over
-    the job's collective) -> device snapshot build of the closure -> the Check kernels.  Every
-    phase is inside the timed region.  Ranks sharing one GPU (KETO_BENCH_BACKEND=gloo, a
-    rehearsal) build their device stores one after another."""
+    """configs[4]: a graph partitioned by object over the ranks (keto_partition_*).  Every rank's
+    partition is built once into a resident snapshot; one step = one batch of this rank's Checks:
+    several ranks run the distributed frontier (csrc/frontier_dist.hip: goal records to the nodes'
+    owners and values back, one all-to-all each per generation), one rank the engine on its
+    resident snapshot (the whole graph).  KETO_PART_CLOSURE=1: the per-batch closure path instead
+    (closure exchange -> closure snapshot build -> the Check kernels).  Ranks sharing one GPU
+    (KETO_BENCH_BACKEND=gloo, a rehearsal) build their partitions one after another
+    (KETO_PART_STAGED)."""
     import torch
 
     import keto_mi355x as km
@@ -497,6 +500,8 @@ def run_c5(args, rank, world, device, dist_on):
         from torch_collective import TorchCollective  # keto_collective over the job's process group
         coll = TorchCollective(device_buffers=True)  # (RCCL: the exchange moves GPU to GPU)
     shared = os.environ.get("KETO_BENCH_BACKEND", "nccl") == "gloo"
+    if dist_on and shared:
+        os.environ["KETO_PART_STAGED"] = "1"  # (created in turn: the slot layout is checked at the first batch)
     eng, n_part = None, 0
     for r in range(world if (dist_on and shared) else 1):
         if not (dist_on and shared) or r == rank:
@@ -523,8 +528,9 @@ def run_c5(args, rank, world, device, dist_on):
     if dist_on:
         import torch.distributed as dist
         dist.barrier()
-    # one batch per call, phase by phase (closure -> build -> check): where a batch's time goes
-    phases = {"closure_s": 0.0, "build_s": 0.0, "run_s": 0.0}
+    # one batch per call, phase by phase (closure -> build -> check; the distributed frontier: its
+    # device time and the time inside the collective): where a batch's time goes
+    phases = {"closure_s": 0.0, "build_s": 0.0, "run_s": 0.0, "device_s": 0.0, "exchange_s": 0.0}
     n_seq = min(args.steps, 4)
     torch.cuda.synchronize()
     t_seq = time.perf_counter()
@@ -532,6 +538,8 @@ def run_c5(args, rank, world, device, dist_on):
         eng.check_batch(q)
         for k in phases:
             phases[k] += eng.last[k]
+    dist_last = dict(eng.last)
+    dist_levels = eng.level_stats()
     seq_ms = (time.perf_counter() - t_seq) / n_seq * 1e3
     # the timed region: K fresh seeded batches through one keto_partition_check_many call, in
     # pinned host memory as the C4 line's (keto_host_alloc: straight DMA for the one-rank path)
@@ -565,9 +573,16 @@ def run_c5(args, rank, world, device, dist_on):
     check_bytes = 8 * cw["rows"][0] + 4 * cw["edges"][0] + 8 * cw["probes"][0] + 17 * cw["queries"][0]
     step_bytes = check_bytes + 3 * 48 * closure_tuples
     achieved = step_bytes / (ms_step * 1e-3) / 1e9
-    resident = eng.last.get("levels", 0) == 0 and closure_tuples == 0
+    distributed = world > 1 and os.environ.get("KETO_PART_CLOSURE") is None
+    resident = world == 1 and os.environ.get("KETO_PART_CLOSURE") is None
+    if distributed:  # the counted batch ran on the closure path: the step itself moves goal records, no tuples
+        step_bytes = check_bytes
+        achieved = step_bytes / (ms_step * 1e-3) / 1e9
     how = ("one rank: the partition is the whole graph, built once into a resident snapshot -- no closure, no "
-           "per-batch build" if resident else f"closure of max_read_depth+1 = {eng.levels()} levels per batch")
+           "per-batch build" if resident else
+           "resident partitions, distributed frontier: goal records to their nodes' owners and values back, one "
+           "all-to-all each per generation -- no closure, no per-batch build" if distributed else
+           f"closure of max_read_depth+1 = {eng.levels()} levels per batch")
     out = {
         "metric": METRIC, "value": value, "unit": "checks/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "per_rank_ms_per_step": ranks_ms,
@@ -577,7 +592,8 @@ def run_c5(args, rank, world, device, dist_on):
         "config": {"workload": f"C5 Drive-style x{args.scale}: {wl.meta['n_tuples']} tuples partitioned by "
                                f"object over {world} rank(s), {args.batch} checks/batch/GPU, {how}",
                    "tuples": int(wl.meta["n_tuples"]), "batch_per_gpu": args.batch,
-                   "parallelism": f"object partition x{world} (RCCL all-to-all closure exchange per level)"},
+                   "parallelism": f"object partition x{world} (" + ("RCCL all-to-all of goal records per generation" if distributed
+                                                                      else "RCCL all-to-all closure exchange per level") + ")"},
         "allowed_fraction": float(allowed.mean()),
         "phases_ms_per_step": {k: v / n_seq * 1e3 for k, v in phases.items()},
         "pipeline": {"what": ("value: the K timed fresh batches (pinned host memory) in one keto_partition_check_many "
@@ -595,11 +611,15 @@ def run_c5(args, rank, world, device, dist_on):
         "closure": {"tuples": eng.last["tuples"], "objects": eng.last["objects"], "levels": eng.last["levels"],
                     "bytes_sent": eng.last["bytes_sent"],
                     "partition_tuples": n_part, "levels_detail": levels_detail},
+        "distributed": ({k: dist_last[k] for k in ("generations", "goals", "routed", "exchange_bytes", "device_s",
+                                                    "exchange_s", "run_s")} | {"generations_detail": dist_levels}
+                        if distributed else None),
         "shared_gpu": bool(dist_on and shared),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": ("the whole step: H2D + check path + D2H on the resident snapshot" if resident else
-                                "the whole step: closure exchange + closure build + check (one rank)"),
+                                "the whole step of this rank: its generations' kernels, the exchanges and waits"
+                                if distributed else "the whole step: closure exchange + closure build + check (one rank)"),
                      "algorithmic_bytes_per_step": int(step_bytes), "check_bytes": int(check_bytes),
                      "closure_tuples": int(closure_tuples),
                      "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (check) + 3*48*closure tuples"},

@@ -22,6 +22,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "device_common.hpp"
@@ -323,7 +324,12 @@ struct XBuf {  // a growable device buffer keeping its first `keep` bytes
         KETO_HIP(hipMalloc(&q, c + 16));
         if (p && keep) KETO_HIP(hipMemcpyAsync(q, p, std::min(keep, cap), hipMemcpyDeviceToDevice, s));
         KETO_HIP(hipStreamSynchronize(s));
-        if (p) KETO_HIP(hipFree(p));
+        if (p) {
+            const hipError_t e = hipFree(p);
+            if (e != hipSuccess)
+                throw Error(KETO_E_DEVICE, std::string("XBuf: hipFree of a ") + std::to_string(cap) + "-byte block (growing to " +
+                                               std::to_string(b) + ") failed: " + hipGetErrorString(e));
+        }
         p = q;
         cap = c;
         return p;

@@ -356,6 +356,7 @@ struct DistEngine {
     hipEvent_t ev[2] = {nullptr, nullptr};
     uint32_t budget = 1024, cus = 1, per_cu = 4;
     bool verbose = false;
+    bool staged = false, agreed = false;
     // per batch (grown, reused)
     Grow dq, rec, sbuf, rbuf, sent_px, arrived, ret, rret, hv, deep, hrouted, outv, fbl;
     Grow arena, occ, dtab, dbits, ctrl, start, subj, home, qrouted, qspawn, ob, dlist, dent, dcnt, dsend;
@@ -423,6 +424,38 @@ void or_across(DistEngine &E, std::vector<uint8_t> &v) {
         for (size_t i = 0; i < v.size(); i++) v[i] |= recv[(size_t)r * v.size() + i];
 }
 
+// The relation flags of the whole graph: a flag only this rank's tuples would clear must not
+// decide another rank's node here (collective).  Staged partitions first check that every rank
+// laid out the same relation slots.
+void agree_flags(DistEngine &D) {
+    Snapshot &s = *D.snap;
+    if (D.staged) {
+        uint64_t h = 0xcbf29ce484222325ull;
+        auto mix = [&](uint64_t x) {
+            h ^= x;
+            h *= 0x100000001b3ull;
+        };
+        for (uint32_t ns = 0; ns < s.n_ns; ns++) mix(s.ns[ns].n_slots);
+        for (uint32_t r : s.slot_rel) mix(r);
+        double w = 0;
+        const std::vector<uint64_t> all = d_alltoall(D, std::vector<uint64_t>(D.world, h), w);
+        for (uint64_t x : all)
+            if (x != h)
+                throw Error(KETO_E_INVALID, "staged partitions disagree on their relation slots: create them together "
+                                            "(without KETO_PART_STAGED)");
+    }
+    std::vector<uint8_t> fl(s.relinfo.size());
+    for (size_t g = 0; g < fl.size(); g++)
+        fl[g] = (uint8_t)((ri_setrows(s.relinfo[g]) ? 1u : 0u) | (ri_idrows(s.relinfo[g]) ? 2u : 0u));
+    or_across(D, fl);
+    for (size_t g = 0; g < fl.size(); g++) {
+        if (fl[g] & 1u) s.relinfo[g] |= RI_SETROWS;
+        if (fl[g] & 2u) s.relinfo[g] |= RI_IDROWS;
+    }
+    if (!s.relinfo.empty())
+        KETO_HIP(hipMemcpy(const_cast<uint32_t *>(s.dev.relinfo), s.relinfo.data(), 4 * s.relinfo.size(), hipMemcpyHostToDevice));
+    D.agreed = true;
+}
 }  // namespace
 
 DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_ptrs,
@@ -446,25 +479,17 @@ DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuple
     BuildOpts o;
     o.no_leaf = true;
     o.no_weights = true;
-    o.agree_used = [&D](std::vector<uint8_t> &used) { or_across(D, used); };
+    // KETO_PART_STAGED (ranks that share one device and so create their partitions one after
+    // another, tests/test_gpu_c5.py): no collective here -- each rank lays out the slots its own
+    // tuples use, and the first batch checks that every rank's layout is the same (an error
+    // otherwise: such partitions must be created together) and agrees on the relation flags
+    E->staged = getenv("KETO_PART_STAGED") != nullptr;
+    if (!E->staged) o.agree_used = [&D](std::vector<uint8_t> &used) { or_across(D, used); };
     E->snap.reset(build_snapshot(cfg, tuples, n, device_ptrs, false, &o));
     Snapshot &s = *E->snap;
     DevSnapshot &V = s.dev;
     if (V.n_nodes >= (1u << 30)) throw Error(KETO_E_LIMIT, "a partition's snapshot holds at most 2^30 nodes (EDGE_REMOTE)");
-    // the relation flags of the whole graph: a flag only this rank's tuples would clear must not
-    // decide another rank's node here
-    {
-        std::vector<uint8_t> fl(s.relinfo.size());
-        for (size_t g = 0; g < fl.size(); g++)
-            fl[g] = (uint8_t)((ri_setrows(s.relinfo[g]) ? 1u : 0u) | (ri_idrows(s.relinfo[g]) ? 2u : 0u));
-        or_across(D, fl);
-        for (size_t g = 0; g < fl.size(); g++) {
-            if (fl[g] & 1u) s.relinfo[g] |= RI_SETROWS;
-            if (fl[g] & 2u) s.relinfo[g] |= RI_IDROWS;
-        }
-        if (!s.relinfo.empty())
-            KETO_HIP(hipMemcpy(const_cast<uint32_t *>(V.relinfo), s.relinfo.data(), 4 * s.relinfo.size(), hipMemcpyHostToDevice));
-    }
+    if (!E->staged) agree_flags(D);
     // visited classes: slots whose ns+"-"+rel strings are equal share one (definitions.go:114-116)
     {
         std::vector<uint32_t> vc(std::max<size_t>(1, s.slot_rel.size()), 0);
@@ -497,7 +522,10 @@ DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuple
 }
 
 void dist_free(DistEngine *E) { delete E; }
-DistView dist_view(DistEngine &E) { return DistView{E.device, E.rank, E.world, &E.coll, E.hs, E.snap.get(), E.limits}; }
+DistView dist_view(DistEngine &E) {
+    if (!E.agreed) agree_flags(E);  // (collective: every dist_view caller is)
+    return DistView{E.device, E.rank, E.world, &E.coll, E.hs, E.snap.get(), E.limits};
+}
 std::vector<uint64_t> dist_alltoall(const DistView &V, const std::vector<uint64_t> &send, double &wait_s) {
     std::vector<uint64_t> recv(V.world, 0);
     const auto t0 = std::chrono::steady_clock::now();
@@ -711,6 +739,7 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
 void dist_check(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, bool err_detail,
                 std::vector<uint32_t> &routed, DistStats &st) {
     KETO_HIP(hipSetDevice(E.device));
+    if (!E.agreed) agree_flags(E);
     ScratchStream on_hs(E.hs);
     const auto t_all = std::chrono::steady_clock::now();
     if (n > FR_MAX_BATCH) throw Error(KETO_E_LIMIT, "a partitioned batch holds at most 2^21 queries");
