@@ -196,14 +196,24 @@ __global__ __launch_bounds__(BLK) void k_validate(const keto_tuple *t, uint64_t 
     F.end();
 }
 
+// a partitioned graph's snapshot (Ghosts::world > 1): a subject-set object another rank owns is
+// an entity of the ghost namespace n_ns + s_ns (keto_object_owner)
+struct Ghosts {
+    uint32_t n_ns, rank, world;
+    __device__ __forceinline__ uint32_t ns_of_set(uint32_t s_ns, uint32_t s_obj) const {
+        if (world <= 1) return s_ns;
+        const uint64_t h = ((((uint64_t)s_ns) << 32) | s_obj) * 0x9E3779B97F4A7C15ull;
+        return (uint32_t)((h >> 32) % world) == rank ? s_ns : n_ns + s_ns;
+    }
+};
 __global__ __launch_bounds__(BLK) void k_entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride,
-                                                     unsigned long long *bits) {
+                                                     unsigned long long *bits, Ghosts G) {
     const uint64_t i = gid();
     const bool in = i < n;
     const keto_tuple x = in ? t[i] : keto_tuple{};
     const uint64_t ck = x.ns * stride + x.obj;
     run_atomic_or(bits, ck >> 6, 1ull << (ck & 63), in);
-    const uint64_t cs = x.s_ns * stride + x.s_obj;
+    const uint64_t cs = (uint64_t)(in && x.subj_kind == 1 ? G.ns_of_set(x.s_ns, x.s_obj) : 0u) * stride + x.s_obj;
     run_atomic_or(bits, cs >> 6, 1ull << (cs & 63), in && x.subj_kind == 1);
 }
 __global__ __launch_bounds__(BLK) void k_popc(const unsigned long long *bits, uint64_t nblk, uint32_t *cnt) {
@@ -241,9 +251,10 @@ struct NodeMap {
     const unsigned long long *bits;
     const uint32_t *rank;
     const NsDev *ns;
-    const uint32_t *slot_of;  // [n_ns * n_rel]
+    const uint32_t *slot_of;  // [ns table entries * n_rel]
     uint64_t stride;
     uint32_t n_rel, n_uuids;
+    Ghosts G;
 };
 __device__ __forceinline__ uint32_t node_of(const NodeMap &M, uint32_t ns, uint32_t obj, uint32_t rel) {
     const uint64_t ck = ns * M.stride + obj;
@@ -261,7 +272,7 @@ __global__ __launch_bounds__(BLK) void k_src_dst(const keto_tuple *t, uint64_t n
     if (in) {
         const keto_tuple x = t[i];
         s = node_of(M, x.ns, x.obj, x.rel);
-        const uint32_t d = x.subj_kind == 1 ? node_of(M, x.s_ns, x.s_obj, x.s_rel) : x.s_obj;
+        const uint32_t d = x.subj_kind == 1 ? node_of(M, M.G.ns_of_set(x.s_ns, x.s_obj), x.s_obj, x.s_rel) : x.s_obj;
         src[i] = s;
         dst[i] = x.subj_kind == 1 ? (d | SKEY_SET) : d;
         skey[i] = shard_hi(x);
@@ -462,21 +473,11 @@ __global__ __launch_bounds__(BLK) void k_alias_mark(uint32_t *set_dst, uint64_t 
     if (i < n && vkey[set_dst[i]] != set_dst[i]) set_dst[i] |= EDGE_ALIAS;
 }
 
-__global__ __launch_bounds__(BLK) void k_remote_mark(uint32_t *set_dst, uint64_t n, const NsDev *ns, uint32_t n_ns,
-                                                    const uint32_t *ent_obj, uint32_t rank, uint32_t world) {
+// a ghost child (another rank's object) is a remote edge
+__global__ __launch_bounds__(BLK) void k_remote_mark(uint32_t *set_dst, uint64_t n, uint32_t n_owned) {
     const uint64_t i = gid();
     if (i >= n) return;
-    const uint32_t c = set_dst[i] & ~(EDGE_ALIAS | EDGE_REMOTE);
-    uint32_t lo = 0, hi = n_ns;  // last namespace whose node_base <= c
-    while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (ns[m].node_base <= c) lo = m;
-        else hi = m;
-    }
-    const NsDev nd = ns[lo];
-    const uint32_t obj = ent_obj[nd.ent_base + (c - nd.node_base) / nd.n_slots];
-    const uint64_t h = ((((uint64_t)lo) << 32) | obj) * 0x9E3779B97F4A7C15ull;  // keto_object_owner
-    if ((uint32_t)((h >> 32) % world) != rank) set_dst[i] |= EDGE_REMOTE;
+    if ((set_dst[i] & ~(EDGE_ALIAS | EDGE_REMOTE)) >= n_owned) set_dst[i] |= EDGE_REMOTE;
 }
 __global__ __launch_bounds__(BLK) void k_leaf_mark(uint32_t *set_dst, uint64_t n, const uint4 *set_row) {
     const uint64_t i = gid();
@@ -541,8 +542,8 @@ void validate(const keto_tuple *t, uint64_t n, uint32_t n_ns, uint32_t n_rel_cal
 }
 
 void entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride, unsigned long long *bits, uint64_t nblk,
-                 uint32_t *rank) {
-    hipLaunchKernelGGL(k_entity_bits, grid_for(n), dim3(BLK), 0, 0, t, n, stride, bits);
+                 uint32_t *rank, uint32_t n_ns, uint32_t part_rank, uint32_t part_world) {
+    hipLaunchKernelGGL(k_entity_bits, grid_for(n), dim3(BLK), 0, 0, t, n, stride, bits, Ghosts{n_ns, part_rank, part_world});
     hipLaunchKernelGGL(k_popc, grid_for(nblk), dim3(BLK), 0, 0, bits, nblk, rank);
     KETO_HIP(hipGetLastError());
     scan_excl(rank, nblk);
@@ -567,7 +568,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         fprintf(stderr, "[keto build]   rows/%-12s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
         tp = now;
     };
-    NodeMap map{in.bits, in.rank, in.ns, in.slot_of, in.stride, in.n_rel, in.n_uuids};
+    NodeMap map{in.bits, in.rank, in.ns, in.slot_of, in.stride, in.n_rel, in.n_uuids, Ghosts{in.n_ns, in.part_rank, in.part_world}};
     DevBuf src(4 * n), dst(4 * n), skey(8 * n);
     KETO_HIP(hipMemset(out.all_off, 0, 4 * (N + 1)));
     KETO_HIP(hipMemset(out.rev_off, 0, 4 * (M + 1)));
@@ -696,9 +697,8 @@ void leaf_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows) {
     KETO_HIP(hipGetLastError());
 }
 
-void remote_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns,
-                 const uint32_t *ent_obj, uint32_t rank, uint32_t world) {
-    if (n) hipLaunchKernelGGL(k_remote_mark, grid_for(n), dim3(BLK), 0, 0, set_dst, n, ns, n_ns, ent_obj, rank, world);
+void remote_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows, uint32_t n_owned) {
+    if (n) hipLaunchKernelGGL(k_remote_mark, grid_for(n), dim3(BLK), 0, 0, set_dst, n, n_owned);
     hipLaunchKernelGGL(k_row_inline, grid_for(n_rows), dim3(BLK), 0, 0, set_row, n_rows, set_dst);  // inline copies too
     KETO_HIP(hipGetLastError());
     KETO_HIP(hipStreamSynchronize(nullptr));

@@ -30,8 +30,10 @@ __device__ __forceinline__ uint32_t pick(const uint32_t *a, uint32_t i, const ui
 
 // (ns, obj) -> entity id through the rank table (one 16-byte load); NONE32 if the object holds
 // no tuple in ns (the caller then uses the namespace's phantom entity)
-__device__ __forceinline__ uint32_t ent_lookup(const DevSnapshot &s, uint32_t ns, uint32_t obj) {
-    if (ns >= s.n_ns || obj >= s.n_uuids) return NONE32;
+__device__ __forceinline__ uint32_t ent_lookup(const DevSnapshot &s, uint32_t ns, uint32_t obj, bool ghost = false) {
+    if (ghost) ns += s.n_ns;  // (the caller checked that the snapshot has ghost namespaces)
+    else if (ns >= s.n_ns) return NONE32;
+    if (obj >= s.n_uuids) return NONE32;
     const uint64_t ck = (uint64_t)ns * s.ent_stride + obj;
     const uint4 b = s.ent_rank[ck >> 6];
     const uint64_t m = (uint64_t)b.x | ((uint64_t)b.y << 32);
@@ -57,10 +59,14 @@ struct Tables {
     const uint32_t *op_items;
     const uint2 *or_items;
     uint32_t n_ns, n_rel;
+    uint32_t n_ns_x;  // ns table entries (ghost namespaces of a partitioned graph's snapshot included)
 };
+__device__ __forceinline__ uint32_t ns_entries(const DevSnapshot &s) { return s.n_ns_x ? s.n_ns_x : s.n_ns; }
+// a ghost namespace's namespace (partitioned graphs; identity otherwise)
+__device__ __forceinline__ uint32_t t_real_ns(const Tables &T, uint32_t ns) { return ns >= T.n_ns ? ns - T.n_ns : ns; }
 
 __device__ __forceinline__ uint32_t t_ns_of(const Tables &T, uint32_t node) {
-    uint32_t lo = 0, hi = T.n_ns;  // last namespace whose node_base <= node
+    uint32_t lo = 0, hi = T.n_ns_x;  // last namespace whose node_base <= node
     while (hi - lo > 1) {
         uint32_t m = (lo + hi) >> 1;
         if (T.ns[m].node_base <= node) lo = m;
@@ -106,7 +112,7 @@ __device__ __forceinline__ uint32_t t_sibling(const Tables &T, uint32_t node, co
     rel = t_rel(T, rel);
     const uint32_t w = T.nsrel[(size_t)ni.ns * T.n_rel + rel];
     uint32_t slot = nr_slot(w);
-    if (slot == NO_SLOT || (node & VIRT_BIT)) return VIRT_BIT | (ni.ns << 16) | (rel & 0xFFFFu);
+    if (slot == NO_SLOT || (node & VIRT_BIT)) return VIRT_BIT | (t_real_ns(T, ni.ns) << 16) | (rel & 0xFFFFu);
     return node - ni.slot + slot;
 }
 
@@ -124,6 +130,7 @@ __device__ __forceinline__ Tables stage_tables(const DevSnapshot &s, char *lds) 
     Tables T;
     T.n_ns = s.n_ns;
     T.n_rel = s.n_rel;
+    T.n_ns_x = ns_entries(s);
     const uint4 *src[7] = {reinterpret_cast<const uint4 *>(s.ns), reinterpret_cast<const uint4 *>(s.relinfo),
                            reinterpret_cast<const uint4 *>(s.nsrel), reinterpret_cast<const uint4 *>(s.ops),
                            reinterpret_cast<const uint4 *>(s.op_children), reinterpret_cast<const uint4 *>(s.op_items),
@@ -148,7 +155,7 @@ __device__ __forceinline__ Tables stage_tables(const DevSnapshot &s, char *lds) 
 }
 
 __device__ __forceinline__ Tables global_tables(const DevSnapshot &s) {
-    return Tables{s.ns, s.relinfo, s.nsrel, s.ops, s.op_children, s.op_items, s.or_items, s.n_ns, s.n_rel};
+    return Tables{s.ns, s.relinfo, s.nsrel, s.ops, s.op_children, s.op_items, s.or_items, s.n_ns, s.n_rel, ns_entries(s)};
 }
 
 }  // namespace keto

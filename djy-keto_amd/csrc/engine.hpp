@@ -43,6 +43,9 @@ struct BuildOpts {
     std::function<void(std::vector<uint8_t> &used)> agree_used;
     bool no_leaf = false;     // no EDGE_LEAF marks (the bit is such a snapshot's EDGE_REMOTE)
     bool no_weights = false;  // no scheduling-weight array at all (DevSnapshot::weight null)
+    // rank `part_rank` of a job of part_world > 1 ranks: subject-set objects another rank owns
+    // (keto_object_owner) are entities of ghost namespaces -- every row array stops at them
+    uint32_t part_rank = 0, part_world = 1;
 };
 
 // Host mirror of the snapshot + its device buffers.
@@ -112,7 +115,7 @@ uint32_t read_u32(const uint32_t *d, uint64_t i);
 void validate(const keto_tuple *t, uint64_t n, uint32_t n_ns, uint32_t n_rel_caller, uint32_t n_uuids, uint32_t n_rel,
               uint32_t *used, unsigned long long *bad);
 void entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride, unsigned long long *bits, uint64_t nblk,
-                 uint32_t *rank);
+                 uint32_t *rank, uint32_t n_ns = 0, uint32_t part_rank = 0, uint32_t part_world = 1);
 void entity_ids(const unsigned long long *bits, uint32_t *rank, uint64_t nblk, uint64_t bpn, uint64_t stride,
                 const uint32_t *ent_base, const uint32_t *rank0, uint32_t *ent_obj, uint4 *table);
 struct RowsIn {
@@ -126,6 +129,7 @@ struct RowsIn {
     uint64_t stride;
     uint32_t n_rel, n_uuids;
     bool weights = true;            // scheduling weights (false: all 1, e.g. per-batch closure snapshots)
+    uint32_t n_ns = 0, part_rank = 0, part_world = 1;  // (ghost namespaces: BuildOpts::part_world > 1)
 };
 struct RowsOut {
     uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *weight;  // caller-allocated
@@ -136,10 +140,9 @@ struct RowsOut {
 void rows(const RowsIn &in, RowsOut &out);
 void alias_mark(uint32_t *set_dst, uint64_t n, const uint32_t *vkey, uint4 *set_row, uint64_t n_rows);
 void leaf_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows);
-// EDGE_REMOTE on every edge into a node whose object `rank` does not own (keto_object_owner over
-// `world`); the inline copies in set_row follow
-void remote_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns,
-                 const uint32_t *ent_obj, uint32_t rank, uint32_t world);
+// EDGE_REMOTE on every edge into a ghost node (>= n_owned: an object another rank owns); the
+// inline copies in set_row follow
+void remote_mark(uint32_t *set_dst, uint64_t n, uint4 *set_row, uint64_t n_rows, uint32_t n_owned);
 // flag[global slot] |= 1 where a row of the slot holds a subject set (flag zeroed by the caller)
 void slot_setrows(const uint4 *set_row, uint64_t n_rows, const NsDev *ns, uint32_t n_ns, uint32_t *flag, uint32_t n_slots);
 void slot_idrows(const keto_tuple *t, uint64_t n, const uint32_t *slot_of, uint32_t n_rel, const NsDev *ns, uint32_t *flag,

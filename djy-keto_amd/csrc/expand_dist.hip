@@ -96,7 +96,7 @@ __global__ __launch_bounds__(XB) void kx_row_fill(DevSnapshot s, const uint64_t 
             const NsDev nd = T.ns[cns];
             const uint32_t co = c - nd.node_base;
             o[j - b] = make_uint2(s.ent_obj[nd.ent_base + co / nd.n_slots],
-                                  XE_SET | cns | (s.slot_rel[nd.slot_base + co % nd.n_slots] << 15));
+                                  XE_SET | t_real_ns(T, cns) | (s.slot_rel[nd.slot_base + co % nd.n_slots] << 15));
         }
     }
 }

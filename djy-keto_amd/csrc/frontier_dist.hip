@@ -479,6 +479,8 @@ DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuple
     BuildOpts o;
     o.no_leaf = true;
     o.no_weights = true;
+    o.part_rank = E->rank;  // ghost namespaces for other ranks' subject sets
+    o.part_world = E->world;
     // KETO_PART_STAGED (ranks that share one device and so create their partitions one after
     // another, tests/test_gpu_c5.py): no collective here -- each rank lays out the slots its own
     // tuples use, and the first batch checks that every rank's layout is the same (an error
@@ -505,8 +507,7 @@ DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuple
         KETO_HIP(hipMemcpy(d, vc.data(), 4 * vc.size(), hipMemcpyHostToDevice));
         V.vclass = d;
     }
-    build::remote_mark(const_cast<uint32_t *>(V.set_dst), s.info.n_set_edges, const_cast<uint4 *>(V.set_row), V.n_nodes, V.ns,
-                       s.n_ns, V.ent_obj, E->rank, E->world);
+    build::remote_mark(const_cast<uint32_t *>(V.set_dst), s.info.n_set_edges, const_cast<uint4 *>(V.set_row), V.n_owned, V.n_owned);
     V.edge_mask = ~(EDGE_ALIAS | EDGE_REMOTE);
     V.edge_leaf = 0;
     const bool lds_tables = V.lds_bytes <= LDS_TABLE_LIMIT;
@@ -572,7 +573,7 @@ void ensure_batch(DistEngine &E, uint64_t n) {
         const char *e = getenv("KETO_FR_GOALS_PER_QUERY");
         return e ? std::max<uint64_t>(1, strtoull(e, nullptr, 10)) : (uint64_t)KETO_FR_GOALS_PER_QUERY;
     }();
-    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>({n * per_query, 2 * E.last_goals, 1u << 20}), 1ull << 29) /
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>({n * per_query, E.last_goals + E.last_goals / 2, 1u << 20}), 1ull << 29) /
                           FR_SHARDS * FR_SHARDS;
     hipStream_t s = E.hs;
     if (want > E.cap) {

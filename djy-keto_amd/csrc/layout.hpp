@@ -116,6 +116,11 @@ struct DevSnapshot {
     uint32_t probe_mask;  // bucket count - 1
     uint32_t probe_k;     // reverse rows up to this length are kept in VGPRs instead
     uint32_t n_ns, n_rel, n_nodes, n_uuids;
+    // partitioned graphs' snapshots (frontier_dist.hip): every namespace ns has a ghost namespace
+    // n_ns + ns (same slots) holding the subject-set objects other ranks own; n_ns_x = the ns
+    // table's entries (0 = n_ns), n_owned = the first ghost node (node-indexed row arrays -- set_row,
+    // all_off -- cover [0, n_owned) only: ghosts hold no rows here)
+    uint32_t n_ns_x, n_owned;
     int32_t strict;
     // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children, op_items, or_items:
     // staged in LDS

@@ -349,7 +349,7 @@ __device__ __forceinline__ keto_tuple tuple_at(const Lookup &L, uint64_t key, ui
     const uint32_t sub = S.all_subj[j];
     if (sub & SKEY_SET) {
         const uint32_t c = sub & ~SKEY_SET;
-        uint32_t lo = 0, hi = S.n_ns;  // last namespace whose node_base <= c
+        uint32_t lo = 0, hi = ns_entries(S);  // last ns table entry whose node_base <= c (ghosts included)
         while (hi - lo > 1) {
             const uint32_t m = (lo + hi) >> 1;
             if (S.ns[m].node_base <= c) lo = m;
@@ -357,7 +357,7 @@ __device__ __forceinline__ keto_tuple tuple_at(const Lookup &L, uint64_t key, ui
         }
         const NsDev n2 = S.ns[lo];
         t.subj_kind = 1;
-        t.s_ns = lo;
+        t.s_ns = lo >= S.n_ns ? lo - S.n_ns : lo;
         t.s_obj = S.ent_obj[n2.ent_base + (c - n2.node_base) / n2.n_slots];
         t.s_rel = S.slot_rel[n2.slot_base + (c - n2.node_base) % n2.n_slots];
     } else {

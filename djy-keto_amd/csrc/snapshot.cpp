@@ -334,6 +334,20 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
             s.nsrel[(size_t)ns * s.n_rel + r] = slot_of[(size_t)ns * s.n_rel + r] | (status << 16);
         }
     }
+    // partitioned graphs (BuildOpts::part_world > 1): a ghost namespace n_ns + ns per namespace, with
+    // the namespace's slots (its slot_base: relation info and names are the namespace's), holds the
+    // subject-set objects other ranks own
+    const bool ghosts = opts && opts->part_world > 1;
+    const uint32_t NX = ghosts ? 2 * s.n_ns : s.n_ns;
+    if (ghosts) {
+        if (s.n_ns >= (1u << 14)) throw Error(KETO_E_LIMIT, "a partitioned graph holds at most 16383 namespaces");
+        s.ns.resize(NX + 1);
+        for (uint32_t ns = 0; ns < s.n_ns; ns++) s.ns[s.n_ns + ns] = NsDev{0, 0, s.ns[ns].n_slots, s.ns[ns].slot_base};
+        s.nsrel.resize((size_t)NX * s.n_rel);
+        std::copy(s.nsrel.begin(), s.nsrel.begin() + NR, s.nsrel.begin() + NR);
+        slot_of.resize((size_t)NX * s.n_rel);
+        std::copy(slot_of.begin(), slot_of.begin() + NR, slot_of.begin() + NR);
+    }
     s.relinfo.resize(total_slots);
     for (uint32_t ns = 0; ns < s.n_ns; ns++)
         for (uint32_t k = 0; k < s.ns[ns].n_slots; k++) {
@@ -357,15 +371,16 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     // 16-byte block {bits lo, bits hi, entity of the block's first set bit, 0} answers
     // (ns, obj) -> entity with one load (resolve / expand kernels, and the build itself).
     const uint64_t stride = ((uint64_t)s.n_uuids + 63) / 64 * 64;
-    const uint64_t nblk = (uint64_t)s.n_ns * stride / 64, bpn = stride / 64;
+    const uint64_t nblk = (uint64_t)NX * stride / 64, bpn = stride / 64;
     if (nblk > (1ull << 31)) throw Error(KETO_E_LIMIT, "n_namespaces * n_uuids exceeds the entity rank table (2^37 ids)");
     DevBuf d_bits(8 * nblk), d_rank(4 * (nblk + 1));
     KETO_HIP(hipMemset(d_bits.p, 0, 8 * nblk));
-    build::entity_bits(dt, n, stride, static_cast<unsigned long long *>(d_bits.p), nblk, d_rank.u32());
-    std::vector<uint32_t> n_real(s.n_ns, 0), rank0(s.n_ns + 1);
-    for (uint32_t ns = 0; ns <= s.n_ns; ns++) rank0[ns] = build::read_u32(d_rank.u32(), ns * bpn);
+    build::entity_bits(dt, n, stride, static_cast<unsigned long long *>(d_bits.p), nblk, d_rank.u32(), s.n_ns,
+                       ghosts ? opts->part_rank : 0, ghosts ? opts->part_world : 1);
+    std::vector<uint32_t> n_real(NX, 0), rank0(NX + 1);
+    for (uint32_t ns = 0; ns <= NX; ns++) rank0[ns] = build::read_u32(d_rank.u32(), ns * bpn);
     uint64_t ent_total = 0, node_total = 0;
-    std::vector<uint32_t> ent_base(s.n_ns);
+    std::vector<uint32_t> ent_base(NX);
     bool with_spares = opts && opts->spares;
     if (with_spares) {
         // the room a store snapshot keeps for new objects must not cost the snapshot its format:
@@ -402,15 +417,24 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         node_total += ne * s.ns[ns].n_slots;
         if (node_total >= VIRT_BIT || ent_total >= VIRT_BIT) throw Error(KETO_E_LIMIT, "node space exceeds 2^31");
     }
-    s.ns[s.n_ns] = NsDev{(uint32_t)ent_total, (uint32_t)node_total, 0, total_slots};
-    const uint32_t N = (uint32_t)node_total;
+    const uint64_t node_owned = node_total;  // (ghost nodes follow: no rows here)
+    for (uint32_t g = s.n_ns; g < NX; g++) {  // ghost namespaces: their objects only, no phantom
+        n_real[g] = rank0[g + 1] - rank0[g];
+        s.ns[g].ent_base = ent_base[g] = (uint32_t)ent_total;
+        s.ns[g].node_base = (uint32_t)node_total;
+        ent_total += n_real[g];
+        node_total += (uint64_t)n_real[g] * s.ns[g].n_slots;
+        if (node_total >= VIRT_BIT || ent_total >= VIRT_BIT) throw Error(KETO_E_LIMIT, "node space exceeds 2^31");
+    }
+    s.ns[NX] = NsDev{(uint32_t)ent_total, (uint32_t)node_total, 0, total_slots};
+    const uint32_t N = (uint32_t)node_total, NO = (uint32_t)node_owned;
     if ((uint64_t)s.n_uuids + N + 1 >= (1ull << 32)) throw Error(KETO_E_LIMIT, "n_uuids + nodes exceeds 2^32");
     DevSnapshot &D = s.dev;
     {
-        DevBuf d_eb(4 * s.n_ns), d_r0(4 * s.n_ns);
+        DevBuf d_eb(4 * NX), d_r0(4 * NX);
         uint32_t *d_eo = static_cast<uint32_t *>(dalloc(4 * ent_total));  // kept: Expand output mapping
-        KETO_HIP(hipMemcpy(d_eb.p, ent_base.data(), 4 * s.n_ns, hipMemcpyHostToDevice));
-        KETO_HIP(hipMemcpy(d_r0.p, rank0.data(), 4 * s.n_ns, hipMemcpyHostToDevice));
+        KETO_HIP(hipMemcpy(d_eb.p, ent_base.data(), 4 * NX, hipMemcpyHostToDevice));
+        KETO_HIP(hipMemcpy(d_r0.p, rank0.data(), 4 * NX, hipMemcpyHostToDevice));
         KETO_HIP(hipMemset(d_eo, 0xFF, 4 * ent_total));  // phantoms: NONE32
         uint4 *table = static_cast<uint4 *>(dalloc(16 * nblk));
         build::entity_ids(static_cast<unsigned long long *>(d_bits.p), d_rank.u32(), nblk, bpn, stride, d_eb.u32(),
@@ -430,19 +454,24 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.ns = static_cast<const NsDev *>(dalloc(sizeof(NsDev) * s.ns.size()));
     KETO_HIP(hipMemcpy(const_cast<NsDev *>(D.ns), s.ns.data(), sizeof(NsDev) * s.ns.size(), hipMemcpyHostToDevice));
     build::RowsOut ro;
-    ro.all_off = static_cast<uint32_t *>(dalloc(4 * ((uint64_t)N + 1)));
+    // node-indexed row arrays cover the owned nodes (every tuple's object is one); the subject
+    // index covers ghosts too (a subject set another rank owns is a subject of tuples here)
+    ro.all_off = static_cast<uint32_t *>(dalloc(4 * ((uint64_t)NO + 1)));
     ro.rev_off = static_cast<uint32_t *>(dalloc(4 * (n_subj_idx + 1)));
     ro.all_subj = static_cast<uint32_t *>(dalloc(4 * n));
     ro.rev_nodes = static_cast<uint32_t *>(dalloc(4 * n));
-    ro.set_row = static_cast<uint4 *>(dalloc(16 * (uint64_t)N));
-    ro.weight = (opts && opts->no_weights) ? nullptr : static_cast<uint32_t *>(dalloc(4 * (uint64_t)N));
+    ro.set_row = static_cast<uint4 *>(dalloc(16 * (uint64_t)NO));
+    ro.weight = (opts && opts->no_weights) ? nullptr : static_cast<uint32_t *>(dalloc(4 * (uint64_t)NO));
     std::vector<uint32_t> idrows(total_slots, 0);  // slots holding a subject-id tuple (RI_IDROWS)
     {
-        DevBuf d_slot(4 * NR);
-        KETO_HIP(hipMemcpy(d_slot.p, slot_of.data(), 4 * NR, hipMemcpyHostToDevice));
-        build::RowsIn ri{dt, device_tuples ? nullptr : tuples, n, N, n_subj_idx, static_cast<const unsigned long long *>(d_bits.p), d_rank.u32(),
+        DevBuf d_slot(4 * slot_of.size());
+        KETO_HIP(hipMemcpy(d_slot.p, slot_of.data(), 4 * slot_of.size(), hipMemcpyHostToDevice));
+        build::RowsIn ri{dt, device_tuples ? nullptr : tuples, n, NO, n_subj_idx, static_cast<const unsigned long long *>(d_bits.p), d_rank.u32(),
                          D.ns, d_slot.u32(), stride, s.n_rel, s.n_uuids};
         ri.weights = sched_weights;
+        ri.n_ns = s.n_ns;
+        ri.part_rank = ghosts ? opts->part_rank : 0;
+        ri.part_world = ghosts ? opts->part_world : 1;
         build::rows(ri, ro);
         if (total_slots) {
             DevBuf flag(4ull * total_slots);
@@ -512,7 +541,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
             }
             uint32_t *dv = static_cast<uint32_t *>(dalloc(4ull * N));
             KETO_HIP(hipMemcpy(dv, vkey.data(), 4ull * N, hipMemcpyHostToDevice));
-            build::alias_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, dv, ro.set_row, N);
+            build::alias_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, dv, ro.set_row, NO);
             D.vkey = dv;
         }
     }
@@ -521,7 +550,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.edge_mask = ~EDGE_ALIAS;
     D.edge_leaf = 0;
     if (N < (1ull << 30) && ro.n_set && !(opts && opts->no_leaf)) {
-        build::leaf_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, ro.set_row, N);
+        build::leaf_mark(const_cast<uint32_t *>(D.set_dst), ro.n_set, ro.set_row, NO);
         D.edge_mask = ~(EDGE_ALIAS | EDGE_LEAF);
         D.edge_leaf = 1;
     }
@@ -529,7 +558,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     if (total_slots) {
         DevBuf flag(4ull * total_slots);
         KETO_HIP(hipMemset(flag.p, 0, 4ull * total_slots));
-        build::slot_setrows(ro.set_row, N, D.ns, s.n_ns, flag.u32(), total_slots);
+        build::slot_setrows(ro.set_row, NO, D.ns, s.n_ns, flag.u32(), total_slots);
         std::vector<uint32_t> hf(total_slots);
         KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * total_slots, hipMemcpyDeviceToHost));
         for (uint32_t gs = 0; gs < total_slots; gs++) {
@@ -596,6 +625,8 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.lds_bytes = 0;
     for (uint32_t b : D.tab_bytes) D.lds_bytes += b;
     D.n_ns = s.n_ns;
+    D.n_ns_x = NX;
+    D.n_owned = NO;
     D.n_rel = s.n_rel;
     D.n_nodes = N;
     D.n_uuids = s.n_uuids;
@@ -700,6 +731,7 @@ constexpr size_t STAGE = 64u << 20;  // device <-> file through a pinned buffer 
 }  // namespace
 
 void save_snapshot(const Snapshot &s, const char *path) {
+    if (s.dev.n_ns_x != s.n_ns) throw Error(KETO_E_INVALID, "a partition's snapshot (ghost namespaces) is not saved");
     KETO_HIP(hipSetDevice(s.device));
     File F(path, "wb");
     const uint64_t magic = SNAP_MAGIC;
