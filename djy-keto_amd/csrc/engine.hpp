@@ -84,6 +84,8 @@ struct Snapshot {
 
 Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_tuples,
                          bool sched_weights = true, const BuildOpts *opts = nullptr);
+// reach.hip: the snapshot's reachability tables (s.dev.reach_*), or none
+void build_reach(Snapshot &s);
 // 64-bit FNV-1a of everything a snapshot compiles from its configuration (name tables, AST JSON,
 // strict mode; not the device, not n_uuids): equal hashes = the same compiled tables
 uint64_t config_hash(const keto_snapshot_config *cfg);

@@ -365,6 +365,7 @@ struct DistEngine {
     uint64_t last_goals = 0, last_pos = 0, last_ob = 0;
     uint32_t *hpin = nullptr;  // pinned control read-backs
     std::vector<Level> levels;
+    std::vector<keto_partition_level> level_acc;  // the last batch's generations, its chunks summed
     ~DistEngine() {
         if (hpin) (void)hipHostFree(hpin);
         for (auto e : ev)
@@ -556,9 +557,7 @@ void dist_alltoallv(const DistView &V, const void *src, const std::vector<uint64
 }
 const Snapshot &dist_snapshot(const DistEngine &E) { return *E.snap; }
 std::vector<keto_partition_level> dist_levels(const DistEngine &E) {
-    std::vector<keto_partition_level> v;
-    for (auto &l : E.levels) v.push_back(l.stat);
-    return v;
+    return E.level_acc;
 }
 
 namespace {
@@ -737,13 +736,11 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
 
 }  // namespace
 
-void dist_check(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, bool err_detail,
-                std::vector<uint32_t> &routed, DistStats &st) {
-    KETO_HIP(hipSetDevice(E.device));
-    if (!E.agreed) agree_flags(E);
+namespace {
+void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, bool err_detail,
+                 std::vector<uint32_t> &routed, DistStats &st) {
     ScratchStream on_hs(E.hs);
     const auto t_all = std::chrono::steady_clock::now();
-    if (n > FR_MAX_BATCH) throw Error(KETO_E_LIMIT, "a partitioned batch holds at most 2^21 queries");
     hipStream_t s = E.hs;
     const uint32_t W = E.world;
     double wait_s = 0, dev_ms = 0;
@@ -951,6 +948,61 @@ void dist_check(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowed
                 "%llu decisive; device %.2f ms, collective %.2f ms, wall %.2f ms\n",
                 E.rank, (unsigned long long)n, G, (unsigned long long)total_goals, (unsigned long long)sent_total, bytes / 1e6, nfb,
                 (unsigned long long)st.decisive, dev_ms, wait_s * 1e3, st.wall_s * 1e3);
+}
+}  // namespace
+
+// A batch runs in chunks of at most KETO_PART_CHUNK queries (default: one chunk of up to 2^21):
+// the arena, the positions and the per-generation exchange buffers scale with a chunk, which
+// bounds a rank's memory beside its resident partition (ranks that share a device).  Every rank
+// runs the job-wide chunk count -- the largest batch's -- so the collectives stay in step; a rank
+// whose batch ran out takes part with empty chunks.
+void dist_check(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, bool err_detail,
+                std::vector<uint32_t> &routed, DistStats &st) {
+    KETO_HIP(hipSetDevice(E.device));
+    if (!E.agreed) agree_flags(E);
+    if (n > FR_MAX_BATCH) throw Error(KETO_E_LIMIT, "a partitioned batch holds at most 2^21 queries");
+    static const uint64_t chunk = [] {
+        const char *e = getenv("KETO_PART_CHUNK");
+        const uint64_t c = e ? strtoull(e, nullptr, 10) : 0;
+        return c ? std::min<uint64_t>(c, FR_MAX_BATCH) : (uint64_t)FR_MAX_BATCH;
+    }();
+    const auto t_all = std::chrono::steady_clock::now();
+    double wait_s = 0;
+    uint64_t chunks = (n + chunk - 1) / chunk;
+    if (chunk < FR_MAX_BATCH)
+        for (uint64_t c : d_alltoall(E, std::vector<uint64_t>(E.world, chunks), wait_s)) chunks = std::max(chunks, c);
+    chunks = std::max<uint64_t>(chunks, 1);
+    st = DistStats{};
+    st.exchange_s = wait_s;
+    routed.clear();
+    std::vector<keto_partition_level> acc;
+    for (uint64_t c = 0; c < chunks; c++) {
+        const uint64_t b = std::min(n, c * chunk), m = std::min(n, b + chunk) - b;
+        std::vector<uint32_t> r;
+        DistStats cs;
+        check_chunk(E, q + b, m, allowed + b, err + b, err_detail, r, cs);
+        for (uint32_t i : r) routed.push_back((uint32_t)(b + i));
+        st.generations = std::max(st.generations, cs.generations);
+        st.goals += cs.goals;
+        st.positions += cs.positions;
+        st.routed += cs.routed;
+        st.records_sent += cs.records_sent;
+        st.bytes_exchanged += cs.bytes_exchanged;
+        st.decisive += cs.decisive;
+        st.device_s += cs.device_s;
+        st.exchange_s += cs.exchange_s;
+        for (size_t g = 0; g < E.levels.size(); g++) {
+            if (acc.size() <= g) acc.push_back(keto_partition_level{});
+            const keto_partition_level &l = E.levels[g].stat;
+            acc[g].objects += l.objects;
+            acc[g].request_bytes += l.request_bytes;
+            acc[g].tuples += l.tuples;
+            acc[g].tuple_bytes_sent += l.tuple_bytes_sent;
+            acc[g].ms += l.ms;
+        }
+    }
+    E.level_acc = std::move(acc);
+    st.wall_s = ms_since(t_all) / 1e3;
 }
 
 }  // namespace keto

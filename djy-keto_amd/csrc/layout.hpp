@@ -121,6 +121,11 @@ struct DevSnapshot {
     // table's entries (0 = n_ns), n_owned = the first ghost node (node-indexed row arrays -- set_row,
     // all_off -- cover [0, n_owned) only: ghosts hold no rows here)
     uint32_t n_ns_x, n_owned;
+    // reachability tables (reach.hip): a tabled node's reach over subject-set rows, for the
+    // frontier's spawn-time NotMember (frontier_goal.inc reach_prunes); null when none
+    const uint32_t *reach_base;  // [total slots] first reach_idx entry of a tabled slot, NONE32
+    const uint2 *reach_idx;      // [tabled slots' entities] {offset, count | NONE32: not tabled}
+    const uint32_t *reach_pool;  // the reaches (nodes; the node itself not listed)
     int32_t strict;
     // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children, op_items, or_items:
     // staged in LDS
@@ -128,6 +133,7 @@ struct DevSnapshot {
     uint32_t lds_bytes;
 };
 
+constexpr uint32_t REACH_CAP = 128;        // nodes of a tabled reach, the node itself included (oracle REACH_CAP)
 constexpr uint32_t WEIGHT_ROUNDS = 12;     // path-count relaxation rounds (> typical max depth)
 constexpr uint32_t WEIGHT_CAP = 1u << 20;
 constexpr uint32_t HEAVY_WEIGHT = 32;      // roots at or above this weight are scheduled first

@@ -867,6 +867,9 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     s.info.n_tuples = n_all;
     s.info.n_set_edges = n_set;
     s.info.n_rev_entries = n_all;
+    // the reachability tables again: the rows this patch changed move reaches anywhere above them
+    build_reach(s);
+    phase("reach");
     s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (verbose)
         fprintf(stderr, "[keto patch] %llu touched tuples: %u rows, %u subjects, %llu store matches, %zu leaf flips, "

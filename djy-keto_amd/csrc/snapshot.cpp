@@ -631,6 +631,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.n_nodes = N;
     D.n_uuids = s.n_uuids;
     D.strict = s.strict;
+    build_reach(s);
     KETO_HIP(hipStreamSynchronize(nullptr));  // the build ran on the null stream; engines read it from theirs
     phase("finish");
     s.info.n_entities = ent_total;
@@ -726,6 +727,9 @@ void dev_ptrs(DevSnapshot &D, F &&f) {
     f(reinterpret_cast<const void *&>(D.ent_rank));
     f(reinterpret_cast<const void *&>(D.ext));
     f(reinterpret_cast<const void *&>(D.probe));
+    f(reinterpret_cast<const void *&>(D.reach_base));
+    f(reinterpret_cast<const void *&>(D.reach_idx));
+    f(reinterpret_cast<const void *&>(D.reach_pool));
 }
 constexpr size_t STAGE = 64u << 20;  // device <-> file through a pinned buffer of this size
 }  // namespace
@@ -812,7 +816,7 @@ Snapshot *load_snapshot(const char *path, int device) {
     std::vector<size_t> bytes;
     F.get_v(idx);
     F.get_v(bytes);
-    if (idx.size() != 20) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+    if (idx.size() != 23) throw Error(KETO_E_INVALID, "snapshot file corrupt");
     void *stage = nullptr;
     KETO_HIP(hipHostMalloc(&stage, STAGE, 0));
     try {

@@ -41,7 +41,8 @@ class SnapshotConfig(ctypes.Structure):
 class SnapshotInfo(ctypes.Structure):
     _fields_ = [("n_tuples", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64), ("n_entities", ctypes.c_uint64),
                 ("n_set_edges", ctypes.c_uint64), ("n_rev_entries", ctypes.c_uint64),
-                ("device_bytes", ctypes.c_uint64), ("build_seconds", ctypes.c_double), ("version", ctypes.c_uint64)]
+                ("device_bytes", ctypes.c_uint64), ("build_seconds", ctypes.c_double), ("version", ctypes.c_uint64),
+                ("n_reach", ctypes.c_uint64)]
 
 
 class Limits(ctypes.Structure):

@@ -113,6 +113,7 @@ typedef struct keto_snapshot_info {
     uint64_t device_bytes;
     double build_seconds;
     uint64_t version; /* keto_store version it was cut from (the snaptoken); 0 if built directly */
+    uint64_t n_reach; /* nodes with a reachability table (the frontier's spawn-time NotMember) */
 } keto_snapshot_info;
 
 /* limit.max_read_depth / limit.max_read_width (internal/driver/config/provider.go:180-185) */

@@ -49,6 +49,9 @@ struct rs_db {
     int32_t *children;
     uint32_t *vclass;
     uint8_t *ssrel;    /* [n_ns * n_relnames]: some tuple of (ns, rel) has a subject set */
+    uint8_t *sstarget; /* [n_ns * n_relnames]: some tuple's subject set is a (ns, ., rel) */
+    int32_t aliased;   /* two relation slots share a visited class (the engine's vkey table) */
+    int32_t no_reach;  /* rs_set_reach(db, 0) / RS_NO_REACH=1: the engine built without tables */
     uint32_t n_ns, n_relnames, empty_rel, n_rels, n_ast, n_children;
     int32_t strict, max_depth, max_width;
 };
@@ -317,11 +320,40 @@ rs_db *rs_build(const rs_tuple *tuples, size_t n, const rs_config *cfg) {
     db->strict = cfg->strict;
     db->max_depth = cfg->max_depth;
     db->max_width = cfg->max_width;
-    db->ssrel = calloc((size_t)db->n_ns * db->n_relnames + 1, 1);
+    const size_t NR = (size_t)db->n_ns * db->n_relnames;
+    db->ssrel = calloc(NR + 1, 1);
+    db->sstarget = calloc(NR + 1, 1);
+    uint8_t *slot = calloc(NR + 1, 1); /* the engine's relation slots: declared or used pairs */
     for (size_t i = 0; i < n; i++) {
         const key7 *t = &db->rt[i];
-        if (t->kind == 1 && t->ns < db->n_ns && t->rel < db->n_relnames) db->ssrel[(size_t)t->ns * db->n_relnames + t->rel] = 1;
+        if (t->ns < db->n_ns && t->rel < db->n_relnames) slot[(size_t)t->ns * db->n_relnames + t->rel] = 1;
+        if (t->kind != 1) continue;
+        if (t->ns < db->n_ns && t->rel < db->n_relnames) db->ssrel[(size_t)t->ns * db->n_relnames + t->rel] = 1;
+        if (t->sns < db->n_ns && t->srel < db->n_relnames) {
+            db->sstarget[(size_t)t->sns * db->n_relnames + t->srel] = 1;
+            slot[(size_t)t->sns * db->n_relnames + t->srel] = 1;
+        }
     }
+    for (uint32_t a = 0; a < db->n_ns; a++)
+        if (db->ns[a].configured)
+            for (int i = 0; i < db->ns[a].rel_count; i++) {
+                const uint32_t r = db->rels[db->ns[a].rel_begin + i].name;
+                if (r < db->n_relnames) slot[(size_t)a * db->n_relnames + r] = 1;
+            }
+    /* csrc/snapshot.cpp "visited keys": slots whose ns+"-"+rel strings are equal */
+    uint32_t maxc = 0;
+    for (size_t i = 0; i < NR; i++)
+        if (slot[i] && db->vclass[i] > maxc) maxc = db->vclass[i];
+    uint8_t *seen = calloc((size_t)maxc + 2, 1);
+    for (size_t i = 0; i < NR; i++)
+        if (slot[i]) {
+            if (seen[db->vclass[i]]) db->aliased = 1;
+            seen[db->vclass[i]] = 1;
+        }
+    free(seen);
+    free(slot);
+    const char *nr = getenv("RS_NO_REACH"); /* (the product's KETO_NO_REACH=1) */
+    db->no_reach = nr && *nr == '1';
     return db;
 }
 
@@ -336,6 +368,7 @@ void rs_free(rs_db *db) {
     free(db->ast);
     free(db->children);
     free(db->vclass);
+    free(db->sstarget);
     free(db->ssrel);
     free(db);
 }
@@ -1131,6 +1164,8 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
 static res u_rw(uctx *u, uint32_t ns, uint32_t obj, int ai, int d, uint32_t scope, uint32_t gen);
 static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen, int chain);
 
+static int u_reach_prunes(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel);
+
 /* a relation whose rows can hold subject sets: some tuple of (ns, rel) has one (per snapshot) */
 static int has_set_rows(const rs_db *db, uint32_t ns, uint32_t rel) {
     return ns < db->n_ns && rel < db->n_relnames && db->ssrel[(size_t)ns * db->n_relnames + rel];
@@ -1188,13 +1223,65 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
         *out = R_IS;
         return 0;
     }
-    if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && (!node_check || node_has_set_rows(db, ns, obj, rel))) {
+    if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && (!node_check || node_has_set_rows(db, ns, obj, rel)) &&
+        !u_reach_prunes(u, ns, obj, rel)) {
         if (!u_spawn(u, gen + 1)) return 0;
         *out = u_es(u, ns, obj, rel, d - 1, scope, gen + 1, 1);
         return 1;
     }
     *out = R_NOT;
     return 0;
+}
+
+/* Reachability pruning (csrc/reach.hip; the engine's REACH_CAP).  Reach(n) = n and every node
+ * reachable from it over subject-set rows.  A node n is "tabled" when its relation slot is pure
+ * (no rewrite, no ASTRelationFor error), holds subject-set rows and is some tuple's subject-set
+ * relation, every node of Reach(n) is pure, and |Reach(n)| <= REACH_CAP -- and the snapshot has no
+ * aliased visited keys.  Then checkIsAllowed(n, d > 1) can only be IsMember through a node of
+ * Reach(n) whose own row holds the subject: with none, it is NotMember whatever the visited set
+ * and depth do (a pure node yields IsMember or NotMember, never an error or a bare Unknown, at
+ * d > 1), and no key of Reach(n) can be a decisive occurrence for this subject anywhere in the
+ * query (each such node's own reach is inside Reach(n)), so no routing decision depends on
+ * them.  The engine decides such a sub-check NotMember where it is spawned (no goal). */
+#define REACH_CAP 128
+static int rel_pure(const rs_db *db, uint32_t ns, uint32_t rel) {
+    int err;
+    const int ri = ast_relation_for(db, ns, rel, &err);
+    return !err && (ri < 0 || db->rels[ri].rewrite < 0);
+}
+void rs_set_reach(rs_db *db, int on) { db->no_reach = !on; }
+static int u_reach_prunes(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel) {
+    const rs_db *db = u->c->db;
+    if (db->no_reach || db->aliased || ns >= db->n_ns || rel >= db->n_relnames) return 0;
+    const size_t nr = (size_t)ns * db->n_relnames + rel;
+    if (!db->ssrel[nr] || !db->sstarget[nr] || !rel_pure(db, ns, rel)) return 0;
+    uint32_t lst[REACH_CAP][3];
+    uint32_t cnt = 1, head = 0;
+    lst[0][0] = ns;
+    lst[0][1] = obj;
+    lst[0][2] = rel;
+    while (head < cnt) {
+        const uint32_t a = lst[head][0], o = lst[head][1], r = lst[head][2];
+        head++;
+        if (!rel_pure(db, a, r)) return 0;
+        size_t lo, hi;
+        node_rows(db, a, o, r, &lo, &hi);
+        for (size_t i = lo; i < hi; i++) {
+            const key7 *t = ROW(db, i);
+            if (t->kind != 1) continue;
+            int dup = 0;
+            for (uint32_t k = 0; k < cnt && !dup; k++) dup = lst[k][0] == t->sns && lst[k][1] == t->sid && lst[k][2] == t->srel;
+            if (dup) continue;
+            if (cnt == REACH_CAP) return 0;
+            lst[cnt][0] = t->sns;
+            lst[cnt][1] = t->sid;
+            lst[cnt][2] = t->srel;
+            cnt++;
+        }
+    }
+    for (uint32_t k = 0; k < cnt; k++)
+        if (exists(u->c, lst[k][0], lst[k][1], lst[k][2])) return 0;
+    return 1;
 }
 
 /* u_sub's shaping decision without evaluating anything: 1 when it would spawn a goal */
@@ -1208,7 +1295,7 @@ static int u_sub_spawns(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d,
     if (err) return 0;
     const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
     if (!skip && d - 1 > 0 && exists(u->c, ns, obj, rel)) return 0;
-    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel);
+    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && !u_reach_prunes(u, ns, obj, rel);
 }
 
 /* A NOT whose operand is decided where it is spawned -- a malformed NOT, a computed userset
@@ -1501,7 +1588,8 @@ static int u_es_child_is_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, in
     const int ri = ast_relation_for(db, ns, rel, &err);
     if (err || (ri >= 0 && db->rels[ri].rewrite >= 0)) return 0; /* an IA goal */
     const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
-    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && node_has_set_rows(db, ns, obj, rel);
+    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && node_has_set_rows(db, ns, obj, rel) &&
+           !u_reach_prunes(u, ns, obj, rel);
 }
 
 /* chain: an expand-subject whose row holds exactly one subject set, kept, that would be an ES
@@ -1569,7 +1657,8 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
     res rr = R_NOT, er = R_NOT;
     if (has_rewrite && u_spawn(u, gen + 1)) rr = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
     const int direct_is = (!db->strict || !has_rewrite) && !skip && d - 1 > 0 && exists(u->c, ns, obj, rel);
-    if (can_ss && !direct_is && d - 1 > 0 && has_set_rows(db, ns, rel) && u_spawn(u, gen + 1))
+    if (can_ss && !direct_is && d - 1 > 0 && has_set_rows(db, ns, rel) && !u_reach_prunes(u, ns, obj, rel) &&
+        u_spawn(u, gen + 1))
         er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1, 1);
     if (decisive(rr)) return rr;
     if (direct_is) return R_IS;

@@ -108,6 +108,9 @@ typedef struct rs_db rs_db;
 rs_db *rs_build(const rs_tuple *tuples, size_t n, const rs_config *cfg);
 void rs_free(rs_db *db);
 void rs_set_limits(rs_db *db, int32_t max_depth, int32_t max_width);
+/* the frontier restatement's reachability rule (u_reach_prunes) on / off (default on, unless
+ * RS_NO_REACH=1): the product's snapshots carry the tables unless KETO_NO_REACH=1 */
+void rs_set_reach(rs_db *db, int on);
 
 /* Returns membership; *err receives the error code. */
 int rs_check(rs_db *db, const rs_query *q, int32_t *err, rs_stats *st);

@@ -63,6 +63,7 @@ def lib():
         L.rs_build.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Cfg)]
         L.rs_free.argtypes = [ctypes.c_void_p]
         L.rs_set_limits.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        L.rs_set_reach.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.rs_check.restype = ctypes.c_int
         L.rs_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
                                ctypes.POINTER(Stats)]
@@ -318,6 +319,10 @@ class Oracle:
 
     def set_limits(self, max_depth: int, max_width: int):
         lib().rs_set_limits(self.db, max_depth, max_width)
+
+    def set_reach(self, on: bool):
+        """the frontier restatement's reachability rule (rs_check_u): on by default"""
+        lib().rs_set_reach(self.db, int(bool(on)))
 
     def _check_ids(self, q: np.ndarray):
         if len(q) and (int(q["ns"].max()) >= self.n_ns or int(q["rel"].max()) >= self.n_rel or

@@ -45,6 +45,8 @@ def _free_port():
 def _worker(rank, world, port, lib, case, seeds, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KETO_MI355X_ALLOW_OVERRIDE="tools",
                       KETO_MI355X_LIB_OVERRIDE=lib)
+    if case == "drive_chunked":  # the batch in chunks of 700 queries (the ranks' chunk counts differ)
+        os.environ["KETO_PART_CHUNK"] = "700"
     for p in (ROOT, os.path.join(ROOT, "djy-keto_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -77,7 +79,7 @@ def _worker(rank, world, port, lib, case, seeds, out):
                 wl = synth.drive(depth=4, fanout=3, acl_per_node=6, n_groups=200, members_per_group=6, n_users=600,
                                  seed=seed)
                 tup = wl.tuples
-                q = synth.drive_queries(wl, 3000, seed=seed + 7)
+                q = synth.drive_queries(wl, 3000 - 500 * rank * (case == "drive_chunked"), seed=seed + 7)
                 ns_cfg, ns_names, rel_names = wl.namespaces, wl.ns_names, wl.rel_names
                 n_uuids, strict, depth, width = wl.n_uuids, wl.strict, wl.max_depth, wl.max_width
                 w, _ = world_from_workload(wl, with_tuples=False)
@@ -143,9 +145,9 @@ def test_random_worlds_match_oracle(emu_lib, world):
     assert routed < 0.25 * total, (routed, total)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_small_drive_matches_oracle(emu_lib, world):
-    res = _run(emu_lib, world, "drive", [5])
+@pytest.mark.parametrize("world,case", [(2, "drive"), (3, "drive"), (3, "drive_chunked")])
+def test_small_drive_matches_oracle(emu_lib, world, case):
+    res = _run(emu_lib, world, case, [5])
     for r in range(world):
         for x in res[r]:
             assert x["dmis"] == 0 and x["emis"] == 0, (r, x)

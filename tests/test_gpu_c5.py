@@ -106,7 +106,8 @@ def _worker(rank, world, port, out):
     # the slot layout is checked and the relation flags agreed at the first batch), the allocation
     # caches stay small, and the engine's arena holds fewer goals per query than a GPU of its own
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KETO_POOL_CAP_MB="1", KETO_SCRATCH_CAP_MB="1",
-                      KETO_PART_TRIM="1", KETO_PART_STAGED="1", KETO_FR_GOALS_PER_QUERY=os.environ.get("KETO_C5_GOALS_PER_QUERY", "96"))
+                      KETO_PART_TRIM="1", KETO_PART_STAGED="1", KETO_FR_GOALS_PER_QUERY=os.environ.get("KETO_C5_GOALS_PER_QUERY", "160"),
+                      KETO_PART_CHUNK=os.environ.get("KETO_C5_CHUNK", "262144"))
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=30))
     try:
         import keto_mi355x as km
