@@ -71,6 +71,11 @@ struct Snapshot {
     uint64_t cfg_hash = 0;     // config_hash of the configuration it was compiled from (patches keep it)
     uint64_t probe_used = 0;   // probe-hash slots holding a key or a tombstone (patches keep the load bounded)
     std::shared_ptr<Spares> spares;  // (store snapshots: room for new objects)
+    // reachability tables (reach.hip), host side: each global slot's first candidate (NONE32: not
+    // tabled), the candidates and the pool entries in use -- what a patch's incremental rebuild
+    // compares and extends (empty after keto_snapshot_load: a patch then rebuilds them whole)
+    std::vector<uint32_t> reach_slots;
+    uint64_t reach_cand = 0, reach_pool_n = 0;
     std::vector<uint4> ext;          // {obj, ns, entity, 0} of the objects placed on spares (dev.ext's entries)
 
     // a device allocation of this snapshot (back to the pool with its last sharer)
@@ -86,6 +91,11 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
                          bool sched_weights = true, const BuildOpts *opts = nullptr);
 // reach.hip: the snapshot's reachability tables (s.dev.reach_*), or none
 void build_reach(Snapshot &s);
+// reach.hip: the tables of a patched snapshot s from its base's: only the tabled nodes whose
+// reach can have changed -- the touched rows' nodes and their ancestors over subject-set rows
+// within REACH_CAP - 1 hops -- are walked again; anything else (the tabled slots changed, the base
+// has no host record) rebuilds them whole
+void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &touched_nodes);
 // 64-bit FNV-1a of everything a snapshot compiles from its configuration (name tables, AST JSON,
 // strict mode; not the device, not n_uuids): equal hashes = the same compiled tables
 uint64_t config_hash(const keto_snapshot_config *cfg);

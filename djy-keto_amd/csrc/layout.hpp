@@ -48,6 +48,8 @@ __host__ __device__ inline bool ri_shared(uint32_t ri) { return (ri >> 20) & 1u;
 constexpr uint32_t RI_SETROWS = 1u << 21;
 __host__ __device__ inline bool ri_setrows(uint32_t ri) { return (ri >> 21) & 1u; }
 constexpr uint32_t RI_IDROWS = 1u << 22;
+// bit 23: the slot's nodes have reachability tables (reach.hip; DevSnapshot::reach_base)
+constexpr uint32_t RI_REACH = 1u << 23;
 __host__ __device__ inline bool ri_idrows(uint32_t ri) { return (ri >> 22) & 1u; }
 __host__ __device__ inline uint32_t make_ri(uint32_t op, bool rw, bool ss, uint32_t status, bool shared) {
     return (op & 0xFFFFu) | (uint32_t(rw) << 16) | (uint32_t(ss) << 17) | (status << 18) | (uint32_t(shared) << 20);
@@ -124,8 +126,9 @@ struct DevSnapshot {
     // reachability tables (reach.hip): a tabled node's reach over subject-set rows, for the
     // frontier's spawn-time NotMember (frontier_goal.inc reach_prunes); null when none
     const uint32_t *reach_base;  // [total slots] first reach_idx entry of a tabled slot, NONE32
-    const uint2 *reach_idx;      // [tabled slots' entities] {offset, count | NONE32: not tabled}
-    const uint32_t *reach_pool;  // the reaches (nodes; the node itself not listed)
+    const uint4 *reach_idx;      // [tabled slots' entities] {count | NONE32: not tabled, entry 0, entry 1,
+                                 //  pool offset of entries 2.. (runs padded to 4 entries)}
+    const uint32_t *reach_pool;  // the reaches past their first two entries (nodes; the node itself not listed)
     int32_t strict;
     // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children, op_items, or_items:
     // staged in LDS
@@ -133,7 +136,9 @@ struct DevSnapshot {
     uint32_t lds_bytes;
 };
 
-constexpr uint32_t REACH_CAP = 128;        // nodes of a tabled reach, the node itself included (oracle REACH_CAP)
+constexpr uint32_t REACH_CAP = 32;         // nodes of a tabled reach, the node itself included (oracle reach_cap;
+                                           // KETO_REACH_CAP <= REACH_CAP_MAX for A/B builds)
+constexpr uint32_t REACH_CAP_MAX = 128;
 constexpr uint32_t WEIGHT_ROUNDS = 12;     // path-count relaxation rounds (> typical max depth)
 constexpr uint32_t WEIGHT_CAP = 1u << 20;
 constexpr uint32_t HEAVY_WEIGHT = 32;      // roots at or above this weight are scheduled first

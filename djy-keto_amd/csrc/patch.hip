@@ -867,8 +867,12 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     s.info.n_tuples = n_all;
     s.info.n_set_edges = n_set;
     s.info.n_rev_entries = n_all;
-    // the reachability tables again: the rows this patch changed move reaches anywhere above them
-    build_reach(s);
+    // the reachability tables: the rows this patch changed move the reaches of their ancestors
+    {
+        std::vector<uint32_t> tnodes(tn.size());
+        for (size_t j = 0; j < tn.size(); j++) tnodes[j] = tn[j].idx;
+        patch_reach(s, B, tnodes);
+    }
     phase("reach");
     s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (verbose)

@@ -36,6 +36,7 @@ struct ReachIn {
     const uint4 *tslots;  // {first candidate, ns, slot in ns, 0} per tabled slot, ascending
     uint32_t n_tslots;
     uint64_t n_cand;
+    uint32_t cap;  // REACH_CAP, or KETO_REACH_CAP (A/B)
 };
 
 __device__ __forceinline__ uint32_t ns_of_node(const NsDev *ns, uint32_t n_ns, uint32_t node) {
@@ -66,13 +67,18 @@ __global__ __launch_bounds__(RB) void k_slot_targets(const uint32_t *set_dst, ui
 
 // One wave per candidate node: a breadth-first walk of its reach with the list in registers
 // (entry k on lane k % 64, register k / 64).  Pass 1 (FILL = false) counts, pass 2 writes the
-// list at the offset pass 1's scan gave.
+// record {count, entry 0, entry 1, pool offset} and the entries past the first two at the offset
+// pass 1's scan gave (pool runs padded to 4 entries: the engine reads them in 16-byte windows).
+// `list` (incremental builds): the candidates to walk, else all of them.
+__device__ __forceinline__ uint32_t pool_need(uint32_t n) { return n > 2 ? (n - 2 + 3) & ~3u : 0u; }
 template <bool FILL>
-__global__ __launch_bounds__(RB) void k_reach(ReachIn R, uint2 *idx, uint32_t *lens, uint32_t *pool, unsigned long long *total) {
-    static_assert(REACH_CAP <= 128, "two list registers per lane");
+__global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, uint64_t n_items, uint4 *idx, uint32_t *lens,
+                                              uint32_t *pool, uint32_t pool_base, unsigned long long *total) {
+    static_assert(REACH_CAP_MAX <= 128, "two list registers per lane");
     const uint32_t wpb = blockDim.x >= 64 ? blockDim.x / 64 : 1;  // (the CPU emulation: one-lane blocks)
     const uint64_t nw = (uint64_t)gridDim.x * wpb;
-    for (uint64_t t = (uint64_t)blockIdx.x * wpb + threadIdx.x / 64; t < R.n_cand; t += nw) {
+    for (uint64_t i = (uint64_t)blockIdx.x * wpb + threadIdx.x / 64; i < n_items; i += nw) {
+        const uint64_t t = list ? list[i] : i;
         uint32_t lo = 0, hi = R.n_tslots;  // the candidate's slot
         while (hi - lo > 1) {
             const uint32_t m = (lo + hi) >> 1;
@@ -85,7 +91,7 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, uint2 *idx, uint32_t *l
         uint32_t cnt = 1, head = 0;
         bool ok = true;
 #ifdef KETO_CPUEMU  // one lane: the list in an array
-        uint32_t L[REACH_CAP];
+        uint32_t L[REACH_CAP_MAX];
         L[0] = g;
         while (ok && head < cnt) {
             const uint32_t n = L[head++];
@@ -100,19 +106,26 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, uint2 *idx, uint32_t *l
                 for (uint32_t k = 0; k < cnt; k++)
                     if (L[k] == c) fresh = false;
                 if (!fresh) continue;
-                if (cnt == REACH_CAP) ok = false;
+                if (cnt == R.cap) ok = false;
                 else L[cnt++] = c;
             }
         }
+        const uint32_t n = ok ? cnt - 1 : 0u;  // the reach without g
         if constexpr (!FILL) {
-            lens[t] = ok ? cnt - 1 : 0u;
-            idx[t] = make_uint2(0u, ok ? cnt - 1 : NONE32);
-            if (ok && cnt > 1) atomicAdd(total, (unsigned long long)(cnt - 1));
-            if (ok) atomicAdd(total + 1, 1ull);
-        } else if (ok) {
-            const uint32_t off = lens[t];
-            for (uint32_t k = 1; k < cnt; k++) pool[off + k - 1] = L[k];
-            idx[t].x = off;
+            lens[i] = pool_need(n);
+            if (ok) {
+                atomicAdd(total, (unsigned long long)pool_need(n));
+                atomicAdd(total + 1, 1ull);
+            }
+        } else {
+            if (!ok) {
+                idx[t] = make_uint4(NONE32, NONE32, NONE32, 0u);
+            } else {
+                const uint32_t off = pool_base + lens[i];
+                for (uint32_t k = 2; k < n; k++) pool[off + k - 2] = L[k + 1];
+                for (uint32_t k = n; k < pool_need(n) + 2 && k >= 2; k++) pool[off + k - 2] = NONE32;
+                idx[t] = make_uint4(n, n > 0 ? L[1] : NONE32, n > 1 ? L[2] : NONE32, off);
+            }
         }
 #else
         const uint32_t lane = threadIdx.x & 63u;
@@ -135,7 +148,7 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, uint2 *idx, uint32_t *l
                 while (m) {  // the new children in edge order, each once
                     const int lead = __ffsll((long long)m) - 1;
                     const uint32_t v = __shfl(c, lead);
-                    if (cnt == REACH_CAP) {
+                    if (cnt == R.cap) {
                         ok = false;
                         break;
                     }
@@ -148,23 +161,104 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, uint2 *idx, uint32_t *l
                 }
             }
         }
+        const uint32_t n = ok ? cnt - 1 : 0u;  // the reach without g: entry k is list entry k + 1
         if constexpr (!FILL) {
             if (lane == 0) {
-                lens[t] = ok ? cnt - 1 : 0u;
-                idx[t] = make_uint2(0u, ok ? cnt - 1 : NONE32);
-                if (ok && cnt > 1) atomicAdd(total, (unsigned long long)(cnt - 1));
-                if (ok) atomicAdd(total + 1, 1ull);
+                lens[i] = pool_need(n);
+                if (ok) {
+                    atomicAdd(total, (unsigned long long)pool_need(n));
+                    atomicAdd(total + 1, 1ull);
+                }
             }
-        } else if (ok) {
-            const uint32_t off = lens[t];  // (pass 1's counts, scanned)
-            if (lane >= 1 && lane < cnt) pool[off + lane - 1] = e0;
-            if (64 + lane < cnt) pool[off + 63 + lane] = e1;
-            if (lane == 0) idx[t].x = off;
+        } else {
+            const uint32_t x1 = __shfl(e0, 1), x2 = __shfl(e0, 2);
+            if (!ok) {
+                if (lane == 0) idx[t] = make_uint4(NONE32, NONE32, NONE32, 0u);
+            } else {
+                const uint32_t off = pool_base + lens[i], need = pool_need(n);
+                // list entry L = lane (e0) / 64 + lane (e1) is reach entry L - 1, pool slot L - 3
+                if (lane >= 3 && lane - 3 < need) pool[off + lane - 3] = lane <= n ? e0 : NONE32;
+                if (64 + lane - 3 < need) pool[off + 61 + lane] = 64 + lane <= n ? e1 : NONE32;
+                if (lane == 0) idx[t] = make_uint4(n, n > 0 ? x1 : NONE32, n > 1 ? x2 : NONE32, off);
+            }
         }
 #endif
     }
 }
 
+
+// a patch's ancestor walk: the parents (over subject-set rows: the reverse rows of the nodes as
+// subjects) of this level's nodes not seen yet, into the next level
+__global__ __launch_bounds__(RB) void k_anc_level(const uint32_t *front, uint32_t n, const uint32_t *rev_off, const uint32_t *rev_nodes,
+                                                  uint32_t n_uuids, uint32_t *seen, uint32_t *next, uint32_t *next_n, uint32_t cap) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t si = (uint64_t)n_uuids + front[i];
+        for (uint32_t j = rev_off[si], e = rev_off[si + 1]; j < e; j++) {
+            const uint32_t p = rev_nodes[j], bit = 1u << (p & 31u);
+            if (seen[p >> 5] & bit) continue;
+            if (atomicOr(&seen[p >> 5], bit) & bit) continue;
+            const uint32_t at = atomicAdd(next_n, 1u);
+            if (at < cap) next[at] = p;
+        }
+    }
+}
+__global__ __launch_bounds__(RB) void k_count_tabled(const uint4 *idx, uint64_t n, unsigned long long *out) {
+    unsigned long long c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        c += idx[i].x != NONE32;
+    if (c) atomicAdd(out, c);
+}
+// the candidates among nodes (tabled slots' nodes), compacted
+__global__ __launch_bounds__(RB) void k_cand_of(const uint32_t *nodes, uint32_t n, const NsDev *ns, uint32_t n_ns, const uint32_t *base,
+                                                uint32_t *out, uint32_t *out_n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = nodes[i];
+        const NsDev nd = ns[ns_of_node(ns, n_ns, c)];
+        const uint32_t b = base[nd.slot_base + (c - nd.node_base) % nd.n_slots];
+        if (b != NONE32) out[atomicAdd(out_n, 1u)] = b + (c - nd.node_base) / nd.n_slots;
+    }
+}
+}  // namespace
+
+namespace {
+// the tabled slots of s: base[global slot] = first candidate or NONE32, ts = {first candidate, ns,
+// slot, 0} per tabled slot; the candidate count (0: none, or past the index's range)
+uint64_t tabled_slots(Snapshot &s, std::vector<uint32_t> &base, std::vector<uint4> &ts) {
+    using build::DevBuf;
+    DevSnapshot &D = s.dev;
+    const uint32_t n_slots = (uint32_t)s.relinfo.size();
+    std::vector<uint32_t> target(n_slots, 0);
+    {
+        DevBuf flag(4ull * n_slots);
+        KETO_HIP(hipMemset(flag.p, 0, 4ull * n_slots));
+        const uint64_t ne = s.info.n_set_edges;
+        hipLaunchKernelGGL(k_slot_targets, dim3((uint32_t)std::min<uint64_t>(8192, (ne + RB - 1) / RB)), dim3(RB), 0, 0, D.set_dst,
+                           ne, D.edge_mask, D.ns, D.n_ns, flag.u32());
+        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemcpy(target.data(), flag.p, 4ull * n_slots, hipMemcpyDeviceToHost));
+    }
+    base.assign(n_slots, NONE32);
+    ts.clear();
+    uint64_t n_cand = 0;
+    for (uint32_t ns = 0; ns < s.n_ns; ns++)
+        for (uint32_t k = 0; k < s.ns[ns].n_slots; k++) {
+            const uint32_t g = s.ns[ns].slot_base + k, ri = s.relinfo[g];
+            if (!target[g] || !ri_setrows(ri) || ri_rw(ri) || ri_status(ri) == REL_ERROR) continue;
+            base[g] = (uint32_t)n_cand;
+            ts.push_back(make_uint4((uint32_t)n_cand, ns, k, 0));
+            n_cand += s.ns[ns + 1].ent_base - s.ns[ns].ent_base;
+            if (n_cand >= (1ull << 31)) return 0;  // (past the index's range: no tables)
+        }
+    return n_cand;
+}
+// RI_REACH on the tabled slots (a fresh relinfo copy: a patched snapshot may share its base's)
+void reach_bits(Snapshot &s, const std::vector<uint32_t> &base) {
+    for (size_t g = 0; g < s.relinfo.size(); g++)
+        s.relinfo[g] = (s.relinfo[g] & ~RI_REACH) | (g < base.size() && base[g] != NONE32 ? RI_REACH : 0u);
+    uint32_t *ri = static_cast<uint32_t *>(s.alloc(4 * std::max<size_t>(1, s.relinfo.size()) + 16));
+    if (!s.relinfo.empty()) KETO_HIP(hipMemcpy(ri, s.relinfo.data(), 4 * s.relinfo.size(), hipMemcpyHostToDevice));
+    s.dev.relinfo = ri;
+}
 }  // namespace
 
 // The tables of snapshot s (its rows, relation info and ns table are on the device); nothing
@@ -177,43 +271,35 @@ void build_reach(Snapshot &s) {
     D.reach_idx = nullptr;
     D.reach_pool = nullptr;
     s.info.n_reach = 0;
+    s.reach_slots.clear();
+    s.reach_cand = s.reach_pool_n = 0;
+    bool had = false;
+    for (uint32_t ri : s.relinfo) had |= (ri & RI_REACH) != 0;
+    if (had) reach_bits(s, {});
     static const bool off = [] {
         const char *e = getenv("KETO_NO_REACH");
         return e && *e == '1';
     }();
     const uint32_t n_slots = (uint32_t)s.relinfo.size();
     if (off || D.vkey || D.n_ns_x != D.n_ns || !n_slots || !s.info.n_set_edges) return;
-    std::vector<uint32_t> target(n_slots, 0);
-    {
-        DevBuf flag(4ull * n_slots);
-        KETO_HIP(hipMemset(flag.p, 0, 4ull * n_slots));
-        const uint64_t ne = s.info.n_set_edges;
-        hipLaunchKernelGGL(k_slot_targets, dim3((uint32_t)std::min<uint64_t>(8192, (ne + RB - 1) / RB)), dim3(RB), 0, 0, D.set_dst,
-                           ne, D.edge_mask, D.ns, D.n_ns, flag.u32());
-        KETO_HIP(hipGetLastError());
-        KETO_HIP(hipMemcpy(target.data(), flag.p, 4ull * n_slots, hipMemcpyDeviceToHost));
-    }
-    std::vector<uint32_t> base(n_slots, NONE32);
+    std::vector<uint32_t> base;
     std::vector<uint4> ts;
-    uint64_t n_cand = 0;
-    for (uint32_t ns = 0; ns < s.n_ns; ns++)
-        for (uint32_t k = 0; k < s.ns[ns].n_slots; k++) {
-            const uint32_t g = s.ns[ns].slot_base + k, ri = s.relinfo[g];
-            if (!target[g] || !ri_setrows(ri) || ri_rw(ri) || ri_status(ri) == REL_ERROR) continue;
-            base[g] = (uint32_t)n_cand;
-            ts.push_back(make_uint4((uint32_t)n_cand, ns, k, 0));
-            n_cand += s.ns[ns + 1].ent_base - s.ns[ns].ent_base;
-            if (n_cand >= (1ull << 31)) return;  // (past the index's range: no tables)
-        }
+    const uint64_t n_cand = tabled_slots(s, base, ts);
+    if (!n_cand) return;
     if (ts.empty()) return;
-    uint2 *idx = static_cast<uint2 *>(s.alloc(8 * n_cand + 16));
+    uint4 *idx = static_cast<uint4 *>(s.alloc(16 * n_cand + 16));
     DevBuf lens(4 * n_cand + 16), tot(16), d_ts(16 * ts.size());
     KETO_HIP(hipMemset(tot.p, 0, 16));
     KETO_HIP(hipMemcpy(d_ts.p, ts.data(), 16 * ts.size(), hipMemcpyHostToDevice));
+    static const uint32_t cap = [] {
+        const char *e = getenv("KETO_REACH_CAP");
+        const uint32_t c = e ? (uint32_t)atoi(e) : REACH_CAP;
+        return c >= 1 && c <= REACH_CAP_MAX ? c : REACH_CAP;
+    }();
     ReachIn R{D.set_row, D.set_dst, D.edge_mask, D.ns, D.n_ns, D.relinfo, static_cast<const uint4 *>(d_ts.p), (uint32_t)ts.size(),
-              n_cand};
+              n_cand, cap};
     const dim3 grid((uint32_t)std::min<uint64_t>(65536, (n_cand + RB / 64 - 1) / (RB / 64)));  // (4 waves a block)
-    hipLaunchKernelGGL(k_reach<false>, grid, dim3(RB), 0, 0, R, idx, lens.u32(), nullptr,
+    hipLaunchKernelGGL(k_reach<false>, grid, dim3(RB), 0, 0, R, nullptr, n_cand, idx, lens.u32(), nullptr, 0u,
                        static_cast<unsigned long long *>(tot.p));
     KETO_HIP(hipGetLastError());
     unsigned long long cn[2] = {0, 0};
@@ -222,7 +308,7 @@ void build_reach(Snapshot &s) {
     if (total >= (1ull << 31)) return;  // (the allocation of idx goes back with the snapshot)
     build::scan_excl(lens.u32(), n_cand);
     uint32_t *pool = static_cast<uint32_t *>(s.alloc(4 * total + 16));
-    hipLaunchKernelGGL(k_reach<true>, grid, dim3(RB), 0, 0, R, idx, lens.u32(), pool, nullptr);
+    hipLaunchKernelGGL(k_reach<true>, grid, dim3(RB), 0, 0, R, nullptr, n_cand, idx, lens.u32(), pool, 0u, nullptr);
     KETO_HIP(hipGetLastError());
     uint32_t *d_base = static_cast<uint32_t *>(s.alloc(4ull * n_slots + 16));
     KETO_HIP(hipMemcpy(d_base, base.data(), 4ull * n_slots, hipMemcpyHostToDevice));
@@ -231,6 +317,118 @@ void build_reach(Snapshot &s) {
     D.reach_idx = idx;
     D.reach_pool = pool;
     s.info.n_reach = cn[1];
+    reach_bits(s, base);
+    s.reach_slots = std::move(base);
+    s.reach_cand = n_cand;
+    s.reach_pool_n = total;
+}
+
+void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &touched_nodes) {
+    using build::DevBuf;
+    DevSnapshot &D = s.dev;
+    const DevSnapshot &Bd = B.dev;
+    if (!Bd.reach_idx || B.reach_slots.empty() || D.vkey || D.n_ns_x != D.n_ns) return build_reach(s);
+    std::vector<uint32_t> base;
+    std::vector<uint4> ts;
+    const uint64_t n_cand = tabled_slots(s, base, ts);
+    if (n_cand != B.reach_cand || base != B.reach_slots) return build_reach(s);  // (the tabled slots changed)
+    // the touched nodes and their ancestors within cap - 1 hops: a node farther from every
+    // touched node reaches one only over a path of more than cap nodes whose edges the patch left
+    // alone -- untabled before and after
+    static const uint32_t cap = [] {
+        const char *e = getenv("KETO_REACH_CAP");
+        const uint32_t c = e ? (uint32_t)atoi(e) : REACH_CAP;
+        return c >= 1 && c <= REACH_CAP_MAX ? c : REACH_CAP;
+    }();
+    constexpr uint32_t VCAP = 1u << 24;  // ancestors walked at most (more: rebuild whole)
+    const uint64_t words = ((uint64_t)D.n_nodes + 31) / 32;
+    DevBuf seen(4 * words + 16), lv(4ull * VCAP + 16), cnt(16);
+    KETO_HIP(hipMemset(seen.p, 0, 4 * words));
+    std::vector<uint32_t> t0(touched_nodes);
+    std::sort(t0.begin(), t0.end());
+    t0.erase(std::unique(t0.begin(), t0.end()), t0.end());
+    if (t0.size() > VCAP) return build_reach(s);
+    uint32_t *all = lv.u32();
+    if (!t0.empty()) KETO_HIP(hipMemcpy(all, t0.data(), 4 * t0.size(), hipMemcpyHostToDevice));
+    uint64_t total = t0.size(), lo = 0;
+    {   // the touched nodes are seen (their bits, word by word)
+        std::vector<std::pair<uint64_t, uint32_t>> wb;
+        for (uint32_t k : t0) wb.emplace_back(k >> 5, 1u << (k & 31u));
+        std::sort(wb.begin(), wb.end());
+        std::vector<uint32_t> widx, wval;
+        for (auto &x : wb) {
+            if (!widx.empty() && widx.back() == x.first) wval.back() |= x.second;
+            else {
+                widx.push_back((uint32_t)x.first);
+                wval.push_back(x.second);
+            }
+        }
+        for (size_t i = 0; i < widx.size(); i++)
+            KETO_HIP(hipMemcpy(seen.u32() + widx[i], &wval[i], 4, hipMemcpyHostToDevice));
+    }
+    for (uint32_t level = 1; level < cap && lo < total; level++) {
+        const uint64_t n = total - lo;
+        KETO_HIP(hipMemset(cnt.p, 0, 4));
+        hipLaunchKernelGGL(k_anc_level, dim3((uint32_t)std::min<uint64_t>(4096, (n + RB - 1) / RB)), dim3(RB), 0, 0, all + lo, (uint32_t)n,
+                           D.rev_off, D.rev_nodes, D.n_uuids, seen.u32(), all + total, cnt.u32(), (uint32_t)(VCAP - total));
+        KETO_HIP(hipGetLastError());
+        uint32_t got = 0;
+        KETO_HIP(hipMemcpy(&got, cnt.p, 4, hipMemcpyDeviceToHost));
+        if (total + got > VCAP) return build_reach(s);
+        lo = total;
+        total += got;
+    }
+    // their candidates, walked again into a copy of the base's tables with the new lists appended
+    DevBuf cl(4 * total + 16), d_base(4ull * base.size() + 16), d_ts(16 * ts.size()), lens(4 * total + 16), tot(16);
+    KETO_HIP(hipMemcpy(d_base.p, base.data(), 4ull * base.size(), hipMemcpyHostToDevice));
+    KETO_HIP(hipMemcpy(d_ts.p, ts.data(), 16 * ts.size(), hipMemcpyHostToDevice));
+    KETO_HIP(hipMemset(cnt.p, 0, 4));
+    KETO_HIP(hipMemset(tot.p, 0, 16));
+    if (total)
+        hipLaunchKernelGGL(k_cand_of, dim3((uint32_t)std::min<uint64_t>(4096, (total + RB - 1) / RB)), dim3(RB), 0, 0, all, (uint32_t)total,
+                           D.ns, D.n_ns, d_base.u32(), cl.u32(), cnt.u32());
+    KETO_HIP(hipGetLastError());
+    uint32_t nc = 0;
+    KETO_HIP(hipMemcpy(&nc, cnt.p, 4, hipMemcpyDeviceToHost));
+    ReachIn R{D.set_row, D.set_dst, D.edge_mask, D.ns, D.n_ns, D.relinfo, static_cast<const uint4 *>(d_ts.p), (uint32_t)ts.size(),
+              n_cand, cap};
+    const dim3 grid((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, ((uint64_t)nc + RB / 64 - 1) / (RB / 64))));
+    uint4 *idx = static_cast<uint4 *>(s.alloc(16 * n_cand + 16));
+    KETO_HIP(hipMemcpy(idx, Bd.reach_idx, 16 * n_cand, hipMemcpyDeviceToDevice));
+    if (nc) {
+        hipLaunchKernelGGL(k_reach<false>, grid, dim3(RB), 0, 0, R, cl.u32(), (uint64_t)nc, idx, lens.u32(), nullptr, 0u,
+                           static_cast<unsigned long long *>(tot.p));
+        KETO_HIP(hipGetLastError());
+    }
+    unsigned long long cn[2] = {0, 0};
+    KETO_HIP(hipMemcpy(cn, tot.p, 16, hipMemcpyDeviceToHost));
+    const uint64_t pool_n = B.reach_pool_n + cn[0];
+    if (pool_n >= (1ull << 31)) return build_reach(s);
+    if (nc) build::scan_excl(lens.u32(), nc);
+    uint32_t *pool = static_cast<uint32_t *>(s.alloc(4 * pool_n + 16));
+    if (B.reach_pool_n) KETO_HIP(hipMemcpy(pool, Bd.reach_pool, 4 * B.reach_pool_n, hipMemcpyDeviceToDevice));
+    if (nc) {
+        hipLaunchKernelGGL(k_reach<true>, grid, dim3(RB), 0, 0, R, cl.u32(), (uint64_t)nc, idx, lens.u32(), pool,
+                           (uint32_t)B.reach_pool_n, nullptr);
+        KETO_HIP(hipGetLastError());
+    }
+    uint32_t *db = static_cast<uint32_t *>(s.alloc(4ull * base.size() + 16));
+    KETO_HIP(hipMemcpy(db, base.data(), 4ull * base.size(), hipMemcpyHostToDevice));
+    KETO_HIP(hipStreamSynchronize(nullptr));
+    D.reach_base = db;
+    D.reach_idx = idx;
+    D.reach_pool = pool;
+    reach_bits(s, base);
+    s.reach_slots = std::move(base);
+    s.reach_cand = n_cand;
+    s.reach_pool_n = pool_n;
+    KETO_HIP(hipMemset(cnt.p, 0, 8));
+    hipLaunchKernelGGL(k_count_tabled, dim3((uint32_t)std::min<uint64_t>(4096, (n_cand + RB - 1) / RB)), dim3(RB), 0, 0, idx, n_cand,
+                       static_cast<unsigned long long *>(cnt.p));
+    KETO_HIP(hipGetLastError());
+    unsigned long long nt = 0;
+    KETO_HIP(hipMemcpy(&nt, cnt.p, 8, hipMemcpyDeviceToHost));
+    s.info.n_reach = nt;
 }
 
 }  // namespace keto

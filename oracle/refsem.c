@@ -30,6 +30,7 @@
 #include <string.h>
 
 #define MAX_RECURSION 4096
+#define REACH_CAP_MAX 128 /* u_reach_prunes: RS_REACH_CAP (A/B runs; the product's KETO_REACH_CAP), default 32 */
 
 typedef struct {
     uint32_t ns, obj, rel, kind, sid, sns, srel;
@@ -52,6 +53,7 @@ struct rs_db {
     uint8_t *sstarget; /* [n_ns * n_relnames]: some tuple's subject set is a (ns, ., rel) */
     int32_t aliased;   /* two relation slots share a visited class (the engine's vkey table) */
     int32_t no_reach;  /* rs_set_reach(db, 0) / RS_NO_REACH=1: the engine built without tables */
+    uint32_t reach_cap;
     uint32_t n_ns, n_relnames, empty_rel, n_rels, n_ast, n_children;
     int32_t strict, max_depth, max_width;
 };
@@ -354,6 +356,9 @@ rs_db *rs_build(const rs_tuple *tuples, size_t n, const rs_config *cfg) {
     free(slot);
     const char *nr = getenv("RS_NO_REACH"); /* (the product's KETO_NO_REACH=1) */
     db->no_reach = nr && *nr == '1';
+    const char *rc = getenv("RS_REACH_CAP");
+    db->reach_cap = rc ? (uint32_t)atoi(rc) : 32;
+    if (db->reach_cap < 1 || db->reach_cap > REACH_CAP_MAX) db->reach_cap = 32;
     return db;
 }
 
@@ -1223,8 +1228,7 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
         *out = R_IS;
         return 0;
     }
-    if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && (!node_check || node_has_set_rows(db, ns, obj, rel)) &&
-        !u_reach_prunes(u, ns, obj, rel)) {
+    if (can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && (!node_check || node_has_set_rows(db, ns, obj, rel))) {
         if (!u_spawn(u, gen + 1)) return 0;
         *out = u_es(u, ns, obj, rel, d - 1, scope, gen + 1, 1);
         return 1;
@@ -1236,14 +1240,14 @@ static int u_sub(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int sk
 /* Reachability pruning (csrc/reach.hip; the engine's REACH_CAP).  Reach(n) = n and every node
  * reachable from it over subject-set rows.  A node n is "tabled" when its relation slot is pure
  * (no rewrite, no ASTRelationFor error), holds subject-set rows and is some tuple's subject-set
- * relation, every node of Reach(n) is pure, and |Reach(n)| <= REACH_CAP -- and the snapshot has no
- * aliased visited keys.  Then checkIsAllowed(n, d > 1) can only be IsMember through a node of
- * Reach(n) whose own row holds the subject: with none, it is NotMember whatever the visited set
- * and depth do (a pure node yields IsMember or NotMember, never an error or a bare Unknown, at
- * d > 1), and no key of Reach(n) can be a decisive occurrence for this subject anywhere in the
+ * relation, every node of Reach(n) is pure, and |Reach(n)| <= reach_cap -- and the snapshot has no
+ * aliased visited keys.  Then checkExpandSubject(n, d >= 1) can only be IsMember through a node of
+ * Reach(n) \ {n} whose own row holds the subject: with none, it is NotMember whatever the visited
+ * set and depth do (a pure node yields IsMember or NotMember, never an error or a bare Unknown,
+ * at d > 1), and no key below n can be a decisive occurrence for this subject anywhere in the
  * query (each such node's own reach is inside Reach(n)), so no routing decision depends on
- * them.  The engine decides such a sub-check NotMember where it is spawned (no goal). */
-#define REACH_CAP 128
+ * them.  The engine's expand-subject goal on such a node decides NotMember at once: no scope, no
+ * children (u_es). */
 static int rel_pure(const rs_db *db, uint32_t ns, uint32_t rel) {
     int err;
     const int ri = ast_relation_for(db, ns, rel, &err);
@@ -1255,7 +1259,7 @@ static int u_reach_prunes(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel) {
     if (db->no_reach || db->aliased || ns >= db->n_ns || rel >= db->n_relnames) return 0;
     const size_t nr = (size_t)ns * db->n_relnames + rel;
     if (!db->ssrel[nr] || !db->sstarget[nr] || !rel_pure(db, ns, rel)) return 0;
-    uint32_t lst[REACH_CAP][3];
+    uint32_t lst[REACH_CAP_MAX][3];
     uint32_t cnt = 1, head = 0;
     lst[0][0] = ns;
     lst[0][1] = obj;
@@ -1272,14 +1276,14 @@ static int u_reach_prunes(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel) {
             int dup = 0;
             for (uint32_t k = 0; k < cnt && !dup; k++) dup = lst[k][0] == t->sns && lst[k][1] == t->sid && lst[k][2] == t->srel;
             if (dup) continue;
-            if (cnt == REACH_CAP) return 0;
+            if (cnt == db->reach_cap) return 0;
             lst[cnt][0] = t->sns;
             lst[cnt][1] = t->sid;
             lst[cnt][2] = t->srel;
             cnt++;
         }
     }
-    for (uint32_t k = 0; k < cnt; k++)
+    for (uint32_t k = 1; k < cnt; k++) /* (n's own row: the expand-subject never reads it) */
         if (exists(u->c, lst[k][0], lst[k][1], lst[k][2])) return 0;
     return 1;
 }
@@ -1295,7 +1299,7 @@ static int u_sub_spawns(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d,
     if (err) return 0;
     const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
     if (!skip && d - 1 > 0 && exists(u->c, ns, obj, rel)) return 0;
-    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && !u_reach_prunes(u, ns, obj, rel);
+    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel);
 }
 
 /* A NOT whose operand is decided where it is spawned -- a malformed NOT, a computed userset
@@ -1588,8 +1592,7 @@ static int u_es_child_is_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, in
     const int ri = ast_relation_for(db, ns, rel, &err);
     if (err || (ri >= 0 && db->rels[ri].rewrite >= 0)) return 0; /* an IA goal */
     const int can_ss = !db->strict || ri < 0 || db->rels[ri].has_ss_type;
-    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && node_has_set_rows(db, ns, obj, rel) &&
-           !u_reach_prunes(u, ns, obj, rel);
+    return can_ss && d - 1 > 0 && has_set_rows(db, ns, rel) && node_has_set_rows(db, ns, obj, rel);
 }
 
 /* chain: an expand-subject whose row holds exactly one subject set, kept, that would be an ES
@@ -1600,6 +1603,8 @@ static int u_es_child_is_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, in
  * (csrc/frontier.hip G_ES "chain") */
 static res u_es(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, uint32_t scope, uint32_t gen, int chain) {
     const rs_db *db = u->c->db;
+    /* a goal of its own (chain: not the chained child run inside its parent's goal): the reach */
+    if (chain && node_has_set_rows(db, ns, obj, rel) && u_reach_prunes(u, ns, obj, rel)) return R_NOT;
     size_t lo, hi;
     node_rows(db, ns, obj, rel, &lo, &hi);
     size_t nres = 0;
@@ -1657,8 +1662,7 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
     res rr = R_NOT, er = R_NOT;
     if (has_rewrite && u_spawn(u, gen + 1)) rr = u_rw(u, ns, obj, db->rels[ri].rewrite, d, scope, gen + 1);
     const int direct_is = (!db->strict || !has_rewrite) && !skip && d - 1 > 0 && exists(u->c, ns, obj, rel);
-    if (can_ss && !direct_is && d - 1 > 0 && has_set_rows(db, ns, rel) && !u_reach_prunes(u, ns, obj, rel) &&
-        u_spawn(u, gen + 1))
+    if (can_ss && !direct_is && d - 1 > 0 && has_set_rows(db, ns, rel) && u_spawn(u, gen + 1))
         er = u_es(u, ns, obj, rel, d - 1, scope, gen + 1, 1);
     if (decisive(rr)) return rr;
     if (direct_is) return R_IS;

