@@ -189,13 +189,18 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
 
 // a patch's ancestor walk: the parents (over subject-set rows: the reverse rows of the nodes as
 // subjects) of this level's nodes not seen yet, into the next level
+// (only parents in tabled slots: every node of a tabled reach but its root is some row's subject
+// set, pure, with subject-set rows -- a node of a tabled slot)
 __global__ __launch_bounds__(RB) void k_anc_level(const uint32_t *front, uint32_t n, const uint32_t *rev_off, const uint32_t *rev_nodes,
-                                                  uint32_t n_uuids, uint32_t *seen, uint32_t *next, uint32_t *next_n, uint32_t cap) {
+                                                  uint32_t n_uuids, const NsDev *ns, uint32_t n_ns, const uint32_t *relinfo,
+                                                  uint32_t *seen, uint32_t *next, uint32_t *next_n, uint32_t cap) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t si = (uint64_t)n_uuids + front[i];
         for (uint32_t j = rev_off[si], e = rev_off[si + 1]; j < e; j++) {
             const uint32_t p = rev_nodes[j], bit = 1u << (p & 31u);
             if (seen[p >> 5] & bit) continue;
+            const NsDev nd = ns[ns_of_node(ns, n_ns, p)];
+            if (!(relinfo[nd.slot_base + (p - nd.node_base) % nd.n_slots] & RI_REACH)) continue;
             if (atomicOr(&seen[p >> 5], bit) & bit) continue;
             const uint32_t at = atomicAdd(next_n, 1u);
             if (at < cap) next[at] = p;
@@ -366,11 +371,16 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
         for (size_t i = 0; i < widx.size(); i++)
             KETO_HIP(hipMemcpy(seen.u32() + widx[i], &wval[i], 4, hipMemcpyHostToDevice));
     }
+    std::vector<uint32_t> ri(s.relinfo);  // (the slot flags of the new tables, before reach_bits sets them)
+    for (size_t g = 0; g < ri.size(); g++) ri[g] = (ri[g] & ~RI_REACH) | (base[g] != NONE32 ? RI_REACH : 0u);
+    DevBuf d_ri(4 * std::max<size_t>(1, ri.size()) + 16);
+    if (!ri.empty()) KETO_HIP(hipMemcpy(d_ri.p, ri.data(), 4 * ri.size(), hipMemcpyHostToDevice));
     for (uint32_t level = 1; level < cap && lo < total; level++) {
         const uint64_t n = total - lo;
         KETO_HIP(hipMemset(cnt.p, 0, 4));
         hipLaunchKernelGGL(k_anc_level, dim3((uint32_t)std::min<uint64_t>(4096, (n + RB - 1) / RB)), dim3(RB), 0, 0, all + lo, (uint32_t)n,
-                           D.rev_off, D.rev_nodes, D.n_uuids, seen.u32(), all + total, cnt.u32(), (uint32_t)(VCAP - total));
+                           D.rev_off, D.rev_nodes, D.n_uuids, D.ns, D.n_ns, d_ri.u32(), seen.u32(), all + total, cnt.u32(),
+                           (uint32_t)(VCAP - total));
         KETO_HIP(hipGetLastError());
         uint32_t got = 0;
         KETO_HIP(hipMemcpy(&got, cnt.p, 4, hipMemcpyDeviceToHost));

@@ -192,7 +192,8 @@ def lib():
         if L.keto_abi_version() != ABI_VERSION:
             raise RuntimeError("libketo_mi355x ABI version mismatch")
         _lib = L
-        atexit.register(_shutdown)
+        if not os.environ.get("KETO_MI355X_NO_TEARDOWN"):  # (tools/exit_probe.py "leak": diagnostics only)
+            atexit.register(_shutdown)
     return _lib
 
 
