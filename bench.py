@@ -55,7 +55,7 @@ def lib_sha256():
 
 
 def committed_traffic(workload: str, kname: str):
-    """HBM bytes per tier-0 launch from the newest committed PMC passes (tools/pmc_traffic.sh ->
+    """HBM bytes per tier-0 launch from the newest committed PMC passes (tools/gpu_round.sh OUT traffic ->
     profiles/r*_traffic_<workload>.json) -- only if they profiled THIS library build (sha256 of
     libketo_mi355x.so); a kernel change makes the figure stale and it is dropped (null)."""
     tf = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{workload}.json")))

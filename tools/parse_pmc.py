@@ -1,5 +1,5 @@
 """Per-launch FETCH_SIZE / WRITE_SIZE of bench.py's dominant kernel (tier-0 launches of the
-uncounted Check interpreter) from tools/pmc_traffic.sh output -> JSON for bench.py."""
+uncounted Check interpreter) from tools/gpu_round.sh OUT traffic output -> JSON for bench.py."""
 import csv
 import glob
 import hashlib

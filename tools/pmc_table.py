@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc passes (tools/prof_pmc.sh output) per kernel: counter sums per
+"""Summarise rocprofv3 --pmc passes (rocprofv3 --pmc output) per kernel: counter sums per
 dispatch for the Check interpreters' tier-0 launches.  usage: pmc_table.py gpurun_out/pmc_c2"""
 import csv
 import glob
