@@ -16,9 +16,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
+#include "device_common.hpp"
 #include "engine.hpp"
 
 namespace keto {
@@ -54,15 +57,31 @@ __device__ __forceinline__ bool node_pure(const ReachIn &R, uint32_t node) {
     return ri_status(ri) != REL_ERROR && !ri_rw(ri);
 }
 
-// slots some subject-set edge points into
+// slots some subject-set edge points into: the ns table and the flags in LDS when they fit (one
+// global store per flag and block), else straight to memory
+constexpr uint32_t T_NS = 256, T_FLAGS = 4096;
 __global__ __launch_bounds__(RB) void k_slot_targets(const uint32_t *set_dst, uint64_t n, uint32_t edge_mask, const NsDev *ns,
-                                                     uint32_t n_ns, uint32_t *flag) {
+                                                     uint32_t n_ns, uint32_t *flag, uint32_t n_flags) {
+    __shared__ NsDev lns[T_NS + 1];
+    __shared__ uint32_t lf[T_FLAGS];
+    const bool lt = n_ns < T_NS, lfl = n_flags <= T_FLAGS;
+    if (lt)
+        for (uint32_t t = threadIdx.x; t <= n_ns; t += blockDim.x) lns[t] = ns[t];
+    if (lfl)
+        for (uint32_t t = threadIdx.x; t < n_flags; t += blockDim.x) lf[t] = 0;
+    __syncthreads();
+    const NsDev *nst = lt ? lns : ns;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t c = set_dst[i] & edge_mask;
-        const NsDev nd = ns[ns_of_node(ns, n_ns, c)];
+        const NsDev nd = nst[ns_of_node(nst, n_ns, c)];
         const uint32_t g = nd.slot_base + (c - nd.node_base) % nd.n_slots;
-        if (!flag[g]) atomicOr(&flag[g], 1u);  // (read first: most edges find the flag set)
+        if (lfl) lf[g] = 1;
+        else if (!flag[g]) atomicOr(&flag[g], 1u);  // (read first: most edges find the flag set)
     }
+    if (!lfl) return;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n_flags; t += blockDim.x)
+        if (lf[t] && !flag[t]) flag[t] = 1;
 }
 
 // One wave per candidate node: a breadth-first walk of its reach with the list in registers
@@ -188,20 +207,36 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
 
 
 // a patch's ancestor walk: the parents (over subject-set rows: the reverse rows of the nodes as
-// subjects) of this level's nodes not seen yet, into the next level
+// subjects) of this level's nodes not seen yet, into the next level.  seen: open addressing over
+// node + 1 (0 = empty), a power-of-two table the caller sizes past twice the walk's bound
 // (only parents in tabled slots: every node of a tabled reach but its root is some row's subject
 // set, pure, with subject-set rows -- a node of a tabled slot)
+__device__ __forceinline__ bool seen_insert(uint32_t *seen, uint32_t mask, uint32_t node) {
+    const uint32_t key = node + 1u;
+    for (uint32_t h = (uint32_t)mix64(key) & mask;; h = (h + 1) & mask) {
+        const uint32_t v = seen[h];
+        if (v == key) return false;
+        if (v == 0) {
+            const uint32_t o = atomicCAS(&seen[h], 0u, key);
+            if (o == 0) return true;
+            if (o == key) return false;
+        }
+    }
+}
+__global__ __launch_bounds__(RB) void k_seen_init(const uint32_t *nodes, uint32_t n, uint32_t *seen, uint32_t mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        (void)seen_insert(seen, mask, nodes[i]);
+}
 __global__ __launch_bounds__(RB) void k_anc_level(const uint32_t *front, uint32_t n, const uint32_t *rev_off, const uint32_t *rev_nodes,
                                                   uint32_t n_uuids, const NsDev *ns, uint32_t n_ns, const uint32_t *relinfo,
-                                                  uint32_t *seen, uint32_t *next, uint32_t *next_n, uint32_t cap) {
+                                                  uint32_t *seen, uint32_t mask, uint32_t *next, uint32_t *next_n, uint32_t cap) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t si = (uint64_t)n_uuids + front[i];
         for (uint32_t j = rev_off[si], e = rev_off[si + 1]; j < e; j++) {
-            const uint32_t p = rev_nodes[j], bit = 1u << (p & 31u);
-            if (seen[p >> 5] & bit) continue;
+            const uint32_t p = rev_nodes[j];
             const NsDev nd = ns[ns_of_node(ns, n_ns, p)];
             if (!(relinfo[nd.slot_base + (p - nd.node_base) % nd.n_slots] & RI_REACH)) continue;
-            if (atomicOr(&seen[p >> 5], bit) & bit) continue;
+            if (!seen_insert(seen, mask, p)) continue;
             const uint32_t at = atomicAdd(next_n, 1u);
             if (at < cap) next[at] = p;
         }
@@ -237,8 +272,8 @@ uint64_t tabled_slots(Snapshot &s, std::vector<uint32_t> &base, std::vector<uint
         DevBuf flag(4ull * n_slots);
         KETO_HIP(hipMemset(flag.p, 0, 4ull * n_slots));
         const uint64_t ne = s.info.n_set_edges;
-        hipLaunchKernelGGL(k_slot_targets, dim3((uint32_t)std::min<uint64_t>(8192, (ne + RB - 1) / RB)), dim3(RB), 0, 0, D.set_dst,
-                           ne, D.edge_mask, D.ns, D.n_ns, flag.u32());
+        hipLaunchKernelGGL(k_slot_targets, dim3((uint32_t)std::min<uint64_t>(2048, (ne + RB - 1) / RB)), dim3(RB), 0, 0, D.set_dst,
+                           ne, D.edge_mask, D.ns, D.n_ns, flag.u32(), n_slots);
         KETO_HIP(hipGetLastError());
         KETO_HIP(hipMemcpy(target.data(), flag.p, 4ull * n_slots, hipMemcpyDeviceToHost));
     }
@@ -330,6 +365,15 @@ void build_reach(Snapshot &s) {
 
 void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &touched_nodes) {
     using build::DevBuf;
+    static const bool verbose = getenv("KETO_PATCH_VERBOSE") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto phase = [&](const char *what) {  // KETO_PATCH_VERBOSE: the walk's parts
+        if (!verbose) return;
+        KETO_HIP(hipDeviceSynchronize());
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[keto patch]     reach %-10s %.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
     DevSnapshot &D = s.dev;
     const DevSnapshot &Bd = B.dev;
     if (!Bd.reach_idx || B.reach_slots.empty() || D.vkey || D.n_ns_x != D.n_ns) return build_reach(s);
@@ -337,6 +381,7 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
     std::vector<uint4> ts;
     const uint64_t n_cand = tabled_slots(s, base, ts);
     if (n_cand != B.reach_cand || base != B.reach_slots) return build_reach(s);  // (the tabled slots changed)
+    phase("slots");
     // the touched nodes and their ancestors within cap - 1 hops: a node farther from every
     // touched node reaches one only over a path of more than cap nodes whose edges the patch left
     // alone -- untabled before and after
@@ -345,32 +390,24 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
         const uint32_t c = e ? (uint32_t)atoi(e) : REACH_CAP;
         return c >= 1 && c <= REACH_CAP_MAX ? c : REACH_CAP;
     }();
-    constexpr uint32_t VCAP = 1u << 24;  // ancestors walked at most (more: rebuild whole)
-    const uint64_t words = ((uint64_t)D.n_nodes + 31) / 32;
-    DevBuf seen(4 * words + 16), lv(4ull * VCAP + 16), cnt(16);
-    KETO_HIP(hipMemset(seen.p, 0, 4 * words));
+    // (the walk's nodes at most VCAP -- more: rebuild whole; a hash set of 4 VCAP slots, 4 MB +
+    // a 2 MB level list: no allocation that grows with the graph)
+    constexpr uint32_t VCAP = 1u << 19;
     std::vector<uint32_t> t0(touched_nodes);
     std::sort(t0.begin(), t0.end());
     t0.erase(std::unique(t0.begin(), t0.end()), t0.end());
-    if (t0.size() > VCAP) return build_reach(s);
+    if (t0.size() > VCAP / 2) return build_reach(s);
+    DevBuf seen(16ull * VCAP + 16), lv(4ull * VCAP + 16), cnt(16);
+    KETO_HIP(hipMemset(seen.p, 0, 16ull * VCAP));
+    const uint32_t mask = 4 * VCAP - 1;
     uint32_t *all = lv.u32();
-    if (!t0.empty()) KETO_HIP(hipMemcpy(all, t0.data(), 4 * t0.size(), hipMemcpyHostToDevice));
-    uint64_t total = t0.size(), lo = 0;
-    {   // the touched nodes are seen (their bits, word by word)
-        std::vector<std::pair<uint64_t, uint32_t>> wb;
-        for (uint32_t k : t0) wb.emplace_back(k >> 5, 1u << (k & 31u));
-        std::sort(wb.begin(), wb.end());
-        std::vector<uint32_t> widx, wval;
-        for (auto &x : wb) {
-            if (!widx.empty() && widx.back() == x.first) wval.back() |= x.second;
-            else {
-                widx.push_back((uint32_t)x.first);
-                wval.push_back(x.second);
-            }
-        }
-        for (size_t i = 0; i < widx.size(); i++)
-            KETO_HIP(hipMemcpy(seen.u32() + widx[i], &wval[i], 4, hipMemcpyHostToDevice));
+    if (!t0.empty()) {
+        KETO_HIP(hipMemcpy(all, t0.data(), 4 * t0.size(), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_seen_init, dim3((uint32_t)std::min<uint64_t>(1024, (t0.size() + RB - 1) / RB)), dim3(RB), 0, 0, all,
+                           (uint32_t)t0.size(), seen.u32(), mask);
+        KETO_HIP(hipGetLastError());
     }
+    uint64_t total = t0.size(), lo = 0;
     std::vector<uint32_t> ri(s.relinfo);  // (the slot flags of the new tables, before reach_bits sets them)
     for (size_t g = 0; g < ri.size(); g++) ri[g] = (ri[g] & ~RI_REACH) | (base[g] != NONE32 ? RI_REACH : 0u);
     DevBuf d_ri(4 * std::max<size_t>(1, ri.size()) + 16);
@@ -379,7 +416,7 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
         const uint64_t n = total - lo;
         KETO_HIP(hipMemset(cnt.p, 0, 4));
         hipLaunchKernelGGL(k_anc_level, dim3((uint32_t)std::min<uint64_t>(4096, (n + RB - 1) / RB)), dim3(RB), 0, 0, all + lo, (uint32_t)n,
-                           D.rev_off, D.rev_nodes, D.n_uuids, D.ns, D.n_ns, d_ri.u32(), seen.u32(), all + total, cnt.u32(),
+                           D.rev_off, D.rev_nodes, D.n_uuids, D.ns, D.n_ns, d_ri.u32(), seen.u32(), mask, all + total, cnt.u32(),
                            (uint32_t)(VCAP - total));
         KETO_HIP(hipGetLastError());
         uint32_t got = 0;
@@ -388,6 +425,7 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
         lo = total;
         total += got;
     }
+    phase("ancestors");
     // their candidates, walked again into a copy of the base's tables with the new lists appended
     DevBuf cl(4 * total + 16), d_base(4ull * base.size() + 16), d_ts(16 * ts.size()), lens(4 * total + 16), tot(16);
     KETO_HIP(hipMemcpy(d_base.p, base.data(), 4ull * base.size(), hipMemcpyHostToDevice));
@@ -422,6 +460,9 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
                            (uint32_t)B.reach_pool_n, nullptr);
         KETO_HIP(hipGetLastError());
     }
+    if (verbose) fprintf(stderr, "[keto patch]     reach: %zu touched nodes, %llu with ancestors, %u tabled walked again\n", t0.size(),
+                         (unsigned long long)total, nc);
+    phase("walks");
     uint32_t *db = static_cast<uint32_t *>(s.alloc(4ull * base.size() + 16));
     KETO_HIP(hipMemcpy(db, base.data(), 4ull * base.size(), hipMemcpyHostToDevice));
     KETO_HIP(hipStreamSynchronize(nullptr));

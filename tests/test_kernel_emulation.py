@@ -27,7 +27,8 @@ def test_one_transition_per_step_matches_oracle(tmp_path):
     env = dict(os.environ, KETO_MI355X_ALLOW_OVERRIDE="tools", KETO_MI355X_LIB_OVERRIDE=str(lib))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
                         os.path.join(ROOT, "tests", "test_gpu_parity.py"), os.path.join(ROOT, "tests", "test_gpu_frontier.py"),
-                        "-k", "golden or random_worlds or synthetic_small or frontier or routed"],
+                        os.path.join(ROOT, "tests", "test_gpu_reach.py"),
+                        "-k", "golden or random_worlds or synthetic_small or frontier or routed or reach"],
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert " passed" in r.stdout
