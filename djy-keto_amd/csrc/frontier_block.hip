@@ -264,8 +264,9 @@ __global__ __launch_bounds__(BB, KETO_FRB_WAVES) void fr_block(BlockParams P) {
                     if (!(ts & VIRT_BIT)) rnode = ts;
                 }
                 const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
+                const uint4 rrec = (live && kind == G_ES) ? reach_record(s, T, node) : make_uint4(NONE32, NONE32, NONE32, 0);
                 const Subject q = live ? subject_of(C.start[2 * pos + 1]) : Subject{0, false, make_uint4(0, 0, 0, 0)};
-                const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W);
+                const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W, rrec);
                 uint32_t nc = pa.nc;
                 // routing: a row too long for the record, a routed query, the generation cap, a goal
                 // with more children than the budget, and the query's goal count past the budget
