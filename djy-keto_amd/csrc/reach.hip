@@ -96,6 +96,7 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
     static_assert(REACH_CAP_MAX <= 128, "two list registers per lane");
     const uint32_t wpb = blockDim.x >= 64 ? blockDim.x / 64 : 1;  // (the CPU emulation: one-lane blocks)
     const uint64_t nw = (uint64_t)gridDim.x * wpb;
+    unsigned long long acc_pool = 0, acc_tabled = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * wpb + threadIdx.x / 64; i < n_items; i += nw) {
         const uint64_t t = list ? list[i] : i;
         uint32_t lo = 0, hi = R.n_tslots;  // the candidate's slot
@@ -133,8 +134,8 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
         if constexpr (!FILL) {
             lens[i] = pool_need(n);
             if (ok) {
-                atomicAdd(total, (unsigned long long)pool_need(n));
-                atomicAdd(total + 1, 1ull);
+                acc_pool += pool_need(n);
+                acc_tabled++;
             }
         } else {
             if (!ok) {
@@ -182,12 +183,10 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
         }
         const uint32_t n = ok ? cnt - 1 : 0u;  // the reach without g: entry k is list entry k + 1
         if constexpr (!FILL) {
-            if (lane == 0) {
-                lens[i] = pool_need(n);
-                if (ok) {
-                    atomicAdd(total, (unsigned long long)pool_need(n));
-                    atomicAdd(total + 1, 1ull);
-                }
+            if (lane == 0) lens[i] = pool_need(n);
+            if (ok) {  // (summed per wave, added once at the end: same-address atomics serialise)
+                acc_pool += pool_need(n);
+                acc_tabled++;
             }
         } else {
             const uint32_t x1 = __shfl(e0, 1), x2 = __shfl(e0, 2);
@@ -202,6 +201,12 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
             }
         }
 #endif
+    }
+    if constexpr (!FILL) {
+        if ((threadIdx.x & 63u) == 0 && acc_tabled) {
+            atomicAdd(total, acc_pool);
+            atomicAdd(total + 1, acc_tabled);
+        }
     }
 }
 
