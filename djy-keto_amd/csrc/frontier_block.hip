@@ -194,7 +194,7 @@ __global__ __launch_bounds__(BB, KETO_FRB_WAVES) void fr_block(BlockParams P) {
             const uint32_t d = r0.z & 0xFFFFu;
             C.qcnt[t] = 1;
             C.qrt[t] = d > GD_MAX ? 1u : 0u;  // deeper than a goal word holds: the interpreter
-            C.gbuf[0][t] = make_uint4(r0.x, t, gword(G_IA, d), NONE32);
+            C.gbuf[0][t] = make_uint4(r0.x, t, root_word(s, T, subject_of(r1), r0.x, d), NONE32);
         }
         if (tid == 0) {
             C.gs[0] = 0;

@@ -167,10 +167,18 @@ __global__ __launch_bounds__(DBLK) void k_arrive(FrontierParams P, const uint4 *
             subj[pos] = make_uint2(r0.z, r0.w);
             home[pos] = r1.z;
             P.qspawn[pos] = 0;
+            // an IA record shaped here as its sender would have shaped a local sub-check (frontier_goal.inc
+            // sub_check): a rewrite with neither a direct check nor an expand-subject to run is its RW
+            // goal -- one generation less per remote hop (Drive's parents.traverse(view))
+            uint32_t w = r1.x;
+            if (((w >> 12) & 7u) == G_IA && !(w & (GF_FOUND | GF_PROBE | GF_ESCHILD | GF_ALIAS)) && (w & GD_MAX) >= 1) {
+                const uint32_t sw = sub_check(s, T, subject_of(R), a.x, w & GD_MAX, (w & GF_SKIP) != 0, 0).word;
+                if (sw && ((sw >> 12) & 7u) == G_RW) w = sw;
+            }
             const uint32_t b = P.gbase[sl * GEN_STRIDE + gen], o = s_base + threadIdx.x;
             if ((uint64_t)b + o < P.scap) {
                 const uint32_t idx = sl * P.scap + b + o;
-                P.g0[idx] = make_uint4(a.x, pos, r1.x, r1.y);
+                P.g0[idx] = make_uint4(a.x, pos, w, r1.y);
                 arrived[i] = idx;
             } else {
                 arrived[i] = NONE32;

@@ -1670,6 +1670,15 @@ static res u_ia(uctx *u, uint32_t ns, uint32_t obj, uint32_t rel, int d, int ski
     return R_NOT;
 }
 
+static int rs_root_ia(void) { /* RS_IA_ROOT=1: roots as IA goals (an engine built with KETO_FR_IAROOT) */
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("RS_IA_ROOT");
+        v = e && *e == '1';
+    }
+    return v;
+}
+
 int rs_check_u(rs_db *db, const rs_query *q, uint32_t budget, int32_t *err, uint32_t *routed, uint32_t *goals,
                uint32_t *gens) {
     rs_stats dummy = {0, 0, 0, 0};
@@ -1681,7 +1690,20 @@ int rs_check_u(rs_db *db, const rs_query *q, uint32_t budget, int32_t *err, uint
     int d = q->depth;
     if (d <= 0 || db->max_depth < d) d = db->max_depth; /* engine.go:82-84 */
     res r = R_NOT;
-    if (u_spawn(&u, 0)) r = u_ia(&u, q->ns, q->obj, q->rel, d, 0, U_NONE, 0);
+    if (u_spawn(&u, 0)) {
+        /* the root shaped as u_sub shapes a sub-check (csrc/frontier_goal.inc root_word): a
+         * rewrite with neither a direct check nor an expand-subject to run is its RW goal */
+        int err;
+        const int ri = ast_relation_for(db, q->ns, q->rel, &err);
+        int rw_root = 0;
+        if (!err && ri >= 0 && db->rels[ri].rewrite >= 0 && d >= 1 && !rs_root_ia()) {
+            const int can_ss_rw = !db->strict || db->rels[ri].has_ss_type;
+            const int direct = !db->strict && d - 1 > 0 && exists(&c, q->ns, q->obj, q->rel);
+            const int es = can_ss_rw && d - 1 > 0 && has_set_rows(db, q->ns, q->rel);
+            rw_root = !direct && !es;
+        }
+        r = rw_root ? u_rw(&u, q->ns, q->obj, db->rels[ri].rewrite, d, U_NONE, 0) : u_ia(&u, q->ns, q->obj, q->rel, d, 0, U_NONE, 0);
+    }
     for (size_t i = 0; i < u.cap; i++)
         if (u.set[i].used > 1 && u.set[i].decisive) u.routed = 1;
     free(u.set);

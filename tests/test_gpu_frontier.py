@@ -128,7 +128,9 @@ def test_nested_groups_small_frontier_vs_oracle(stream):
 
 
 def test_every_query_routed_matches_oracle(budget):
-    """budget 1: every query with a sub-check goes to the DFS interpreter through the routed list"""
+    """budget 1: every query whose root goal has a sub-check goes to the DFS interpreter through the
+    routed list (rs_check_u's count with the same budget: a root the shaping makes a rewrite goal
+    that decides alone -- an IN-shortcut hit -- is not routed)"""
     from keto_mi355x import synth
     stream = budget(1)
     wl = synth.drive(depth=5, n_groups=500, n_users=2000, seed=8)
@@ -142,7 +144,8 @@ def test_every_query_routed_matches_oracle(budget):
     allowed, gerr, fs = _frontier_batch(stream, eng, q)
     np.testing.assert_array_equal(gerr, err)
     np.testing.assert_array_equal(allowed, dec)
-    assert fs["routed"] == len(q)
+    _, _, routed, _, _ = orc.check_u_batch(queries_to_oracle(q), threads=8, budget=1)
+    assert fs["routed"] == int(routed.sum()) > len(q) // 2
 
 
 @pytest.mark.parametrize("seed", [3, 17, 41])
