@@ -64,6 +64,9 @@ namespace {
 #include "resolve_query.inc"
 
 constexpr uint32_t DBLK = 256;
+// a goal record on the wire: the outbox's 32 bytes without the sender's proxy word (the sender
+// keeps its proxies in send order, sent_px; values come back in receive order)
+constexpr uint32_t WIRE_WORDS = 7, WIRE_BYTES = 4 * WIRE_WORDS;
 constexpr uint32_t HOME_BITS = 21;  // home = rank << 21 | query index (batches of <= FR_MAX_BATCH)
 constexpr uint32_t DIST_MAX_WORLD = 1u << (32 - HOME_BITS);
 
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(DBLK) void k_dest_count(const uint4 *rec, uint32_t 
 // records grouped by destination (cursor[r] = r's first slot, advanced); the sender's proxy of
 // each sent record, in send order, for the returns
 __global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_t n, uint32_t world, uint32_t *cursor,
-                                                       uint4 *out, uint32_t *sent_px) {
+                                                       uint32_t *out, uint32_t *sent_px) {
     __shared__ uint32_t h[LDS_W], base[LDS_W];
     for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += dstride()) {
         for (uint32_t t = threadIdx.x; t < world; t += blockDim.x) h[t] = 0;
@@ -131,8 +134,14 @@ __global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_
         __syncthreads();
         if (live) {
             const uint32_t p = base[dst] + at;
-            out[2 * (size_t)p] = r0;
-            out[2 * (size_t)p + 1] = r1;
+            uint32_t *o = out + (size_t)WIRE_WORDS * p;
+            o[0] = r0.x;
+            o[1] = r0.y;
+            o[2] = r0.z;
+            o[3] = r0.w;
+            o[4] = r1.x;
+            o[5] = r1.y;
+            o[6] = r1.z;
             sent_px[p] = r1.w;
         }
         __syncthreads();
@@ -144,7 +153,7 @@ __global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_
 // a phantom when it holds no tuple -- and the subject's membership record).  A block reserves its
 // goals in one slice with one atomic; arrived[i] = the goal's arena index (NONE32: the slice was
 // full, the position is routed and its return says so).
-__global__ __launch_bounds__(DBLK) void k_arrive(FrontierParams P, const uint4 *rec, uint32_t n, uint32_t pos0, uint32_t gen,
+__global__ __launch_bounds__(DBLK) void k_arrive(FrontierParams P, const uint32_t *rec, uint32_t n, uint32_t pos0, uint32_t gen,
                                                  int32_t max_depth, uint4 *start, uint2 *subj, uint32_t *home, uint32_t *arrived) {
     const DevSnapshot &s = P.s;
     const Tables T = global_tables(s);
@@ -156,7 +165,8 @@ __global__ __launch_bounds__(DBLK) void k_arrive(FrontierParams P, const uint4 *
         __syncthreads();
         const uint64_t i = i0 + threadIdx.x;
         if (i < n) {
-            const uint4 r0 = rec[2 * i], r1 = rec[2 * i + 1];
+            const uint32_t *wr = rec + (size_t)WIRE_WORDS * i;
+            const uint4 r0 = make_uint4(wr[0], wr[1], wr[2], wr[3]), r1 = make_uint4(wr[4], wr[5], wr[6], 0u);
             const uint32_t pos = pos0 + (uint32_t)i;
             uint4 a, R;
             uint32_t wgt = 0;
@@ -704,7 +714,7 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
         std::vector<uint32_t> cur(W, 0);
         for (uint32_t r = 1; r < W; r++) cur[r] = cur[r - 1] + cnt[r - 1];
         KETO_HIP(hipMemcpyAsync(h, cur.data(), (size_t)W * 4, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_dest_scatter, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, W, h, E.sbuf.as<uint4>(),
+        hipLaunchKernelGGL(k_dest_scatter, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, W, h, E.sbuf.as<uint32_t>(),
                            E.sent_px.as<uint32_t>() + L.sent_off);
         KETO_HIP(hipGetLastError());
     }
@@ -727,16 +737,16 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
     L.any = any_sent;
     uint64_t bytes_out = 0;
     for (uint32_t r = 0; r < W; r++)
-        if (r != E.rank) bytes_out += L.sent[r] * 32;
+        if (r != E.rank) bytes_out += L.sent[r] * WIRE_BYTES;
     L.stat.request_bytes = bytes_out;
     L.stat.tuples = nr;
     if (any_sent) {
         std::vector<uint64_t> sb(W), rb(W);
         for (uint32_t r = 0; r < W; r++) {
-            sb[r] = L.sent[r] * 32;
-            rb[r] = L.recv[r] * 32;
+            sb[r] = L.sent[r] * WIRE_BYTES;
+            rb[r] = L.recv[r] * WIRE_BYTES;
         }
-        E.rbuf.reserve(std::max<uint64_t>(1, nr) * 32, 0, s);
+        E.rbuf.reserve(std::max<uint64_t>(1, nr) * WIRE_BYTES, 0, s);
         d_alltoallv(E, E.sbuf.p, sb, E.rbuf.p, rb, wait_s);
     }
     return nr;
@@ -787,7 +797,7 @@ void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowe
             E.arrived.reserve((L.recv_off + nr) * 4 + 16, L.recv_off * 4, s);
             FrontierParams P = params(E);
             if (nr) {
-                hipLaunchKernelGGL(k_arrive, dgrid(nr, 8192), dim3(DBLK), 0, s, P, E.rbuf.as<uint4>(), (uint32_t)nr, (uint32_t)npos, k,
+                hipLaunchKernelGGL(k_arrive, dgrid(nr, 8192), dim3(DBLK), 0, s, P, E.rbuf.as<uint32_t>(), (uint32_t)nr, (uint32_t)npos, k,
                                    E.limits.max_read_depth, E.start.as<uint4>(), E.subj.as<uint2>(), E.home.as<uint32_t>(),
                                    E.arrived.as<uint32_t>() + L.recv_off);
                 KETO_HIP(hipGetLastError());
