@@ -64,9 +64,11 @@ namespace {
 #include "resolve_query.inc"
 
 constexpr uint32_t DBLK = 256;
-// a goal record on the wire: the outbox's 32 bytes without the sender's proxy word (the sender
-// keeps its proxies in send order, sent_px; values come back in receive order)
-constexpr uint32_t WIRE_WORDS = 7, WIRE_BYTES = 4 * WIRE_WORDS;
+// a goal record on the wire: {obj, ns | rel << 16, word, scope, home} -- the outbox's 32 bytes
+// without the query subject (every rank holds the batch's subjects, exchanged once per chunk:
+// subject = the table's entry for the record's home) and without the sender's proxy word (the
+// sender keeps its proxies in send order, sent_px; values come back in receive order)
+constexpr uint32_t WIRE_WORDS = 5, WIRE_BYTES = 4 * WIRE_WORDS;
 constexpr uint32_t HOME_BITS = 21;  // home = rank << 21 | query index (batches of <= FR_MAX_BATCH)
 constexpr uint32_t DIST_MAX_WORLD = 1u << (32 - HOME_BITS);
 
@@ -96,6 +98,14 @@ __global__ __launch_bounds__(DBLK) void k_root_records(const keto_query *q, uint
         rec[2 * i] = make_uint4(x.obj, dist_pack_ns_rel(x.ns, x.rel), x.s_obj,
                                 std::min(x.s_ns, 0x7FFFu) | ((x.subj_kind & 1u) << 15) | (std::min(x.s_rel, 0xFFFFu) << 16));
         rec[2 * i + 1] = make_uint4(gword(G_IA, std::min(d, GD_MAX)), NONE32, (rank << HOME_BITS) | (uint32_t)i, (uint32_t)i);
+    }
+}
+
+// the chunk's query subjects as the records carry them, for the job-wide subject table
+__global__ __launch_bounds__(DBLK) void k_subjects(const uint4 *rec, uint32_t n, uint2 *out) {
+    for (uint64_t i = dgid(); i < n; i += dstride()) {
+        const uint4 r0 = rec[2 * i];
+        out[i] = make_uint2(r0.z, r0.w);
     }
 }
 
@@ -137,11 +147,9 @@ __global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_
             uint32_t *o = out + (size_t)WIRE_WORDS * p;
             o[0] = r0.x;
             o[1] = r0.y;
-            o[2] = r0.z;
-            o[3] = r0.w;
-            o[4] = r1.x;
-            o[5] = r1.y;
-            o[6] = r1.z;
+            o[2] = r1.x;
+            o[3] = r1.y;
+            o[4] = r1.z;
             sent_px[p] = r1.w;
         }
         __syncthreads();
@@ -154,7 +162,8 @@ __global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_
 // goals in one slice with one atomic; arrived[i] = the goal's arena index (NONE32: the slice was
 // full, the position is routed and its return says so).
 __global__ __launch_bounds__(DBLK) void k_arrive(FrontierParams P, const uint32_t *rec, uint32_t n, uint32_t pos0, uint32_t gen,
-                                                 int32_t max_depth, uint4 *start, uint2 *subj, uint32_t *home, uint32_t *arrived) {
+                                                 int32_t max_depth, uint4 *start, uint2 *subj, uint32_t *home, uint32_t *arrived,
+                                                 const uint2 *stab, const uint32_t *stab_off) {
     const DevSnapshot &s = P.s;
     const Tables T = global_tables(s);
     __shared__ uint32_t s_base;
@@ -166,7 +175,9 @@ __global__ __launch_bounds__(DBLK) void k_arrive(FrontierParams P, const uint32_
         const uint64_t i = i0 + threadIdx.x;
         if (i < n) {
             const uint32_t *wr = rec + (size_t)WIRE_WORDS * i;
-            const uint4 r0 = make_uint4(wr[0], wr[1], wr[2], wr[3]), r1 = make_uint4(wr[4], wr[5], wr[6], 0u);
+            const uint32_t hm = wr[4];
+            const uint2 sj = stab[stab_off[hm >> HOME_BITS] + (hm & ((1u << HOME_BITS) - 1u))];  // (the query's subject)
+            const uint4 r0 = make_uint4(wr[0], wr[1], sj.x, sj.y), r1 = make_uint4(wr[2], wr[3], hm, 0u);
             const uint32_t pos = pos0 + (uint32_t)i;
             uint4 a, R;
             uint32_t wgt = 0;
@@ -376,7 +387,7 @@ struct DistEngine {
     bool verbose = false;
     bool staged = false, agreed = false;
     // per batch (grown, reused)
-    Grow dq, rec, sbuf, rbuf, sent_px, arrived, ret, rret, hv, deep, hrouted, outv, fbl;
+    Grow dq, rec, sbuf, rbuf, sent_px, arrived, ret, rret, hv, deep, hrouted, outv, fbl, ssend, stab, stab_off;
     Grow arena, occ, dtab, dbits, ctrl, start, subj, home, qrouted, qspawn, ob, dlist, dent, dcnt, dsend;
     uint64_t cap = 0, ocap = 0, dcap = 0, pos_cap = 0, ob_cap = 0;
     uint32_t epoch = 1;
@@ -784,7 +795,29 @@ void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowe
     uint64_t npos = 0, total_goals = 0, sent_total = 0;
     // level 0: the queries' roots to their objects' owners
     bool any_local = false, any_sent = false;
+    // the chunk's query subjects to every rank, once: the goal records carry only their home
+    uint64_t subj_bytes = 0;
+    {
+        const std::vector<uint64_t> nq = d_alltoall(E, std::vector<uint64_t>(W, n), wait_s);
+        std::vector<uint32_t> off(W + 1, 0);
+        for (uint32_t r = 0; r < W; r++) off[r + 1] = off[r] + (uint32_t)nq[r];
+        E.ssend.reserve(std::max<uint64_t>(1, n) * 8 * W + 16, 0, s);
+        if (n) {
+            hipLaunchKernelGGL(k_subjects, dgrid(n), dim3(DBLK), 0, s, E.rec.as<uint4>(), (uint32_t)n, E.ssend.as<uint2>());
+            KETO_HIP(hipGetLastError());
+            for (uint32_t r = 1; r < W; r++)
+                KETO_HIP(hipMemcpyAsync(E.ssend.as<uint8_t>() + (size_t)r * n * 8, E.ssend.p, n * 8, hipMemcpyDeviceToDevice, s));
+        }
+        E.stab.reserve(std::max<uint64_t>(1, off[W]) * 8 + 16, 0, s);
+        E.stab_off.reserve(4 * (W + 1) + 16, 0, s);
+        KETO_HIP(hipMemcpyAsync(E.stab_off.p, off.data(), 4 * (W + 1), hipMemcpyHostToDevice, s));
+        std::vector<uint64_t> sb(W, n * 8), rb(W);
+        for (uint32_t r = 0; r < W; r++) rb[r] = nq[r] * 8;
+        d_alltoallv(E, E.ssend.p, sb, E.stab.p, rb, wait_s);
+        subj_bytes = n * 8 * (W - 1);
+    }
     uint64_t nr = send_level(E, E.rec.as<uint4>(), n, E.levels[0], false, any_local, any_sent, wait_s);
+    E.levels[0].stat.request_bytes += subj_bytes;  // (counted with the roots' records)
     sent_total += E.levels[0].n_sent;
     uint32_t G = 0;
     if (any_sent) {
@@ -799,7 +832,7 @@ void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowe
             if (nr) {
                 hipLaunchKernelGGL(k_arrive, dgrid(nr, 8192), dim3(DBLK), 0, s, P, E.rbuf.as<uint32_t>(), (uint32_t)nr, (uint32_t)npos, k,
                                    E.limits.max_read_depth, E.start.as<uint4>(), E.subj.as<uint2>(), E.home.as<uint32_t>(),
-                                   E.arrived.as<uint32_t>() + L.recv_off);
+                                   E.arrived.as<uint32_t>() + L.recv_off, E.stab.as<uint2>(), E.stab_off.as<uint32_t>());
                 KETO_HIP(hipGetLastError());
             }
             npos += nr;
