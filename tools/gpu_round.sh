@@ -19,7 +19,7 @@ cd "$(dirname "$0")/.." && export TMPDIR=/tmp
 OUT=gpurun_out/$1; CMD=$2; shift 2
 mkdir -p $OUT
 QUIET="--no-cpu-baseline --serve-clients 0 --latency-iters 0 --no-store-probe"
-line() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); f=d.get('frontier') or {}; print(sys.argv[2], 'value %.1fM' % (d['value']/1e6), 'ms/step %.3f' % d['ms_per_step'], 'check path %.3f ms' % d['roofline']['kernel_ms'], 'goals', f.get('goals_per_batch'), 'gens', f.get('generations_max'))" "$1" "$2"; }
+line() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); f=d.get('frontier') or {}; print(sys.argv[2], 'value %.1fM' % (d['value']/1e6), 'ms/step %.3f' % d['ms_per_step'], 'check path %s ms' % d['roofline'].get('kernel_ms'), 'goals', f.get('goals_per_batch'), 'gens', f.get('generations_max'))" "$1" "$2"; }
 case $CMD in
 tests)
   timeout -k 10 1300 python3 -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests > $OUT/tests.log 2>&1
