@@ -346,9 +346,12 @@ def synth_new_files(wl, ids, parents, rng):
 def store_probe(km, wl, q, n_ins: int = 600, n_del: int = 400):
     """Incremental snapshots at the workload's size: the graph in a
     device tuple store (keto_store_*), a TransactRelationTuples of n_ins + n_del rows (new ACL rows
-    on existing objects, deletes of stored rows), then the new version cut by patching the previous
-    snapshot (keto_store_snapshot_patch) -- timed beside the full device build of the same version,
-    and checked against it on the bench's query batch."""
+    on existing objects, deletes of stored rows), then the new version cut two ways -- by patching
+    a copy of the previous snapshot (keto_store_snapshot_patch: O(graph) copies, the base stays
+    valid) and by advancing the previous snapshot in place (keto_store_snapshot_advance: work in
+    proportion to the touched rows) -- timed beside the full device build of the same version and
+    checked against it on the bench's query batch; then a second transaction creating 100 new
+    files, advanced in place too."""
     import torch
 
     rng = np.random.default_rng(21)
@@ -367,16 +370,28 @@ def store_probe(km, wl, q, n_ins: int = 600, n_del: int = 400):
     t0 = time.perf_counter()
     st.transact(ins, dele)
     transact_ms = (time.perf_counter() - t0) * 1e3
+
+    def checks(snap, qq):
+        return km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(qq)
+
+    # the copy patch (base untouched), then the in-place advance of base to the same version
     t0 = time.perf_counter()
     patched = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict, store=st,
                           base=base)
     patch_ms = (time.perf_counter() - t0) * 1e3
     was_patched = patched.patched
-    base.close()
-    res = [km.CheckEngine(patched, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)]
+    res_patch = checks(patched, q)
+    pi = patched.info()
+    patched.close()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    advanced = base.advance(st)
+    advance_ms = (time.perf_counter() - t0) * 1e3
+    res_adv = checks(base, q)
+    ai = base.info()
     # a second transaction creates objects (verdict r3: Keto's most common write is a new file):
-    # 100 new files, a parent tuple + 9 ACL rows each, ids past the graph's -- patched onto the
-    # previous version's spare entities
+    # 100 new files, a parent tuple + 9 ACL rows each, ids past the graph's -- advanced in place
+    # onto the snapshot's spare entities
     n_new = 100
     new_ids = wl.n_uuids + np.arange(n_new)
     ins2 = synth_new_files(wl, new_ids, rng.integers(0, wl.meta["n_folders"], n_new), rng)
@@ -384,42 +399,44 @@ def store_probe(km, wl, q, n_ins: int = 600, n_del: int = 400):
     st.transact(ins2, None)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    patched2 = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids2, strict=wl.strict, store=st,
-                           base=patched)
-    patch2_ms = (time.perf_counter() - t0) * 1e3
+    advanced2 = base.advance(st)
+    advance2_ms = (time.perf_counter() - t0) * 1e3
     q2 = q.copy()
     k = min(len(q2), 1 << 16)  # view / edit of the new files by random users
     q2["ns"][:k], q2["obj"][:k] = wl.ns_names.index("File"), rng.choice(new_ids, k)
     q2["rel"][:k] = rng.choice([wl.rel_names.index("view"), wl.rel_names.index("edit")], k)
     q2["subj_kind"][:k], q2["s_ns"][:k], q2["s_rel"][:k], q2["max_depth"][:k] = 0, 0, 0, 0
     q2["s_obj"][:k] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], k)
-    res2 = [km.CheckEngine(patched2, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q2)]
-    new_objs = {"transaction_rows": int(len(ins2)), "new_files": n_new, "patched": patched2.patched,
-                "patch_ms": patch2_ms, "new_file_checks_allowed": float(res2[0][0][:k].mean())}
-    pi = patched.info()
-    patched.close()  # (device memory: the full builds of the same versions come next)
-    patched2.close()
+    res2 = [checks(base, q2)]
+    new_objs = {"transaction_rows": int(len(ins2)), "new_files": n_new, "advanced": advanced2, "advance_ms": advance2_ms,
+                "new_file_checks_allowed": float(res2[0][0][:k].mean())}
+    base.close()  # (device memory: the full builds of the same versions come next)
     t0 = time.perf_counter()
     full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids2, strict=wl.strict, store=st)
     full_ms = (time.perf_counter() - t0) * 1e3
-    res2.append(km.CheckEngine(full, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q2))
+    res2.append(checks(full, q2))
     new_objs["checks_vs_full_build"] = {"n": int(len(q2)), "mismatches": int((res2[0][0] != res2[1][0]).sum()
                                                                            + (res2[0][1] != res2[1][1]).sum())}
     # version 1 against a full build of it: the store without the second transaction's rows
     st.transact(None, ins2)
     full.close()
     full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids2, strict=wl.strict, store=st)
-    res.append(km.CheckEngine(full, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q))
+    res_full = checks(full, q)
     fi = full.info()
-    out = {"transaction_rows": n_ins + n_del, "patched": was_patched, "patch_ms": patch_ms, "full_build_ms": full_ms,
+
+    def mism(a):
+        return int((a[0] != res_full[0]).sum() + (a[1] != res_full[1]).sum())
+
+    out = {"transaction_rows": n_ins + n_del, "advanced": advanced, "advance_ms": advance_ms,
+           "patched": was_patched, "patch_ms": patch_ms, "full_build_ms": full_ms,
            "new_objects": new_objs,
-           "transact_ms": transact_ms, "store_load_s": load_s, "version": int(pi["version"]),
-           "n_tuples_equal": pi["n_tuples"] == fi["n_tuples"],
-           "checks_vs_full_build": {"n": int(len(q)), "mismatches": int((res[0][0] != res[1][0]).sum()
-                                                                         + (res[0][1] != res[1][1]).sum())},
-           "what": "keto_store_transact of the rows, then keto_store_snapshot_patch of the previous snapshot "
-                   "(host API call to a usable snapshot); full_build_ms: keto_store_snapshot of the same version; "
-                   "new_objects: a second transaction creating 100 files, patched onto the first patch"}
+           "transact_ms": transact_ms, "store_load_s": load_s, "version": int(ai["version"]),
+           "n_tuples_equal": pi["n_tuples"] == fi["n_tuples"] == ai["n_tuples"],
+           "checks_vs_full_build": {"n": int(len(q)), "mismatches_advanced": mism(res_adv), "mismatches_patched": mism(res_patch)},
+           "what": "keto_store_transact of the rows; then the version cut by keto_store_snapshot_patch of the previous "
+                   "snapshot (a copy, base untouched) and by keto_store_snapshot_advance of the previous snapshot in "
+                   "place (host API call to a usable snapshot each); full_build_ms: keto_store_snapshot of the same "
+                   "version; new_objects: a second transaction creating 100 files, advanced in place"}
     full.close()
     st.close()
     torch.cuda.empty_cache()
@@ -960,7 +977,8 @@ def main(argv=None):
             snap.close()
             torch.cuda.empty_cache()
         store = store_probe(km, wl, q)
-        log(f"[rank {rank}] store probe: patch {store['patch_ms']:.1f} ms (patched {store['patched']}), full build "
+        log(f"[rank {rank}] store probe: advance {store['advance_ms']:.1f} ms (advanced {store['advanced']}), copy patch "
+            f"{store['patch_ms']:.1f} ms (patched {store['patched']}), full build "
             f"{store['full_build_ms']:.0f} ms ({time.perf_counter() - t_setup:.1f}s since start)")
 
     achieved = bytes_t0 / (kernel_ms * 1e-3) / 1e9

@@ -350,13 +350,15 @@ __global__ __launch_bounds__(BLK) void k_gather(const keto_tuple *t, const uint3
 }
 
 __global__ __launch_bounds__(BLK) void k_row_fill(const uint32_t *off, uint64_t n_rows, const uint32_t *row_idx,
-                                                  const uint32_t *dst, uint32_t *all_subj, uint32_t *set_cnt) {
+                                                  const uint32_t *dst, uint32_t *all_subj, uint32_t *set_cnt,
+                                                  const unsigned long long *skey, unsigned long long *all_shard) {
     const uint64_t v = gid();
     if (v >= n_rows) return;
     uint32_t c = 0;
     for (uint32_t p = off[v]; p < off[v + 1]; p++) {
         const uint32_t d = dst[row_idx[p]];
         all_subj[p] = d;
+        if (all_shard) all_shard[p] = skey[row_idx[p]];
         c += (d & SKEY_SET) ? 1 : 0;
     }
     set_cnt[v] = c;
@@ -628,11 +630,11 @@ void rows(const RowsIn &in, RowsOut &out) {
     {
         DevBuf set_cnt(4 * (N + 1));
         hipLaunchKernelGGL(k_row_fill, grid_for(N), dim3(BLK), 0, 0, out.all_off, N, row_idx.u32(), dst.u32(), out.all_subj,
-                           set_cnt.u32());
+                           set_cnt.u32(), reinterpret_cast<const unsigned long long *>(skey.p), out.all_shard);
         KETO_HIP(hipGetLastError());
         scan_excl(set_cnt.u32(), N);
         out.n_set = read_u32(set_cnt.u32(), N);
-        out.set_dst = DevBuf(4ull * out.n_set + 16);
+        out.set_dst = DevBuf(4ull * (out.n_set + out.set_slack) + 16);
         hipLaunchKernelGGL(k_set_fill, grid_for(N), dim3(BLK), 0, 0, out.all_off, set_cnt.u32(), N, out.all_subj,
                            out.set_dst.u32());
         hipLaunchKernelGGL(k_set_row, grid_for(N), dim3(BLK), 0, 0, set_cnt.u32(), N, out.set_dst.u32(), out.set_row);

@@ -594,6 +594,15 @@ int keto_store_snapshot_patch(keto_store *st, const keto_snapshot *base, const k
     });
 }
 
+int keto_store_snapshot_advance(keto_store *st, keto_snapshot *snap, int32_t *advanced) {
+    if (!st || !snap) return fail(KETO_E_INVALID, "null argument");
+    if (advanced) *advanced = 0;
+    return guarded([&] {
+        const bool a = keto::store_snapshot_advance(*reinterpret_cast<keto::TupleStore *>(st), *SN(snap));
+        if (advanced) *advanced = a ? 1 : 0;
+    });
+}
+
 int keto_store_info(keto_store *st, uint64_t *n_tuples, uint64_t *version) {
     if (!st) return fail(KETO_E_INVALID, "null store");
     keto::store_info(*reinterpret_cast<keto::TupleStore *>(st), n_tuples, version);

@@ -38,6 +38,7 @@ struct Spares {
 struct BuildOpts {
     uint32_t uuid_capacity = 0;  // id space (>= cfg n_uuids): ids past the caller's are unknown until written
     bool spares = false;         // spare entities per namespace (n_real / 16 + 256)
+    bool room = false;           // in-place advance room (Snapshot::Room): row slack, relocation table, shard keys
     // A partitioned graph's snapshots (frontier_dist.hip) share one node arithmetic: the (ns, rel)
     // pairs the job's tuples use are agreed on (OR over the ranks) before slots are laid out
     std::function<void(std::vector<uint8_t> &used)> agree_used;
@@ -77,12 +78,26 @@ struct Snapshot {
     std::vector<uint32_t> reach_slots;
     uint64_t reach_cand = 0, reach_pool_n = 0;
     std::vector<uint4> ext;          // {obj, ns, entity, 0} of the objects placed on spares (dev.ext's entries)
+    uint64_t reach_pool_cap = 0;     // reach_pool entries allocated (> reach_pool_n: room to append)
+    // in-place advance (advance in patch.hip; store snapshots only, BuildOpts::room): the row value
+    // arrays' capacities and next free entries past the rows, the relocation table (dev.reloc), and
+    // each all_subj entry's shard key -- the high 64 bits of its shard_id, the order of a row
+    struct Room {
+        uint64_t all_cap = 0, all_tail = 0, rev_cap = 0, rev_tail = 0, set_cap = 0, set_tail = 0;
+        uint32_t reloc_cap = 0, reloc_used = 0;
+        unsigned long long *all_shard = nullptr;
+        bool moved = false;  // an advance ran: rows live outside their CSR extents (no save, no copy patch)
+    } room;
 
     // a device allocation of this snapshot (back to the pool with its last sharer)
     void own(void *p, size_t bytes);
     void *alloc(size_t bytes);  // own(pool_acquire(bytes))
     // the allocation of `o` holding p, shared (p must be one of o's arrays)
     void share(const Snapshot &o, const void *p);
+    // this snapshot's own allocation p: no other snapshot shares it / let go of it (back to the
+    // pool with its last sharer)
+    bool sole(const void *p) const;
+    void drop(const void *p);
     // node -> (ns, entity, slot) on the host (for Expand output conversion)
     uint32_t ns_of(uint32_t node) const;
 };
@@ -95,6 +110,7 @@ void build_reach(Snapshot &s);
 // reach can have changed -- the touched rows' nodes and their ancestors over subject-set rows
 // within REACH_CAP - 1 hops -- are walked again; anything else (the tabled slots changed, the base
 // has no host record) rebuilds them whole
+// (&s == &B: an in-place advance -- the tables are updated where they lie)
 void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &touched_nodes);
 // 64-bit FNV-1a of everything a snapshot compiles from its configuration (name tables, AST JSON,
 // strict mode; not the device, not n_uuids): equal hashes = the same compiled tables
@@ -146,6 +162,8 @@ struct RowsIn {
 struct RowsOut {
     uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *weight;  // caller-allocated
     uint4 *set_row;
+    unsigned long long *all_shard = nullptr;  // caller-allocated or null: shard_hi of each all_subj entry
+    uint64_t set_slack = 0;                   // set_dst entries allocated past the rows
     DevBuf set_dst, probe;
     uint64_t n_set = 0, probe_buckets = 0, probe_keys = 0;
 };
@@ -370,6 +388,12 @@ Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const
 // base has no node for some touched tuple, or its probe hash is too full -- build in full)
 Snapshot *patch_snapshot(const Snapshot &base, const keto_tuple *store_rows, uint64_t n_store, const keto_tuple *touched,
                          const uint8_t *touched_is_ins, uint64_t n_touched);
+// the store's current content in `snap` itself (cut from this store, no batch in flight on it):
+// false when the delta needs a full build -- snap is then unchanged
+bool store_snapshot_advance(const TupleStore &st, Snapshot &snap);
+// patch.hip: snap + the touched tuples applied to its rows where they lie (false: nothing changed)
+bool advance_snapshot(Snapshot &snap, const keto_tuple *touched, const uint8_t *touched_is_ins, uint64_t n_touched,
+                      uint64_t n_store);
 void store_free(TupleStore *st);
 void store_info(const TupleStore &st, uint64_t *n, uint64_t *version);
 

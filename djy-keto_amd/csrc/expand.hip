@@ -136,7 +136,8 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams P) {
             uint32_t key = root;
             if (s.vkey && ri_shared(node_ri(s, root))) key = s.vkey[root];
             vis_insert(vis, vmask, epoch, key, vcount, P.vcap, ovf);  // visited includes the root (:69-72)
-            uint32_t b = s.all_off[root], e = s.all_off[root + 1];
+            uint32_t b, e;
+            row_span(s.all_off, s.reloc, root, b, e);
             rows++;
             if (b != e) {  // no tuples on the first page -> nil (:97-99)
                 if (d <= 1) emit(4, SKEY_SET | root, 0);  // :101-104
@@ -165,7 +166,8 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams P) {
                             continue;
                         }
                         if (ovf) break;
-                        uint32_t cb = s.all_off[c], ce = s.all_off[c + 1];
+                        uint32_t cb, ce;
+                        row_span(s.all_off, s.reloc, c, cb, ce);
                         rows++;
                         if (cb == ce || cd <= 1) {
                             emit(4, sk, 0);
@@ -294,7 +296,8 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
             uint32_t key = root;
             if (s.vkey && ri_shared(node_ri(s, root))) key = s.vkey[root];
             visit(key);  // the root is visited (:69-72)
-            const uint32_t b = s.all_off[root], e = s.all_off[root + 1];
+            uint32_t b, e;
+            row_span(s.all_off, s.reloc, root, b, e);
             rows++;
             if (b != e && e - b >= XR_UNION) fail = true;  // (a row past 2^31 tuples: the fallback)
             if (b != e && !fail) {  // no tuples on the first page -> nil (:97-99)
@@ -318,8 +321,7 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
                         const uint32_t c = sk & ~SKEY_SET;
                         ck = c;
                         if (s.vkey && ri_shared(node_ri(s, c))) ck = s.vkey[c];
-                        cb = s.all_off[c];
-                        ce = s.all_off[c + 1];
+                        row_span(s.all_off, s.reloc, c, cb, ce);
                     }
                     const unsigned long long setm = __ballot(set);
                     uint32_t pos = 0;

@@ -68,8 +68,7 @@ __device__ __forceinline__ void row_of(const DevSnapshot &s, const Tables &T, ui
     if (en == NONE32) return;  // no tuple of the object
     const uint32_t node = t_node(T, ns, en, rel);
     if (node & VIRT_BIT) return;
-    b = s.all_off[node];
-    e = s.all_off[node + 1];
+    row_span(s.all_off, s.reloc, node, b, e);
 }
 __global__ __launch_bounds__(XB) void kx_row_len(DevSnapshot s, const uint64_t *req, uint32_t n, uint32_t *len) {
     const Tables T = global_tables(s);

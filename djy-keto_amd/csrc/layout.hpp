@@ -95,8 +95,12 @@ struct DevSnapshot {
     const uint32_t *vclass;    // [total slots] partitioned graphs: visited class of a slot (frontier_goal.inc gkey)
     const uint32_t *all_off;   // [n_nodes+1]  every tuple of a node, shard order (Expand)
     const uint32_t *all_subj;  // subject id, or SKEY_SET|node
-    const uint32_t *rev_off;   // [n_uuids + n_nodes + 1]  subject -> sorted nodes containing it
+    const uint32_t *rev_off;   // [n_uuids + n_nodes + 1]  subject -> the nodes holding it (a multiset)
     const uint32_t *rev_nodes;
+    // rows an in-place advance (advance.hip) moved: an all_off / rev_off word with ROW_MOVED is
+    // the index of the row's {begin, end, the word's original offset, 0} here; null on every
+    // snapshot that cannot be advanced in place (read rows through row_span)
+    const uint4 *reloc;
     const NsDev *ns;           // [n_ns + 1] (sentinel: node_base = n_nodes)
     const uint32_t *relinfo;   // [total slots]
     const uint32_t *nsrel;     // [n_ns * n_rel]
@@ -135,6 +139,24 @@ struct DevSnapshot {
     uint32_t tab_bytes[7];
     uint32_t lds_bytes;
 };
+
+constexpr uint32_t ROW_MOVED = 1u << 31;  // all_off / rev_off word of a moved row (DevSnapshot::reloc)
+// row i of an offset array (all_off, rev_off): [off[i], off[i+1]) unless the advance moved row i
+// (its own word flagged: the relocated extent) or row i+1 (the flagged next word's original
+// offset ends row i)
+__device__ __forceinline__ void row_span(const uint32_t *off, const uint4 *reloc, uint64_t i, uint32_t &b, uint32_t &e) {
+    b = off[i];
+    e = off[i + 1];
+    if (reloc && ((b | e) & ROW_MOVED)) {
+        if (b & ROW_MOVED) {
+            const uint4 r = reloc[b & ~ROW_MOVED];
+            b = r.x;
+            e = r.y;
+        } else {
+            e = reloc[e & ~ROW_MOVED].z;
+        }
+    }
+}
 
 constexpr uint32_t REACH_CAP = 32;         // nodes of a tabled reach, the node itself included (oracle reach_cap;
                                            // KETO_REACH_CAP <= REACH_CAP_MAX for A/B builds)

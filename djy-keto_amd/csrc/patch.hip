@@ -270,7 +270,9 @@ __global__ __launch_bounds__(BLK) void k_flip_leaf(DevSnapshot s, const uint4 *s
     const uint32_t c = flip[blockIdx.x];
     const bool leaf = set_row[c].x == set_row[c].y;
     const uint64_t v = (uint64_t)s.n_uuids + c;
-    for (uint32_t r = rev_off[v] + threadIdx.x; r < rev_off[v + 1]; r += blockDim.x) {
+    uint32_t rb, re;
+    row_span(rev_off, s.reloc, v, rb, re);
+    for (uint32_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
         const uint4 row = set_row[rev_nodes[r]];
         for (uint32_t k = row.x; k < row.y; k++) {
             const uint32_t e = set_dst[k];
@@ -284,7 +286,9 @@ __global__ __launch_bounds__(BLK) void k_fix_inline(DevSnapshot s, uint4 *set_ro
                                                     uint32_t m) {
     if (blockIdx.x >= m) return;
     const uint64_t v = (uint64_t)s.n_uuids + flip[blockIdx.x];
-    for (uint32_t r = rev_off[v] + threadIdx.x; r < rev_off[v + 1]; r += blockDim.x) {
+    uint32_t rb, re;
+    row_span(rev_off, s.reloc, v, rb, re);
+    for (uint32_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
         const uint32_t p = rev_nodes[r];
         uint4 row = set_row[p];
         row.z = row.y > row.x ? set_dst[row.x] : NONE32;
@@ -345,31 +349,15 @@ struct Touched {  // a touched row or subject, keyed for the scan
     uint32_t idx;  // node / subject index
 };
 
-}  // namespace
-
-Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_store, const keto_tuple *touched,
-                         const uint8_t *is_ins, uint64_t n_touched) {
-    using build::DevBuf;
-    auto t0 = std::chrono::steady_clock::now();
-    KETO_HIP(hipSetDevice(B.device));
-    static const bool verbose = getenv("KETO_PATCH_VERBOSE") != nullptr;
-    auto tp = t0;
-    auto phase = [&](const char *what) {  // KETO_PATCH_VERBOSE: where the time goes
-        if (!verbose) return;
-        KETO_HIP(hipDeviceSynchronize());
-        const auto now = std::chrono::steady_clock::now();
-        fprintf(stderr, "[keto patch]   %-10s %.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
-        tp = now;
-    };
-    const DevSnapshot &D = B.dev;
-    const uint32_t N = D.n_nodes;
-    const uint64_t M = (uint64_t)D.n_uuids + N;  // subject index space
-    if (n_store >= (1ull << 32) || n_touched >= (1ull << 31)) return nullptr;
-    // ---- 1. place the touched tuples in the base's node space -----------------------------------
-    std::vector<keto_tuple> ht(n_touched);
-    std::vector<uint4> pl(n_touched);
-    DevSnapshot Dp = D;  // the base's view, plus the objects this patch creates (step 0 below)
-    std::vector<uint4> ext = B.ext;
+// The touched tuples placed in the base's node space (step 1 of both the copy patch and the
+// advance): pl[i] = place() of tuple i, with the objects the inserts create put on spares first.
+struct Placed {
+    std::vector<keto_tuple> ht;  // the touched tuples, host copy
+    std::vector<uint4> pl;
+    DevSnapshot Dp{};            // the base's view, plus the objects this patch creates
+    std::vector<uint4> ext;      // the family's ext entries, this patch's included
+    std::vector<uint2> ent_set;  // {spare entity, obj} taken here
+    std::unique_ptr<void, void (*)(void *)> ext_dev{nullptr, [](void *p) { (void)hipFree(p); }};  // a new ext table
     // spares this patch takes go back if it then falls back to the full build (or throws), as
     // long as no later patch of the family took spares since
     struct Taken {
@@ -383,11 +371,21 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
                 if (spares->used[ns] == to[ns]) spares->used[ns] = from[ns];
         }
     } taken;
-    void *ext_dev = nullptr;  // a new ext table (owned by the new snapshot once it exists)
-    std::vector<uint2> ent_set;  // {spare entity, obj}
+};
+
+// false: a new object cannot go on a spare (aliased visited keys, out of spares) -- build in full
+bool place_touched(const Snapshot &B, const keto_tuple *touched, const uint8_t *is_ins, uint64_t n_touched, Placed &P) {
+    using build::DevBuf;
+    const DevSnapshot &D = B.dev;
+    std::vector<keto_tuple> &ht = P.ht;
+    std::vector<uint4> &pl = P.pl;
+    ht.resize(n_touched);
+    pl.resize(n_touched);
+    P.Dp = D;
+    P.ext = B.ext;
     auto place_all = [&] {
         DevBuf d_pl(sizeof(uint4) * n_touched);
-        hipLaunchKernelGGL(k_place, grid_for(n_touched), dim3(BLK), 0, 0, Dp, touched, n_touched, static_cast<uint4 *>(d_pl.p));
+        hipLaunchKernelGGL(k_place, grid_for(n_touched), dim3(BLK), 0, 0, P.Dp, touched, n_touched, static_cast<uint4 *>(d_pl.p));
         KETO_HIP(hipGetLastError());
         KETO_HIP(hipMemcpy(pl.data(), d_pl.p, sizeof(uint4) * n_touched, hipMemcpyDeviceToHost));
     };
@@ -434,7 +432,7 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
             }
             DevBuf dq(sizeof(keto_tuple) * q.size()), dp(sizeof(uint4) * q.size());
             KETO_HIP(hipMemcpy(dq.p, q.data(), sizeof(keto_tuple) * q.size(), hipMemcpyHostToDevice));
-            hipLaunchKernelGGL(k_place, grid_for(q.size()), dim3(BLK), 0, 0, Dp, static_cast<const keto_tuple *>(dq.p), q.size(),
+            hipLaunchKernelGGL(k_place, grid_for(q.size()), dim3(BLK), 0, 0, P.Dp, static_cast<const keto_tuple *>(dq.p), q.size(),
                                static_cast<uint4 *>(dp.p));
             KETO_HIP(hipGetLastError());
             KETO_HIP(hipMemcpy(probe.data(), dp.p, sizeof(uint4) * q.size(), hipMemcpyDeviceToHost));
@@ -447,49 +445,82 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
             if (probe[k].x != NONE32) continue;  // it has an entity
             const uint32_t ns = fresh_objs[k].first;
             for (uint32_t sl = 0; sl < B.ns[ns].n_slots; sl++)
-                if ((B.relinfo[B.ns[ns].slot_base + sl] >> 20) & 1u) return nullptr;  // aliased visited keys
-            if (B.spares->used[ns] + ++want[ns] > B.spares->count[ns]) return nullptr;  // out of spares
+                if ((B.relinfo[B.ns[ns].slot_base + sl] >> 20) & 1u) return false;  // aliased visited keys
+            if (B.spares->used[ns] + ++want[ns] > B.spares->count[ns]) return false;  // out of spares
         }
         for (size_t k = 0; k < fresh_objs.size(); k++) {
             if (probe[k].x != NONE32) continue;
             const uint32_t ns = fresh_objs[k].first, obj = fresh_objs[k].second;
             const uint32_t e = B.spares->first[ns] + B.spares->used[ns]++;
-            ext.push_back(make_uint4(obj, ns, e, 0));
-            ent_set.push_back(make_uint2(e, obj));
+            P.ext.push_back(make_uint4(obj, ns, e, 0));
+            P.ent_set.push_back(make_uint2(e, obj));
         }
-        taken.spares = B.spares;
-        taken.from.assign(B.n_ns, 0);
-        taken.to.assign(B.n_ns, 0);
+        P.taken.spares = B.spares;
+        P.taken.from.assign(B.n_ns, 0);
+        P.taken.to.assign(B.n_ns, 0);
         for (uint32_t ns = 0; ns < B.n_ns; ns++) {
-            taken.to[ns] = B.spares->used[ns];
-            taken.from[ns] = taken.to[ns] - want[ns];
+            P.taken.to[ns] = B.spares->used[ns];
+            P.taken.from[ns] = P.taken.to[ns] - want[ns];
         }
     }
-    std::unique_ptr<void, void (*)(void *)> ext_guard(nullptr, [](void *p) { (void)hipFree(p); });
-    if (!ent_set.empty()) {
+    if (!P.ent_set.empty()) {
         // the ext table of the new snapshot: every object placed on a spare so far in this family line
         uint32_t size = 64;
-        while (size < 2 * ext.size()) size <<= 1;
+        while (size < 2 * P.ext.size()) size <<= 1;
         std::vector<uint4> tab(size, make_uint4(0, 0, NONE32, 0));
-        for (const uint4 &x : ext) {
+        for (const uint4 &x : P.ext) {
             uint32_t h = (uint32_t)mix64((((uint64_t)x.y << 32) | x.x) + 1) & (size - 1);
             while (tab[h].z != NONE32) h = (h + 1) & (size - 1);
             tab[h] = x;
         }
+        void *ext_dev = nullptr;
         KETO_HIP(hipMalloc(&ext_dev, 16ull * size));
-        ext_guard.reset(ext_dev);
+        P.ext_dev.reset(ext_dev);
         KETO_HIP(hipMemcpy(ext_dev, tab.data(), 16ull * size, hipMemcpyHostToDevice));
-        Dp.ext = static_cast<const uint4 *>(ext_dev);
-        Dp.ext_mask = size - 1;
+        P.Dp.ext = static_cast<const uint4 *>(ext_dev);
+        P.Dp.ext_mask = size - 1;
         // the spares' uuid ids for Expand output: words of the shared ent_obj no snapshot of the
         // family reads before this one (a spare is handed out once)
-        DevBuf d_set(sizeof(uint2) * ent_set.size());
-        KETO_HIP(hipMemcpy(d_set.p, ent_set.data(), sizeof(uint2) * ent_set.size(), hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(k_ent_obj_set, grid_for(ent_set.size()), dim3(BLK), 0, 0, const_cast<uint32_t *>(D.ent_obj),
-                           static_cast<const uint2 *>(d_set.p), (uint32_t)ent_set.size());
+        DevBuf d_set(sizeof(uint2) * P.ent_set.size());
+        KETO_HIP(hipMemcpy(d_set.p, P.ent_set.data(), sizeof(uint2) * P.ent_set.size(), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_ent_obj_set, grid_for(P.ent_set.size()), dim3(BLK), 0, 0, const_cast<uint32_t *>(D.ent_obj),
+                           static_cast<const uint2 *>(d_set.p), (uint32_t)P.ent_set.size());
         KETO_HIP(hipGetLastError());
         place_all();
     }
+    return true;
+}
+
+}  // namespace
+
+Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_store, const keto_tuple *touched,
+                         const uint8_t *is_ins, uint64_t n_touched) {
+    using build::DevBuf;
+    auto t0 = std::chrono::steady_clock::now();
+    KETO_HIP(hipSetDevice(B.device));
+    static const bool verbose = getenv("KETO_PATCH_VERBOSE") != nullptr;
+    auto tp = t0;
+    auto phase = [&](const char *what) {  // KETO_PATCH_VERBOSE: where the time goes
+        if (!verbose) return;
+        KETO_HIP(hipDeviceSynchronize());
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[keto patch]   %-10s %.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
+    const DevSnapshot &D = B.dev;
+    const uint32_t N = D.n_nodes;
+    const uint64_t M = (uint64_t)D.n_uuids + N;  // subject index space
+    if (n_store >= (1ull << 32) || n_touched >= (1ull << 31)) return nullptr;
+    // a base advanced in place holds rows outside its CSR extents: the shifted copies below
+    // assume none (a full build instead)
+    if (B.room.moved) return nullptr;
+    // ---- 1. place the touched tuples in the base's node space -----------------------------------
+    Placed P;
+    if (!place_touched(B, touched, is_ins, n_touched, P)) return nullptr;
+    const std::vector<keto_tuple> &ht = P.ht;
+    const std::vector<uint4> &pl = P.pl;
+    const DevSnapshot &Dp = P.Dp;
+    const std::vector<uint4> &ext = P.ext;
     std::unordered_map<uint32_t, size_t> node_at, subj_at;  // node / subject index -> position in the sorted lists
     std::vector<Touched> tn, ts;
     std::vector<uint32_t> idrow_slots;
@@ -704,12 +735,13 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     s.ext = ext;
     DevSnapshot &X = s.dev;
     X = Dp;  // (the base's arrays, its ext table or this patch's)
+    X.reloc = nullptr;  // (a copy patch is not advanced in place: no room kept)
     for (const void *p : {(const void *)D.weight, (const void *)D.ent_obj, (const void *)D.slot_rel, (const void *)D.vkey,
                           (const void *)D.ns, (const void *)D.nsrel, (const void *)D.ops, (const void *)D.op_children,
                           (const void *)D.op_items, (const void *)D.or_items, (const void *)D.ent_rank})
         s.share(B, p);
-    if (ext_dev) {
-        s.own(ext_guard.release(), 16ull * ((uint64_t)Dp.ext_mask + 1));
+    if (P.ext_dev) {
+        s.own(P.ext_dev.release(), 16ull * ((uint64_t)Dp.ext_mask + 1));
     } else if (D.ext) {
         s.share(B, D.ext);
     }
@@ -880,8 +912,416 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
                         "probe +%zu -%zu keys, %.2f ms\n", (unsigned long long)n_touched, m, ms,
                 (unsigned long long)(rmatch.size() + smatch.size()), flip.size(), ins_keys.size(), del_keys.size(),
                 s.info.build_seconds * 1e3);
-    taken.keep = true;
+    P.taken.keep = true;
     return S.release();
+}
+
+// ---- the in-place advance ---------------------------------------------------------------------
+// keto_store_snapshot_advance: the transactions since a store snapshot's version applied to its own
+// rows, work proportional to the rows they name -- the reference's write path touches only its
+// rows (persistence/sql/relationtuples.go:104-126 WriteRelationTuples, :168-189 DeleteRelationTuples,
+// :277-287 TransactRelationTuples).  A store snapshot keeps room for it (snapshot.cpp, BuildOpts::room):
+//   - every all-row entry's shard key (the high 64 bits of its shard_id): a row is kept in shard
+//     order (traverser.go:88, relationtuples.go:216) by inserting a new tuple before the first key
+//     above its own; a key equal to its own cannot be ordered without the low half and the store
+//     position -- the advance declines (a full build orders it);
+//   - slack past the value arrays (all_subj, rev_nodes, set_dst): a row that grows is rewritten at
+//     the tail, one that does not where it lies;
+//   - a relocation table for the offset arrays (all_off, rev_off): a moved row's word becomes
+//     ROW_MOVED | its entry {begin, end, the word's original offset} (layout.hpp row_span), set_row
+//     is an extent already.
+// The probe hash, EDGE_LEAF flags, relation info and reachability tables follow as in the copy
+// patch, where they lie.  Nothing in flight may read the snapshot: the caller serves from another
+// one meanwhile.  Every way to decline (placement, spares, a key tie, slack, relocation entries,
+// probe load) is decided before the first write, so a declined advance leaves it as it was.
+namespace {
+// old rows of the touched nodes: {offset word, begin, end, original offset of a moved row}, set row
+__global__ __launch_bounds__(BLK) void k_adv_old_nodes(DevSnapshot s, const uint32_t *nodes, uint32_t m, uint4 *all, uint4 *set) {
+    const uint64_t j = gid();
+    if (j >= m) return;
+    const uint32_t c = nodes[j], w = s.all_off[c];
+    uint32_t b, e;
+    row_span(s.all_off, s.reloc, c, b, e);
+    all[j] = make_uint4(w, b, e, (w & ROW_MOVED) ? s.reloc[w & ~ROW_MOVED].z : 0u);
+    set[j] = s.set_row[c];
+}
+__global__ __launch_bounds__(BLK) void k_adv_old_subjects(DevSnapshot s, const uint32_t *subj, uint32_t m, uint4 *out) {
+    const uint64_t j = gid();
+    if (j >= m) return;
+    const uint32_t v = subj[j], w = s.rev_off[v];
+    uint32_t b, e;
+    row_span(s.rev_off, s.reloc, v, b, e);
+    out[j] = make_uint4(w, b, e, (w & ROW_MOVED) ? s.reloc[w & ~ROW_MOVED].z : 0u);
+}
+__global__ __launch_bounds__(BLK) void k_gather_ranges64(const unsigned long long *src, const uint2 *ranges, const uint32_t *dst_off,
+                                                         uint32_t m, unsigned long long *dst) {
+    const uint64_t i = gid();
+    if (i >= m) return;
+    for (uint32_t k = ranges[i].x, o = dst_off[i]; k < ranges[i].y; k++, o++) dst[o] = src[k];
+}
+// new row contents: row j = {destination, source offset in vals, length, 0}
+template <class T>
+__global__ __launch_bounds__(BLK) void k_put_vals(T *dst, const uint4 *rows, uint32_t m, const T *vals) {
+    const uint64_t j = gid();
+    if (j >= m) return;
+    const uint4 r = rows[j];
+    for (uint32_t k = 0; k < r.z; k++) dst[r.x + k] = vals[r.y + k];
+}
+__global__ __launch_bounds__(BLK) void k_put_words(uint32_t *dst, const uint2 *iv, uint32_t m) {
+    const uint64_t j = gid();
+    if (j < m) dst[iv[j].x] = iv[j].y;
+}
+__global__ __launch_bounds__(BLK) void k_put_reloc(uint4 *reloc, const uint32_t *at, const uint4 *val, uint32_t m) {
+    const uint64_t j = gid();
+    if (j < m) reloc[at[j]] = val[j];
+}
+uint64_t shard_hi_host(const keto_tuple &t) {
+    uint64_t h = 0;
+    for (int k = 0; k < 8; k++) h = (h << 8) | t.shard_id[k];
+    return h;
+}
+}  // namespace
+
+bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_ins, uint64_t n_touched, uint64_t n_store) {
+    using build::DevBuf;
+    const auto t0 = std::chrono::steady_clock::now();
+    KETO_HIP(hipSetDevice(S.device));
+    static const bool verbose = getenv("KETO_PATCH_VERBOSE") != nullptr;
+    auto tp = t0;
+    auto phase = [&](const char *what) {
+        if (!verbose) return;
+        KETO_HIP(hipDeviceSynchronize());
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[keto advance] %-10s %.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
+    Snapshot::Room &R = S.room;
+    DevSnapshot &D = S.dev;
+    if (!R.all_shard || !D.reloc || n_touched >= (1ull << 31) || n_store >= ROW_MOVED) return false;
+    for (const void *p : {(const void *)D.all_off, (const void *)D.all_subj, (const void *)D.rev_off, (const void *)D.rev_nodes,
+                          (const void *)D.set_row, (const void *)D.set_dst, (const void *)D.probe, (const void *)D.reloc,
+                          (const void *)R.all_shard})
+        if (!S.sole(p)) return false;  // an array another snapshot shares is not this one's to rewrite
+    // ---- 1. placement (new objects on spares), as the copy patch ---------------------------------
+    Placed P;
+    if (!place_touched(S, touched, is_ins, n_touched, P)) return false;
+    const std::vector<keto_tuple> &ht = P.ht;
+    const std::vector<uint4> &pl = P.pl;
+    // the log entries naming each touched row / subject, in log order
+    std::unordered_map<uint32_t, uint32_t> node_at, subj_at;
+    std::vector<uint32_t> key_n, key_s, idrow_nodes;
+    std::vector<std::vector<uint32_t>> ops_n, ops_s;
+    for (uint64_t i = 0; i < n_touched; i++) {
+        if (pl[i].x == NONE32 || pl[i].y == NONE32) {
+            if (is_ins[i]) return false;  // an insert with no place: build in full
+            continue;                     // a delete naming no node deletes nothing the snapshot holds
+        }
+        auto a = node_at.emplace(pl[i].x, (uint32_t)key_n.size());
+        if (a.second) {
+            key_n.push_back(pl[i].x);
+            ops_n.emplace_back();
+        }
+        ops_n[a.first->second].push_back((uint32_t)i);
+        auto b = subj_at.emplace(pl[i].z, (uint32_t)key_s.size());
+        if (b.second) {
+            key_s.push_back(pl[i].z);
+            ops_s.emplace_back();
+        }
+        ops_s[b.first->second].push_back((uint32_t)i);
+        if (is_ins[i] && ht[i].subj_kind == 0) idrow_nodes.push_back(pl[i].x);
+    }
+    const uint32_t m = (uint32_t)key_n.size(), ms = (uint32_t)key_s.size();
+    auto up = [](const auto &v) {
+        using T = typename std::decay_t<decltype(v)>::value_type;
+        DevBuf b(std::max<size_t>(1, v.size()) * sizeof(T));
+        if (!v.empty()) KETO_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+        return b;
+    };
+    phase("place");
+    // ---- 2. the touched rows as they are ----------------------------------------------------------
+    std::vector<uint4> old_all(m), old_set(m), old_rev(ms);
+    DevBuf d_key_n = up(key_n), d_key_s = up(key_s);
+    if (m) {
+        DevBuf a(16ull * m), b(16ull * m);
+        hipLaunchKernelGGL(k_adv_old_nodes, grid_for(m), dim3(BLK), 0, 0, D, d_key_n.u32(), m, static_cast<uint4 *>(a.p),
+                           static_cast<uint4 *>(b.p));
+        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemcpy(old_all.data(), a.p, 16ull * m, hipMemcpyDeviceToHost));
+        KETO_HIP(hipMemcpy(old_set.data(), b.p, 16ull * m, hipMemcpyDeviceToHost));
+    }
+    if (ms) {
+        DevBuf a(16ull * ms);
+        hipLaunchKernelGGL(k_adv_old_subjects, grid_for(ms), dim3(BLK), 0, 0, D, d_key_s.u32(), ms, static_cast<uint4 *>(a.p));
+        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemcpy(old_rev.data(), a.p, 16ull * ms, hipMemcpyDeviceToHost));
+    }
+    auto gather = [&](const std::vector<uint4> &old, const uint32_t *src32, const unsigned long long *src64, std::vector<uint32_t> &off,
+                      std::vector<uint32_t> &v32, std::vector<unsigned long long> &v64) {
+        const uint32_t k = (uint32_t)old.size();
+        std::vector<uint2> rng(k);
+        off.assign(k + 1, 0);
+        for (uint32_t j = 0; j < k; j++) {
+            rng[j] = make_uint2(old[j].y, old[j].z);
+            off[j + 1] = off[j] + (old[j].z - old[j].y);
+        }
+        v32.resize(off[k]);
+        if (!k || !off[k]) return;
+        DevBuf d_rng = up(rng), d_off = up(off), g(4ull * off[k]);
+        hipLaunchKernelGGL(k_gather_ranges, grid_for(k), dim3(BLK), 0, 0, src32, static_cast<const uint2 *>(d_rng.p), d_off.u32(), k,
+                           g.u32());
+        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemcpy(v32.data(), g.p, 4ull * off[k], hipMemcpyDeviceToHost));
+        if (src64) {
+            v64.resize(off[k]);
+            DevBuf g64(8ull * off[k]);
+            hipLaunchKernelGGL(k_gather_ranges64, grid_for(k), dim3(BLK), 0, 0, src64, static_cast<const uint2 *>(d_rng.p), d_off.u32(),
+                               k, static_cast<unsigned long long *>(g64.p));
+            KETO_HIP(hipGetLastError());
+            KETO_HIP(hipMemcpy(v64.data(), g64.p, 8ull * off[k], hipMemcpyDeviceToHost));
+        }
+    };
+    std::vector<uint32_t> all_off0, all_v0, rev_off0, rev_v0;
+    std::vector<unsigned long long> shard_v0, unused;
+    gather(old_all, D.all_subj, R.all_shard, all_off0, all_v0, shard_v0);
+    gather(old_rev, D.rev_nodes, nullptr, rev_off0, rev_v0, unused);
+    phase("gather");
+    // ---- 3. the new rows: the log applied in order (inserts then deletes of each transaction) ------
+    std::vector<uint32_t> all_v, set_v, rev_v, all_len(m), set_len(m), rev_len(ms);
+    std::vector<unsigned long long> shard_v;
+    long long d_all = 0, d_set = 0, d_rev = 0;
+    for (uint32_t j = 0; j < m; j++) {
+        std::vector<std::pair<unsigned long long, uint32_t>> row;
+        for (uint32_t k = all_off0[j]; k < all_off0[j + 1]; k++) row.emplace_back(shard_v0[k], all_v0[k]);
+        for (uint32_t i : ops_n[j]) {
+            const uint32_t v = pl[i].y;
+            if (is_ins[i]) {
+                const unsigned long long h = shard_hi_host(ht[i]);
+                auto it = std::lower_bound(row.begin(), row.end(), h,
+                                           [](const std::pair<unsigned long long, uint32_t> &x, unsigned long long k) { return x.first < k; });
+                if (it != row.end() && it->first == h) return false;  // a key tie: only the full build orders it
+                row.insert(it, std::make_pair(h, v));
+            } else {  // every tuple of the row with this subject (relationtuples.go:168-189)
+                row.erase(std::remove_if(row.begin(), row.end(), [v](const std::pair<unsigned long long, uint32_t> &x) { return x.second == v; }),
+                          row.end());
+            }
+        }
+        all_len[j] = (uint32_t)row.size();
+        uint32_t ns = 0;
+        for (const auto &x : row) {
+            all_v.push_back(x.second);
+            shard_v.push_back(x.first);
+            if (x.second & SKEY_SET) {
+                set_v.push_back(x.second & ~SKEY_SET);
+                ns++;
+            }
+        }
+        set_len[j] = ns;
+        d_all += (long long)all_len[j] - (old_all[j].z - old_all[j].y);
+        d_set += (long long)ns - (old_set[j].y - old_set[j].x);
+    }
+    std::vector<unsigned long long> ins_keys, del_keys;  // probe keys: a heavy subject's distinct nodes
+    for (uint32_t j = 0; j < ms; j++) {
+        std::vector<uint32_t> row(rev_v0.begin() + rev_off0[j], rev_v0.begin() + rev_off0[j + 1]), old = row;
+        for (uint32_t i : ops_s[j]) {
+            const uint32_t node = pl[i].x;
+            if (is_ins[i]) row.push_back(node);
+            else row.erase(std::remove(row.begin(), row.end(), node), row.end());
+        }
+        std::sort(row.begin(), row.end());
+        rev_len[j] = (uint32_t)row.size();
+        rev_v.insert(rev_v.end(), row.begin(), row.end());
+        d_rev += (long long)rev_len[j] - (long long)old.size();
+        const bool was_heavy = old.size() > PROBE_K, heavy = row.size() > PROBE_K;
+        std::sort(old.begin(), old.end());
+        old.erase(std::unique(old.begin(), old.end()), old.end());
+        row.erase(std::unique(row.begin(), row.end()), row.end());
+        if (!was_heavy) old.clear();
+        if (!heavy) row.clear();
+        const uint64_t v = key_s[j];
+        std::vector<uint32_t> d;
+        std::set_difference(row.begin(), row.end(), old.begin(), old.end(), std::back_inserter(d));
+        for (uint32_t x : d) ins_keys.push_back(((v << 32) | x) + 1);
+        d.clear();
+        std::set_difference(old.begin(), old.end(), row.begin(), row.end(), std::back_inserter(d));
+        for (uint32_t x : d) del_keys.push_back(((v << 32) | x) + 1);
+    }
+    if ((long long)S.info.n_tuples + d_all != (long long)n_store || d_rev != d_all) return false;  // (the log and the store disagree)
+    const uint64_t probe_slots = 2ull * ((uint64_t)D.probe_mask + 1);
+    if (S.probe_used + ins_keys.size() > probe_slots * 3 / 4) return false;  // too full: build in full
+    // ---- 4. where each row goes: where it lies if it fits, else the tail; moved offset rows get a
+    // relocation entry -------------------------------------------------------------------------------
+    uint64_t at_all = R.all_tail, at_rev = R.rev_tail, at_set = R.set_tail;
+    uint32_t n_reloc = R.reloc_used;
+    std::vector<uint4> put_all, put_rev;  // {destination, source, length, 0}
+    std::vector<uint2> all_words, rev_words;
+    std::vector<uint32_t> reloc_at;
+    std::vector<uint4> reloc_val;
+    auto place_row = [&](const uint4 &old, uint32_t len, uint32_t src, uint32_t key, uint64_t &tail, std::vector<uint4> &put,
+                         std::vector<uint2> &words) {
+        const uint32_t ob = old.y, oe = old.z;
+        uint32_t nb = ob;
+        if (len > oe - ob) {
+            nb = (uint32_t)tail;
+            tail += len;
+        }
+        if (len) put.push_back(make_uint4(nb, src, len, 0));
+        if (nb == ob && len == oe - ob) return;  // the same extent
+        if (old.x & ROW_MOVED) {
+            reloc_at.push_back(old.x & ~ROW_MOVED);
+            reloc_val.push_back(make_uint4(nb, nb + len, old.w, 0));
+        } else {
+            reloc_at.push_back(n_reloc);
+            reloc_val.push_back(make_uint4(nb, nb + len, old.x, 0));
+            words.push_back(make_uint2(key, ROW_MOVED | n_reloc));
+            n_reloc++;
+        }
+    };
+    std::vector<uint32_t> set_begin(m), set_voff(m + 1, 0);
+    for (uint32_t j = 0, src = 0; j < m; j++) {
+        place_row(old_all[j], all_len[j], src, key_n[j], at_all, put_all, all_words);
+        src += all_len[j];
+        const uint32_t ob = old_set[j].x, oe = old_set[j].y;
+        set_begin[j] = ob;
+        if (set_len[j] > oe - ob) {
+            set_begin[j] = (uint32_t)at_set;
+            at_set += set_len[j];
+        }
+        set_voff[j + 1] = set_voff[j] + set_len[j];
+    }
+    for (uint32_t j = 0, src = 0; j < ms; j++) {
+        place_row(old_rev[j], rev_len[j], src, key_s[j], at_rev, put_rev, rev_words);
+        src += rev_len[j];
+    }
+    if (at_all > R.all_cap || at_rev > R.rev_cap || at_set > R.set_cap || n_reloc > R.reloc_cap) return false;  // no room left
+    phase("rows");
+    // ---- 5. the writes (committed from here on) -----------------------------------------------------
+    P.taken.keep = true;
+    if (P.ext_dev) {  // the objects this advance created: the new ext table replaces the old one
+        const void *old_ext = D.ext;
+        S.own(P.ext_dev.release(), 16ull * ((uint64_t)P.Dp.ext_mask + 1));
+        D.ext = P.Dp.ext;
+        D.ext_mask = P.Dp.ext_mask;
+        if (old_ext) S.drop(old_ext);
+        S.ext = P.ext;
+    }
+    uint32_t *all_off = const_cast<uint32_t *>(D.all_off), *rev_off = const_cast<uint32_t *>(D.rev_off);
+    uint32_t *all_subj = const_cast<uint32_t *>(D.all_subj), *rev_nodes = const_cast<uint32_t *>(D.rev_nodes);
+    uint32_t *set_dst = const_cast<uint32_t *>(D.set_dst);
+    uint4 *set_row = const_cast<uint4 *>(D.set_row), *reloc = const_cast<uint4 *>(D.reloc);
+    DevBuf d_all_v = up(all_v), d_shard_v = up(shard_v), d_rev_v = up(rev_v), d_put_all = up(put_all), d_put_rev = up(put_rev);
+    if (!put_all.empty()) {
+        hipLaunchKernelGGL(k_put_vals<uint32_t>, grid_for(put_all.size()), dim3(BLK), 0, 0, all_subj, static_cast<const uint4 *>(d_put_all.p),
+                           (uint32_t)put_all.size(), d_all_v.u32());
+        hipLaunchKernelGGL(k_put_vals<unsigned long long>, grid_for(put_all.size()), dim3(BLK), 0, 0, R.all_shard,
+                           static_cast<const uint4 *>(d_put_all.p), (uint32_t)put_all.size(),
+                           static_cast<const unsigned long long *>(d_shard_v.p));
+    }
+    if (!put_rev.empty())
+        hipLaunchKernelGGL(k_put_vals<uint32_t>, grid_for(put_rev.size()), dim3(BLK), 0, 0, rev_nodes, static_cast<const uint4 *>(d_put_rev.p),
+                           (uint32_t)put_rev.size(), d_rev_v.u32());
+    KETO_HIP(hipGetLastError());
+    if (!reloc_at.empty()) {
+        DevBuf d_at = up(reloc_at), d_val = up(reloc_val);
+        hipLaunchKernelGGL(k_put_reloc, grid_for(reloc_at.size()), dim3(BLK), 0, 0, reloc, d_at.u32(), static_cast<const uint4 *>(d_val.p),
+                           (uint32_t)reloc_at.size());
+        KETO_HIP(hipGetLastError());
+    }
+    for (int w = 0; w < 2; w++) {
+        const std::vector<uint2> &words = w ? rev_words : all_words;
+        if (words.empty()) continue;
+        DevBuf d_w = up(words);
+        hipLaunchKernelGGL(k_put_words, grid_for(words.size()), dim3(BLK), 0, 0, w ? rev_off : all_off, static_cast<const uint2 *>(d_w.p),
+                           (uint32_t)words.size());
+        KETO_HIP(hipGetLastError());
+    }
+    // set rows: extents, then edges (flags from the new rows) and their inline copies
+    if (m) {
+        DevBuf d_sb = up(set_begin), d_sl = up(set_len), d_sv = up(set_v), d_svo = up(set_voff);
+        hipLaunchKernelGGL(k_put_setrow_extent, grid_for(m), dim3(BLK), 0, 0, set_row, d_key_n.u32(), d_sb.u32(), d_sl.u32(), m);
+        hipLaunchKernelGGL(k_put_edges, grid_for(m), dim3(BLK), 0, 0, D, set_row, set_dst, d_key_n.u32(), d_sv.u32(), d_svo.u32(), m);
+        KETO_HIP(hipGetLastError());
+    }
+    std::vector<uint32_t> flip;  // set rows that changed between empty and not: their parents' EDGE_LEAF
+    for (uint32_t j = 0; j < m; j++)
+        if ((set_len[j] == 0) != (old_set[j].x == old_set[j].y)) flip.push_back(key_n[j]);
+    if (D.edge_leaf && !flip.empty()) {
+        DevBuf d_flip = up(flip);
+        hipLaunchKernelGGL(k_flip_leaf, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, D, set_row, set_dst, rev_off, rev_nodes,
+                           d_flip.u32(), (uint32_t)flip.size());
+        hipLaunchKernelGGL(k_fix_inline, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, D, set_row, set_dst, rev_off, rev_nodes,
+                           d_flip.u32(), (uint32_t)flip.size());
+        KETO_HIP(hipGetLastError());
+    }
+    if (!ins_keys.empty() || !del_keys.empty()) {
+        std::vector<unsigned long long> keys(ins_keys);
+        keys.insert(keys.end(), del_keys.begin(), del_keys.end());
+        DevBuf d_keys = up(keys);
+        hipLaunchKernelGGL(k_probe_apply, grid_for(keys.size()), dim3(BLK), 0, 0,
+                           reinterpret_cast<unsigned long long *>(const_cast<uint4 *>(D.probe)), (uint64_t)D.probe_mask,
+                           static_cast<const unsigned long long *>(d_keys.p), (uint32_t)ins_keys.size(), (uint32_t)del_keys.size());
+        KETO_HIP(hipGetLastError());
+    }
+    phase("write");
+    // relation info: RI_SETROWS of the slots whose rows flipped (a slot emptied keeps it while any
+    // row of it holds a subject set), RI_IDROWS grows by the inserts
+    {
+        auto slot_of = [&](uint32_t node) {
+            const uint32_t ns = S.ns_of(node);
+            return S.ns[ns].slot_base + (node - S.ns[ns].node_base) % S.ns[ns].n_slots;
+        };
+        std::vector<uint32_t> emptied;
+        for (uint32_t j = 0; j < m; j++) {
+            if ((set_len[j] == 0) == (old_set[j].x == old_set[j].y)) continue;
+            const uint32_t gs = slot_of(key_n[j]);
+            if (set_len[j]) S.relinfo[gs] |= RI_SETROWS;
+            else emptied.push_back(gs);
+        }
+        std::sort(emptied.begin(), emptied.end());
+        emptied.erase(std::unique(emptied.begin(), emptied.end()), emptied.end());
+        if (!emptied.empty()) {
+            std::vector<uint4> job;  // {global slot, first node, nodes, stride}
+            for (uint32_t gs : emptied) {
+                uint32_t ns = 0;
+                while (ns + 1 < S.n_ns && S.ns[ns + 1].slot_base <= gs) ns++;
+                const NsDev &nd = S.ns[ns];
+                const uint32_t ents = (S.ns[ns + 1].node_base - nd.node_base) / std::max(1u, nd.n_slots);
+                job.push_back(make_uint4(gs, nd.node_base + (gs - nd.slot_base), ents, nd.n_slots));
+            }
+            DevBuf d_job = up(job), flag(4ull * job.size());
+            KETO_HIP(hipMemset(flag.p, 0, 4ull * job.size()));
+            hipLaunchKernelGGL(k_slot_any, dim3((uint32_t)num_cus(S.device) * 4), dim3(BLK), 0, 0, set_row,
+                               static_cast<const uint4 *>(d_job.p), (uint32_t)job.size(), flag.u32());
+            KETO_HIP(hipGetLastError());
+            std::vector<uint32_t> hf(job.size());
+            KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * job.size(), hipMemcpyDeviceToHost));
+            for (size_t k = 0; k < job.size(); k++)
+                S.relinfo[job[k].x] = (S.relinfo[job[k].x] & ~RI_SETROWS) | (hf[k] ? RI_SETROWS : 0u);
+        }
+        for (uint32_t node : idrow_nodes) S.relinfo[slot_of(node)] |= RI_IDROWS;
+        uint32_t *ri = S.sole(D.relinfo) ? const_cast<uint32_t *>(D.relinfo)
+                                         : static_cast<uint32_t *>(S.alloc(std::max<size_t>(1, S.relinfo.size()) * 4 + 16));
+        if (!S.relinfo.empty()) KETO_HIP(hipMemcpy(ri, S.relinfo.data(), 4 * S.relinfo.size(), hipMemcpyHostToDevice));
+        D.relinfo = ri;
+    }
+    R.all_tail = at_all;
+    R.rev_tail = at_rev;
+    R.set_tail = at_set;
+    R.reloc_used = n_reloc;
+    R.moved = true;
+    S.probe_used += ins_keys.size();
+    S.info.n_tuples = n_store;
+    S.info.n_rev_entries = n_store;
+    S.info.n_set_edges = (uint64_t)((long long)S.info.n_set_edges + d_set);
+    KETO_HIP(hipDeviceSynchronize());
+    phase("relinfo");
+    patch_reach(S, S, key_n);  // the reaches the changed rows move, where they lie
+    phase("reach");
+    S.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (verbose)
+        fprintf(stderr, "[keto advance] %llu touched tuples: %u rows, %u subjects, %zu moved, %zu leaf flips, probe +%zu -%zu keys, "
+                        "%.2f ms\n", (unsigned long long)n_touched, m, ms, reloc_at.size(), flip.size(), ins_keys.size(),
+                del_keys.size(), S.info.build_seconds * 1e3);
+    return true;
 }
 
 }  // namespace keto

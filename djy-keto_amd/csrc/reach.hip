@@ -232,12 +232,14 @@ __global__ __launch_bounds__(RB) void k_seen_init(const uint32_t *nodes, uint32_
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         (void)seen_insert(seen, mask, nodes[i]);
 }
-__global__ __launch_bounds__(RB) void k_anc_level(const uint32_t *front, uint32_t n, const uint32_t *rev_off, const uint32_t *rev_nodes,
-                                                  uint32_t n_uuids, const NsDev *ns, uint32_t n_ns, const uint32_t *relinfo,
+__global__ __launch_bounds__(RB) void k_anc_level(const uint32_t *front, uint32_t n, const uint32_t *rev_off, const uint4 *reloc,
+                                                  const uint32_t *rev_nodes, uint32_t n_uuids, const NsDev *ns, uint32_t n_ns, const uint32_t *relinfo,
                                                   uint32_t *seen, uint32_t mask, uint32_t *next, uint32_t *next_n, uint32_t cap) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t si = (uint64_t)n_uuids + front[i];
-        for (uint32_t j = rev_off[si], e = rev_off[si + 1]; j < e; j++) {
+        uint32_t j, e;
+        row_span(rev_off, reloc, si, j, e);
+        for (; j < e; j++) {
             const uint32_t p = rev_nodes[j];
             const NsDev nd = ns[ns_of_node(ns, n_ns, p)];
             if (!(relinfo[nd.slot_base + (p - nd.node_base) % nd.n_slots] & RI_REACH)) continue;
@@ -300,7 +302,9 @@ uint64_t tabled_slots(Snapshot &s, std::vector<uint32_t> &base, std::vector<uint
 void reach_bits(Snapshot &s, const std::vector<uint32_t> &base) {
     for (size_t g = 0; g < s.relinfo.size(); g++)
         s.relinfo[g] = (s.relinfo[g] & ~RI_REACH) | (g < base.size() && base[g] != NONE32 ? RI_REACH : 0u);
-    uint32_t *ri = static_cast<uint32_t *>(s.alloc(4 * std::max<size_t>(1, s.relinfo.size()) + 16));
+    // (an advance writes the snapshot's own array where it lies: engines read s.dev at launch)
+    uint32_t *ri = s.dev.relinfo && s.sole(s.dev.relinfo) ? const_cast<uint32_t *>(s.dev.relinfo)
+                                                          : static_cast<uint32_t *>(s.alloc(4 * std::max<size_t>(1, s.relinfo.size()) + 16));
     if (!s.relinfo.empty()) KETO_HIP(hipMemcpy(ri, s.relinfo.data(), 4 * s.relinfo.size(), hipMemcpyHostToDevice));
     s.dev.relinfo = ri;
 }
@@ -312,9 +316,12 @@ void reach_bits(Snapshot &s, const std::vector<uint32_t> &base) {
 void build_reach(Snapshot &s) {
     using build::DevBuf;
     DevSnapshot &D = s.dev;
+    for (const void *p : {(const void *)D.reach_base, (const void *)D.reach_idx, (const void *)D.reach_pool})
+        if (p && s.sole(p)) s.drop(p);  // (an advance rebuilding its own tables)
     D.reach_base = nullptr;
     D.reach_idx = nullptr;
     D.reach_pool = nullptr;
+    s.reach_pool_cap = 0;
     s.info.n_reach = 0;
     s.reach_slots.clear();
     s.reach_cand = s.reach_pool_n = 0;
@@ -352,7 +359,8 @@ void build_reach(Snapshot &s) {
     const unsigned long long total = cn[0];
     if (total >= (1ull << 31)) return;  // (the allocation of idx goes back with the snapshot)
     build::scan_excl(lens.u32(), n_cand);
-    uint32_t *pool = static_cast<uint32_t *>(s.alloc(4 * total + 16));
+    const uint64_t pool_cap = s.room.reloc_cap ? total + total / 16 + (1u << 16) : total;  // (advances append)
+    uint32_t *pool = static_cast<uint32_t *>(s.alloc(4 * pool_cap + 16));
     hipLaunchKernelGGL(k_reach<true>, grid, dim3(RB), 0, 0, R, nullptr, n_cand, idx, lens.u32(), pool, 0u, nullptr);
     KETO_HIP(hipGetLastError());
     uint32_t *d_base = static_cast<uint32_t *>(s.alloc(4ull * n_slots + 16));
@@ -366,6 +374,7 @@ void build_reach(Snapshot &s) {
     s.reach_slots = std::move(base);
     s.reach_cand = n_cand;
     s.reach_pool_n = total;
+    s.reach_pool_cap = pool_cap;
 }
 
 void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &touched_nodes) {
@@ -421,7 +430,7 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
         const uint64_t n = total - lo;
         KETO_HIP(hipMemset(cnt.p, 0, 4));
         hipLaunchKernelGGL(k_anc_level, dim3((uint32_t)std::min<uint64_t>(4096, (n + RB - 1) / RB)), dim3(RB), 0, 0, all + lo, (uint32_t)n,
-                           D.rev_off, D.rev_nodes, D.n_uuids, D.ns, D.n_ns, d_ri.u32(), seen.u32(), mask, all + total, cnt.u32(),
+                           D.rev_off, D.reloc, D.rev_nodes, D.n_uuids, D.ns, D.n_ns, d_ri.u32(), seen.u32(), mask, all + total, cnt.u32(),
                            (uint32_t)(VCAP - total));
         KETO_HIP(hipGetLastError());
         uint32_t got = 0;
@@ -446,8 +455,11 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
     ReachIn R{D.set_row, D.set_dst, D.edge_mask, D.ns, D.n_ns, D.relinfo, static_cast<const uint4 *>(d_ts.p), (uint32_t)ts.size(),
               n_cand, cap};
     const dim3 grid((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, ((uint64_t)nc + RB / 64 - 1) / (RB / 64))));
-    uint4 *idx = static_cast<uint4 *>(s.alloc(16 * n_cand + 16));
-    KETO_HIP(hipMemcpy(idx, Bd.reach_idx, 16 * n_cand, hipMemcpyDeviceToDevice));
+    // a copy of the base's records, or (an advance) the snapshot's own, rewritten where they lie
+    const bool in_place = &s == &B && s.sole(D.reach_idx) && s.sole(D.reach_pool);
+    const uint64_t base_pool_n = B.reach_pool_n;
+    uint4 *idx = in_place ? const_cast<uint4 *>(D.reach_idx) : static_cast<uint4 *>(s.alloc(16 * n_cand + 16));
+    if (!in_place) KETO_HIP(hipMemcpy(idx, Bd.reach_idx, 16 * n_cand, hipMemcpyDeviceToDevice));
     if (nc) {
         hipLaunchKernelGGL(k_reach<false>, grid, dim3(RB), 0, 0, R, cl.u32(), (uint64_t)nc, idx, lens.u32(), nullptr, 0u,
                            static_cast<unsigned long long *>(tot.p));
@@ -455,29 +467,41 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
     }
     unsigned long long cn[2] = {0, 0};
     KETO_HIP(hipMemcpy(cn, tot.p, 16, hipMemcpyDeviceToHost));
-    const uint64_t pool_n = B.reach_pool_n + cn[0];
+    const uint64_t pool_n = base_pool_n + cn[0];
     if (pool_n >= (1ull << 31)) return build_reach(s);
     if (nc) build::scan_excl(lens.u32(), nc);
-    uint32_t *pool = static_cast<uint32_t *>(s.alloc(4 * pool_n + 16));
-    if (B.reach_pool_n) KETO_HIP(hipMemcpy(pool, Bd.reach_pool, 4 * B.reach_pool_n, hipMemcpyDeviceToDevice));
+    uint32_t *pool;
+    uint64_t pool_cap = pool_n;
+    if (in_place && pool_n <= s.reach_pool_cap) {
+        pool = const_cast<uint32_t *>(D.reach_pool);  // appended past the entries in use
+        pool_cap = s.reach_pool_cap;
+    } else {
+        if (in_place) pool_cap = pool_n + pool_n / 16 + (1u << 16);
+        pool = static_cast<uint32_t *>(s.alloc(4 * pool_cap + 16));
+        if (base_pool_n) KETO_HIP(hipMemcpy(pool, Bd.reach_pool, 4 * base_pool_n, hipMemcpyDeviceToDevice));
+        if (in_place) s.drop(D.reach_pool);
+    }
     if (nc) {
         hipLaunchKernelGGL(k_reach<true>, grid, dim3(RB), 0, 0, R, cl.u32(), (uint64_t)nc, idx, lens.u32(), pool,
-                           (uint32_t)B.reach_pool_n, nullptr);
+                           (uint32_t)base_pool_n, nullptr);
         KETO_HIP(hipGetLastError());
     }
     if (verbose) fprintf(stderr, "[keto patch]     reach: %zu touched nodes, %llu with ancestors, %u tabled walked again\n", t0.size(),
                          (unsigned long long)total, nc);
     phase("walks");
-    uint32_t *db = static_cast<uint32_t *>(s.alloc(4ull * base.size() + 16));
-    KETO_HIP(hipMemcpy(db, base.data(), 4ull * base.size(), hipMemcpyHostToDevice));
+    if (!in_place) {  // (in place: the same slots, the same array)
+        uint32_t *db = static_cast<uint32_t *>(s.alloc(4ull * base.size() + 16));
+        KETO_HIP(hipMemcpy(db, base.data(), 4ull * base.size(), hipMemcpyHostToDevice));
+        D.reach_base = db;
+    }
     KETO_HIP(hipStreamSynchronize(nullptr));
-    D.reach_base = db;
     D.reach_idx = idx;
     D.reach_pool = pool;
     reach_bits(s, base);
     s.reach_slots = std::move(base);
     s.reach_cand = n_cand;
     s.reach_pool_n = pool_n;
+    s.reach_pool_cap = pool_cap;
     KETO_HIP(hipMemset(cnt.p, 0, 8));
     hipLaunchKernelGGL(k_count_tabled, dim3((uint32_t)std::min<uint64_t>(4096, (n_cand + RB - 1) / RB)), dim3(RB), 0, 0, idx, n_cand,
                        static_cast<unsigned long long *>(cnt.p));

@@ -132,6 +132,23 @@ void Snapshot::share(const Snapshot &o, const void *p) {
     throw Error(KETO_E_INVALID, "shared array outside the base snapshot's allocations");
 }
 
+bool Snapshot::sole(const void *p) const {
+    for (size_t i = 0; i < allocs.size(); i++)
+        if (allocs[i] == p) return owned[i].use_count() == 1;
+    return false;
+}
+
+void Snapshot::drop(const void *p) {
+    for (size_t i = 0; i < allocs.size(); i++)
+        if (allocs[i] == p) {
+            info.device_bytes -= alloc_bytes[i];
+            allocs.erase(allocs.begin() + (ptrdiff_t)i);
+            alloc_bytes.erase(alloc_bytes.begin() + (ptrdiff_t)i);
+            owned.erase(owned.begin() + (ptrdiff_t)i);
+            return;
+        }
+}
+
 uint32_t Snapshot::ns_of(uint32_t node) const {
     // last ns with node_base <= node (empty namespaces share bases; take the last)
     uint32_t lo = 0, hi = n_ns;
@@ -458,9 +475,19 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     // index covers ghosts too (a subject set another rank owns is a subject of tuples here)
     ro.all_off = static_cast<uint32_t *>(dalloc(4 * ((uint64_t)NO + 1)));
     ro.rev_off = static_cast<uint32_t *>(dalloc(4 * (n_subj_idx + 1)));
-    ro.all_subj = static_cast<uint32_t *>(dalloc(4 * n));
-    ro.rev_nodes = static_cast<uint32_t *>(dalloc(4 * n));
+    // a store snapshot keeps room to be advanced in place (patch.hip advance_snapshot): slack past
+    // the value arrays' rows, a relocation table, every all-row entry's shard key -- offsets stay
+    // below ROW_MOVED
+    const uint64_t slack = n / 16 + (1u << 20);
+    const bool room = opts && opts->room && !ghosts && n + slack < ROW_MOVED;
+    const uint64_t row_cap = room ? n + slack : n;
+    ro.all_subj = static_cast<uint32_t *>(dalloc(4 * row_cap + 64));
+    ro.rev_nodes = static_cast<uint32_t *>(dalloc(4 * row_cap + 64));
     ro.set_row = static_cast<uint4 *>(dalloc(16 * (uint64_t)NO));
+    if (room) {
+        ro.all_shard = static_cast<unsigned long long *>(dalloc(8 * row_cap));
+        ro.set_slack = slack;
+    }
     ro.weight = (opts && opts->no_weights) ? nullptr : static_cast<uint32_t *>(dalloc(4 * (uint64_t)NO));
     std::vector<uint32_t> idrows(total_slots, 0);  // slots holding a subject-id tuple (RI_IDROWS)
     {
@@ -497,6 +524,17 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.probe_k = PROBE_K;
     s.info.n_set_edges = ro.n_set;
     s.info.n_rev_entries = n;
+    if (room) {
+        constexpr uint32_t RELOC_CAP = 1u << 20;
+        Snapshot::Room &R = s.room;
+        R.all_cap = R.rev_cap = row_cap;
+        R.all_tail = R.rev_tail = n;
+        R.set_cap = ro.n_set + slack;
+        R.set_tail = ro.n_set;
+        R.reloc_cap = RELOC_CAP;
+        R.all_shard = ro.all_shard;
+        D.reloc = static_cast<const uint4 *>(dalloc(16ull * RELOC_CAP));
+    }
 
     // ---- visited keys: UUIDv5(obj, ns+"-"+rel) (relationtuple/definitions.go:114-116) -------
     D.vkey = nullptr;
@@ -736,6 +774,7 @@ constexpr size_t STAGE = 64u << 20;  // device <-> file through a pinned buffer 
 
 void save_snapshot(const Snapshot &s, const char *path) {
     if (s.dev.n_ns_x != s.n_ns) throw Error(KETO_E_INVALID, "a partition's snapshot (ghost namespaces) is not saved");
+    if (s.room.moved) throw Error(KETO_E_INVALID, "a snapshot advanced in place holds moved rows: save a full build");
     KETO_HIP(hipSetDevice(s.device));
     File F(path, "wb");
     const uint64_t magic = SNAP_MAGIC;
@@ -847,6 +886,7 @@ Snapshot *load_snapshot(const char *path, int device) {
         p = i < 0 ? nullptr : s.allocs[(size_t)i];
     });
     s.dev.vclass = nullptr;  // (partitioned graphs' snapshots are never saved)
+    s.dev.reloc = nullptr;   // (nor advanced ones: a loaded snapshot is not advanced in place)
     s.probe_used = (uint64_t)s.dev.probe_mask + 1;  // (not in the file: assume the build's bound, half the slots)
     s.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return S.release();

@@ -210,6 +210,20 @@ void store_transact(TupleStore &st, const keto_tuple *ins, uint64_t n_ins, const
     }
 }
 
+static bool log_since(const TupleStore &st, uint64_t version, build::DevBuf &rows, std::vector<uint8_t> &is_ins);
+
+bool store_snapshot_advance(const TupleStore &st, Snapshot &snap) {
+    // the same compiled configuration is implied: snap was cut from this store and keeps its tables
+    if (snap.store_id != st.id || snap.device != st.device || snap.info.version > st.version) return false;
+    if (snap.info.version == st.version) return true;
+    build::DevBuf rows;
+    std::vector<uint8_t> is_ins;
+    if (!log_since(st, snap.info.version, rows, is_ins)) return false;
+    if (!advance_snapshot(snap, static_cast<const keto_tuple *>(rows.p), is_ins.data(), is_ins.size(), st.n)) return false;
+    snap.info.version = st.version;
+    return true;
+}
+
 void store_free(TupleStore *st) { delete st; }
 
 void store_info(const TupleStore &st, uint64_t *n, uint64_t *version) {
@@ -237,11 +251,38 @@ Snapshot *store_snapshot(const TupleStore &st, const keto_snapshot_config *cfg) 
     BuildOpts o;
     o.uuid_capacity = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, (uint64_t)cfg->n_uuids + cfg->n_uuids / 16 + 65536);
     o.spares = true;
+    o.room = true;  // (keto_store_snapshot_advance)
     Snapshot *s = build_snapshot(cfg, st.rows(), st.n, true, true, &o);
     s->info.version = st.version;
     s->store_id = st.id;
     reserve_next_patch(*s);
     return s;
+}
+
+// the rows of every transaction after `version`, in order (each one's inserts, then its deletes);
+// false when the log no longer holds them all, each once
+static bool log_since(const TupleStore &st, uint64_t version, build::DevBuf &rows, std::vector<uint8_t> &is_ins) {
+    uint64_t want = version + 1, n_rows = 0;
+    bool covered = true;
+    for (const auto &c : st.log)
+        if (c.version > version) {
+            if (c.version != want) covered = false;
+            want++;
+            n_rows += c.n_ins + c.n_del;
+        }
+    if (!covered || want != st.version + 1) return false;
+    KETO_HIP(hipSetDevice(st.device));
+    rows = build::DevBuf(sizeof(keto_tuple) * std::max<uint64_t>(1, n_rows));
+    is_ins.assign(n_rows, 0);
+    uint64_t at = 0;
+    for (const auto &c : st.log) {
+        if (c.version <= version) continue;
+        const uint64_t k = c.n_ins + c.n_del;
+        if (k) KETO_HIP(hipMemcpy(static_cast<keto_tuple *>(rows.p) + at, c.rows.p, k * sizeof(keto_tuple), hipMemcpyDeviceToDevice));
+        std::fill(is_ins.begin() + at, is_ins.begin() + at + c.n_ins, 1);
+        at += k;
+    }
+    return true;
 }
 
 Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const keto_snapshot_config *cfg, bool *patched) {
@@ -250,30 +291,10 @@ Snapshot *store_snapshot_patch(const TupleStore &st, const Snapshot &base, const
     // configuration (a namespace reload, renamed relations or a larger uuid space build in full)
     if (base.store_id == st.id && base.device == st.device && base.info.version <= st.version &&
         base.cfg_hash == config_hash(cfg) && cfg->n_uuids <= base.n_uuids) {
-        // the log must hold every version after the base's, each once, in order (the gather
-        // below takes exactly the entries this loop counts)
-        uint64_t want = base.info.version + 1, n_rows = 0;
-        bool covered = true;
-        for (const auto &c : st.log)
-            if (c.version > base.info.version) {
-                if (c.version != want) covered = false;
-                want++;
-                n_rows += c.n_ins + c.n_del;
-            }
-        covered = covered && want == st.version + 1;
-        if (covered) {
-            KETO_HIP(hipSetDevice(st.device));
-            build::DevBuf rows(sizeof(keto_tuple) * std::max<uint64_t>(1, n_rows));
-            std::vector<uint8_t> is_ins(n_rows);
-            uint64_t at = 0;
-            for (const auto &c : st.log) {
-                if (c.version <= base.info.version) continue;
-                const uint64_t k = c.n_ins + c.n_del;
-                if (k) KETO_HIP(hipMemcpy(static_cast<keto_tuple *>(rows.p) + at, c.rows.p, k * sizeof(keto_tuple), hipMemcpyDeviceToDevice));
-                std::fill(is_ins.begin() + at, is_ins.begin() + at + c.n_ins, 1);
-                at += k;
-            }
-            Snapshot *s = patch_snapshot(base, st.rows(), st.n, static_cast<const keto_tuple *>(rows.p), is_ins.data(), n_rows);
+        build::DevBuf rows;
+        std::vector<uint8_t> is_ins;
+        if (log_since(st, base.info.version, rows, is_ins)) {
+            Snapshot *s = patch_snapshot(base, st.rows(), st.n, static_cast<const keto_tuple *>(rows.p), is_ins.data(), is_ins.size());
             if (s) {
                 s->info.version = st.version;
                 s->store_id = st.id;

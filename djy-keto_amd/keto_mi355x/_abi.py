@@ -95,7 +95,7 @@ class PartitionLevel(ctypes.Structure):
 
 
 # keto_collective callbacks
-ABI_VERSION = 5  # include/keto_mi355x.h KETO_ABI_VERSION
+ABI_VERSION = 6  # include/keto_mi355x.h KETO_ABI_VERSION
 
 ALLTOALL_U64_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                    ctypes.POINTER(ctypes.c_uint64))
@@ -146,6 +146,7 @@ SIGNATURES = {
     "keto_store_snapshot": (ctypes.c_int, [_VP, ctypes.POINTER(SnapshotConfig), ctypes.POINTER(_VP)]),
     "keto_store_snapshot_patch": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(SnapshotConfig), ctypes.POINTER(_VP),
                                                  ctypes.POINTER(_I32)]),
+    "keto_store_snapshot_advance": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_I32)]),
     "keto_store_info": (ctypes.c_int, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "keto_store_free": (ctypes.c_int, [_VP]),
     "keto_dispatcher_create": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherConfig), ctypes.POINTER(_VP)]),

@@ -98,6 +98,14 @@ class Snapshot:
         check(lib().keto_snapshot_info_get(self.handle, ctypes.byref(inf)))
         return {k: getattr(inf, k) for k, _ in inf._fields_}
 
+    def advance(self, store: "TupleStore") -> bool:
+        """this store snapshot advanced in place to the store's current version
+        (keto_store_snapshot_advance): False = unchanged, the delta needs a full build.  No batch
+        may be in flight on it."""
+        a = ctypes.c_int32()
+        check(lib().keto_store_snapshot_advance(store.handle, self.handle, ctypes.byref(a)))
+        return bool(a.value)
+
     def save(self, path: str):
         """the snapshot to a file (keto_snapshot_save): the restart artefact"""
         check(lib().keto_snapshot_save(self.handle, str(path).encode()))

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 5
+#define KETO_ABI_VERSION 6
 
 /* status codes */
 #define KETO_OK 0
@@ -244,6 +244,19 @@ int keto_store_snapshot(keto_store *st, const keto_snapshot_config *cfg, keto_sn
  * full device build runs instead; *patched (optional) says which ran.  base stays valid. */
 int keto_store_snapshot_patch(keto_store *st, const keto_snapshot *base, const keto_snapshot_config *cfg,
                               keto_snapshot **out, int32_t *patched);
+/* ABI 6.  The store's current content in `snap` itself, advanced in place by the transactions
+ * since its version -- work proportional to the rows they name, not to the graph (the
+ * reference's write path touches only its rows: persistence/sql/relationtuples.go:104-126,
+ * 168-189, 277-287).  snap must be a snapshot keto_store_snapshot cut from this store (advanced
+ * any number of times since), with its version still in the change log, and NO batch may be in
+ * flight on it: serve from a second snapshot meanwhile (keto_dispatcher_set_snapshot) and advance
+ * the two in turn.  Rows that grow move into slack the snapshot keeps past its rows.
+ * *advanced = 0 (snap unchanged, still at its version): the delta needs a full build -- a new
+ * (namespace, relation) pair, a uuid past the id room, a namespace out of spare entities, a
+ * shard-id tie in a row, the slack or relocation room spent, snap not this store's; cut a new one
+ * with keto_store_snapshot.  An advanced snapshot is not saved (keto_snapshot_save refuses) nor
+ * the base of keto_store_snapshot_patch (that call builds in full). */
+int keto_store_snapshot_advance(keto_store *st, keto_snapshot *snap, int32_t *advanced);
 int keto_store_info(keto_store *st, uint64_t *n_tuples, uint64_t *version);
 int keto_store_free(keto_store *st);
 

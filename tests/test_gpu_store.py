@@ -384,3 +384,138 @@ def test_patch_creates_objects():
         full.close()
         snaps.append(snap)
     st.close()
+
+
+def test_advanced_snapshots_equal_full_builds():
+    """keto_store_snapshot_advance: the same chain of transactions as the patch test -- ACL rows in
+    and out, duplicates, nested-group edges in and out (leaf flags), subjects crossing the heavy
+    threshold -- applied to ONE store snapshot in place, rows moved into its slack: after each,
+    every Check (depth truncation included), goal count and Expand tree equals a full build of the
+    same store version, and the oracle over the host-side transaction result agrees"""
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=8)
+    rng = np.random.default_rng(3)
+    st = km.TupleStore(wl.tuples)
+    host = wl.tuples.copy()
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    q = synth.drive_queries(wl, 20_000, seed=6)
+    q["max_depth"][:500] = rng.integers(1, 5, 500)
+    roots = _roots(wl, rng)
+    w, _ = world_from_workload(wl)
+    for step in range(4):
+        ins, dele = _delta(wl, rng, 1500, 1000) if step % 2 == 0 else _edge_delta(wl, rng, host)
+        st.transact(ins, dele)
+        host = transact(host, ins, dele)
+        if step == 2:  # two transactions behind: both applied in one advance, in order
+            ins2, dele2 = _delta(wl, rng, 200, 100)
+            st.transact(ins2, dele2)
+            host = transact(host, ins2, dele2)
+        assert snap.advance(st), f"step {step}: declined"
+        full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+        pi, fi = snap.info(), full.info()
+        for k in ("n_tuples", "n_set_edges", "version", "n_reach"):
+            assert pi[k] == fi[k], (step, k)
+        allowed = _compare(wl, snap, full, q, roots)
+        orc = refsem.Oracle(w, host.view(refsem.TUPLE_DT).copy(), shard_bytes=True)
+        orc.set_limits(wl.max_depth, wl.max_width)
+        dec, err, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+        np.testing.assert_array_equal(allowed, dec)
+        full.close()
+    assert snap.advance(st)  # (already at the store's version: nothing to do)
+    base = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    a0, _ = km.CheckEngine(base, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    assert (a0 != allowed).any()
+    st.close()
+
+
+def test_advance_creates_objects():
+    """the new-file transactions of test_patch_creates_objects (100 new files, then a new folder
+    with 20 files under it) advanced into one store snapshot in place: new objects on spare
+    entities, every answer, goal count and Expand tree equal to a full build, oracle agreeing"""
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=8)
+    rng = np.random.default_rng(11)
+    st = km.TupleStore(wl.tuples)
+    host = wl.tuples.copy()
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    w, _ = world_from_workload(wl)
+    folders = rng.integers(0, wl.meta["n_folders"], 100)
+    n_uuids = wl.n_uuids
+    new_ids = n_uuids + np.arange(100)
+    ins = synth.drive_new_files(wl, new_ids, folders, rng)
+    for step in range(2):
+        if step == 1:
+            fo_ns = wl.ns_names.index("Folder")
+            new_folder = n_uuids
+            files = n_uuids + 1 + np.arange(20)
+            ins = synth.drive_new_files(wl, files, np.full(20, new_folder), rng)
+            up = ins[:1].copy()
+            up["ns"], up["obj"], up["s_obj"] = fo_ns, new_folder, int(folders[0])
+            ins = np.concatenate([up, ins])
+            new_ids = np.concatenate([[new_folder], files])
+        n_uuids = int(new_ids.max()) + 1
+        st.transact(ins, None)
+        host = transact(host, ins, ins[:0])
+        assert snap.advance(st), f"step {step}: declined"
+        full = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, n_uuids, store=st)
+        q = synth.drive_queries(wl, 8192, seed=20 + step)
+        k = 4096
+        q["ns"][:k] = wl.ns_names.index("File") if step == 0 else np.where(np.arange(k) % 21 == 0, wl.ns_names.index("Folder"),
+                                                                              wl.ns_names.index("File"))
+        q["obj"][:k] = rng.choice(new_ids, k)
+        q["rel"][:k] = rng.choice([wl.rel_names.index("view"), wl.rel_names.index("edit")], k)
+        q["subj_kind"][:k], q["s_ns"][:k], q["s_rel"][:k] = 0, 0, 0
+        q["s_obj"][:k] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], k)
+        q["max_depth"][:k] = 0
+        roots = _roots(wl, rng, 64)
+        roots["ns"][:32], roots["obj"][:32] = wl.ns_names.index("File"), rng.choice(new_ids, 32)
+        roots["rel"][:32] = wl.rel_names.index("viewers")
+        allowed = _compare(wl, snap, full, q, roots)
+        assert allowed[:k].any()
+        orc = refsem.Oracle(w, host.view(refsem.TUPLE_DT).copy(), shard_bytes=True)
+        orc.set_limits(wl.max_depth, wl.max_width)
+        dec, err, _ = orc.check_batch(queries_to_oracle(q), threads=8)
+        np.testing.assert_array_equal(allowed, dec)
+        full.close()
+    st.close()
+
+
+def test_advance_declines_and_leaves_the_snapshot(tmp_path):
+    """what the advance cannot do it declines before writing anything: an insert whose shard_id's
+    high half ties a tuple of its row (only the full build orders it), a snapshot that is not this
+    store's; a declined snapshot still answers its own version.  An advanced snapshot is neither
+    saved nor the base of a copy patch (that builds in full)."""
+    wl = synth.drive(depth=4, n_groups=500, n_users=1000, seed=4)
+    t = wl.tuples
+    st = km.TupleStore(t)
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    q = synth.drive_queries(wl, 4096, seed=2)
+    before = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    tie = t[:1].copy()  # the same row, another subject, a shard_id equal in its high half
+    tie["subj_kind"], tie["s_obj"], tie["s_ns"], tie["s_rel"] = 0, wl.meta["ubase"] + 3, 0, 0
+    tie["shard_id"][0, 8:] ^= 0x5A
+    st.transact(tie, None)
+    assert not snap.advance(st)
+    assert snap.info()["version"] == 0
+    after = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    np.testing.assert_array_equal(before[0], after[0])
+    np.testing.assert_array_equal(before[1], after[1])
+    other = km.TupleStore(t)
+    assert not snap.advance(other)
+    plain = km.Snapshot(wl.namespaces, t, wl.ns_names, wl.rel_names, wl.n_uuids)
+    assert not plain.advance(st)
+    # a fresh cut advances; then save refuses it and a copy patch of it builds in full
+    snap2 = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    snap2.save(str(tmp_path / "fresh.snap"))  # (not advanced yet: saved)
+    ins = t[5:6].copy()
+    ins["subj_kind"], ins["s_obj"], ins["s_ns"], ins["s_rel"] = 0, wl.meta["ubase"] + 9, 0, 0
+    ins["shard_id"] = np.random.default_rng(2).integers(0, 256, (1, 16), dtype=np.uint8)
+    st.transact(ins, None)
+    assert snap2.advance(st)
+    with pytest.raises(Exception):
+        snap2.save(str(tmp_path / "advanced.snap"))
+    st.transact(None, ins)
+    nxt = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=snap2)
+    assert not nxt.patched
+    for s in (snap, snap2, nxt, plain):
+        s.close()
+    other.close()
+    st.close()

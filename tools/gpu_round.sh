@@ -45,7 +45,7 @@ ab)
   done ;;
 patch)
   KETO_PATCH_VERBOSE=1 timeout -k 10 400 python3 -u tools/patch_probe.py 10 > $OUT/patch.log 2>&1 || { tail -5 $OUT/patch.log; exit 1; }
-  grep -E "keto patch" $OUT/patch.log | head -40 ;;
+  grep -E "keto (patch|advance)|advance_ms" $OUT/patch.log | cut -c1-900 | head -60 ;;
 c5)
   S=${1:-40}; B=${2:-10}
   KETO_C5_SCALE=$S timeout -k 10 1100 python3 -u -m pytest -x -v -s --timeout 1080 --timeout-method thread tests/test_gpu_c5.py \
