@@ -188,3 +188,73 @@ def test_native_closed_loop_load():
     assert r["requests"] > 0 and r["checks"] == 32 * r["requests"]
     assert st["queries"] >= r["checks"]  # every request went through the dispatcher's batches
     assert 0 < r["p50_ms"] <= r["p99_ms"] <= r["max_ms"]
+
+
+def test_two_snapshot_rotation_with_in_place_advance():
+    """the serving pattern keto_store_snapshot_advance asks for: two store snapshots, one served,
+    one idle.  Per transaction the idle one is advanced in place, swapped in (set_snapshot waits
+    for the old one's batches), and the old one -- idle now -- advanced in turn.  Under 16 busy
+    clients every answer is the oracle's at the version served when the request was issued (or the
+    next one, if a swap landed during it)"""
+    from store_ref import transact
+
+    wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=9)
+    q = synth.drive_queries(wl, 8192, seed=1)
+    rng = np.random.default_rng(4)
+    st = km.TupleStore(wl.tuples)
+    snaps = [km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st) for _ in range(2)]
+    host = wl.tuples.copy()
+    answers = [_oracle_answers(_oracle(wl, host), q)[0]]
+    d = km.Dispatcher(snaps[0], wl.max_depth, wl.max_width, max_batch=2048, inflight=4)
+    stop = threading.Event()
+    swaps, log, errors = [], [], []
+
+    def client(t):
+        r = np.random.default_rng(100 + t)
+        try:
+            while not stop.is_set():
+                i = int(r.integers(0, len(q) - 64))
+                t0 = time.monotonic()
+                a, _ = d.check(q[i:i + 64])
+                log.append((t0, i, a.copy()))
+        except Exception as ex:
+            errors.append(ex)
+
+    th = [threading.Thread(target=client, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    served = 0
+    for step in range(3):
+        time.sleep(0.3)
+        t = host
+        ins = t[rng.choice(len(t), 800, replace=False)].copy()
+        ins["subj_kind"], ins["s_ns"], ins["s_rel"] = 0, 0, 0
+        ins["s_obj"] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], len(ins))
+        ins["shard_id"] = rng.integers(0, 256, (len(ins), 16), dtype=np.uint8)
+        dele = t[rng.choice(len(t), 1500, replace=False)].copy()
+        st.transact(ins, dele)
+        host = transact(host, ins, dele)
+        answers.append(_oracle_answers(_oracle(wl, host), q)[0])
+        idle = 1 - served
+        assert snaps[idle].advance(st)
+        d.set_snapshot(snaps[idle])
+        swaps.append(time.monotonic())
+        served = idle
+        assert snaps[1 - served].advance(st)  # the old one: idle once set_snapshot returned
+    time.sleep(0.3)
+    stop.set()
+    for x in th:
+        x.join()
+    d.close()
+    assert not errors
+    assert (answers[0] != answers[-1]).sum() > 100
+    late = 0
+    for ts, i, a in log:
+        v = sum(1 for s in swaps if s < ts)
+        ok = [answers[v][i:i + 64]] + ([answers[v + 1][i:i + 64]] if v + 1 < len(answers) else [])
+        assert any((a == w).all() for w in ok), (v, i)
+        late += v == len(swaps)
+    assert late > 10
+    for s in snaps:
+        s.close()
+    st.close()
