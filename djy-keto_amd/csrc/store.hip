@@ -11,11 +11,12 @@
 //     on subject_id alone, a subject set on its three fields (whereSubject, :128-150).
 // The shim supplies the inserted rows' shard_ids (it writes the same rows to SQL).
 //
-// On the device: inserts are appended; deletes go through an open-addressing hash of the
-// delete keys and one pass over the store that flags matching rows.  Survivors are then
-// compacted in place: the deleted slots below the new length are filled with the live rows
-// above it.  Row order does not matter, because the snapshot builder orders every row by
-// shard_id.  A snapshot of the current content is stamped with the store's version: the
+// On the device: inserts are appended; deletes find their rows through the store's content
+// index -- open addressing over {32-bit tag of the content hash, row position}, every stored row
+// once, the reference's SQL index on the same columns -- so a transaction costs its own rows, not
+// the store.  Survivors are then compacted in place: the deleted slots below the new length are
+// filled with the live rows above it (the index entries of the moved rows repointed).  Row order
+// does not matter, because the snapshot builder orders every row by shard_id.  A snapshot of the current content is stamped with the store's version: the
 // snaptoken the reference leaves unimplemented (check/handler.go:327-330).  It is either one
 // device build (keto_snapshot_build_device, ~2 s at 1B tuples) or a patch of an earlier
 // snapshot of this store (patch.hip): the store keeps every transaction's rows in a change log
@@ -23,6 +24,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <deque>
 #include <memory>
@@ -60,51 +63,68 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
     return h;
 }
 
-// slot = index of a delete key + 1 (0 = empty); duplicates of one key may share the table
-__global__ __launch_bounds__(BLK) void k_del_insert(const keto_tuple *del, uint64_t n, uint32_t *slots, uint64_t mask) {
-    const uint64_t i = gid();
-    if (i >= n) return;
-    uint64_t h = key_hash(key_of(del[i])) & mask;
-    for (;;) {
-        if (atomicCAS(&slots[h], 0u, (uint32_t)(i + 1)) == 0u) return;
-        h = (h + 1) & mask;
-    }
-}
+// ---- the content index: entry = tag << 32 | position (IX_EMPTY: free, IX_TOMB: a deleted row's) ----
+constexpr uint32_t IX_EMPTY = 0xFFFFFFFFu, IX_TOMB = 0xFFFFFFFEu;
+struct Ix {
+    unsigned long long *slot;
+    uint32_t n;  // slots (< 2^32: home = multiply-shift of the hash's low word)
+};
+__device__ __forceinline__ uint32_t ix_home(const Ix &x, uint64_t h) { return (uint32_t)(((h & 0xFFFFFFFFull) * x.n) >> 32); }
+__device__ __forceinline__ uint32_t ix_next(const Ix &x, uint32_t b) { return b + 1 == x.n ? 0u : b + 1; }
 
-__global__ __launch_bounds__(BLK) void k_mark(const keto_tuple *t, uint64_t n, const keto_tuple *del,
-                                              const uint32_t *slots, uint64_t mask, uint8_t *dead,
-                                              unsigned long long *n_dead) {
+__global__ __launch_bounds__(BLK) void k_ix_insert(const keto_tuple *t, uint64_t first, uint64_t n, Ix x) {
     const uint64_t i = gid();
     if (i >= n) return;
-    const Key k = key_of(t[i]);
-    uint64_t h = key_hash(k) & mask;
-    bool hit = false;
-    for (;;) {
-        const uint32_t s = slots[h];
-        if (s == 0u) break;
-        if (same(key_of(del[s - 1]), k)) {
-            hit = true;
-            break;
+    const uint64_t pos = first + i, h = key_hash(key_of(t[pos]));
+    const unsigned long long e = (h >> 32) << 32 | pos;
+    for (uint32_t b = ix_home(x, h);; b = ix_next(x, b)) {
+        unsigned long long cur = x.slot[b];
+        while ((uint32_t)cur == IX_EMPTY) {
+            const unsigned long long was = atomicCAS(&x.slot[b], cur, e);
+            if (was == cur) return;
+            cur = was;
         }
-        h = (h + 1) & mask;
     }
-    dead[i] = hit ? 1 : 0;
-    if (hit) atomicAdd(n_dead, 1ull);
 }
 
-// holes: dead rows below the new length; movers: live rows at or above it (equal counts)
-__global__ __launch_bounds__(BLK) void k_holes_movers(const uint8_t *dead, uint64_t n, uint64_t keep, uint64_t *holes,
-                                                      uint64_t *movers, unsigned long long *cnt) {
+// every live row matching a delete key: its entry becomes a tombstone (one CAS: a key listed twice
+// takes each row once) and its position goes to the dead list
+__global__ __launch_bounds__(BLK) void k_ix_delete(const keto_tuple *t, const keto_tuple *del, uint64_t n_del, Ix x, uint32_t *dead,
+                                                   uint64_t cap, unsigned long long *n_dead) {
     const uint64_t i = gid();
-    if (i >= n) return;
-    if (i < keep && dead[i]) holes[atomicAdd(&cnt[0], 1ull)] = i;
-    if (i >= keep && !dead[i]) movers[atomicAdd(&cnt[1], 1ull)] = i;
+    if (i >= n_del) return;
+    const Key k = key_of(del[i]);
+    const uint64_t h = key_hash(k);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    for (uint32_t b = ix_home(x, h);; b = ix_next(x, b)) {
+        const unsigned long long cur = x.slot[b];
+        const uint32_t pos = (uint32_t)cur;
+        if (pos == IX_EMPTY) return;
+        if (pos == IX_TOMB || (uint32_t)(cur >> 32) != tag || !same(key_of(t[pos]), k)) continue;
+        if (atomicCAS(&x.slot[b], cur, (unsigned long long)tag << 32 | IX_TOMB) == cur) {
+            const unsigned long long at = atomicAdd(n_dead, 1ull);
+            if (at < cap) dead[at] = pos;
+        }
+    }
 }
 
-__global__ __launch_bounds__(BLK) void k_move(keto_tuple *t, const uint64_t *holes, const uint64_t *movers, uint64_t m) {
+// the live rows above the new length into the deleted slots below it, their entries repointed
+__global__ __launch_bounds__(BLK) void k_ix_move(keto_tuple *t, const uint2 *moves, uint64_t m, Ix x) {
     const uint64_t i = gid();
     if (i >= m) return;
-    t[holes[i]] = t[movers[i]];
+    const uint32_t from = moves[i].x, to = moves[i].y;
+    const keto_tuple row = t[from];
+    t[to] = row;
+    const uint64_t h = key_hash(key_of(row));
+    const unsigned long long e = (h >> 32) << 32 | from;
+    for (uint32_t b = ix_home(x, h);; b = ix_next(x, b)) {
+        const unsigned long long cur = x.slot[b];
+        if ((uint32_t)cur == IX_EMPTY) return;  // (not reached: every stored row has its entry)
+        if (cur == e) {
+            x.slot[b] = (h >> 32) << 32 | to;
+            return;
+        }
+    }
 }
 
 }  // namespace
@@ -122,13 +142,36 @@ struct TupleStore {
     std::deque<Change> log;
     uint64_t log_rows = 0;
     static constexpr uint64_t LOG_MAX_ROWS = 1ull << 22;
+    // the content index: 3/2 slots per row of capacity, entries and tombstones counted
+    build::DevBuf ix;
+    uint64_t ix_slots = 0, ix_used = 0;
+    bool ix_dirty = false;  // a transaction threw part-way: entries past n may exist (re-index first)
     keto_tuple *rows() const { return static_cast<keto_tuple *>(buf.p); }
     uint64_t cap() const { return buf.bytes / sizeof(keto_tuple); }
+    Ix index() const { return Ix{static_cast<unsigned long long *>(ix.p), (uint32_t)ix_slots}; }
     void reserve(uint64_t need) {
         if (need <= cap()) return;
-        build::DevBuf nb(std::max<uint64_t>(need, cap() + cap() / 4) * sizeof(keto_tuple));
+        if (need >= 0xFFFFFFF0ull) throw Error(KETO_E_LIMIT, "a store of 2^32 rows");
+        build::DevBuf nb(std::min<uint64_t>(0xFFFFFFF0ull, std::max<uint64_t>(need, cap() + cap() / 4)) * sizeof(keto_tuple));
         if (n) KETO_HIP(hipMemcpy(nb.p, buf.p, n * sizeof(keto_tuple), hipMemcpyDeviceToDevice));
         buf = std::move(nb);
+        reindex();
+    }
+    // every stored row entered afresh (a grown store, or tombstones past the load bound)
+    void reindex() {
+        const uint64_t slots = std::min<uint64_t>(0xFFFFFFFFull, cap() + cap() / 2 + 64);
+        if (ix_slots != slots) {
+            ix = build::DevBuf();
+            ix = build::DevBuf(8 * slots);
+            ix_slots = slots;
+        }
+        KETO_HIP(hipMemset(ix.p, 0xFF, 8 * slots));
+        if (n) hipLaunchKernelGGL(k_ix_insert, grid_for(n), dim3(BLK), 0, 0, rows(), 0, n, index());
+        KETO_HIP(hipGetLastError());
+        if (getenv("KETO_PATCH_VERBOSE"))
+            fprintf(stderr, "[keto store] index: %llu rows, %llu slots (%llu entries and tombstones before)\n", (unsigned long long)n,
+                    (unsigned long long)slots, (unsigned long long)ix_used);
+        ix_used = n;
     }
 };
 
@@ -143,6 +186,8 @@ TupleStore *store_create(int device, const keto_tuple *tuples, uint64_t n, bool 
         KETO_HIP(hipMemcpy(st->rows(), tuples, n * sizeof(keto_tuple),
                            device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
     st->n = n;
+    st->reindex();
+    KETO_HIP(hipDeviceSynchronize());
     return st.release();
 }
 
@@ -157,50 +202,77 @@ void store_transact(TupleStore &st, const keto_tuple *ins, uint64_t n_ins, const
     if (n_ins) KETO_HIP(hipMemcpy(c.rows.p, ins, n_ins * sizeof(keto_tuple), kind));
     if (n_del) KETO_HIP(hipMemcpy(static_cast<keto_tuple *>(c.rows.p) + n_ins, del, n_del * sizeof(keto_tuple), kind));
     const uint64_t n_before = st.n;
-    if (n_ins) {  // WriteRelationTuples: appended rows, fresh shard_ids from the caller
-        st.reserve(st.n + n_ins);
+    // tombstones and the new rows' entries within 3/4 of the index, or every row entered afresh
+    // (amortised: a transaction of k rows spends k of the quarter's headroom)
+    if ((st.ix_dirty || st.ix_used + n_ins > st.ix_slots / 4 * 3) && st.cap() >= st.n + n_ins) st.reindex();
+    st.ix_dirty = true;  // (until the transaction is applied)
+    if (n_ins) {  // WriteRelationTuples: appended rows, fresh shard_ids from the caller, indexed
+        st.reserve(st.n + n_ins);  // (a grown store is indexed afresh, these rows not yet)
         KETO_HIP(hipMemcpy(st.rows() + st.n, ins, n_ins * sizeof(keto_tuple), kind));
+        hipLaunchKernelGGL(k_ix_insert, grid_for(n_ins), dim3(BLK), 0, 0, st.rows(), n_before, n_ins, st.index());
+        KETO_HIP(hipGetLastError());
+        st.ix_used += n_ins;
     }
     // (the appended rows count only once the deletes below went through: st.n stays n_before
-    // until the end, so a throw leaves the store's content as it was)
+    // until the end.  A throw part-way leaves the index ahead of st.n: ix_dirty, and the next
+    // transaction re-indexes first)
     const uint64_t n_all = n_before + n_ins;
     uint64_t n_after = n_all;
     if (n_del && n_all) {  // DeleteRelationTuples over everything, the new rows included
-        build::DevBuf d(n_del * sizeof(keto_tuple));
+        build::DevBuf d(n_del * sizeof(keto_tuple)), cnt(8);
         KETO_HIP(hipMemcpy(d.p, del, n_del * sizeof(keto_tuple), kind));
-        uint64_t size = 64;
-        while (size < 2 * n_del) size <<= 1;
-        build::DevBuf slots(size * 4), dead(n_all), cnt(3 * sizeof(unsigned long long));
-        KETO_HIP(hipMemset(slots.p, 0, size * 4));
-        KETO_HIP(hipMemset(cnt.p, 0, 3 * sizeof(unsigned long long)));
-        auto *cn = static_cast<unsigned long long *>(cnt.p);
-        hipLaunchKernelGGL(k_del_insert, grid_for(n_del), dim3(BLK), 0, 0, static_cast<const keto_tuple *>(d.p), n_del,
-                           slots.u32(), size - 1);
-        KETO_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_mark, grid_for(n_all), dim3(BLK), 0, 0, st.rows(), n_all,
-                           static_cast<const keto_tuple *>(d.p), slots.u32(), size - 1,
-                           static_cast<uint8_t *>(dead.p), cn + 2);
-        KETO_HIP(hipGetLastError());
+        KETO_HIP(hipMemset(cnt.p, 0, 8));
+        // (a delete key matches any number of rows: the dead list is sized by a first count)
+        uint64_t cap_dead = std::max<uint64_t>(1024, 4 * n_del);
         unsigned long long n_dead = 0;
-        KETO_HIP(hipMemcpy(&n_dead, cn + 2, sizeof(n_dead), hipMemcpyDeviceToHost));
+        build::DevBuf dead(4 * cap_dead);
+        for (;;) {
+            hipLaunchKernelGGL(k_ix_delete, grid_for(n_del), dim3(BLK), 0, 0, st.rows(), static_cast<const keto_tuple *>(d.p), n_del,
+                               st.index(), dead.u32(), cap_dead, static_cast<unsigned long long *>(cnt.p));
+            KETO_HIP(hipGetLastError());
+            KETO_HIP(hipMemcpy(&n_dead, cnt.p, 8, hipMemcpyDeviceToHost));
+            if (n_dead <= cap_dead) break;
+            // more rows than the list held: the tombstoned ones are gone from the index already,
+            // so the whole index is rebuilt from the rows and the deletes run again into a list
+            // of the right size
+            st.n = n_all;  // (index every row, the appended ones included)
+            st.reindex();
+            st.n = n_before;
+            cap_dead = n_dead;
+            dead = build::DevBuf(4 * cap_dead);
+            KETO_HIP(hipMemset(cnt.p, 0, 8));
+        }
         if (n_dead) {
+            std::vector<uint32_t> dl(n_dead);
+            KETO_HIP(hipMemcpy(dl.data(), dead.p, 4 * n_dead, hipMemcpyDeviceToHost));
+            std::sort(dl.begin(), dl.end());
             const uint64_t keep = n_all - n_dead;
-            build::DevBuf holes(n_dead * 8), movers(n_dead * 8);
-            hipLaunchKernelGGL(k_holes_movers, grid_for(n_all), dim3(BLK), 0, 0, static_cast<const uint8_t *>(dead.p),
-                               n_all, keep, static_cast<uint64_t *>(holes.p), static_cast<uint64_t *>(movers.p), cn);
-            KETO_HIP(hipGetLastError());
-            unsigned long long m[2] = {0, 0};
-            KETO_HIP(hipMemcpy(m, cn, sizeof(m), hipMemcpyDeviceToHost));
-            if (m[0] != m[1]) throw Error(KETO_E_DEVICE, "compaction lists disagree");
-            hipLaunchKernelGGL(k_move, grid_for(m[0]), dim3(BLK), 0, 0, st.rows(),
-                               static_cast<const uint64_t *>(holes.p), static_cast<const uint64_t *>(movers.p), m[0]);
-            KETO_HIP(hipGetLastError());
+            // holes: dead positions below keep; movers: live positions at or above it (as many)
+            std::vector<uint2> moves;
+            size_t h = 0, dk = (size_t)(std::lower_bound(dl.begin(), dl.end(), (uint32_t)keep) - dl.begin());
+            for (uint64_t p = keep; p < n_all; p++) {
+                if (dk < dl.size() && dl[dk] == p) {
+                    dk++;
+                    continue;
+                }
+                moves.push_back(make_uint2((uint32_t)p, dl[h++]));
+            }
+            if (h != (size_t)(std::lower_bound(dl.begin(), dl.end(), (uint32_t)keep) - dl.begin()))
+                throw Error(KETO_E_DEVICE, "compaction lists disagree");
+            if (!moves.empty()) {
+                build::DevBuf dm(sizeof(uint2) * moves.size());
+                KETO_HIP(hipMemcpy(dm.p, moves.data(), sizeof(uint2) * moves.size(), hipMemcpyHostToDevice));
+                hipLaunchKernelGGL(k_ix_move, grid_for(moves.size()), dim3(BLK), 0, 0, st.rows(), static_cast<const uint2 *>(dm.p),
+                                   (uint64_t)moves.size(), st.index());
+                KETO_HIP(hipGetLastError());
+            }
             n_after = keep;
         }
     }
     KETO_HIP(hipDeviceSynchronize());
     // applied: the new content, its version and its log entry together
     st.n = n_after;
+    st.ix_dirty = false;
     st.version++;
     st.log_rows += n_ins + n_del;
     st.log.push_back(std::move(c));

@@ -519,3 +519,51 @@ def test_advance_declines_and_leaves_the_snapshot(tmp_path):
         s.close()
     other.close()
     st.close()
+
+
+def test_store_index_churn_and_mass_delete():
+    """the store's content index (store.hip): 90 transactions of inserts and deletes on a small
+    store fill the index with tombstones past its load bound (re-indexed on the way), and one
+    delete key matching 3,001 duplicate rows overflows the first dead list (re-indexed, run again);
+    the store's content stays the host restatement's -- the same count, and a snapshot of it equal
+    to a full build of the host rows in every Check answer and Expand tree (rows in shard order:
+    the duplicates' shard_ids included)"""
+    wl = synth.drive(depth=3, n_groups=100, n_users=300, seed=2)
+    rng = np.random.default_rng(9)
+    st = km.TupleStore(wl.tuples)
+    host = wl.tuples.copy()
+    for step in range(90):
+        ins = host[rng.choice(len(host), 1000)].copy()
+        acl = rng.random(len(ins)) < 0.8  # mostly new keys (other users), the rest duplicates of stored rows
+        ins["subj_kind"][acl], ins["s_ns"][acl], ins["s_rel"][acl] = 0, 0, 0
+        ins["s_obj"][acl] = wl.meta["ubase"] + rng.integers(0, wl.meta["n_users"], int(acl.sum()))
+        ins["shard_id"] = rng.integers(0, 256, (len(ins), 16), dtype=np.uint8)
+        dele = host[rng.choice(len(host), min(700, len(host) // 2), replace=False)].copy()
+        st.transact(ins, dele)
+        host = transact(host, ins, dele)
+        assert st.info()[0] == len(host), step
+    dup = np.repeat(host[:1], 3001)
+    dup["shard_id"] = rng.integers(0, 256, (len(dup), 16), dtype=np.uint8)
+    st.transact(dup, None)
+    host = transact(host, dup, dup[:0])
+    extra = host[5:9].copy()
+    extra["shard_id"] = rng.integers(0, 256, (len(extra), 16), dtype=np.uint8)
+    st.transact(extra, host[:1])  # one key: 3,002 rows
+    host = transact(host, extra, host[:1])
+    assert st.info()[0] == len(host)
+    inc = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    full = km.Snapshot(wl.namespaces, host, wl.ns_names, wl.rel_names, wl.n_uuids)
+    q = synth.drive_queries(wl, 4096, seed=5)
+    roots = np.zeros(len(host), dtype=km.SUBJSET_DT)
+    roots["ns"], roots["obj"], roots["rel"] = host["ns"], host["obj"], host["rel"]
+    roots = np.unique(roots)[:512]
+    out = []
+    for snap in (inc, full):
+        a, e = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+        nodes, offs, xerr = km.ExpandEngine(snap, max_read_depth=wl.max_depth).build_trees(roots)
+        out.append((a, e, nodes.tobytes(), offs, xerr))
+    for x, y in zip(*out):
+        np.testing.assert_array_equal(x, y)
+    inc.close()
+    full.close()
+    st.close()
