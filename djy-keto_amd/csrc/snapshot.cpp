@@ -478,7 +478,9 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     // a store snapshot keeps room to be advanced in place (patch.hip advance_snapshot): slack past
     // the value arrays' rows, a relocation table, every all-row entry's shard key -- offsets stay
     // below ROW_MOVED
-    const uint64_t slack = n / 16 + (1u << 20);
+    // (KETO_ADVANCE_SLACK / KETO_ADVANCE_RELOC: smaller room, for the tests that spend it)
+    const char *slack_env = getenv("KETO_ADVANCE_SLACK");
+    const uint64_t slack = slack_env ? strtoull(slack_env, nullptr, 10) : n / 16 + (1u << 20);
     const bool room = opts && opts->room && !ghosts && n + slack < ROW_MOVED;
     const uint64_t row_cap = room ? n + slack : n;
     ro.all_subj = static_cast<uint32_t *>(dalloc(4 * row_cap + 64));
@@ -525,7 +527,8 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     s.info.n_set_edges = ro.n_set;
     s.info.n_rev_entries = n;
     if (room) {
-        constexpr uint32_t RELOC_CAP = 1u << 20;
+        const char *reloc_env = getenv("KETO_ADVANCE_RELOC");
+        const uint32_t RELOC_CAP = reloc_env ? (uint32_t)std::max(1, atoi(reloc_env)) : 1u << 20;
         Snapshot::Room &R = s.room;
         R.all_cap = R.rev_cap = row_cap;
         R.all_tail = R.rev_tail = n;

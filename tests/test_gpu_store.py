@@ -567,3 +567,50 @@ def test_store_index_churn_and_mass_delete():
     inc.close()
     full.close()
     st.close()
+
+
+@pytest.mark.parametrize("room", [{"KETO_ADVANCE_SLACK": "6000"}, {"KETO_ADVANCE_RELOC": "3000"}])
+def test_advance_declines_once_its_room_is_spent(room, monkeypatch):
+    """a store snapshot's room -- slack past its rows, relocation entries -- is finite: transactions
+    advance it until one would not fit, which declines and leaves it at its version (every answer
+    still the previous version's); a fresh cut then carries on.  (Room shrunk by the env knobs.)"""
+    for k, v in room.items():
+        monkeypatch.setenv(k, v)
+    wl = synth.drive(depth=4, n_groups=500, n_users=1000, seed=4)
+    rng = np.random.default_rng(6)
+    st = km.TupleStore(wl.tuples)
+    host = wl.tuples.copy()
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    q = synth.drive_queries(wl, 4096, seed=8)
+    advanced = 0
+    for step in range(40):
+        ins, dele = _delta(wl, rng, 600, 300)
+        prev = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+        version = snap.info()["version"]
+        st.transact(ins, dele)
+        host = transact(host, ins, dele)
+        if not snap.advance(st):
+            assert snap.info()["version"] == version
+            now = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+            np.testing.assert_array_equal(prev[0], now[0])
+            np.testing.assert_array_equal(prev[1], now[1])
+            break
+        advanced += 1
+    else:
+        pytest.fail("the room never ran out")
+    assert advanced >= 1
+    snap.close()
+    monkeypatch.delenv(next(iter(room)))
+    fresh = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    ins, dele = _delta(wl, rng, 600, 300)
+    st.transact(ins, dele)
+    host = transact(host, ins, dele)
+    assert fresh.advance(st)
+    full = km.Snapshot(wl.namespaces, host, wl.ns_names, wl.rel_names, wl.n_uuids)
+    a = km.CheckEngine(fresh, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    b = km.CheckEngine(full, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    fresh.close()
+    full.close()
+    st.close()
