@@ -88,6 +88,10 @@ struct Snapshot {
         unsigned long long *all_shard = nullptr;
         bool moved = false;  // an advance ran: rows live outside their CSR extents (no save, no copy patch)
     } room;
+    // (room snapshots) per global slot: subject-set edges into the slot's nodes (a reach "target"
+    // slot when > 0) and the slot's nodes with a non-empty set row (RI_SETROWS when > 0) -- kept
+    // by each advance from its own rows, where a scan of set_dst would read moved rows' old copies
+    std::vector<uint64_t> slot_in, slot_rows;
 
     // a device allocation of this snapshot (back to the pool with its last sharer)
     void own(void *p, size_t bytes);
@@ -112,6 +116,8 @@ void build_reach(Snapshot &s);
 // has no host record) rebuilds them whole
 // (&s == &B: an in-place advance -- the tables are updated where they lie)
 void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &touched_nodes);
+// patch.hip: Snapshot::slot_in / slot_rows of a room snapshot, counted over its rows (at its build)
+void room_slot_counts(Snapshot &s);
 // 64-bit FNV-1a of everything a snapshot compiles from its configuration (name tables, AST JSON,
 // strict mode; not the device, not n_uuids): equal hashes = the same compiled tables
 uint64_t config_hash(const keto_snapshot_config *cfg);

@@ -975,12 +975,64 @@ __global__ __launch_bounds__(BLK) void k_put_reloc(uint4 *reloc, const uint32_t 
     const uint64_t j = gid();
     if (j < m) reloc[at[j]] = val[j];
 }
+// per slot: set edges into its nodes, its nodes with a non-empty set row (block counters in LDS)
+constexpr uint32_t SLOT_LDS = 1024;
+__global__ __launch_bounds__(BLK) void k_slot_counts(DevSnapshot s, uint64_t n_rows, uint32_t n_slots, unsigned long long *in_cnt,
+                                                     unsigned long long *row_cnt) {
+    __shared__ uint32_t lin[SLOT_LDS], lrow[SLOT_LDS];
+    const bool lds = n_slots <= SLOT_LDS;
+    for (uint32_t i = threadIdx.x; i < SLOT_LDS; i += blockDim.x) lin[i] = lrow[i] = 0;
+    __syncthreads();
+    auto slot = [&](uint32_t node) {
+        uint32_t lo = 0, hi = s.n_ns;  // last namespace whose node_base <= node
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (s.ns[m].node_base <= node) lo = m;
+            else hi = m;
+        }
+        return s.ns[lo].slot_base + (node - s.ns[lo].node_base) % s.ns[lo].n_slots;
+    };
+    for (uint64_t v = gid(); v < n_rows; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 r = s.set_row[v];
+        if (r.x == r.y) continue;
+        const uint32_t g = slot((uint32_t)v);
+        if (lds) atomicAdd(&lrow[g], 1u);
+        else atomicAdd(&row_cnt[g], 1ull);
+        for (uint32_t k = r.x; k < r.y; k++) {
+            const uint32_t h = slot(s.set_dst[k] & s.edge_mask);
+            if (lds) atomicAdd(&lin[h], 1u);
+            else atomicAdd(&in_cnt[h], 1ull);
+        }
+    }
+    __syncthreads();
+    if (lds)
+        for (uint32_t i = threadIdx.x; i < n_slots; i += blockDim.x) {
+            if (lin[i]) atomicAdd(&in_cnt[i], (unsigned long long)lin[i]);
+            if (lrow[i]) atomicAdd(&row_cnt[i], (unsigned long long)lrow[i]);
+        }
+}
 uint64_t shard_hi_host(const keto_tuple &t) {
     uint64_t h = 0;
     for (int k = 0; k < 8; k++) h = (h << 8) | t.shard_id[k];
     return h;
 }
 }  // namespace
+
+void room_slot_counts(Snapshot &s) {
+    using build::DevBuf;
+    const uint32_t n_slots = (uint32_t)s.relinfo.size();
+    s.slot_in.assign(n_slots, 0);
+    s.slot_rows.assign(n_slots, 0);
+    if (!n_slots || !s.dev.n_owned) return;
+    DevBuf c(16ull * n_slots);
+    KETO_HIP(hipMemset(c.p, 0, 16ull * n_slots));
+    auto *in_cnt = static_cast<unsigned long long *>(c.p);
+    hipLaunchKernelGGL(k_slot_counts, dim3((uint32_t)std::min<uint64_t>(4096, (s.dev.n_owned + BLK - 1) / BLK)), dim3(BLK), 0, 0, s.dev,
+                       (uint64_t)s.dev.n_owned, n_slots, in_cnt, in_cnt + n_slots);
+    KETO_HIP(hipGetLastError());
+    KETO_HIP(hipMemcpy(s.slot_in.data(), in_cnt, 8ull * n_slots, hipMemcpyDeviceToHost));
+    KETO_HIP(hipMemcpy(s.slot_rows.data(), in_cnt + n_slots, 8ull * n_slots, hipMemcpyDeviceToHost));
+}
 
 bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_ins, uint64_t n_touched, uint64_t n_store) {
     using build::DevBuf;
@@ -998,6 +1050,7 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
     Snapshot::Room &R = S.room;
     DevSnapshot &D = S.dev;
     if (!R.all_shard || !D.reloc || n_touched >= (1ull << 31) || n_store >= ROW_MOVED) return false;
+    if (S.slot_in.size() != S.relinfo.size() || S.slot_rows.size() != S.relinfo.size()) return false;
     for (const void *p : {(const void *)D.all_off, (const void *)D.all_subj, (const void *)D.rev_off, (const void *)D.rev_nodes,
                           (const void *)D.set_row, (const void *)D.set_dst, (const void *)D.probe, (const void *)D.reloc,
                           (const void *)R.all_shard})
@@ -1089,9 +1142,17 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
     std::vector<uint32_t> all_v, set_v, rev_v, all_len(m), set_len(m), rev_len(ms);
     std::vector<unsigned long long> shard_v;
     long long d_all = 0, d_set = 0, d_rev = 0;
+    auto slot_of = [&](uint32_t node) {
+        const uint32_t ns = S.ns_of(node);
+        return S.ns[ns].slot_base + (node - S.ns[ns].node_base) % S.ns[ns].n_slots;
+    };
+    std::unordered_map<uint32_t, long long> d_in;  // per slot: the change of its incoming set edges
     for (uint32_t j = 0; j < m; j++) {
         std::vector<std::pair<unsigned long long, uint32_t>> row;
-        for (uint32_t k = all_off0[j]; k < all_off0[j + 1]; k++) row.emplace_back(shard_v0[k], all_v0[k]);
+        for (uint32_t k = all_off0[j]; k < all_off0[j + 1]; k++) {
+            row.emplace_back(shard_v0[k], all_v0[k]);
+            if (all_v0[k] & SKEY_SET) d_in[slot_of(all_v0[k] & ~SKEY_SET)]--;
+        }
         for (uint32_t i : ops_n[j]) {
             const uint32_t v = pl[i].y;
             if (is_ins[i]) {
@@ -1112,6 +1173,7 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
             shard_v.push_back(x.first);
             if (x.second & SKEY_SET) {
                 set_v.push_back(x.second & ~SKEY_SET);
+                d_in[slot_of(x.second & ~SKEY_SET)]++;
                 ns++;
             }
         }
@@ -1262,40 +1324,16 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
         KETO_HIP(hipGetLastError());
     }
     phase("write");
-    // relation info: RI_SETROWS of the slots whose rows flipped (a slot emptied keeps it while any
-    // row of it holds a subject set), RI_IDROWS grows by the inserts
+    // relation info: RI_SETROWS of the slots whose rows flipped -- the slot's count of non-empty
+    // set rows, kept from the rows themselves --, RI_IDROWS grows by the inserts; the per-slot
+    // edge counts the reachability tables read (tabled_slots)
     {
-        auto slot_of = [&](uint32_t node) {
-            const uint32_t ns = S.ns_of(node);
-            return S.ns[ns].slot_base + (node - S.ns[ns].node_base) % S.ns[ns].n_slots;
-        };
-        std::vector<uint32_t> emptied;
+        for (const auto &kv : d_in) S.slot_in[kv.first] = (uint64_t)((long long)S.slot_in[kv.first] + kv.second);
         for (uint32_t j = 0; j < m; j++) {
             if ((set_len[j] == 0) == (old_set[j].x == old_set[j].y)) continue;
             const uint32_t gs = slot_of(key_n[j]);
-            if (set_len[j]) S.relinfo[gs] |= RI_SETROWS;
-            else emptied.push_back(gs);
-        }
-        std::sort(emptied.begin(), emptied.end());
-        emptied.erase(std::unique(emptied.begin(), emptied.end()), emptied.end());
-        if (!emptied.empty()) {
-            std::vector<uint4> job;  // {global slot, first node, nodes, stride}
-            for (uint32_t gs : emptied) {
-                uint32_t ns = 0;
-                while (ns + 1 < S.n_ns && S.ns[ns + 1].slot_base <= gs) ns++;
-                const NsDev &nd = S.ns[ns];
-                const uint32_t ents = (S.ns[ns + 1].node_base - nd.node_base) / std::max(1u, nd.n_slots);
-                job.push_back(make_uint4(gs, nd.node_base + (gs - nd.slot_base), ents, nd.n_slots));
-            }
-            DevBuf d_job = up(job), flag(4ull * job.size());
-            KETO_HIP(hipMemset(flag.p, 0, 4ull * job.size()));
-            hipLaunchKernelGGL(k_slot_any, dim3((uint32_t)num_cus(S.device) * 4), dim3(BLK), 0, 0, set_row,
-                               static_cast<const uint4 *>(d_job.p), (uint32_t)job.size(), flag.u32());
-            KETO_HIP(hipGetLastError());
-            std::vector<uint32_t> hf(job.size());
-            KETO_HIP(hipMemcpy(hf.data(), flag.p, 4ull * job.size(), hipMemcpyDeviceToHost));
-            for (size_t k = 0; k < job.size(); k++)
-                S.relinfo[job[k].x] = (S.relinfo[job[k].x] & ~RI_SETROWS) | (hf[k] ? RI_SETROWS : 0u);
+            S.slot_rows[gs] = set_len[j] ? S.slot_rows[gs] + 1 : S.slot_rows[gs] - 1;
+            S.relinfo[gs] = (S.relinfo[gs] & ~RI_SETROWS) | (S.slot_rows[gs] ? RI_SETROWS : 0u);
         }
         for (uint32_t node : idrow_nodes) S.relinfo[slot_of(node)] |= RI_IDROWS;
         uint32_t *ri = S.sole(D.relinfo) ? const_cast<uint32_t *>(D.relinfo)

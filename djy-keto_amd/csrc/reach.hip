@@ -275,7 +275,9 @@ uint64_t tabled_slots(Snapshot &s, std::vector<uint32_t> &base, std::vector<uint
     DevSnapshot &D = s.dev;
     const uint32_t n_slots = (uint32_t)s.relinfo.size();
     std::vector<uint32_t> target(n_slots, 0);
-    {
+    if (s.slot_in.size() == n_slots) {  // a room snapshot keeps the counts (its set_dst holds moved rows' old copies)
+        for (uint32_t g = 0; g < n_slots; g++) target[g] = s.slot_in[g] != 0;
+    } else {
         DevBuf flag(4ull * n_slots);
         KETO_HIP(hipMemset(flag.p, 0, 4ull * n_slots));
         const uint64_t ne = s.info.n_set_edges;

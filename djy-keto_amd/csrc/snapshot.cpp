@@ -672,6 +672,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.n_nodes = N;
     D.n_uuids = s.n_uuids;
     D.strict = s.strict;
+    if (room) room_slot_counts(s);  // (before the tables: tabled_slots reads them)
     build_reach(s);
     KETO_HIP(hipStreamSynchronize(nullptr));  // the build ran on the null stream; engines read it from theirs
     phase("finish");

@@ -116,3 +116,82 @@ def test_reach_worlds_match_oracle(seed, strict, max_width):
         snap.close()
     finally:
         stream.close()
+
+
+def test_reach_tables_follow_in_place_advances():
+    """keto_store_snapshot_advance keeps the tables exact where the set of tabled slots changes and
+    where reaches cross the cap: transactions on a reach world cut the 140-child group under the
+    cap, make Team#members a target of Folder viewers and then no target at all, grow and break
+    nested-group chains, make Group#owners a target (a newly tabled slot: the tables rebuilt over
+    the moved rows) and no target again -- after each, one store snapshot advanced in place answers, spawns and
+    tables (n_reach) exactly as a full build of the same version (the decisions also as the oracle's)"""
+    import json
+
+    from product_helpers import tuples_to_product
+    from store_ref import transact
+
+    w, t, q = reach_world(4, False, 100)
+    rng = np.random.default_rng(40)
+    names = (json.dumps(w.namespaces), w.ns_names.names, w.rel_names.names)
+    host = tuples_to_product(t)
+    st = km.TupleStore(host)
+    n_uuids = max(1, len(w.uuids.names))
+    snap = km.Snapshot(names[0], None, names[1], names[2], n_uuids, store=st)
+    qp = queries_to_product(q)
+
+    def rows(lines):
+        hi, lo = refsem.seeded_shard_ids(len(lines), int(rng.integers(1 << 30)))
+        return tuples_to_product(w.tuple_array(lines, hi, lo))
+
+    def _rs(p):  # product records back to the oracle's layout
+        out = np.zeros(len(p), dtype=refsem.TUPLE_DT)
+        for a, b in (("ns", "ns"), ("obj", "obj"), ("rel", "rel"), ("subj_kind", "kind"), ("s_obj", "sid"),
+                     ("s_ns", "sns"), ("s_rel", "srel")):
+            out[b] = p[a]
+        sb = p["shard_id"].astype(np.uint64)
+        out["shard_hi"] = sum(sb[:, k] << np.uint64(8 * (7 - k)) for k in range(8))
+        out["shard_lo"] = sum(sb[:, 8 + k] << np.uint64(8 * (7 - k)) for k in range(8))
+        return out
+
+    steps = [
+        (None, [f"Group:big#members@Group:g{k}#members" for k in range(120)]),  # the big group falls under the cap
+        ([f"Folder:f{f}#viewers@Team:t{f % 7}#members" for f in range(20)]  # Team#members: a target of viewers
+         + [f"Group:g{g}#members@Group:g{g + 1}#members" for g in range(30, 60)]
+         + ["Folder:f3#viewers@Group:g5#owners"], None),  # Group#owners a target: a newly tabled slot
+        (None, [f"Folder:f{f}#viewers@Team:t{f % 7}#members" for f in range(20)]  # ... and none again
+         + [f"Group:g{g}#members@Team:t{g % 7}#members" for g in range(220)]
+         + ["Folder:f3#viewers@Group:g5#owners"]),  # Group#owners untabled again
+        ([f"Group:big#members@Group:g{k}#members" for k in range(150, 219)], [f"Group:g{g}#members@Group:g{g + 1}#members"
+                                                                            for g in range(40, 50)]),
+    ]
+    for i, (ins, dele) in enumerate(steps):
+        ins_p = rows(ins) if ins else host[:0]
+        del_p = rows(dele) if dele else host[:0]
+        st.transact(ins_p, del_p)
+        host = transact(host, ins_p, del_p)
+        assert snap.advance(st), i
+        full = km.Snapshot(names[0], None, names[1], names[2], n_uuids, store=st)  # (spares alike: n_reach counts them)
+        out = []
+        for s in (snap, full):
+            stream = km.Stream(0)
+            eng = km.CheckEngine(s, stream, max_read_depth=w.max_depth, max_read_width=w.max_width)
+            stream.frontier_stats(reset=True)
+            a, e = eng.check_batch(qp)
+            fs = stream.frontier_stats(reset=True)
+            out.append((a, e, fs["goals"], fs["routed"], s.info()["n_reach"]))
+            stream.close()
+        (a1, e1, g1, r1, n1), (a2, e2, g2, r2, n2) = out
+        np.testing.assert_array_equal(a1, a2)
+        np.testing.assert_array_equal(e1, e2)
+        assert n1 == n2, (i, n1, n2)
+        assert r1 == r2
+        if r1 == 0:
+            assert g1 == g2, (i, g1, g2)
+        orc = refsem.Oracle(w, _rs(host))
+        orc.set_limits(w.max_depth, w.max_width)
+        dec, err, _ = orc.check_batch(q, threads=4)
+        np.testing.assert_array_equal(a1, dec)
+        np.testing.assert_array_equal(e1, err)
+        full.close()
+    snap.close()
+    st.close()
