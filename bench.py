@@ -585,8 +585,9 @@ def run_c5(args, rank, world, device, dist_on):
     ranks_ms = per_rank_ms(elapsed_local / args.steps * 1e3, f"cuda:{device}" if dist_on else "cpu")
     ms_step = elapsed_local / args.steps * 1e3
     # roofline of the step (this rank): the check's algorithmic bytes (BASELINE.md model, counted
-    # on the closure snapshot) + the closure the step moves (each tuple gathered -- read + written
-    # -- and read by the build: 3 x 48 B) over the whole step's time
+    # by the DFS interpreter on the batch's closure snapshot) + on the closure path the closure the
+    # step moves (each tuple gathered -- read + written -- and read by the build: 3 x 48 B), over
+    # the whole step's time
     check_bytes = 8 * cw["rows"][0] + 4 * cw["edges"][0] + 8 * cw["probes"][0] + 17 * cw["queries"][0]
     step_bytes = check_bytes + 3 * 48 * closure_tuples
     achieved = step_bytes / (ms_step * 1e-3) / 1e9
@@ -639,7 +640,9 @@ def run_c5(args, rank, world, device, dist_on):
                                 if distributed else "the whole step: closure exchange + closure build + check (one rank)"),
                      "algorithmic_bytes_per_step": int(step_bytes), "check_bytes": int(check_bytes),
                      "closure_tuples": int(closure_tuples),
-                     "bytes_model": "8*rows + 4*edges + 8*probes + 17*queries (check) + 3*48*closure tuples"},
+                     "bytes_model": ("8*rows + 4*edges + 8*probes + 17*queries (check; the goal records and values "
+                                     "the step exchanges are in distributed.exchange_bytes)" if distributed or resident else
+                                     "8*rows + 4*edges + 8*probes + 17*queries (check) + 3*48*closure tuples")},
         "cpu_baseline": None,
     }
     if rank == 0 and not args.no_cpu_baseline:
