@@ -222,31 +222,47 @@ __global__ void k_gen_total(const uint32_t *gbase, const uint32_t *gcount, uint3
 }
 
 // Returns: the values of the goals that arrived at a generation, in receive order: {value, goals
-// below | routed << 31}
-__global__ __launch_bounds__(DBLK) void k_ret_gather(FrontierParams P, const uint32_t *arrived, uint32_t n, uint2 *ret) {
+// below | routed << 31}, 8 bytes -- or 4 when the job's values fit (`narrow`: relation name ids
+// below 2^15 for the NO_RELATION detail, a goal budget below VAL_GOALS_SAT, which the goal count
+// saturates at: any count past the budget routes alike)
+constexpr uint32_t VAL_GOALS_SAT = 2047;
+__device__ __forceinline__ uint32_t val_pack(uint32_t x, uint32_t y) {
+    // membership 2 bits, FOUND_BIT, error code (<= 3) 2 bits, relation name 15 bits, goals 11 bits, routed
+    return (x & 3u) | ((x >> 4) & 1u) << 2 | ((x >> 8) & 3u) << 3 | ((x >> 16) & 0x7FFFu) << 5 |
+           std::min(y & 0x7FFFFFFFu, VAL_GOALS_SAT) << 20 | (y & (1u << 31));
+}
+__device__ __forceinline__ uint2 val_unpack(uint32_t p) {
+    return make_uint2((p & 3u) | ((p >> 2) & 1u) << 4 | ((p >> 3) & 3u) << 8 | ((p >> 5) & 0x7FFFu) << 16,
+                      ((p >> 20) & 0x7FFu) | (p & (1u << 31)));
+}
+__device__ __forceinline__ uint2 ret_read(const void *ret, uint64_t i, bool narrow) {
+    return narrow ? val_unpack(static_cast<const uint32_t *>(ret)[i]) : static_cast<const uint2 *>(ret)[i];
+}
+__global__ __launch_bounds__(DBLK) void k_ret_gather(FrontierParams P, const uint32_t *arrived, uint32_t n, void *ret, bool narrow) {
     for (uint64_t i = dgid(); i < n; i += dstride()) {
         const uint32_t idx = arrived[i];
-        if (idx == NONE32) {
-            ret[i] = make_uint2(M_UNK, 1u << 31);
-            continue;
+        uint2 r = make_uint2(M_UNK, 1u << 31);
+        if (idx != NONE32) {
+            const uint2 v = P.gvs[idx];
+            const uint32_t pos = P.g0[idx].y;
+            r = make_uint2(v.x, std::min(v.y, 0x7FFFFFFFu) | (routed(P, pos) ? 1u << 31 : 0u));
         }
-        const uint2 v = P.gvs[idx];
-        const uint32_t pos = P.g0[idx].y;
-        ret[i] = make_uint2(v.x, std::min(v.y, 0x7FFFFFFFu) | (routed(P, pos) ? 1u << 31 : 0u));
+        if (narrow) static_cast<uint32_t *>(ret)[i] = val_pack(r.x, r.y);
+        else static_cast<uint2 *>(ret)[i] = r;
     }
 }
 // ... into the proxies that sent them (send order), before the generation above is reduced
-__global__ __launch_bounds__(DBLK) void k_ret_apply(FrontierParams P, const uint32_t *sent_px, uint32_t n, const uint2 *ret) {
+__global__ __launch_bounds__(DBLK) void k_ret_apply(FrontierParams P, const uint32_t *sent_px, uint32_t n, const void *ret, bool narrow) {
     for (uint64_t i = dgid(); i < n; i += dstride()) {
         const uint32_t px = sent_px[i];
-        const uint2 r = ret[i];
+        const uint2 r = ret_read(ret, i, narrow);
         P.gvs[px] = make_uint2(r.x, r.y & 0x7FFFFFFFu);
         if (r.y >> 31) route(P, P.g0[px].y);
     }
 }
 // ... or, generation 0, to the queries' homes
-__global__ __launch_bounds__(DBLK) void k_ret_home(const uint32_t *sent_px, uint32_t n, const uint2 *ret, uint2 *hv) {
-    for (uint64_t i = dgid(); i < n; i += dstride()) hv[sent_px[i]] = ret[i];
+__global__ __launch_bounds__(DBLK) void k_ret_home(const uint32_t *sent_px, uint32_t n, const void *ret, bool narrow, uint2 *hv) {
+    for (uint64_t i = dgid(); i < n; i += dstride()) hv[sent_px[i]] = ret_read(ret, i, narrow);
 }
 
 // Job-wide repeats.  Every rank holds the job's decisive entries {scope, key, home}, grouped by
@@ -876,7 +892,11 @@ void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowe
         }
     }
     // bottom-up: each generation reduced on every rank, then the values of the goals other ranks
-    // sent back to their proxies (generation 0: to the homes)
+    // sent back to their proxies (generation 0: to the homes) -- 4 bytes each when they fit
+    // (KETO_DIST_WIDE_VALUES=1: always 8, A/B)
+    static const bool wide_env = getenv("KETO_DIST_WIDE_VALUES") != nullptr;
+    const bool narrow = !wide_env && std::max(E.snap->n_rel, E.snap->n_rel_caller) <= 0x8000u && E.budget < VAL_GOALS_SAT;
+    const uint64_t vbytes = narrow ? 4 : 8;
     E.hv.reserve(std::max<uint64_t>(1, n) * 8, 0, s);
     KETO_HIP(hipMemsetAsync(E.hv.p, 0, std::max<uint64_t>(1, n) * 8, s));
     for (int32_t j = (int32_t)G - 1; j >= 0; j--) {
@@ -889,7 +909,7 @@ void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowe
         if (L.n_recv) {
             E.ret.reserve(L.n_recv * 8, 0, s);
             hipLaunchKernelGGL(k_ret_gather, dgrid(L.n_recv), dim3(DBLK), 0, s, P, E.arrived.as<uint32_t>() + L.recv_off,
-                               (uint32_t)L.n_recv, E.ret.as<uint2>());
+                               (uint32_t)L.n_recv, E.ret.p, narrow);
             KETO_HIP(hipGetLastError());
         }
         KETO_HIP(hipEventRecord(E.ev[1], s));
@@ -897,8 +917,8 @@ void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowe
             std::vector<uint64_t> sb(W), rb(W);
             uint64_t back = 0;
             for (uint32_t r = 0; r < W; r++) {
-                sb[r] = L.recv[r] * 8;
-                rb[r] = L.sent[r] * 8;
+                sb[r] = L.recv[r] * vbytes;
+                rb[r] = L.sent[r] * vbytes;
                 if (r != E.rank) back += sb[r];
             }
             L.stat.tuple_bytes_sent = back;
@@ -907,10 +927,10 @@ void check_chunk(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowe
             if (L.n_sent) {
                 if (j > 0)
                     hipLaunchKernelGGL(k_ret_apply, dgrid(L.n_sent), dim3(DBLK), 0, s, P, E.sent_px.as<uint32_t>() + L.sent_off,
-                                       (uint32_t)L.n_sent, E.rret.as<uint2>());
+                                       (uint32_t)L.n_sent, (const void *)E.rret.p, narrow);
                 else
                     hipLaunchKernelGGL(k_ret_home, dgrid(L.n_sent), dim3(DBLK), 0, s, E.sent_px.as<uint32_t>() + L.sent_off,
-                                       (uint32_t)L.n_sent, E.rret.as<uint2>(), E.hv.as<uint2>());
+                                       (uint32_t)L.n_sent, (const void *)E.rret.p, narrow, E.hv.as<uint2>());
                 KETO_HIP(hipGetLastError());
             }
         }
