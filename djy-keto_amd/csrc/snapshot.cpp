@@ -419,54 +419,17 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         s.spares->count.resize(s.n_ns);
         s.spares->used.assign(s.n_ns, 0);
     }
-    // Slot padding: a namespace's slots rounded up to 1, 2, 4, 8 or a multiple of 8, and its entity
-    // count so its nodes fill whole groups of 8 -- an entity's set rows (16 B each) then sit in one
-    // 128-B line (Drive's 7 relations: 112 B, straddling two lines for about half the entities;
-    // a goal walking a folder reads 5 of them).  The extra slots name no relation (nsrel never
-    // maps to them) and their nodes hold no rows; the extra entities are phantoms (no object).
-    // Not where it would cost the node-id format (2^30: EDGE_LEAF) or the id space; KETO_SLOT_PAD=0: off (A/B).
-    auto padded = [](uint32_t k) -> uint32_t { return k <= 1 ? k : (k <= 2 ? 2 : (k <= 4 ? 4 : (k + 7) / 8 * 8)); };
-    auto spares_of = [&](uint32_t ns) -> uint64_t { return with_spares && s.ns[ns].n_slots ? (uint64_t)(rank0[ns + 1] - rank0[ns]) / 16 + 256 : 0; };
-    bool pad = !(getenv("KETO_SLOT_PAD") && getenv("KETO_SLOT_PAD")[0] == '0') && !ghosts;
-    if (pad) {
-        uint64_t raw = 0, with = 0;
-        for (uint32_t ns = 0; ns < s.n_ns; ns++) {
-            const uint64_t ne = (uint64_t)(rank0[ns + 1] - rank0[ns]) + spares_of(ns) + 1, sl = s.ns[ns].n_slots, ps = padded((uint32_t)sl);
-            raw += ne * sl;
-            with += (ps ? (ne * ps + 7) / 8 * 8 : 0);
-        }
-        bool same = true;
-        for (uint32_t ns = 0; ns < s.n_ns; ns++) same = same && padded(s.ns[ns].n_slots) == s.ns[ns].n_slots;
-        if ((with >= (1ull << 30) && raw < (1ull << 30)) || with >= VIRT_BIT || (uint64_t)s.n_uuids + with + 1 >= (1ull << 32)) pad = false;
-        if (pad && !same) {  // the slot tables again, with the extra slots
-            std::vector<uint32_t> slot_rel2, relinfo2;
-            for (uint32_t ns = 0; ns < s.n_ns; ns++) {
-                const uint32_t k = s.ns[ns].n_slots, b = s.ns[ns].slot_base, pk = padded(k);
-                const uint32_t nb = (uint32_t)slot_rel2.size();
-                for (uint32_t j = 0; j < pk; j++) {
-                    slot_rel2.push_back(j < k ? s.slot_rel[b + j] : NONE32);  // (an extra slot: no relation)
-                    relinfo2.push_back(j < k ? s.relinfo[b + j] : s.relinfo[b] & ~(RI_SETROWS | RI_IDROWS | RI_REACH));
-                }
-                s.ns[ns].slot_base = nb;
-                s.ns[ns].n_slots = pk;
-            }
-            s.slot_rel.swap(slot_rel2);
-            s.relinfo.swap(relinfo2);
-            total_slots = (uint32_t)s.relinfo.size();
-        }
-    }
     for (uint32_t ns = 0; ns < s.n_ns; ns++) {
         n_real[ns] = rank0[ns + 1] - rank0[ns];
         s.ns[ns].ent_base = ent_base[ns] = (uint32_t)ent_total;
         s.ns[ns].node_base = (uint32_t)node_total;
         // real entities, then the spares a store snapshot keeps for new objects, then the phantom
-        const uint32_t spare = (uint32_t)spares_of(ns);
+        const uint32_t spare = with_spares && s.ns[ns].n_slots ? n_real[ns] / 16 + 256 : 0;
         if (s.spares) {
             s.spares->first[ns] = ent_base[ns] + n_real[ns];
             s.spares->count[ns] = spare;
         }
         uint64_t ne = (uint64_t)n_real[ns] + spare + 1;  // + phantom
-        if (pad && s.ns[ns].n_slots) ne = (ne * s.ns[ns].n_slots + 7) / 8 * 8 / s.ns[ns].n_slots;  // (phantoms)
         ent_total += ne;
         node_total += ne * s.ns[ns].n_slots;
         if (node_total >= VIRT_BIT || ent_total >= VIRT_BIT) throw Error(KETO_E_LIMIT, "node space exceeds 2^31");
@@ -582,8 +545,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         std::unordered_map<std::string, std::vector<uint32_t>> cls;  // class string -> global slots
         for (uint32_t ns = 0; ns < s.n_ns; ns++)
             for (uint32_t k = 0; k < s.ns[ns].n_slots; k++)
-                if (s.slot_rel[s.ns[ns].slot_base + k] != NONE32)  // (padding slots have no relation, no class)
-                    cls[s.ns_names[ns] + "-" + s.rel_names[s.slot_rel[s.ns[ns].slot_base + k]]].push_back(s.ns[ns].slot_base + k);
+                cls[s.ns_names[ns] + "-" + s.rel_names[s.slot_rel[s.ns[ns].slot_base + k]]].push_back(s.ns[ns].slot_base + k);
         bool any_shared = false;
         for (auto &kv : cls)
             if (kv.second.size() > 1) any_shared = true;
