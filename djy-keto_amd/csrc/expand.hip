@@ -535,11 +535,12 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
     if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
     auto &X = st.xw;
     const uint32_t cus = (uint32_t)num_cus(s.device);
-    // one-wave blocks of 9 KB LDS each, KETO_XW_BPC per CU (default 8).  C4, 4,096 roots: 8 per CU
-    // (two roots after another per wave) 0.67 ms, 16 per CU (every root at once) 0.73 ms
+    // one-wave blocks of 9 KB LDS each, KETO_XW_BPC per CU (default 4).  C4, 4,096 roots (round 5):
+    // 2 per CU 0.665 ms, 3-5 per CU 0.605-0.616 ms, 6 0.619, 8 0.633, 12 0.659 (round 4: 16 per CU,
+    // every root at once, 0.73 ms): fewer waves in flight wait less on the rows they share
     static const uint64_t bpc = [] {
         const char *e = getenv("KETO_XW_BPC");
-        return e ? (uint64_t)std::max(1, std::min(atoi(e), 17)) : 8ull;
+        return e ? (uint64_t)std::max(1, std::min(atoi(e), 17)) : 4ull;
     }();
     const uint64_t grid = (uint64_t)cus * bpc;
     if (!X.mem || X.ncap < n || X.grid < grid) {
