@@ -159,10 +159,11 @@ __device__ __forceinline__ void add_dec(const BlockParams &P, Chunk &C, uint32_t
     C.ndec = 1;
 }
 
-// 5 waves per SIMD (96 VGPRs): with the spine's state, 6 waves spilled 41 VGPRs; C4 p99 of 64Ki
-// batches 0.566 / 0.562 vs 0.583 / 0.586 ms at 6 (profiles/r04_waves_ab.txt)
+// 7 waves per SIMD (72 VGPRs, spilling): round 5, C4 p99 of 64Ki batches 0.645 / 0.640 vs 0.663 /
+// 0.658 ms at 5 (the generation engine likewise, frontier_kernels.inc).  (Round 4, before the
+// reachability tables: 5 waves 0.566 / 0.562 vs 0.583 / 0.586 ms at 6, profiles/r04_waves_ab.txt)
 #ifndef KETO_FRB_WAVES
-#define KETO_FRB_WAVES 5
+#define KETO_FRB_WAVES 7
 #endif
 
 template <bool LDS_TABLES>
