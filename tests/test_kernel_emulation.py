@@ -86,15 +86,15 @@ def test_unserved_lanes_lose_operands_but_stay_in_range(tmp_path):
 def test_patched_snapshots_exact_under_emulation(tmp_path):
     """keto_store_snapshot_patch and _advance under the CPU emulation (one lane at a time, so even
     routed queries' goal counts are deterministic): patched and advanced snapshots equal full builds
-    in every answer, goal count and Expand tree (tests/test_gpu_store.py, the patch and advance
-    cases)"""
+    in every answer, goal count and Expand tree; the store's content index through churn and a mass
+    delete (tests/test_gpu_store.py, the patch, advance and index cases)"""
     lib = tmp_path / "libketo_emu_patch.so"
     jobs = str(min(8, os.cpu_count() or 1))
     subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(ROOT, "tools", "cpuemu"),
                     f"OBJDIR={tmp_path / 'obj'}", f"LIB={lib}", "OPT=-O1"], check=True, timeout=600)
     env = dict(os.environ, KETO_MI355X_ALLOW_OVERRIDE="tools", KETO_MI355X_LIB_OVERRIDE=str(lib))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
-                        os.path.join(ROOT, "tests", "test_gpu_store.py"), "-k", "patch or advance"],
+                        os.path.join(ROOT, "tests", "test_gpu_store.py"), "-k", "patch or advance or index"],
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "8 passed" in r.stdout
+    assert "11 passed" in r.stdout
