@@ -159,11 +159,12 @@ __device__ __forceinline__ void add_dec(const BlockParams &P, Chunk &C, uint32_t
     C.ndec = 1;
 }
 
-// 7 waves per SIMD (72 VGPRs, spilling): round 5, C4 p99 of 64Ki batches 0.645 / 0.640 vs 0.663 /
-// 0.658 ms at 5 (the generation engine likewise, frontier_kernels.inc).  (Round 4, before the
-// reachability tables: 5 waves 0.566 / 0.562 vs 0.583 / 0.586 ms at 6, profiles/r04_waves_ab.txt)
+// 4 waves per SIMD (108 VGPRs, 32 B of scratch; the 25 KB of LDS per workgroup caps it at 6
+// anyway): round 5, C4 p99 of 64Ki batches 0.645 / 0.640 vs 0.663 / 0.658 ms at 5 (96 VGPRs,
+// 64 B of scratch).  (Round 4, before the reachability tables: 5 waves 0.566 / 0.562 vs 0.583 /
+// 0.586 ms at 6, profiles/r04_waves_ab.txt)
 #ifndef KETO_FRB_WAVES
-#define KETO_FRB_WAVES 7
+#define KETO_FRB_WAVES 4
 #endif
 
 template <bool LDS_TABLES>
