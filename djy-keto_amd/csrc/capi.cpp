@@ -50,6 +50,7 @@ Stream::~Stream() {
     if (check_scratch.mem) (void)hipFree(check_scratch.mem);
     if (expand_scratch.mem) (void)hipFree(expand_scratch.mem);
     if (frontier.mem) (void)hipFree(frontier.mem);
+    if (frontier.stash) (void)hipFree(frontier.stash);
     if (frontier.host_ctrl) (void)hipHostFree(frontier.host_ctrl);
     if (frontier.host_gens) (void)hipHostFree(frontier.host_gens);
     if (frontier.gens_ev) (void)hipEventDestroy(frontier.gens_ev);
@@ -124,6 +125,8 @@ void Stream::harvest() {
 // the opaque ABI handles are the internal objects themselves
 static keto::Snapshot *SN(keto_snapshot *p) { return reinterpret_cast<keto::Snapshot *>(p); }
 static const keto::Snapshot *SN(const keto_snapshot *p) { return reinterpret_cast<const keto::Snapshot *>(p); }
+// a snapshot whose in-place advance failed after its first write (Snapshot::broken)
+static const char *BROKEN = "snapshot unusable: an in-place advance failed after its first write; cut a fresh one";
 static keto::Stream *ST(keto_stream *p) { return reinterpret_cast<keto::Stream *>(p); }
 
 extern "C" {
@@ -170,6 +173,7 @@ int keto_snapshot_build_device(const keto_snapshot_config *cfg, const keto_tuple
 
 int keto_snapshot_save(const keto_snapshot *snap, const char *path) {
     if (!snap || !path) return fail(KETO_E_INVALID, "null argument");
+    if (SN(snap)->broken) return fail(KETO_E_INVALID, BROKEN);
     return guarded([&] { keto::save_snapshot(*SN(snap), path); });
 }
 
@@ -300,6 +304,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
     keto::Snapshot *snap = SN(hsnap);
     keto::Stream *s = ST(hs);
     if (!snap || !s) return fail(KETO_E_INVALID, "null snapshot or stream");
+    if (snap->broken) return fail(KETO_E_INVALID, BROKEN);
     if (n && (!queries || !out_allowed || !out_err)) return fail(KETO_E_INVALID, "null buffer");
     keto_limits lim = limits ? *limits : keto_limits{5, 100};
     if (lim.max_read_depth < 1 || lim.max_read_depth > 65535 || lim.max_read_width < 1 || lim.max_read_width > 65535)
@@ -384,6 +389,7 @@ int keto_expand_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_
     keto::Snapshot *snap = SN(hsnap);
     keto::Stream *s = ST(hs);
     if (!snap || !s) return fail(KETO_E_INVALID, "null snapshot or stream");
+    if (snap->broken) return fail(KETO_E_INVALID, BROKEN);
     if (n && (!roots || !out_offsets || !out_err)) return fail(KETO_E_INVALID, "null buffer");
     keto_limits lim = limits ? *limits : keto_limits{5, 100};
     if (lim.max_read_depth < 1 || lim.max_read_depth > 65535) return fail(KETO_E_INVALID, "max_read_depth out of range");
@@ -458,6 +464,7 @@ int keto_trees_to_proto(const keto_tree_node *nodes, const uint64_t *offsets, ui
 
 int keto_dispatcher_create(keto_snapshot *snap, const keto_dispatcher_config *cfg, keto_dispatcher **out) {
     if (out) *out = nullptr;
+    if (snap && SN(snap)->broken) return fail(KETO_E_INVALID, BROKEN);
     return guarded([&] { keto::dispatcher_create(snap, cfg, out); });
 }
 
@@ -488,6 +495,7 @@ int keto_dispatcher_expand(keto_dispatcher *d, const keto_subject_set *roots, ui
 }
 
 int keto_dispatcher_set_snapshot(keto_dispatcher *d, keto_snapshot *snap) {
+    if (snap && SN(snap)->broken) return fail(KETO_E_INVALID, BROKEN);
     return guarded([&] { keto::dispatcher_set_snapshot(d, snap); });
 }
 
@@ -586,6 +594,7 @@ int keto_store_snapshot_patch(keto_store *st, const keto_snapshot *base, const k
                               keto_snapshot **out, int32_t *patched) {
     if (!st || !base || !out) return fail(KETO_E_INVALID, "null argument");
     *out = nullptr;
+    if (SN(base)->broken) return fail(KETO_E_INVALID, BROKEN);
     return guarded([&] {
         bool p = false;
         *out = reinterpret_cast<keto_snapshot *>(
@@ -597,6 +606,7 @@ int keto_store_snapshot_patch(keto_store *st, const keto_snapshot *base, const k
 int keto_store_snapshot_advance(keto_store *st, keto_snapshot *snap, int32_t *advanced) {
     if (!st || !snap) return fail(KETO_E_INVALID, "null argument");
     if (advanced) *advanced = 0;
+    if (SN(snap)->broken) return fail(KETO_E_INVALID, BROKEN);
     return guarded([&] {
         const bool a = keto::store_snapshot_advance(*reinterpret_cast<keto::TupleStore *>(st), *SN(snap));
         if (advanced) *advanced = a ? 1 : 0;

@@ -58,12 +58,20 @@ struct Tables {
     const uint32_t *op_children;
     const uint32_t *op_items;
     const uint2 *or_items;
+    const double *ns_rcp;
     uint32_t n_ns, n_rel;
     uint32_t n_ns_x;  // ns table entries (ghost namespaces of a partitioned graph's snapshot included)
 };
 __device__ __forceinline__ uint32_t ns_entries(const DevSnapshot &s) { return s.n_ns_x ? s.n_ns_x : s.n_ns; }
 // a ghost namespace's namespace (partitioned graphs; identity otherwise)
 __device__ __forceinline__ uint32_t t_real_ns(const Tables &T, uint32_t ns) { return ns >= T.n_ns ? ns - T.n_ns : ns; }
+
+// (o / n_slots of namespace ns) for an offset o = node - node_base: ((double)o + 0.5) * (1 / n) lies
+// within 3 * 2^-53 * o / n of (o + 0.5) / n, whose distance to the next integers is >= 0.5 / n;
+// exact for o < 2^32 and n < 2^16 (3 * 2^-21 < 0.5 / 65535)
+__device__ __forceinline__ uint32_t t_div_slots(const Tables &T, uint32_t ns, uint32_t o) {
+    return (uint32_t)(((double)o + 0.5) * T.ns_rcp[ns]);
+}
 
 __device__ __forceinline__ uint32_t t_ns_of(const Tables &T, uint32_t node) {
     uint32_t lo = 0, hi = T.n_ns_x;  // last namespace whose node_base <= node
@@ -91,7 +99,8 @@ __device__ __forceinline__ NodeInfo t_node_info(const Tables &T, uint32_t node) 
     }
     r.ns = t_ns_of(T, node);
     const NsDev nd = T.ns[r.ns];
-    r.slot = (node - nd.node_base) % nd.n_slots;
+    const uint32_t o = node - nd.node_base;
+    r.slot = o - t_div_slots(T, r.ns, o) * nd.n_slots;
     r.ri = T.relinfo[nd.slot_base + r.slot];
     return r;
 }
@@ -116,6 +125,23 @@ __device__ __forceinline__ uint32_t t_sibling(const Tables &T, uint32_t node, co
     return node - ni.slot + slot;
 }
 
+// t_sibling and the sibling's node info (= t_node_info of the result) from the node's own: the
+// sibling shares the entity, so its namespace and slot need no search or division
+__device__ __forceinline__ uint32_t t_sibling_ni(const Tables &T, uint32_t node, const NodeInfo &ni, uint32_t rel, NodeInfo &out) {
+    rel = t_rel(T, rel);
+    const uint32_t w = T.nsrel[(size_t)ni.ns * T.n_rel + rel];
+    const uint32_t slot = nr_slot(w);
+    if (slot == NO_SLOT || (node & VIRT_BIT)) {
+        const uint32_t v = VIRT_BIT | (t_real_ns(T, ni.ns) << 16) | (rel & 0xFFFFu);
+        out = t_node_info(T, v);
+        return v;
+    }
+    out.ns = ni.ns;
+    out.slot = slot;
+    out.ri = T.relinfo[T.ns[ni.ns].slot_base + slot];
+    return node - ni.slot + slot;
+}
+
 // node of (ns, entity e, rel) given e; virtual if ns has no slot for rel
 __device__ __forceinline__ uint32_t t_node(const Tables &T, uint32_t ns, uint32_t e, uint32_t rel) {
     rel = t_rel(T, rel);
@@ -131,13 +157,13 @@ __device__ __forceinline__ Tables stage_tables(const DevSnapshot &s, char *lds) 
     T.n_ns = s.n_ns;
     T.n_rel = s.n_rel;
     T.n_ns_x = ns_entries(s);
-    const uint4 *src[7] = {reinterpret_cast<const uint4 *>(s.ns), reinterpret_cast<const uint4 *>(s.relinfo),
+    const uint4 *src[8] = {reinterpret_cast<const uint4 *>(s.ns), reinterpret_cast<const uint4 *>(s.relinfo),
                            reinterpret_cast<const uint4 *>(s.nsrel), reinterpret_cast<const uint4 *>(s.ops),
                            reinterpret_cast<const uint4 *>(s.op_children), reinterpret_cast<const uint4 *>(s.op_items),
-                           reinterpret_cast<const uint4 *>(s.or_items)};
+                           reinterpret_cast<const uint4 *>(s.or_items), reinterpret_cast<const uint4 *>(s.ns_rcp)};
     uint32_t off = 0;
-    char *dst[7];
-    for (int i = 0; i < 7; i++) {
+    char *dst[8];
+    for (int i = 0; i < 8; i++) {
         dst[i] = lds + off;
         const uint32_t n16 = s.tab_bytes[i] / 16;
         for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) reinterpret_cast<uint4 *>(dst[i])[k] = src[i][k];
@@ -151,11 +177,12 @@ __device__ __forceinline__ Tables stage_tables(const DevSnapshot &s, char *lds) 
     T.op_children = reinterpret_cast<const uint32_t *>(dst[4]);
     T.op_items = reinterpret_cast<const uint32_t *>(dst[5]);
     T.or_items = reinterpret_cast<const uint2 *>(dst[6]);
+    T.ns_rcp = reinterpret_cast<const double *>(dst[7]);
     return T;
 }
 
 __device__ __forceinline__ Tables global_tables(const DevSnapshot &s) {
-    return Tables{s.ns, s.relinfo, s.nsrel, s.ops, s.op_children, s.op_items, s.or_items, s.n_ns, s.n_rel, ns_entries(s)};
+    return Tables{s.ns, s.relinfo, s.nsrel, s.ops, s.op_children, s.op_items, s.or_items, s.ns_rcp, s.n_ns, s.n_rel, ns_entries(s)};
 }
 
 }  // namespace keto

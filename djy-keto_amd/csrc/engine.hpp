@@ -92,6 +92,9 @@ struct Snapshot {
     // slot when > 0) and the slot's nodes with a non-empty set row (RI_SETROWS when > 0) -- kept
     // by each advance from its own rows, where a scan of set_dst would read moved rows' old copies
     std::vector<uint64_t> slot_in, slot_rows;
+    // an in-place advance failed after its first write (patch.hip advance_snapshot): rows may be
+    // half-advanced, so the C ABI refuses every further use but keto_snapshot_free
+    bool broken = false;
 
     // a device allocation of this snapshot (back to the pool with its last sharer)
     void own(void *p, size_t bytes);
@@ -225,6 +228,10 @@ struct FrontierScratch {
     bool gens_pending = false;
     uint32_t epoch = 1;  // scope-table epoch of the next batch (frontier.hip TAB_EPOCHS)
     keto_frontier_stats stats{};
+    // phase A's children of rewrite / tuple-to-userset goals, kept for the write-out (frontier_goal.inc
+    // Stash): FR_STASH_K entries of 8 B per resident lane, a column per lane
+    uint2 *stash = nullptr;
+    uint32_t stash_stride = 0;
 };
 
 // per-stream workspace of the block frontier engine (frontier_block.hip)

@@ -185,6 +185,16 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     P.dbits = f.dbits;
     P.dmask = (uint32_t)(f.dcap - 1);
     P.occ = f.occ;
+    // the phase-A stash: a column per resident lane (at most 2048 per CU)
+    static const bool no_stash = getenv("KETO_FR_NOSTASH") != nullptr;  // (A/B: phase B walks every goal again)
+    if (!no_stash && (!f.stash || f.stash_stride < cus * 2048u)) {
+        if (f.stash) KETO_HIP(hipFree(f.stash));
+        f.stash = nullptr;
+        KETO_HIP(hipMalloc(&f.stash, (size_t)FR_STASH_K * cus * 2048u * sizeof(uint2)));
+        f.stash_stride = cus * 2048u;
+    }
+    P.stash = no_stash ? nullptr : f.stash;
+    P.stash_stride = f.stash_stride;
     P.occ_count = f.occ_count;
     P.ocap = (uint32_t)f.ocap;
     P.epoch = f.epoch;
@@ -206,6 +216,26 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     const void *kx = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true, false>) : reinterpret_cast<const void *>(&fr_expand<false, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kx, XBLOCK, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
     const dim3 eg(cus * (uint32_t)std::min(per_cu, (int)(2048 / XBLOCK))), xb(XBLOCK), eb(BLOCK);
+    // generation 0 holds the query roots only (IA or RW goals): an instantiation of its own (KM_ROOT)
+    int per_cu0 = 0;
+    const void *kx0 = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true, false, KM_ROOT>)
+                                 : reinterpret_cast<const void *>(&fr_expand<false, false, KM_ROOT>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu0, kx0, XBLOCK, lds) != hipSuccess || per_cu0 <= 0) per_cu0 = per_cu;
+    const dim3 eg0(cus * (uint32_t)std::min(per_cu0, (int)(2048 / XBLOCK)));
+    auto launch_gen = [&](uint32_t k) {
+        // (A/B: generation 0 on the KM_ROOT instantiation -- round 6, C4: 718 us against the generic
+        // kernel's 618 us with the phase-A stash, so the generic one runs it by default)
+        static const bool root0 = getenv("KETO_FR_ROOT_KERNEL") != nullptr;
+        if (k == 0 && root0) {
+            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false, KM_ROOT>), eg0, xb, lds, st.stream, P);
+            else hipLaunchKernelGGL((fr_expand<false, false, KM_ROOT>), eg0, xb, 0, st.stream, P);
+        } else if (lds_tables) {
+            hipLaunchKernelGGL((fr_expand<true, false>), eg, xb, lds, st.stream, P);
+        } else {
+            hipLaunchKernelGGL((fr_expand<false, false>), eg, xb, 0, st.stream, P);
+        }
+        KETO_HIP(hipGetLastError());
+    };
     if (L.async) {
         // KETO_F_ASYNC: nothing comes back to the host.  The stream's last synchronous batch says
         // how deep a batch goes; G generations (a margin over it) are launched and each one whose
@@ -228,9 +258,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
         P.gen_cap = G;
         for (uint32_t k = 0; k < G; k++) {
             P.gen = k;
-            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false>), eg, xb, lds, st.stream, P);
-            else hipLaunchKernelGGL((fr_expand<false, false>), eg, xb, 0, st.stream, P);
-            KETO_HIP(hipGetLastError());
+            launch_gen(k);
         }
         for (int32_t g = (int32_t)G - 1; g >= 0; g--) {
             P.gen = (uint32_t)g;
@@ -262,13 +290,24 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     const uint64_t scap = f.cap / FR_SHARDS;
     // the first read-back comes after as many generations as the stream's previous batch had (+1,
     // the empty one that ends it): a steady workload pays one host round trip per batch
+    // KETO_FR_GENTIME (diagnostics): HIP events around every generation's expansion, printed per batch
+    static const bool gentime = getenv("KETO_FR_GENTIME") != nullptr;
+    std::vector<hipEvent_t> gev;
     for (uint32_t k = 0; gens == 0;) {
         const uint32_t kend = std::min(k + (k == 0 ? std::max(CHUNK, f.last_gens + 1) : CHUNK), MAX_GEN);
         for (; k < kend; k++) {
             P.gen = k;
-            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false>), eg, xb, lds, st.stream, P);
-            else hipLaunchKernelGGL((fr_expand<false, false>), eg, xb, 0, st.stream, P);
-            KETO_HIP(hipGetLastError());
+            if (gentime) {
+                gev.emplace_back();
+                KETO_HIP(hipEventCreate(&gev.back()));
+                KETO_HIP(hipEventRecord(gev.back(), st.stream));
+            }
+            launch_gen(k);
+        }
+        if (gentime) {
+            gev.emplace_back();
+            KETO_HIP(hipEventCreate(&gev.back()));
+            KETO_HIP(hipEventRecord(gev.back(), st.stream));
         }
         KETO_HIP(hipMemcpyAsync(hc, f.ctrl, 2 * FR_SHARDS * GEN_STRIDE * 4, hipMemcpyDeviceToHost, st.stream));
         KETO_HIP(hipStreamSynchronize(st.stream));
@@ -314,6 +353,16 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     f.stats.goals += top;
     f.stats.generations += gens;
     f.stats.max_generations = std::max<uint64_t>(f.stats.max_generations, gens);
+    if (gentime) {
+        fprintf(stderr, "[gentime] n %llu us:", (unsigned long long)L.n);
+        for (uint32_t g = 0; g + 1 < gev.size() && g <= gens; g++) {
+            float ms = 0;
+            KETO_HIP(hipEventElapsedTime(&ms, gev[g], gev[g + 1]));
+            fprintf(stderr, " %.0f", ms * 1e3);
+        }
+        fprintf(stderr, "\n");
+        for (hipEvent_t e : gev) KETO_HIP(hipEventDestroy(e));
+    }
     static const bool verbose = getenv("KETO_FR_VERBOSE") != nullptr;
     if (verbose) {
         fprintf(stderr, "[frontier] n %llu generations %u goals %llu routed %u:", (unsigned long long)L.n, gens,

@@ -133,10 +133,13 @@ struct DevSnapshot {
     const uint4 *reach_idx;      // [tabled slots' entities] {count | NONE32: not tabled, entry 0, entry 1,
                                  //  pool offset of entries 2.. (runs padded to 4 entries)}
     const uint32_t *reach_pool;  // the reaches past their first two entries (nodes; the node itself not listed)
+    // [ns table entries] 1.0 / n_slots (0 for a namespace without slots): node -> entity without
+    // an integer division (device_common.hpp t_div_slots)
+    const double *ns_rcp;
     int32_t strict;
-    // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children, op_items, or_items:
-    // staged in LDS
-    uint32_t tab_bytes[7];
+    // byte sizes (multiples of 16) of ns, relinfo, nsrel, ops, op_children, op_items, or_items,
+    // ns_rcp: staged in LDS
+    uint32_t tab_bytes[8];
     uint32_t lds_bytes;
 };
 

@@ -738,7 +738,7 @@ Snapshot *patch_snapshot(const Snapshot &B, const keto_tuple *rows, uint64_t n_s
     X.reloc = nullptr;  // (a copy patch is not advanced in place: no room kept)
     for (const void *p : {(const void *)D.weight, (const void *)D.ent_obj, (const void *)D.slot_rel, (const void *)D.vkey,
                           (const void *)D.ns, (const void *)D.nsrel, (const void *)D.ops, (const void *)D.op_children,
-                          (const void *)D.op_items, (const void *)D.or_items, (const void *)D.ent_rank})
+                          (const void *)D.op_items, (const void *)D.or_items, (const void *)D.ent_rank, (const void *)D.ns_rcp})
         s.share(B, p);
     if (P.ext_dev) {
         s.own(P.ext_dev.release(), 16ull * ((uint64_t)Dp.ext_mask + 1));
@@ -1256,7 +1256,22 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
     }
     if (at_all > R.all_cap || at_rev > R.rev_cap || at_set > R.set_cap || n_reloc > R.reloc_cap) return false;  // no room left
     phase("rows");
+    // every staging buffer of the writes, allocated (and filled) before the first write: an
+    // allocation that fails here declines with the snapshot untouched
+    std::vector<uint32_t> flip;  // set rows that changed between empty and not: their parents' EDGE_LEAF
+    for (uint32_t j = 0; j < m; j++)
+        if ((set_len[j] == 0) != (old_set[j].x == old_set[j].y)) flip.push_back(key_n[j]);
+    std::vector<unsigned long long> keys(ins_keys);
+    keys.insert(keys.end(), del_keys.begin(), del_keys.end());
+    DevBuf d_all_v = up(all_v), d_shard_v = up(shard_v), d_rev_v = up(rev_v), d_put_all = up(put_all), d_put_rev = up(put_rev);
+    DevBuf d_at = up(reloc_at), d_val = up(reloc_val), d_words[2] = {up(all_words), up(rev_words)};
+    DevBuf d_sb = up(set_begin), d_sl = up(set_len), d_sv = up(set_v), d_svo = up(set_voff), d_flip = up(flip), d_keys = up(keys);
+    uint32_t *ri_own = S.sole(D.relinfo) ? nullptr : static_cast<uint32_t *>(S.alloc(std::max<size_t>(1, S.relinfo.size()) * 4 + 16));
     // ---- 5. the writes (committed from here on) -----------------------------------------------------
+    // A failure past this point (a launch, a copy, the reachability pool's growth) leaves rows
+    // half-advanced: the snapshot is marked broken and every later call on it is refused
+    // (capi.cpp) until the caller replaces it with a fresh cut.
+    try {
     P.taken.keep = true;
     if (P.ext_dev) {  // the objects this advance created: the new ext table replaces the old one
         const void *old_ext = D.ext;
@@ -1270,7 +1285,6 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
     uint32_t *all_subj = const_cast<uint32_t *>(D.all_subj), *rev_nodes = const_cast<uint32_t *>(D.rev_nodes);
     uint32_t *set_dst = const_cast<uint32_t *>(D.set_dst);
     uint4 *set_row = const_cast<uint4 *>(D.set_row), *reloc = const_cast<uint4 *>(D.reloc);
-    DevBuf d_all_v = up(all_v), d_shard_v = up(shard_v), d_rev_v = up(rev_v), d_put_all = up(put_all), d_put_rev = up(put_rev);
     if (!put_all.empty()) {
         hipLaunchKernelGGL(k_put_vals<uint32_t>, grid_for(put_all.size()), dim3(BLK), 0, 0, all_subj, static_cast<const uint4 *>(d_put_all.p),
                            (uint32_t)put_all.size(), d_all_v.u32());
@@ -1278,12 +1292,13 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
                            static_cast<const uint4 *>(d_put_all.p), (uint32_t)put_all.size(),
                            static_cast<const unsigned long long *>(d_shard_v.p));
     }
+    if (getenv("KETO_FAULT_ADVANCE"))  // (tests only: a failure after the first write)
+        throw Error(KETO_E_DEVICE, "injected fault after the advance's first write (KETO_FAULT_ADVANCE)");
     if (!put_rev.empty())
         hipLaunchKernelGGL(k_put_vals<uint32_t>, grid_for(put_rev.size()), dim3(BLK), 0, 0, rev_nodes, static_cast<const uint4 *>(d_put_rev.p),
                            (uint32_t)put_rev.size(), d_rev_v.u32());
     KETO_HIP(hipGetLastError());
     if (!reloc_at.empty()) {
-        DevBuf d_at = up(reloc_at), d_val = up(reloc_val);
         hipLaunchKernelGGL(k_put_reloc, grid_for(reloc_at.size()), dim3(BLK), 0, 0, reloc, d_at.u32(), static_cast<const uint4 *>(d_val.p),
                            (uint32_t)reloc_at.size());
         KETO_HIP(hipGetLastError());
@@ -1291,33 +1306,24 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
     for (int w = 0; w < 2; w++) {
         const std::vector<uint2> &words = w ? rev_words : all_words;
         if (words.empty()) continue;
-        DevBuf d_w = up(words);
-        hipLaunchKernelGGL(k_put_words, grid_for(words.size()), dim3(BLK), 0, 0, w ? rev_off : all_off, static_cast<const uint2 *>(d_w.p),
+        hipLaunchKernelGGL(k_put_words, grid_for(words.size()), dim3(BLK), 0, 0, w ? rev_off : all_off, static_cast<const uint2 *>(d_words[w].p),
                            (uint32_t)words.size());
         KETO_HIP(hipGetLastError());
     }
     // set rows: extents, then edges (flags from the new rows) and their inline copies
     if (m) {
-        DevBuf d_sb = up(set_begin), d_sl = up(set_len), d_sv = up(set_v), d_svo = up(set_voff);
         hipLaunchKernelGGL(k_put_setrow_extent, grid_for(m), dim3(BLK), 0, 0, set_row, d_key_n.u32(), d_sb.u32(), d_sl.u32(), m);
         hipLaunchKernelGGL(k_put_edges, grid_for(m), dim3(BLK), 0, 0, D, set_row, set_dst, d_key_n.u32(), d_sv.u32(), d_svo.u32(), m);
         KETO_HIP(hipGetLastError());
     }
-    std::vector<uint32_t> flip;  // set rows that changed between empty and not: their parents' EDGE_LEAF
-    for (uint32_t j = 0; j < m; j++)
-        if ((set_len[j] == 0) != (old_set[j].x == old_set[j].y)) flip.push_back(key_n[j]);
     if (D.edge_leaf && !flip.empty()) {
-        DevBuf d_flip = up(flip);
         hipLaunchKernelGGL(k_flip_leaf, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, D, set_row, set_dst, rev_off, rev_nodes,
                            d_flip.u32(), (uint32_t)flip.size());
         hipLaunchKernelGGL(k_fix_inline, dim3((uint32_t)flip.size()), dim3(BLK), 0, 0, D, set_row, set_dst, rev_off, rev_nodes,
                            d_flip.u32(), (uint32_t)flip.size());
         KETO_HIP(hipGetLastError());
     }
-    if (!ins_keys.empty() || !del_keys.empty()) {
-        std::vector<unsigned long long> keys(ins_keys);
-        keys.insert(keys.end(), del_keys.begin(), del_keys.end());
-        DevBuf d_keys = up(keys);
+    if (!keys.empty()) {
         hipLaunchKernelGGL(k_probe_apply, grid_for(keys.size()), dim3(BLK), 0, 0,
                            reinterpret_cast<unsigned long long *>(const_cast<uint4 *>(D.probe)), (uint64_t)D.probe_mask,
                            static_cast<const unsigned long long *>(d_keys.p), (uint32_t)ins_keys.size(), (uint32_t)del_keys.size());
@@ -1336,8 +1342,7 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
             S.relinfo[gs] = (S.relinfo[gs] & ~RI_SETROWS) | (S.slot_rows[gs] ? RI_SETROWS : 0u);
         }
         for (uint32_t node : idrow_nodes) S.relinfo[slot_of(node)] |= RI_IDROWS;
-        uint32_t *ri = S.sole(D.relinfo) ? const_cast<uint32_t *>(D.relinfo)
-                                         : static_cast<uint32_t *>(S.alloc(std::max<size_t>(1, S.relinfo.size()) * 4 + 16));
+        uint32_t *ri = ri_own ? ri_own : const_cast<uint32_t *>(D.relinfo);
         if (!S.relinfo.empty()) KETO_HIP(hipMemcpy(ri, S.relinfo.data(), 4 * S.relinfo.size(), hipMemcpyHostToDevice));
         D.relinfo = ri;
     }
@@ -1354,6 +1359,10 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
     phase("relinfo");
     patch_reach(S, S, key_n);  // the reaches the changed rows move, where they lie
     phase("reach");
+    } catch (...) {
+        S.broken = true;
+        throw;
+    }
     S.info.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (verbose)
         fprintf(stderr, "[keto advance] %llu touched tuples: %u rows, %u subjects, %zu moved, %zu leaf flips, probe +%zu -%zu keys, "

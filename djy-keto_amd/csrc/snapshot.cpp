@@ -656,6 +656,12 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.op_children = upload_small(s.op_children);
     D.op_items = upload_small(s.op_items);
     D.or_items = upload_small(s.or_items);
+    std::vector<double> rcp(s.ns.size(), 0.0);  // (t_div_slots: exact for n_slots < 2^16)
+    for (size_t i = 0; i < s.ns.size(); i++) {
+        if (s.ns[i].n_slots >= 0xFFFFu) throw Error(KETO_E_LIMIT, "a namespace with 65535 or more relations");
+        if (s.ns[i].n_slots) rcp[i] = 1.0 / (double)s.ns[i].n_slots;
+    }
+    D.ns_rcp = upload_small(rcp);
     D.tab_bytes[0] = bytes16(s.ns);
     D.tab_bytes[1] = bytes16(s.relinfo);
     D.tab_bytes[2] = bytes16(s.nsrel);
@@ -663,6 +669,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     D.tab_bytes[4] = bytes16(s.op_children);
     D.tab_bytes[5] = bytes16(s.op_items);
     D.tab_bytes[6] = bytes16(s.or_items);
+    D.tab_bytes[7] = (uint32_t)((s.ns.size() * sizeof(double) + 15) / 16 * 16);
     D.lds_bytes = 0;
     for (uint32_t b : D.tab_bytes) D.lds_bytes += b;
     D.n_ns = s.n_ns;
@@ -772,6 +779,7 @@ void dev_ptrs(DevSnapshot &D, F &&f) {
     f(reinterpret_cast<const void *&>(D.reach_base));
     f(reinterpret_cast<const void *&>(D.reach_idx));
     f(reinterpret_cast<const void *&>(D.reach_pool));
+    f(reinterpret_cast<const void *&>(D.ns_rcp));
 }
 constexpr size_t STAGE = 64u << 20;  // device <-> file through a pinned buffer of this size
 }  // namespace
@@ -859,7 +867,7 @@ Snapshot *load_snapshot(const char *path, int device) {
     std::vector<size_t> bytes;
     F.get_v(idx);
     F.get_v(bytes);
-    if (idx.size() != 23) throw Error(KETO_E_INVALID, "snapshot file corrupt");
+    if (idx.size() != 24) throw Error(KETO_E_INVALID, "snapshot file corrupt");
     void *stage = nullptr;
     KETO_HIP(hipHostMalloc(&stage, STAGE, 0));
     try {

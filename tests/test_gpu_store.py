@@ -478,6 +478,40 @@ def test_advance_creates_objects():
     st.close()
 
 
+def test_advance_failure_after_first_write_breaks_the_snapshot(tmp_path, monkeypatch):
+    """An in-place advance that fails after its first write (KETO_FAULT_ADVANCE injects a failure
+    right after the first rows are written) leaves the snapshot half-advanced: the library marks it
+    broken and refuses every later Check, Expand, advance, copy patch, save and dispatcher on it,
+    while a fresh cut of the same store serves the new version (patch.hip)"""
+    wl = synth.drive(depth=4, n_groups=500, n_users=1000, seed=4)
+    t = wl.tuples
+    st = km.TupleStore(t)
+    snap = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    q = synth.drive_queries(wl, 2048, seed=2)
+    ins = t[5:6].copy()
+    ins["subj_kind"], ins["s_obj"], ins["s_ns"], ins["s_rel"] = 0, wl.meta["ubase"] + 9, 0, 0
+    ins["shard_id"] = np.random.default_rng(2).integers(0, 256, (1, 16), dtype=np.uint8)
+    st.transact(ins, None)
+    monkeypatch.setenv("KETO_FAULT_ADVANCE", "1")
+    with pytest.raises(Exception, match="injected fault"):
+        snap.advance(st)
+    monkeypatch.delenv("KETO_FAULT_ADVANCE")
+    eng = km.CheckEngine(snap, max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    for call in (lambda: eng.check_batch(q), lambda: snap.advance(st), lambda: snap.save(str(tmp_path / "b.snap")),
+                 lambda: km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st, base=snap)):
+        with pytest.raises(Exception, match="unusable"):
+            call()
+    fresh = km.Snapshot(wl.namespaces, None, wl.ns_names, wl.rel_names, wl.n_uuids, store=st)
+    full = km.Snapshot(wl.namespaces, transact(t, ins, ins[:0]), wl.ns_names, wl.rel_names, wl.n_uuids)
+    a = km.CheckEngine(fresh, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    b = km.CheckEngine(full, max_read_depth=wl.max_depth, max_read_width=wl.max_width).check_batch(q)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    for s in (snap, fresh, full):
+        s.close()
+    st.close()
+
+
 def test_advance_declines_and_leaves_the_snapshot(tmp_path):
     """what the advance cannot do it declines before writing anything: an insert whose shard_id's
     high half ties a tuple of its row (only the full build orders it), a snapshot that is not this

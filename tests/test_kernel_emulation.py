@@ -97,4 +97,4 @@ def test_patched_snapshots_exact_under_emulation(tmp_path):
                         os.path.join(ROOT, "tests", "test_gpu_store.py"), "-k", "patch or advance or index"],
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "11 passed" in r.stdout
+    assert "12 passed" in r.stdout

@@ -8,6 +8,10 @@
 #                                             WRITE_SIZE in separate --pmc passes (tools/parse_pmc.py)
 #   tools/gpu_round.sh OUT ab name...         bench.py with the in-tree library and tools/ab/libketo_<name>.so
 #                                             (tools/ab_build.sh), probes off
+#   tools/gpu_round.sh OUT gentime v...       bench.py per variant (base | rootk | nostash | an ab library name) with
+#                                             KETO_FR_GENTIME: the line and the median time of each generation
+#   tools/gpu_round.sh OUT sq [wl]            SQ / TCC counters per kernel of the check path (two --pmc passes,
+#                                             tools/pmc_split.py): issue vs wait, instructions per batch
 #   tools/gpu_round.sh OUT patch              the store probe alone, the patcher's phase times (KETO_PATCH_VERBOSE)
 #   tools/gpu_round.sh OUT c5 [scale]         tests/test_gpu_c5.py (8 gloo ranks sharing the GPU) and the C5
 #                                             bench rehearsal at that scale (default 40 / 10)
@@ -43,6 +47,22 @@ ab)
       > $OUT/ab_$name.log 2>&1 || { echo "$name failed"; tail -5 $OUT/ab_$name.log; exit 1; }
     line $OUT/ab_$name.log $name
   done ;;
+gentime)
+  for name in "$@"; do
+    lib=$PWD/djy-keto_amd/keto_mi355x/libketo_mi355x.so; env=""
+    case $name in base) ;; rootk) env="KETO_FR_ROOT_KERNEL=1" ;; nostash) env="KETO_FR_NOSTASH=1" ;;
+      *) lib=$PWD/tools/ab/libketo_$name.so ;; esac
+    env $env KETO_FR_GENTIME=1 KETO_MI355X_ALLOW_OVERRIDE=tools KETO_MI355X_LIB_OVERRIDE=$lib timeout -k 10 300 \
+      python3 -u bench.py --steps 10 --warmup 3 $QUIET > $OUT/gt_$name.log 2>&1 || { echo "$name failed"; tail -5 $OUT/gt_$name.log; exit 1; }
+    line $OUT/gt_$name.log $name; python3 tools/gentime.py $OUT/gt_$name.log
+  done ;;
+sq)
+  WL=${1:-c4}; A="--workload $WL --steps 3 --warmup 0 $QUIET"
+  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+    -d $OUT/sq1 -o pmc --output-format csv -- python3 bench.py $A > $OUT/sq1.log 2>&1 || exit 1
+  timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY TCC_HIT_sum TCC_MISS_sum \
+    -d $OUT/sq2 -o pmc --output-format csv -- python3 bench.py $A > $OUT/sq2.log 2>&1 || exit 1
+  python3 tools/pmc_split.py $OUT/sq_$WL.json $OUT/sq1 $OUT/sq2 | cut -c1-400 | head -12 ;;
 patch)
   KETO_PATCH_VERBOSE=1 timeout -k 10 400 python3 -u tools/patch_probe.py 10 > $OUT/patch.log 2>&1 || { tail -5 $OUT/patch.log; exit 1; }
   grep -E "keto (patch|advance)|advance_ms" $OUT/patch.log | cut -c1-900 | head -60 ;;
