@@ -216,19 +216,23 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     const void *kx = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true, false>) : reinterpret_cast<const void *>(&fr_expand<false, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kx, XBLOCK, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
     const dim3 eg(cus * (uint32_t)std::min(per_cu, (int)(2048 / XBLOCK))), xb(XBLOCK), eb(BLOCK);
-    // generation 0 holds the query roots only (IA or RW goals): an instantiation of its own (KM_ROOT)
+    // generation 0 (the query roots) runs an instantiation of its own: KETO_FR_WAVES0 waves per SIMD
+    // (KETO_FR_ROOT_KERNEL, A/B: also compiled for IA and RW goals only, KM_ROOT)
+    static const bool root0 = getenv("KETO_FR_ROOT_KERNEL") != nullptr;
     int per_cu0 = 0;
-    const void *kx0 = lds_tables ? reinterpret_cast<const void *>(&fr_expand<true, false, KM_ROOT>)
-                                 : reinterpret_cast<const void *>(&fr_expand<false, false, KM_ROOT>);
+    const void *kx0 = root0 ? (lds_tables ? reinterpret_cast<const void *>(&fr_expand<true, false, KM_ROOT, KETO_FR_WAVES0>)
+                                          : reinterpret_cast<const void *>(&fr_expand<false, false, KM_ROOT, KETO_FR_WAVES0>))
+                            : (lds_tables ? reinterpret_cast<const void *>(&fr_expand<true, false, KM_ALL, KETO_FR_WAVES0>)
+                                          : reinterpret_cast<const void *>(&fr_expand<false, false, KM_ALL, KETO_FR_WAVES0>));
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu0, kx0, XBLOCK, lds) != hipSuccess || per_cu0 <= 0) per_cu0 = per_cu;
     const dim3 eg0(cus * (uint32_t)std::min(per_cu0, (int)(2048 / XBLOCK)));
     auto launch_gen = [&](uint32_t k) {
-        // (A/B: generation 0 on the KM_ROOT instantiation -- round 6, C4: 718 us against the generic
-        // kernel's 618 us with the phase-A stash, so the generic one runs it by default)
-        static const bool root0 = getenv("KETO_FR_ROOT_KERNEL") != nullptr;
-        if (k == 0 && root0) {
-            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false, KM_ROOT>), eg0, xb, lds, st.stream, P);
-            else hipLaunchKernelGGL((fr_expand<false, false, KM_ROOT>), eg0, xb, 0, st.stream, P);
+        if (k == 0 && root0) {  // (round 6, C4 at 7 waves: 718 us against the generic kernel's 618 us)
+            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false, KM_ROOT, KETO_FR_WAVES0>), eg0, xb, lds, st.stream, P);
+            else hipLaunchKernelGGL((fr_expand<false, false, KM_ROOT, KETO_FR_WAVES0>), eg0, xb, 0, st.stream, P);
+        } else if (k == 0) {
+            if (lds_tables) hipLaunchKernelGGL((fr_expand<true, false, KM_ALL, KETO_FR_WAVES0>), eg0, xb, lds, st.stream, P);
+            else hipLaunchKernelGGL((fr_expand<false, false, KM_ALL, KETO_FR_WAVES0>), eg0, xb, 0, st.stream, P);
         } else if (lds_tables) {
             hipLaunchKernelGGL((fr_expand<true, false>), eg, xb, lds, st.stream, P);
         } else {

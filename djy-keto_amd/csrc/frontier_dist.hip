@@ -17,8 +17,11 @@
 //
 // A generation on every rank (frontier_goal.inc / frontier_kernels.inc, DIST instantiations):
 //   * a child on a ghost node is the IA goal checkIsAllowed(child, depth, skip) of its owner --
-//     it leaves as a 32-byte record {global (ns, obj, rel), query subject, word, scope, query
-//     home} and a G_PROXY goal keeps its place among its parent's children;
+//     it leaves as a 20-byte wire record {global obj, ns | rel << 16, word, scope, query home}
+//     (WIRE_BYTES below: the outbox's 32-byte form without the query subject, which every rank
+//     looks up by the record's home in the chunk's subject table, and without the sender's proxy
+//     index, which the sender keeps in send order) and a G_PROXY goal keeps its place among its
+//     parent's children;
 //   * an expand-subject's found-lookahead on a ghost child (traverser.go:73-80: the EXISTS on the
 //     child's own row) is run by the owner before anything else (GF_FOUND; past the width cut
 //     GF_PROBE: the lookahead only);
@@ -26,7 +29,9 @@
 //     generation at a position of its own (its start records resolved against that rank's rows,
 //     resolve_query.inc).
 // Bottom-up, after each generation's fr_reduce on every rank, the values of the goals that came
-// from other ranks go back (8 bytes each, in receive order) into their proxies, before the
+// from other ranks go back (4 bytes each by default -- membership, found bit, error code and
+// relation name beside the subtree's saturated goal count; 8 with KETO_DIST_WIDE_VALUES=1 --
+// in receive order) into their proxies, before the
 // generation above is reduced; a query's root runs at its object's owner and its value goes back
 // to its home, which decides.  So each goal's value is the one the single-snapshot engine
 // computes over the whole graph: first decisive in add order (H0), AND / NOT, the depth ledger

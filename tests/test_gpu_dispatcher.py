@@ -80,7 +80,10 @@ def test_concurrent_callers_match_oracle():
 def test_snapshot_swap_under_load():
     """set_snapshot while 16 clients keep the dispatcher busy: the swap returns (no
     starvation), every answer is the oracle's on the old or the new tuples, and every
-    request issued after the swap returned gets the new snapshot's (oracle) answer."""
+    request issued after the swap returned gets the new snapshot's (oracle) answer.
+    Starvation-freedom is counted in batches, not seconds, so a loaded box does not decide
+    the verdict: while set_snapshot waits, the dispatcher completes at most a few rounds of
+    its inflight slots (the old snapshot's batches drain, new ones run beside them)."""
     wl = synth.drive(depth=5, n_groups=2000, n_users=5000, seed=9)
     q = synth.drive_queries(wl, 8192, seed=1)
     keep = np.random.default_rng(2).random(len(wl.tuples)) < 0.6  # the new snapshot: 60% of the tuples
@@ -111,8 +114,10 @@ def test_snapshot_swap_under_load():
         x.start()
     time.sleep(0.5)
     t0 = time.monotonic()
+    b0 = d.stats()["batches"]
     d.set_snapshot(new)
     swapped_at[0] = time.monotonic()
+    swap_batches = d.stats()["batches"] - b0
     swap_s = swapped_at[0] - t0
     old.close()  # no longer in use once set_snapshot returned
     time.sleep(0.5)
@@ -121,7 +126,8 @@ def test_snapshot_swap_under_load():
         x.join()
     d.close()
     assert not errors
-    assert swap_s < 5.0
+    assert swap_batches <= 16 * 4, f"the swap waited through {swap_batches} batches ({swap_s:.2f} s)"
+    assert swap_s < 120.0  # (a hang guard only)
     after = 0
     for ts, i, a in log:
         want_new, want_old = a_new[i:i + 64], a_old[i:i + 64]
