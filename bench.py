@@ -556,7 +556,7 @@ def run_c5(args, rank, world, device, dist_on):
         for k in phases:
             phases[k] += eng.last[k]
     dist_last = dict(eng.last)
-    dist_levels = eng.level_stats()
+    dist_levels = eng.generation_stats()
     seq_ms = (time.perf_counter() - t_seq) / n_seq * 1e3
     # the timed region: K fresh seeded batches through one keto_partition_check_many call, in
     # pinned host memory as the C4 line's (keto_host_alloc: straight DMA for the one-rank path)

@@ -509,7 +509,7 @@ int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tup
     *out = nullptr;
     return guarded([&] {
         *out = reinterpret_cast<keto_partition *>(
-            keto::partition_create(cfg, tuples, n, (flags & KETO_F_DEVICE_PTRS) != 0, coll, limits));
+            keto::partition_create(cfg, tuples, n, (flags & KETO_F_DEVICE_PTRS) != 0, coll, limits, (flags & KETO_F_PART_DIST) != 0));
     });
 }
 
@@ -552,6 +552,11 @@ int keto_partition_stats_get(keto_partition *p, keto_partition_stats *out) {
     if (!p || !out) return fail(KETO_E_INVALID, "null argument");
     keto::partition_stats(reinterpret_cast<keto::PartitionHandle *>(p), out);
     return KETO_OK;
+}
+
+int keto_partition_generations_get(keto_partition *p, keto_partition_generation *out, uint32_t cap, uint32_t *n) {
+    if (!p || !n || (cap && !out)) return fail(KETO_E_INVALID, "null argument");
+    return guarded([&] { keto::partition_generations(reinterpret_cast<keto::PartitionHandle *>(p), out, cap, n); });
 }
 
 int keto_partition_levels_get(keto_partition *p, keto_partition_level *out, uint32_t cap, uint32_t *n) {

@@ -427,7 +427,8 @@ void sum_u32(const uint32_t *v, uint64_t n, unsigned long long *out, hipStream_t
 // partition.hip: graphs partitioned by object over the ranks of a job (keto_partition_*)
 struct PartitionHandle;
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
-                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits);
+                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits,
+                                  bool force_dist = false);
 void partition_check(PartitionHandle *p, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags);
 void partition_check_many(PartitionHandle *p, uint32_t nb, const keto_query *const *q, const uint64_t *n,
                           uint8_t *const *allowed, int32_t *const *err, uint32_t flags);
@@ -435,6 +436,7 @@ uint64_t partition_expand(PartitionHandle *p, const keto_subject_set *roots, uin
 void partition_expand_result(PartitionHandle *p, keto_tree_node *nodes, uint64_t cap, uint64_t *offsets, int32_t *err);
 void partition_stats(PartitionHandle *p, keto_partition_stats *out);
 void partition_levels(PartitionHandle *p, keto_partition_level *out, uint32_t cap, uint32_t *n);
+void partition_generations(PartitionHandle *p, keto_partition_generation *out, uint32_t cap, uint32_t *n);
 void partition_free(PartitionHandle *p);
 
 }  // namespace keto

@@ -666,6 +666,7 @@ struct Partition {
     uint64_t table_mask = 0, n_seen = 0;
     keto_partition_stats last{};
     std::vector<keto_partition_level> cur_levels, last_levels;  // the closure running / the last batch's
+    std::vector<keto_partition_generation> last_gens;           // the last distributed-frontier batch's generations
     // Expand results between keto_partition_expand and keto_partition_expand_result
     std::vector<keto_tree_node> xnodes;
     std::vector<uint64_t> xoffs;
@@ -1060,7 +1061,7 @@ double secs(std::chrono::steady_clock::time_point a) {
 struct PartitionHandle : Partition {};
 
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
-                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits) {
+                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits, bool force_dist) {
     if (!cfg) throw Error(KETO_E_INVALID, "null config");
     if (n && !tuples) throw Error(KETO_E_INVALID, "null tuples");
     if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "a partition holds at most 2^31 - 1 tuples");
@@ -1072,7 +1073,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     if (coll) {
         if (coll->world < 1 || (uint32_t)coll->world > MAX_WORLD || coll->rank < 0 || coll->rank >= coll->world)
             throw Error(KETO_E_INVALID, "collective rank / world out of range");
-        if (coll->world > 1 && (!coll->alltoall_u64 || !coll->alltoallv || !coll->allreduce_max_u64))
+        if ((coll->world > 1 || force_dist) && (!coll->alltoall_u64 || !coll->alltoallv || !coll->allreduce_max_u64))
             throw Error(KETO_E_INVALID, "collective callbacks missing");
         P->have_coll = true;
         P->coll = *coll;
@@ -1099,8 +1100,9 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     P->trim = getenv("KETO_PART_TRIM") != nullptr;
     if (keto_stream_create(P->device, &P->kstream) != KETO_OK) throw Error(KETO_E_DEVICE, "stream creation failed");
     P->n = n;
-    if (P->world > 1 && !getenv("KETO_PART_CLOSURE")) {
-        // several ranks: the partition resident, the distributed frontier over it
+    if (force_dist && !P->have_coll) throw Error(KETO_E_INVALID, "KETO_F_PART_DIST needs a collective");
+    if ((P->world > 1 || force_dist) && !getenv("KETO_PART_CLOSURE")) {
+        // several ranks (or KETO_F_PART_DIST): the partition resident, the distributed frontier over it
         auto t0 = std::chrono::steady_clock::now();
         P->dist = dist_create(&P->cfg, tuples, n, device_ptrs, P->coll, P->limits);
         if (P->verbose)
@@ -1404,7 +1406,9 @@ void dist_check_many(Partition &P, uint32_t nb, const keto_query *const *q, cons
             routed.resize(n[k]);
             for (uint64_t i = 0; i < n[k]; i++) routed[i] = (uint32_t)i;
             P.last_levels.clear();
+            P.last_gens.clear();
         } else {
+            P.last_levels.clear();  // (the closure of the queries it routes, if any: below)
             DistStats ds{};
             dist_check(*P.dist, q[k], n[k], allowed[k], err[k], (flags & KETO_F_ERR_DETAIL) != 0, routed, ds);
             P.dstats = ds;
@@ -1414,7 +1418,9 @@ void dist_check_many(Partition &P, uint32_t nb, const keto_query *const *q, cons
             st.exchange_bytes = ds.bytes_exchanged;
             st.device_s = ds.device_s;
             st.exchange_s = ds.exchange_s;
-            P.last_levels = dist_levels(*P.dist);
+            P.last_gens.clear();
+            for (const keto_partition_level &l : dist_levels(*P.dist))  // (the engine's per-generation record)
+                P.last_gens.push_back(keto_partition_generation{l.objects, l.request_bytes, l.tuples, l.tuple_bytes_sent, l.ms});
         }
         const uint64_t nr = routed.size();
         if (allreduce_max(P, nr) > 0) {
@@ -1439,7 +1445,7 @@ void dist_check_many(Partition &P, uint32_t nb, const keto_query *const *q, cons
             st.edges = S.st.edges;
             st.probes = S.st.probes;
             st.queries = S.st.queries;
-            if (count) P.last_levels = S.levels;
+            P.last_levels = S.levels;
         }
         st.run_s = secs(t0);
         P.last = st;
@@ -1591,6 +1597,11 @@ void partition_levels(PartitionHandle *PH, keto_partition_level *out, uint32_t c
     const auto &L = PH->last_levels;
     *n = (uint32_t)L.size();
     for (uint32_t i = 0; i < cap && i < L.size(); i++) out[i] = L[i];
+}
+void partition_generations(PartitionHandle *PH, keto_partition_generation *out, uint32_t cap, uint32_t *n) {
+    const auto &G = PH->last_gens;
+    *n = (uint32_t)G.size();
+    for (uint32_t i = 0; i < cap && i < G.size(); i++) out[i] = G[i];
 }
 void partition_free(PartitionHandle *PH) { delete PH; }
 

@@ -18,7 +18,7 @@ if os.environ.get("KETO_MI355X_ALLOW_OVERRIDE") == "tools" and os.environ.get("K
 
 KETO_OK = 0
 KETO_E_INVALID, KETO_E_DEVICE, KETO_E_CAPACITY, KETO_E_LIMIT = -1, -2, -3, -4
-F_DEVICE_PTRS, F_ASYNC, F_COUNT_WORK, F_ERR_DETAIL = 0x1, 0x2, 0x4, 0x8
+F_DEVICE_PTRS, F_ASYNC, F_COUNT_WORK, F_ERR_DETAIL, F_PART_DIST = 0x1, 0x2, 0x4, 0x8, 0x10
 QERR_NONE, QERR_NO_RELATION, QERR_INTERNAL, QERR_NOT_IMPLEMENTED = 0, 1, 2, 3
 
 TUPLE_DT = np.dtype([("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"), ("subj_kind", "<u4"), ("s_obj", "<u4"),
@@ -94,8 +94,13 @@ class PartitionLevel(ctypes.Structure):
                 ("tuple_bytes_sent", ctypes.c_uint64), ("ms", ctypes.c_double)]
 
 
+class PartitionGeneration(ctypes.Structure):
+    _fields_ = [("goals", ctypes.c_uint64), ("record_bytes_out", ctypes.c_uint64), ("records_in", ctypes.c_uint64),
+                ("value_bytes_back", ctypes.c_uint64), ("ms", ctypes.c_double)]
+
+
 # keto_collective callbacks
-ABI_VERSION = 6  # include/keto_mi355x.h KETO_ABI_VERSION
+ABI_VERSION = 7  # include/keto_mi355x.h KETO_ABI_VERSION
 
 ALLTOALL_U64_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                    ctypes.POINTER(ctypes.c_uint64))
@@ -163,6 +168,7 @@ SIGNATURES = {
     "keto_partition_expand_result": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP]),
     "keto_partition_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(PartitionStats)]),
     "keto_partition_levels_get": (ctypes.c_int, [_VP, ctypes.POINTER(PartitionLevel), _U32, ctypes.POINTER(_U32)]),
+    "keto_partition_generations_get": (ctypes.c_int, [_VP, ctypes.POINTER(PartitionGeneration), _U32, ctypes.POINTER(_U32)]),
     "keto_partition_free": (ctypes.c_int, [_VP]),
     "keto_trees_to_json": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),
     "keto_trees_to_proto": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(NameTables), _VP, _U64, _VP]),

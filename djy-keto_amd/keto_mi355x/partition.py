@@ -102,7 +102,7 @@ class PartitionedEngine:
 
     def __init__(self, namespaces, ns_names, rel_names, n_uuids: int, part_tuples=None, *, strict: bool = False,
                  device: int = 0, max_read_depth: int = 5, max_read_width: int = 100, collective=None,
-                 device_tuples: tuple | None = None):
+                 device_tuples: tuple | None = None, distributed: bool = False):
         import json
         if isinstance(namespaces, dict):
             namespaces = json.dumps(namespaces)
@@ -114,17 +114,20 @@ class PartitionedEngine:
         self.max_read_depth, self.max_read_width = max_read_depth, max_read_width
         lim = _abi.Limits(max_read_depth, max_read_width)
         self._coll = None
-        if collective is not None and int(collective.world) > 1:
+        # distributed=True (KETO_F_PART_DIST): the distributed frontier even at world 1, every
+        # exchange going to this rank through the collective
+        if collective is not None and (int(collective.world) > 1 or distributed):
             self._coll = _c_collective(collective)
+        flags = _abi.F_PART_DIST if distributed else 0
         h = ctypes.c_void_p()
         if device_tuples is not None:
             ptr, count = device_tuples
-            check(lib().keto_partition_create(ctypes.byref(cfg), ptr, count, _abi.F_DEVICE_PTRS,
+            check(lib().keto_partition_create(ctypes.byref(cfg), ptr, count, _abi.F_DEVICE_PTRS | flags,
                                               ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
                                               ctypes.byref(h)))
         else:
             t = np.ascontiguousarray(part_tuples, dtype=_abi.TUPLE_DT)
-            check(lib().keto_partition_create(ctypes.byref(cfg), t.ctypes.data if len(t) else None, len(t), 0,
+            check(lib().keto_partition_create(ctypes.byref(cfg), t.ctypes.data if len(t) else None, len(t), flags,
                                               ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
                                               ctypes.byref(h)))
         self.handle = h
@@ -146,6 +149,15 @@ class PartitionedEngine:
         arr = (_abi.PartitionLevel * max(1, n.value))()
         check(lib().keto_partition_levels_get(self.handle, arr, n.value, ctypes.byref(n)))
         return [{k: getattr(arr[i], k) for k, _ in _abi.PartitionLevel._fields_} for i in range(n.value)]
+
+    def generation_stats(self) -> list:
+        """the last distributed-frontier batch generation by generation (keto_partition_generations_get):
+        goals, record_bytes_out, records_in, value_bytes_back, ms"""
+        n = ctypes.c_uint32()
+        check(lib().keto_partition_generations_get(self.handle, None, 0, ctypes.byref(n)))
+        arr = (_abi.PartitionGeneration * max(1, n.value))()
+        check(lib().keto_partition_generations_get(self.handle, arr, n.value, ctypes.byref(n)))
+        return [{k: getattr(arr[i], k) for k, _ in _abi.PartitionGeneration._fields_} for i in range(n.value)]
 
     def check_batch(self, queries: np.ndarray, count_work: bool = False):
         """queries: QUERY_DT (this rank's) -> (allowed u8[n], err i32[n])"""

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define KETO_ABI_VERSION 6
+#define KETO_ABI_VERSION 7
 
 /* status codes */
 #define KETO_OK 0
@@ -152,6 +152,11 @@ typedef struct keto_stream keto_stream;
  * `relation %q does not exist` (internal/namespace/definitions.go:61).  Without the flag
  * out_err[i] is the bare code. */
 #define KETO_F_ERR_DETAIL 0x8u
+/* keto_partition_create (ABI 7): run the distributed frontier even for a job of one rank -- every
+ * goal record, subject table and decision goes to the rank itself through the collective's
+ * exchanges (alltoallv_device included) instead of the resident-snapshot shortcut.  For a host
+ * that wants to check its collective (an RCCL communicator) on one GPU before it scales out. */
+#define KETO_F_PART_DIST 0x10u
 
 int keto_abi_version(void);
 /* copies the thread's last error message; returns its full length */
@@ -399,7 +404,9 @@ typedef struct keto_partition_stats {
 } keto_partition_stats;
 typedef struct keto_partition keto_partition;
 /* tuples: this rank's partition (host, or device memory of cfg->device with
- * KETO_F_DEVICE_PTRS); coll NULL = one rank, no exchange.  The collective is kept by value. */
+ * KETO_F_DEVICE_PTRS); coll NULL = one rank, no exchange (KETO_F_PART_DIST with a one-rank
+ * collective: the distributed frontier over the exchanges regardless).  The collective is kept
+ * by value. */
 int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
                           const keto_collective *coll, const keto_limits *limits, keto_partition **out);
 /* collective: this rank's queries (host) -> decisions, as keto_check_batch (flags: COUNT_WORK,
@@ -434,6 +441,17 @@ typedef struct keto_partition_level {
                                   [device time of the generation's kernels, both passes: no collective wait] */
 } keto_partition_level;
 int keto_partition_levels_get(keto_partition *p, keto_partition_level *out, uint32_t cap, uint32_t *n);
+/* ABI 7: the last distributed-frontier batch generation by generation, under its own names (a
+ * job on the closure path or over one resident snapshot has none): *n = the generations run; the
+ * first min(cap, *n) are copied to out.  A batch run in chunks sums its chunks per generation. */
+typedef struct keto_partition_generation {
+    uint64_t goals;            /* the generation's goals on this rank (proxies of remote children included) */
+    uint64_t record_bytes_out; /* goal records this rank sent to the other ranks, wire bytes */
+    uint64_t records_in;       /* goal records it received: goals of the next generation here */
+    uint64_t value_bytes_back; /* values of received goals it returned to their senders, bytes */
+    double ms;                 /* device time of the generation's kernels, both passes (no collective wait) */
+} keto_partition_generation;
+int keto_partition_generations_get(keto_partition *p, keto_partition_generation *out, uint32_t cap, uint32_t *n);
 int keto_partition_free(keto_partition *p);
 
 /* pinned host memory (hipHostMalloc) for the query / output buffers of KETO_F_ASYNC batches */

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     lib = km.lib()
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.keto_abi_version() == 6
+    assert lib.keto_abi_version() == 7
 
 
 def test_record_layouts_match_header():

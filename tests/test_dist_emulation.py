@@ -93,11 +93,13 @@ def _worker(rank, world, port, lib, case, seeds, out):
                 roots["ns"][12:], roots["rel"][12:] = wl.ns_names.index("Folder"), wl.rel_names.index("viewers")
                 roots["obj"][12:] = rng.integers(0, wl.meta["folders_per_root"], 12)
             own = partition.object_owner(tup["ns"], tup["obj"], world) == rank
+            # (world 1: KETO_F_PART_DIST, the distributed frontier with every exchange to this rank)
             eng = partition.PartitionedEngine(ns_cfg, ns_names, rel_names, n_uuids, tup[own], strict=strict,
-                                              max_read_depth=depth, max_read_width=width, collective=coll)
+                                              max_read_depth=depth, max_read_width=width, collective=coll,
+                                              distributed=world == 1)
             allowed, err = eng.check_batch(q)  # every rank checks the whole batch: each root at its owner
             st = dict(eng.last)
-            lv = eng.level_stats()
+            lv = eng.generation_stats()
             dec, oerr, _ = orc.check_batch(oq, threads=1)
             ok = err != -1
             # Expand: rows fetched from their owners, walked here (csrc/expand_dist.hip): exact trees
@@ -131,7 +133,7 @@ def _run(lib, world, case, seeds):
         return dict(out)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_random_worlds_match_oracle(emu_lib, world):
     res = _run(emu_lib, world, "random", list(range(300, 330)))
     total = routed = 0

@@ -21,7 +21,7 @@ trees") against oracle trees, child order included (internal/expand/engine.go:54
 
 Every rank's phase record (generations, goals, queries routed to the closure path, bytes of goal
 records and values it sent, device time of its kernels, time inside the collective) and its
-exchange generation by generation (keto_partition_levels_get) go to gpurun_out/c5x40_phases.json
+exchange generation by generation (keto_partition_generations_get) go to gpurun_out/c5x40_phases.json
 (profiles/ keeps a copy per round).
 """
 import json
@@ -144,7 +144,7 @@ def _worker(rank, world, port, out):
         t0 = time.perf_counter()
         a2, e2 = eng.check_batch(q)
         wall2 = time.perf_counter() - t0
-        st2, lv2 = dict(eng.last), eng.level_stats()
+        st2, lv2 = dict(eng.last), eng.generation_stats()
         idx = _sample(70 + rank)
         qs = q[idx]
         rows = lambda k: synth.drive_object_tuples(wl, k)  # noqa: E731 -- the generator's rows, not the device's
@@ -214,8 +214,9 @@ def test_c5_x40_eight_ranks_matches_oracle():
                            "per rank the second (warm) 2^20-query check batch through the distributed frontier "
                            "(keto_partition_stats_get: generations, goals, routed, bytes of goal records + values sent to "
                            "other ranks, device time of the generations' kernels, time inside the collective; "
-                           "keto_partition_levels_get: per generation goals, record bytes out, records in, value bytes "
-                           "back, device ms) and one 512-root Expand batch (rows fetched per level, walked on the device)",
+                           "keto_partition_generations_get: per generation goals, record_bytes_out, records_in, "
+                           "value_bytes_back, device ms) and one 512-root Expand batch (keto_partition_levels_get: rows "
+                           "fetched per level, walked on the device)",
                    "ranks": {str(k): v["phases"] for k, v in sorted(res.items())}}, f, indent=1)
     total = res[0]["total"]
     if SCALE == 40:

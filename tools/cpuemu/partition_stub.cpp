@@ -16,6 +16,7 @@ struct PartitionHandle {
     DistEngine *dist = nullptr;
     keto_partition_stats last{};
     std::vector<keto_partition_level> levels;
+    std::vector<keto_partition_generation> gens;
     std::vector<keto_tree_node> xnodes;
     std::vector<uint64_t> xoffs;
     std::vector<int32_t> xerr;
@@ -25,8 +26,8 @@ struct PartitionHandle {
 };
 [[noreturn]] static void unavailable() { throw Error(KETO_E_DEVICE, "the closure path of keto_partition_* is not part of the CPU emulation"); }
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_ptrs,
-                                  const keto_collective *coll, const keto_limits *limits) {
-    if (!coll || coll->world < 2) unavailable();
+                                  const keto_collective *coll, const keto_limits *limits, bool force_dist) {
+    if (!coll || (coll->world < 2 && !force_dist)) unavailable();
     auto P = std::make_unique<PartitionHandle>();
     keto_limits lim = limits ? *limits : keto_limits{5, 100};
     P->dist = dist_create(cfg, tuples, n, device_ptrs, *coll, lim);
@@ -49,7 +50,10 @@ void partition_check_many(PartitionHandle *P, uint32_t nb, const keto_query *con
         P->last.device_s = ds.device_s;
         P->last.exchange_s = ds.exchange_s;
         P->last.run_s = ds.wall_s;
-        P->levels = dist_levels(*P->dist);
+        P->levels.clear();
+        P->gens.clear();
+        for (const keto_partition_level &l : dist_levels(*P->dist))
+            P->gens.push_back(keto_partition_generation{l.objects, l.request_bytes, l.tuples, l.tuple_bytes_sent, l.ms});
     }
 }
 void partition_check(PartitionHandle *P, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags) {
@@ -78,6 +82,10 @@ void partition_stats(PartitionHandle *P, keto_partition_stats *out) { *out = P->
 void partition_levels(PartitionHandle *P, keto_partition_level *out, uint32_t cap, uint32_t *n) {
     *n = (uint32_t)P->levels.size();
     for (uint32_t i = 0; i < cap && i < P->levels.size(); i++) out[i] = P->levels[i];
+}
+void partition_generations(PartitionHandle *P, keto_partition_generation *out, uint32_t cap, uint32_t *n) {
+    *n = (uint32_t)P->gens.size();
+    for (uint32_t i = 0; i < cap && i < P->gens.size(); i++) out[i] = P->gens[i];
 }
 void partition_free(PartitionHandle *P) { delete P; }
 }  // namespace keto
