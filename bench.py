@@ -769,6 +769,8 @@ def main(argv=None):
     ap.add_argument("--engine-streams", type=int, default=int(os.environ.get("KETO_BENCH_STREAMS", "1")),
                     help="value pipeline: batches alternate over this many engine streams")
     ap.add_argument("--latency-batch", type=int, default=1 << 16)
+    ap.add_argument("--query-record", type=int, choices=[16, 32], default=16,
+                    help="value pipeline: request record bytes over PCIe (16: keto_check_batch16)")
     ap.add_argument("--latency-iters", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -898,11 +900,23 @@ def main(argv=None):
         qgen = lambda k: synth.nested_groups_queries(wl, args.batch, seed=shard_seed(7, rank) + 1000 * (k + 1))  # noqa: E731
     else:
         qgen = lambda k: synth.drive_queries(wl, args.batch, seed=shard_seed(11, rank) + 1000 * (k + 1))  # noqa: E731
-    qb = [km.PinnedArray(args.batch, km.QUERY_DT) for _ in range(nb)]
+    # the requests cross PCIe as 16-byte records (keto_check_batch16, ABI 7) when every one fits
+    # that form, else as 32-byte keto_query records; qh keeps the 32-byte form for the parity reruns
+    qh = [qgen(k) for k in range(nb)]
+    rec16 = args.query_record == 16
+    if rec16:
+        try:
+            km.pack_queries16(qh[0][:1])
+        except km.KetoError:
+            rec16 = False
+    qb = [km.PinnedArray(args.batch, km.QUERY16_DT if rec16 else km.QUERY_DT) for _ in range(nb)]
     ab = [km.PinnedArray(args.batch, np.uint8) for _ in range(nb)]
     eb = [km.PinnedArray(args.batch, np.int32) for _ in range(nb)]
     for k in range(nb):
-        qb[k].array[:] = qgen(k)
+        if rec16:
+            km.pack_queries16(qh[k], out=qb[k].array)
+        else:
+            qb[k].array[:] = qh[k]
     # engine streams: consecutive batches alternate between them, so one batch's sparse late
     # generations (a few blocks each) share the GPU with the next batch's dense early ones
     n_es = max(1, args.engine_streams)
@@ -936,14 +950,14 @@ def main(argv=None):
     pipe_err = np.concatenate([eb[k].array for k in range(nb)])
     assert (pipe_err == 0).all(), "unexpected query errors"
     # the pipeline's first batch again, synchronously on the device-resident path: same decisions
-    dq.upload(stream, qb[0].array)
+    dq.upload(stream, qh[0])
     eng.check_batch_device(dq, len(q), da, de, sync=True)
     pipe_vs_resident = int((da.download(stream, np.zeros(len(q), np.uint8)) != pipe_allowed[0]).sum())
     # every distinct timed batch against the DFS interpreter (a counted rerun of the same queries:
     # the reference recursion in its canonical order, pinned to the oracle by the GPU suite)
     pipe_vs_dfs = 0
     for k in range(nb):
-        dq.upload(stream, qb[k].array)
+        dq.upload(stream, qh[k])
         eng.check_batch_device(dq, len(q), da, de, sync=True, count_work=True)
         pipe_vs_dfs += int((da.download(stream, np.zeros(len(q), np.uint8)) != pipe_allowed[k]).sum())
     stream.counters(reset=True)
@@ -1022,6 +1036,7 @@ def main(argv=None):
                              "streams through two staging slots, overlapping the neighbouring batches' kernels; timed "
                              "from the first enqueue until the stream drained",
                      "distinct_batches": nb, "streams": f"{n_es} engine stream(s), each 1 compute + 2 copy",
+                     "query_record_bytes": 16 if rec16 else 32,
                      "kernel_ms_per_batch": [ks / max(1, kn) for ks, kn in pipe_kernel],
                      "first_batch_vs_device_resident_mismatches": pipe_vs_resident,
                      "mismatches": pipe_vs_dfs,
@@ -1060,7 +1075,7 @@ def main(argv=None):
                            "routed_fraction": fr["routed"] / max(1, fr["queries"]), "budget": 1024}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sched, cb, dec = cpu_baseline(wl, q, wl.max_depth, wl.max_width, args.cpu_budget, gpu_allowed=allowed,
-                                      pipe=[(qb[k].array, pipe_allowed[k]) for k in range(nb)])
+                                      pipe=[(qh[k], pipe_allowed[k]) for k in range(nb)])
         out["cpu_baseline"] = cb
         if cpu_baseline.pipe is not None:
             out["pipeline"]["oracle_mismatches"] = cpu_baseline.pipe["mismatches"]

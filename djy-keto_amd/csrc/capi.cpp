@@ -299,8 +299,9 @@ int keto_stream_last_kernel_ms(keto_stream *hs, double *ms) {
     return KETO_OK;
 }
 
-int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *queries, uint64_t n,
-                     const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags) {
+// keto_check_batch / keto_check_batch16: queries are `rec` bytes each (keto_query, keto_query16)
+static int check_batch(keto_snapshot *hsnap, keto_stream *hs, const void *queries, size_t rec, uint64_t n,
+                       const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags) {
     keto::Snapshot *snap = SN(hsnap);
     keto::Stream *s = ST(hs);
     if (!snap || !s) return fail(KETO_E_INVALID, "null snapshot or stream");
@@ -320,6 +321,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         L.err_detail = (flags & KETO_F_ERR_DETAIL) != 0;
         L.budget = s->fr_budget;
         L.async = (flags & KETO_F_ASYNC) != 0 && !L.count;
+        L.q16 = rec == sizeof(keto_query16);
         if (flags & KETO_F_DEVICE_PTRS) {
             L.queries = queries;
             L.out_allowed = out_allowed;
@@ -331,7 +333,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
             }
             return;
         }
-        const size_t qb = n * sizeof(keto_query), ob = n * (1 + sizeof(int32_t));
+        const size_t qb = n * rec, ob = n * (1 + sizeof(int32_t));
         if (flags & KETO_F_ASYNC) {
             // host buffers, enqueue only: slot b's H2D on the h2d stream (after the slot's previous
             // D2H), the kernels on the compute stream (after the H2D), the D2H on the d2h stream
@@ -355,7 +357,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
             KETO_HIP(hipMemcpyAsync(sl.q, queries, qb, hipMemcpyHostToDevice, s->h2d));
             KETO_HIP(hipEventRecord(sl.in, s->h2d));
             KETO_HIP(hipStreamWaitEvent(s->stream, sl.in, 0));
-            L.queries = static_cast<const keto_query *>(sl.q);
+            L.queries = sl.q;
             L.out_allowed = d_allowed;
             L.out_err = d_err;
             keto::run_check(*snap, *s, L);
@@ -372,7 +374,7 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         auto *d_allowed = static_cast<uint8_t *>(s->obuf);
         auto *d_err = reinterpret_cast<int32_t *>(static_cast<char *>(s->obuf) + ((n + 63) / 64) * 64);
         KETO_HIP(hipMemcpyAsync(s->qbuf, queries, qb, hipMemcpyHostToDevice, s->stream));
-        L.queries = static_cast<const keto_query *>(s->qbuf);
+        L.queries = s->qbuf;
         L.out_allowed = d_allowed;
         L.out_err = d_err;
         keto::run_check(*snap, *s, L);
@@ -381,6 +383,31 @@ int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *qu
         KETO_HIP(hipStreamSynchronize(s->stream));
         s->harvest();
     });
+}
+
+int keto_check_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_query *queries, uint64_t n,
+                     const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags) {
+    return check_batch(hsnap, hs, queries, sizeof(keto_query), n, limits, out_allowed, out_err, flags);
+}
+
+int keto_check_batch16(keto_snapshot *hsnap, keto_stream *hs, const keto_query16 *queries, uint64_t n,
+                       const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags) {
+    return check_batch(hsnap, hs, queries, sizeof(keto_query16), n, limits, out_allowed, out_err, flags);
+}
+
+int keto_pack_query16(const keto_query *in, uint64_t n, keto_query16 *out) {
+    if (n && (!in || !out)) return fail(KETO_E_INVALID, "null buffer");
+    for (uint64_t i = 0; i < n; i++) {
+        const keto_query &q = in[i];
+        const bool set = q.subj_kind == 1;
+        if (q.ns >= 4096 || q.rel >= 1024 || q.subj_kind > 1 || (set && (q.s_ns >= 4096 || q.s_rel >= 1024)) ||
+            q.max_depth < -32768 || q.max_depth > 32767)
+            return fail(KETO_E_LIMIT, "query " + std::to_string(i) + " does not fit the 16-byte record");
+        // (a subject id's namespace and relation are never read: resolve_query.inc)
+        out[i] = keto_query16{q.obj, q.s_obj, q.ns | (q.rel << 12) | ((set ? q.s_rel : 0u) << 22),
+                              (set ? q.s_ns : 0u) | (q.subj_kind << 12) | ((uint32_t)(uint16_t)(int16_t)q.max_depth << 16)};
+    }
+    return KETO_OK;
 }
 
 int keto_expand_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_set *roots, uint64_t n,

@@ -533,7 +533,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     const char *fe = getenv("KETO_FRONTIER");
     const bool frontier = !L.count && !(fe && fe[0] == '0');
     if (!frontier) {
-        run_resolve(s, st, L.queries, L.n, L.max_depth);
+        run_resolve(s, st, L.queries, L.q16, L.n, L.max_depth);
         run_dfs(s, st, L, nullptr, nullptr, L.n, true);
         return;
     }
@@ -550,7 +550,7 @@ void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L) {
     const char *ee = getenv("KETO_FR_ENGINE");
     const bool gen = ee ? ee[0] != 'b' : L.n > block_max;
     st.mark_begin();
-    run_resolve(s, st, L.queries, L.n, L.max_depth, false);
+    run_resolve(s, st, L.queries, L.q16, L.n, L.max_depth, false);
     for (uint64_t off = 0; off < L.n; off += FR_MAX_BATCH) {
         CheckLaunch Lp = L;
         Lp.n = std::min<uint64_t>(FR_MAX_BATCH, L.n - off);

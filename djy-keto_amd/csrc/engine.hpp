@@ -327,7 +327,8 @@ void ensure_lists(Stream &st, uint64_t n);
 
 // check.hip / expand.hip
 struct CheckLaunch {
-    const keto_query *queries;
+    const void *queries;  // keto_query records, or keto_query16 (q16)
+    bool q16 = false;
     uint64_t n;
     uint8_t *out_allowed;
     int32_t *out_err;
@@ -339,7 +340,7 @@ struct CheckLaunch {
 };
 // resolve.hip: per-query start records, longest-first, into st.resolved
 // ordered: heavy-first work order for the DFS interpreters (two atomics per wave); else batch order
-void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth,
+void run_resolve(const Snapshot &s, Stream &st, const void *queries, bool q16, uint64_t n, int32_t max_depth,
                  bool ordered = true);
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
 // frontier.hip: L.n resolved queries from batch position pos_base on, breadth-first; returns the

@@ -26,7 +26,7 @@ namespace {
 
 struct ResolveParams {
     DevSnapshot s;
-    const keto_query *queries;
+    const void *queries;  // keto_query (32 B) or keto_query16 records
     uint32_t n;
     int32_t max_depth;
     uint4 *resolved;  // [2n], in work order: heavy from the front, light from the back
@@ -35,6 +35,8 @@ struct ResolveParams {
 
 #include "resolve_query.inc"
 
+// Q16: keto_query16 records (include/keto_mi355x.h: one 16-byte load per query)
+template <bool Q16>
 __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
     const DevSnapshot &s = P.s;
     const Tables T = global_tables(s);
@@ -44,10 +46,16 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
     bool heavy_cls = false;
     uint4 r0 = make_uint4(0, 0, 0, 0), R = make_uint4(NONE32, NONE32, NONE32, NONE32);
     if (valid) {
-        const uint4 *qr = reinterpret_cast<const uint4 *>(P.queries + i);
-        const uint4 a = qr[0], b = qr[1];
         uint32_t wgt = 0;
-        resolve_query(s, T, a.x, a.y, a.z, a.w, b.x, b.y, b.z, (int32_t)b.w, P.max_depth, i, P.ctrl != nullptr, r0, R, wgt);
+        if constexpr (Q16) {
+            const uint4 a = reinterpret_cast<const uint4 *>(P.queries)[i];  // {obj, s_obj, ns | rel | s_rel, s_ns | kind | depth}
+            resolve_query(s, T, a.z & 0xFFFu, a.x, (a.z >> 12) & 0x3FFu, (a.w >> 12) & 1u, a.y, a.w & 0xFFFu, a.z >> 22,
+                          (int32_t)(int16_t)(a.w >> 16), P.max_depth, i, P.ctrl != nullptr, r0, R, wgt);
+        } else {
+            const uint4 *qr = reinterpret_cast<const uint4 *>(static_cast<const keto_query *>(P.queries) + i);
+            const uint4 a = qr[0], b = qr[1];
+            resolve_query(s, T, a.x, a.y, a.z, a.w, b.x, b.y, b.z, (int32_t)b.w, P.max_depth, i, P.ctrl != nullptr, r0, R, wgt);
+        }
         heavy_cls = wgt >= HEAVY_WEIGHT;
     }
     if (!P.ctrl) {  // the frontier engine needs no work order: position = query index, no atomics
@@ -79,7 +87,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(ResolveParams P) {
 
 }  // namespace
 
-void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint64_t n, int32_t max_depth, bool ordered) {
+void run_resolve(const Snapshot &s, Stream &st, const void *queries, bool q16, uint64_t n, int32_t max_depth, bool ordered) {
     ensure_lists(st, n);
     if (ordered) KETO_HIP(hipMemsetAsync(st.order_ctrl, 0, 8, st.stream));
     ResolveParams P{};
@@ -90,7 +98,8 @@ void run_resolve(const Snapshot &s, Stream &st, const keto_query *queries, uint6
     P.resolved = st.resolved;
     P.ctrl = ordered ? st.order_ctrl : nullptr;
     constexpr uint32_t BLOCK = 256;
-    hipLaunchKernelGGL(resolve_kernel, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st.stream, P);
+    if (q16) hipLaunchKernelGGL(resolve_kernel<true>, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st.stream, P);
+    else hipLaunchKernelGGL(resolve_kernel<false>, dim3((uint32_t)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st.stream, P);
     KETO_HIP(hipGetLastError());
 }
 

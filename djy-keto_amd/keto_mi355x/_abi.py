@@ -29,6 +29,9 @@ SUBJSET_DT = np.dtype([("ns", "<u4"), ("obj", "<u4"), ("rel", "<u4"), ("max_dept
 TREE_DT = np.dtype([("type", "<u4"), ("subj_kind", "<u4"), ("s_obj", "<u4"), ("s_ns", "<u4"), ("s_rel", "<u4"),
                     ("n_children", "<u4")])
 assert TUPLE_DT.itemsize == 48 and QUERY_DT.itemsize == 32 and TREE_DT.itemsize == 24
+# keto_query16 (ABI 7): {obj, s_obj, ns | rel << 12 | s_rel << 22, s_ns | subj_kind << 12 | depth << 16}
+QUERY16_DT = np.dtype([("obj", "<u4"), ("s_obj", "<u4"), ("ns_rel", "<u4"), ("s_ns_depth", "<u4")])
+assert QUERY16_DT.itemsize == 16
 
 
 class SnapshotConfig(ctypes.Structure):
@@ -140,6 +143,8 @@ SIGNATURES = {
     "keto_host_free": (ctypes.c_int, [_VP]),
     "keto_stream_kernel_time": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64), _I32]),
     "keto_check_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),
+    "keto_check_batch16": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),
+    "keto_pack_query16": (ctypes.c_int, [_VP, _U64, _VP]),
     "keto_expand_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _U64, _VP, _VP]),
     "keto_device_alloc": (ctypes.c_int, [_I32, _U64, ctypes.POINTER(_VP)]),
     "keto_device_free": (ctypes.c_int, [_VP]),

@@ -287,11 +287,23 @@ class CheckEngine:
     def check_batch_async(self, queries: np.ndarray, allowed: np.ndarray, err: np.ndarray):
         """KETO_F_ASYNC over host buffers (pinned: PinnedArray): H2D of the queries, the kernels
         and D2H of the decisions are enqueued on the stream and the call returns; the outputs are
-        valid after stream.sync()."""
-        assert queries.dtype == _abi.QUERY_DT and queries.flags.c_contiguous
+        valid after stream.sync().  queries: QUERY_DT, or QUERY16_DT records (keto_check_batch16:
+        half the H2D bytes)."""
+        assert queries.dtype in (_abi.QUERY_DT, _abi.QUERY16_DT) and queries.flags.c_contiguous
         assert len(allowed) >= len(queries) and len(err) >= len(queries)
-        check(lib().keto_check_batch(self.snapshot.handle, self.stream.handle, queries.ctypes.data, len(queries),
-                                     ctypes.byref(self.limits), allowed.ctypes.data, err.ctypes.data, _abi.F_ASYNC))
+        fn = lib().keto_check_batch16 if queries.dtype == _abi.QUERY16_DT else lib().keto_check_batch
+        check(fn(self.snapshot.handle, self.stream.handle, queries.ctypes.data, len(queries), ctypes.byref(self.limits),
+                 allowed.ctypes.data, err.ctypes.data, _abi.F_ASYNC))
+
+    def check_batch16(self, queries16: np.ndarray, err_detail: bool = False):
+        """keto_check_batch16: QUERY16_DT records (pack_queries16) -> (allowed uint8[n], err int32[n])"""
+        q = np.ascontiguousarray(queries16, dtype=_abi.QUERY16_DT)
+        allowed = np.zeros(len(q), dtype=np.uint8)
+        err = np.zeros(len(q), dtype=np.int32)
+        check(lib().keto_check_batch16(self.snapshot.handle, self.stream.handle, q.ctypes.data, len(q),
+                                       ctypes.byref(self.limits), allowed.ctypes.data, err.ctypes.data,
+                                       _abi.F_ERR_DETAIL if err_detail else 0))
+        return allowed, err
 
     def check_batch_device(self, d_queries: DeviceBuffer, n: int, d_allowed: DeviceBuffer, d_err: DeviceBuffer,
                            sync: bool = True, count_work: bool = False):
@@ -318,6 +330,17 @@ class CheckEngine:
         if code:
             raise KetoError(code, "not implemented" if code == _abi.QERR_NOT_IMPLEMENTED else "check failed")
         return bool(a[0])
+
+
+def pack_queries16(queries: np.ndarray, out: np.ndarray | None = None) -> np.ndarray:
+    """QUERY_DT records -> QUERY16_DT (keto_pack_query16): KetoError(KETO_E_LIMIT) for a request
+    outside the 16-byte form (namespace >= 4096, relation >= 1024, depth outside int16)"""
+    q = np.ascontiguousarray(queries, dtype=_abi.QUERY_DT)
+    if out is None:
+        out = np.zeros(len(q), dtype=_abi.QUERY16_DT)
+    assert out.dtype == _abi.QUERY16_DT and out.flags.c_contiguous and len(out) >= len(q)
+    check(lib().keto_pack_query16(q.ctypes.data if len(q) else None, len(q), out.ctypes.data if len(out) else None))
+    return out
 
 
 class ExpandEngine:

@@ -77,6 +77,17 @@ typedef struct keto_query {
     int32_t max_depth;
 } keto_query;
 
+/* ABI 7: the same Check in 16 bytes (SURVEY 8.1 A1's request record), for keto_check_batch16:
+ * half the H2D bytes of a host batch.  Holds namespace ids < 4096, relation ids < 1024 and request
+ * depths in [-32768, 32767] (keto_pack_query16 refuses anything else); the decisions are
+ * keto_check_batch's on the unpacked request.
+ *   word 0: obj                 word 1: s_obj (the subject id, or the subject set's object)
+ *   word 2: ns | rel << 12 | s_rel << 22
+ *   word 3: s_ns | subj_kind << 12 | (uint16_t)max_depth << 16 */
+typedef struct keto_query16 {
+    uint32_t obj, s_obj, ns_rel, s_ns_depth;
+} keto_query16;
+
 /* Expand root: a subject set ns:obj#rel (a SubjectID root is answered by the
  * shim itself as a leaf, expand/handler.go:119-126 / expand/engine.go:60-67). */
 typedef struct keto_subject_set {
@@ -217,6 +228,11 @@ int keto_stream_expand_time(keto_stream *s, double *ms_sum, uint64_t *batches, i
  * Replaces check.Engine.CheckIsMember (engine.go:65-71) for a whole batch. */
 int keto_check_batch(keto_snapshot *snap, keto_stream *s, const keto_query *queries, uint64_t n,
                      const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags);
+/* ABI 7: keto_check_batch over 16-byte records (same flags, outputs and errors). */
+int keto_check_batch16(keto_snapshot *snap, keto_stream *stream, const keto_query16 *queries, uint64_t n,
+                       const keto_limits *limits, uint8_t *out_allowed, int32_t *out_err, uint32_t flags);
+/* n keto_query records -> keto_query16 (host); KETO_E_LIMIT when one does not fit the 16-byte form */
+int keto_pack_query16(const keto_query *in, uint64_t n, keto_query16 *out);
 
 /* Expand n roots into one pre-order node buffer; out_offsets[i]..out_offsets[i+1]
  * delimit root i's tree (empty range = nil tree, expand/handler.go:141-143).
