@@ -343,6 +343,7 @@ struct CheckLaunch {
 void run_resolve(const Snapshot &s, Stream &st, const void *queries, bool q16, uint64_t n, int32_t max_depth,
                  bool ordered = true);
 void run_check(const Snapshot &s, Stream &st, const CheckLaunch &L);        // rewrite interpreter
+uint2 *frontier_stash(Stream &st, uint32_t cus);  // frontier.hip: the frontier engines' phase-A stash
 // frontier.hip: L.n resolved queries from batch position pos_base on, breadth-first; returns the
 // number of queries routed to the DFS interpreter (batch positions in st.frontier.fb_list).
 // Batches above FR_MAX_BATCH run as several passes: the arena's goal indices stay in range.

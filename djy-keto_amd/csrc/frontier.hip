@@ -147,6 +147,23 @@ __global__ __launch_bounds__(64) void fr_gens_used(const uint32_t *gbase, const 
     if (sh == 0) *out = gens;
 }
 
+// The phase-A stash of the stream's frontier engines (frontier_goal.inc Stash): a column of
+// FR_STASH_K entries per resident lane (at most 2048 per CU), shared by the generation and block
+// engines (one stream runs one batch at a time); null with KETO_FR_NOSTASH (A/B: phase B walks
+// every goal again)
+uint2 *frontier_stash(Stream &st, uint32_t cus) {
+    static const bool no_stash = getenv("KETO_FR_NOSTASH") != nullptr;
+    if (no_stash) return nullptr;
+    FrontierScratch &f = st.frontier;
+    if (!f.stash || f.stash_stride < cus * 2048u) {
+        if (f.stash) KETO_HIP(hipFree(f.stash));
+        f.stash = nullptr;
+        KETO_HIP(hipMalloc(&f.stash, (size_t)FR_STASH_K * cus * 2048u * sizeof(uint2)));
+        f.stash_stride = cus * 2048u;
+    }
+    return f.stash;
+}
+
 uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint64_t pos_base) {
     FrontierScratch &f = st.frontier;
     if (L.n > FR_MAX_BATCH) throw Error(KETO_E_LIMIT, "frontier pass larger than FR_MAX_BATCH");
@@ -185,15 +202,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     P.dbits = f.dbits;
     P.dmask = (uint32_t)(f.dcap - 1);
     P.occ = f.occ;
-    // the phase-A stash: a column per resident lane (at most 2048 per CU)
-    static const bool no_stash = getenv("KETO_FR_NOSTASH") != nullptr;  // (A/B: phase B walks every goal again)
-    if (!no_stash && (!f.stash || f.stash_stride < cus * 2048u)) {
-        if (f.stash) KETO_HIP(hipFree(f.stash));
-        f.stash = nullptr;
-        KETO_HIP(hipMalloc(&f.stash, (size_t)FR_STASH_K * cus * 2048u * sizeof(uint2)));
-        f.stash_stride = cus * 2048u;
-    }
-    P.stash = no_stash ? nullptr : f.stash;
+    P.stash = frontier_stash(st, cus);
     P.stash_stride = f.stash_stride;
     P.occ_count = f.occ_count;
     P.ocap = (uint32_t)f.ocap;

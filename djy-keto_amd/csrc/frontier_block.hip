@@ -68,6 +68,8 @@ struct BlockParams {
     int32_t *out_err;
     uint32_t *fb_list, *fb_count;   // routed batch positions, for the DFS interpreter
     unsigned long long *stats;      // [0] goals, [1] routed, [2] max generations, [3] chunks
+    uint2 *stash;                   // phase A's children (frontier_goal.inc Stash), a column per lane; or null
+    uint32_t stash_stride;
 };
 
 struct Chunk {  // LDS state of the workgroup's current chunk
@@ -268,7 +270,8 @@ __global__ __launch_bounds__(BB, KETO_FRB_WAVES) void fr_block(BlockParams P) {
                 const uint4 row = rnode != NONE32 ? s.set_row[rnode] : make_uint4(0, 0, 0, 0);
                 const uint4 rrec = (live && kind == G_ES) ? reach_record(s, T, node) : make_uint4(NONE32, NONE32, NONE32, 0);
                 const Subject q = live ? subject_of(C.start[2 * pos + 1]) : Subject{0, false, make_uint4(0, 0, 0, 0)};
-                const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W, rrec);
+                Stash st{P.stash ? P.stash + (blockIdx.x * blockDim.x + tid) : nullptr, P.stash_stride, 0};
+                const PhaseA pa = phase_a(s, T, q, live, node, w, scope, i, row, W, rrec, &st);
                 uint32_t nc = pa.nc;
                 // routing: a row too long for the record, a routed query, the generation cap, a goal
                 // with more children than the budget, and the query's goal count past the budget
@@ -314,7 +317,14 @@ __global__ __launch_bounds__(BB, KETO_FRB_WAVES) void fr_block(BlockParams P) {
                     pg.val[li] = pa.val;
                     pg.occ2[li] = (pa.chain && occ_ok) ? oc : NONE32;
                 }
-                if (nc || (live && kind == G_ES && pa.xrel)) {
+                const bool stashed = st.p && (kind == G_RW || kind == G_TTU) && st.n == pa.nc && nc <= FR_STASH_K;
+                if (nc && stashed) {  // the children phase A kept (as fr_expand)
+                    BlockSink sink{P, C, k, pos};
+                    for (uint32_t j = 0; j < nc; j++) {
+                        const uint2 v = st.p[(size_t)j * st.stride];
+                        sink.spawn(cb + j, v.x, pos, v.y, scope);
+                    }
+                } else if (nc || (live && kind == G_ES && pa.xrel)) {
                     BlockSink sink{P, C, k, pos};
                     PhaseA pb = pa;
                     pb.nc = nc;
@@ -476,6 +486,8 @@ uint32_t run_frontier_block(const Snapshot &s, Stream &st, const CheckLaunch &L,
     P.fb_list = f.fb_list;
     P.fb_count = f.fb_count;
     P.stats = reinterpret_cast<unsigned long long *>(f.ctrl + 4);
+    P.stash = frontier_stash(st, cus);
+    P.stash_stride = st.frontier.stash_stride;
     KETO_HIP(hipMemsetAsync(P.fb_count, 0, 4, st.stream));
     if (lds_tables) hipLaunchKernelGGL(fr_block<true>, dim3(grid), dim3(BB), lds, st.stream, P);
     else hipLaunchKernelGGL(fr_block<false>, dim3(grid), dim3(BB), 0, st.stream, P);
