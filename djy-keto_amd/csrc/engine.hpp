@@ -268,6 +268,7 @@ struct Stream {
         uint64_t *offsets = nullptr;
         int32_t *err = nullptr;
         uint32_t *fb_list = nullptr;
+        uint32_t *order = nullptr;  // the wave kernel's queue: heavy roots first (expand_order)
         hipEvent_t ev[2] = {nullptr, nullptr};  // around the traversal (expand_wave + the fallback's count pass)
         void *hpin = nullptr;                   // pinned read-back of the offsets, errors and stage top
         size_t hpin_bytes = 0;

@@ -233,6 +233,7 @@ struct ExpandWaveParams {
     unsigned long long *sizes, *soff;  // [n]: nodes of each tree, its offset in `stage` (NONE: fallback)
     int32_t *err;
     uint32_t *next;                 // root queue
+    const uint32_t *order;          // queue position -> root (expand_order: heavy roots first); null: batch order
     uint32_t *fb_list, *fb_count;   // roots for expand_kernel
     unsigned long long *counters;   // rows, edges, -, out nodes
 };
@@ -255,6 +256,33 @@ __device__ __forceinline__ uint32_t wave_at(uint32_t x, uint32_t j) {
 #endif
 }
 
+// The wave kernel's queue order: roots whose path-count weight (the snapshot's scheduling weights,
+// a capped count of the paths below a node) reaches `heavy` first, the rest after -- a batch's walk
+// lasts at least as long as its longest tree, which should not start last in some wave's queue.
+// One atomic per class per wave (as resolve.hip's heavy-first work order).
+__global__ __launch_bounds__(256) void expand_order(DevSnapshot s, const keto_subject_set *roots, uint32_t n, uint32_t heavy,
+                                                    uint32_t *order, uint32_t *ctr) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, lane = __lane_id();
+    const bool valid = i < n;
+    bool hv = false;
+    if (valid) {
+        const uint32_t node = resolve_node(s, roots[i].ns, roots[i].obj, roots[i].rel);
+        hv = !(node & VIRT_BIT) && s.weight[node] >= heavy;
+    }
+    const unsigned long long mh = __ballot(valid && hv), ml = __ballot(valid && !hv), below = (1ull << lane) - 1ull;
+    uint32_t bh = 0, bl = 0;
+    const int leader = __ffsll((long long)(mh | ml)) - 1;
+    if ((int)lane == leader) {
+        if (mh) bh = atomicAdd(&ctr[0], (uint32_t)__popcll(mh));
+        if (ml) bl = atomicAdd(&ctr[1], (uint32_t)__popcll(ml));
+    }
+    if (leader >= 0) {
+        bh = __shfl(bh, leader);
+        bl = __shfl(bl, leader);
+    }
+    if (valid) order[hv ? bh + (uint32_t)__popcll(mh & below) : n - 1 - (bl + (uint32_t)__popcll(ml & below))] = i;
+}
+
 // one root per wavefront: see the file comment
 __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
     __shared__ uint32_t vis[XW_VIS];
@@ -268,6 +296,7 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
         if (lane == 0) q = atomicAdd(P.next, 1u);
         q = __shfl(q, 0);
         if (q >= P.n) break;
+        if (P.order) q = P.order[q];
         for (uint32_t i = lane; i < XW_VIS; i += XWW) vis[i] = XW_EMPTY;
         __syncthreads();
         const keto_subject_set R = P.roots[q];
@@ -550,7 +579,7 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         while (nc < n) nc <<= 1;
         const uint64_t sc = std::max<uint64_t>(X.stage_cap, 1u << 22);
         const size_t bytes = xal(64) + xal(grid * XW_PRIV * sizeof(uint2)) + xal(sc * sizeof(uint2)) +
-                             2 * xal(nc * 8) + xal((nc + 1) * 8) + xal(nc * 4) + xal(nc * 4);
+                             2 * xal(nc * 8) + xal((nc + 1) * 8) + 3 * xal(nc * 4);
         KETO_HIP(hipMalloc(&X.mem, bytes));
         char *p = static_cast<char *>(X.mem);
         X.ctrl = reinterpret_cast<unsigned long long *>(p);
@@ -568,6 +597,8 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         X.err = reinterpret_cast<int32_t *>(p);
         p += xal(nc * 4);
         X.fb_list = reinterpret_cast<uint32_t *>(p);
+        p += xal(nc * 4);
+        X.order = reinterpret_cast<uint32_t *>(p);
         X.grid = grid;
         X.stage_cap = sc;
         X.ncap = nc;
@@ -607,6 +638,15 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         for (hipEvent_t &e : X.ev) KETO_HIP(hipEventCreate(&e));
     }
     KETO_HIP(hipEventRecord(X.ev[0], st.stream));
+    // heavy roots first (KETO_XW_HEAVY: the weight threshold, 0 = batch order)
+    const char *xh = getenv("KETO_XW_HEAVY");
+    const uint32_t heavy = xh ? (uint32_t)atoi(xh) : HEAVY_WEIGHT;
+    if (wave && heavy && s.dev.weight) {
+        hipLaunchKernelGGL(expand_order, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st.stream, s.dev, d_roots, (uint32_t)n, heavy,
+                           X.order, reinterpret_cast<uint32_t *>(X.ctrl + 3));
+        KETO_HIP(hipGetLastError());
+        P.order = X.order;
+    }
     if (wave) {
         hipLaunchKernelGGL(expand_wave, dim3((uint32_t)std::min<uint64_t>(grid, n)), dim3(XWW), 0, st.stream, P);
         KETO_HIP(hipGetLastError());
