@@ -79,6 +79,7 @@ struct Snapshot {
     uint64_t reach_cand = 0, reach_pool_n = 0;
     std::vector<uint4> ext;          // {obj, ns, entity, 0} of the objects placed on spares (dev.ext's entries)
     uint64_t reach_pool_cap = 0;     // reach_pool entries allocated (> reach_pool_n: room to append)
+    uint64_t reach_pool_built = 0;   // reach_pool_n at the last full build (an advance declines past 2x + 1Mi)
     // in-place advance (advance in patch.hip; store snapshots only, BuildOpts::room): the row value
     // arrays' capacities and next free entries past the rows, the relocation table (dev.reloc), and
     // each all_subj entry's shard key -- the high 64 bits of its shard_id, the order of a row

@@ -687,8 +687,13 @@ void sync(Partition &P) { KETO_HIP(hipStreamSynchronize(P.hs)); }
 // the closure's owner-side reads from the resident partition (a job of several ranks)
 void snap_source(Partition &P, Lookup &L) {
     if (!P.dist) return;
+    const Snapshot &S = dist_snapshot(*P.dist);
+    // run_of / tuple_at read all_off[node0 .. node0 + n_slots] as one CSR run, without row_span:
+    // only a snapshot no advance ever relocated rows in (partition builds take no room)
+    if (S.dev.reloc || S.room.moved || S.room.reloc_cap)
+        throw Error(KETO_E_DEVICE, "partition snapshot has advance room: its CSR runs are not contiguous");
     L.use_snap = true;
-    L.S = dist_snapshot(*P.dist).dev;
+    L.S = S.dev;
 }
 
 uint64_t d2h_u64(Partition &P, const void *d) {

@@ -1255,6 +1255,10 @@ bool advance_snapshot(Snapshot &S, const keto_tuple *touched, const uint8_t *is_
         src += rev_len[j];
     }
     if (at_all > R.all_cap || at_rev > R.rev_cap || at_set > R.set_cap || n_reloc > R.reloc_cap) return false;  // no room left
+    // the reachability pool: every advance appends its re-walked records and never reclaims the
+    // ones they supersede, so past twice the build's entries (+ 1Mi) the advance declines and the
+    // full build the caller falls back to compacts it
+    if (S.reach_pool_n > 2 * S.reach_pool_built + (1u << 20)) return false;
     phase("rows");
     // every staging buffer of the writes, allocated (and filled) before the first write: an
     // allocation that fails here declines with the snapshot untouched

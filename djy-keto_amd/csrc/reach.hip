@@ -326,7 +326,7 @@ void build_reach(Snapshot &s) {
     s.reach_pool_cap = 0;
     s.info.n_reach = 0;
     s.reach_slots.clear();
-    s.reach_cand = s.reach_pool_n = 0;
+    s.reach_cand = s.reach_pool_n = s.reach_pool_built = 0;
     bool had = false;
     for (uint32_t ri : s.relinfo) had |= (ri & RI_REACH) != 0;
     if (had) reach_bits(s, {});
@@ -375,7 +375,7 @@ void build_reach(Snapshot &s) {
     reach_bits(s, base);
     s.reach_slots = std::move(base);
     s.reach_cand = n_cand;
-    s.reach_pool_n = total;
+    s.reach_pool_n = s.reach_pool_built = total;
     s.reach_pool_cap = pool_cap;
 }
 
@@ -504,6 +504,7 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
     s.reach_cand = n_cand;
     s.reach_pool_n = pool_n;
     s.reach_pool_cap = pool_cap;
+    if (&s != &B) s.reach_pool_built = B.reach_pool_built;  // (a copy patch: the base's build)
     KETO_HIP(hipMemset(cnt.p, 0, 8));
     hipLaunchKernelGGL(k_count_tabled, dim3((uint32_t)std::min<uint64_t>(4096, (n_cand + RB - 1) / RB)), dim3(RB), 0, 0, idx, n_cand,
                        static_cast<unsigned long long *>(cnt.p));

@@ -235,9 +235,14 @@ void store_transact(TupleStore &st, const keto_tuple *ins, uint64_t n_ins, const
             // more rows than the list held: the tombstoned ones are gone from the index already,
             // so the whole index is rebuilt from the rows and the deletes run again into a list
             // of the right size
-            st.n = n_all;  // (index every row, the appended ones included)
-            st.reindex();
-            st.n = n_before;
+            {  // (index every row, the appended ones included; st.n back to n_before on a throw too)
+                struct Restore {
+                    uint64_t &n, v;
+                    ~Restore() { n = v; }
+                } restore{st.n, n_before};
+                st.n = n_all;
+                st.reindex();
+            }
             cap_dead = n_dead;
             dead = build::DevBuf(4 * cap_dead);
             KETO_HIP(hipMemset(cnt.p, 0, 8));
