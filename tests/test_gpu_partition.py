@@ -199,9 +199,13 @@ def _worker(rank, world, port, out, device_buffers=False, mode="dist"):
         lv_bytes = sum(x["request_bytes"] + x["tuple_bytes_sent"] for x in lv)
         if mode == "closure":
             lv_ok = len(lv) == st["levels"] and 0 < lv_bytes <= st["bytes_sent"] and sum(x["objects"] for x in lv) == st["objects"]
-        else:  # the distributed frontier: one level per generation, goal records out and values back
-            lv_ok = len(lv) == st["generations"] and lv_bytes == st["exchange_bytes"] > 0 and \
-                sum(x["objects"] for x in lv) == st["goals"] and (st["build_s"] == 0 or st["routed"] > 0)
+        else:  # the distributed frontier: one generation record each (ABI 7), goal records out and
+            # values back; level_stats holds only the routed queries' closure levels
+            gens = eng.generation_stats()
+            g_bytes = sum(g["record_bytes_out"] + g["value_bytes_back"] for g in gens)
+            lv_ok = len(gens) == st["generations"] and g_bytes == st["exchange_bytes"] > 0 and \
+                sum(g["goals"] for g in gens) == st["goals"] and (st["build_s"] == 0 or st["routed"] > 0) and \
+                len(lv) == st["levels"]  # (any rank's routed queries: every rank joins the closure)
         orc = _oracle(wl)
         dec, oerr, _ = orc.check_batch(queries_to_oracle(q), threads=4)
         roots = _roots(wl, np.random.default_rng(rank), 64)
