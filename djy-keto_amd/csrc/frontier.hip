@@ -366,6 +366,20 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     f.stats.goals += top;
     f.stats.generations += gens;
     f.stats.max_generations = std::max<uint64_t>(f.stats.max_generations, gens);
+#ifdef KETO_FR_KINDSTAT
+    {
+        unsigned long long ks[64 * 8];
+        KETO_HIP(hipMemcpyFromSymbol(ks, HIP_SYMBOL(g_kstat), sizeof ks));
+        static const unsigned long long zero[64 * 8] = {};
+        KETO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_kstat), zero, sizeof zero));
+        fprintf(stderr, "[kinds] n %llu:", (unsigned long long)L.n);
+        for (uint32_t g = 0; g <= gens && g < 64; g++) {
+            fprintf(stderr, " |");
+            for (uint32_t kd = 0; kd < 8; kd++) fprintf(stderr, " %llu", ks[g * 8 + kd]);
+        }
+        fprintf(stderr, "\n");
+    }
+#endif
     if (gentime) {
         fprintf(stderr, "[gentime] n %llu us:", (unsigned long long)L.n);
         for (uint32_t g = 0; g + 1 < gev.size() && g <= gens; g++) {

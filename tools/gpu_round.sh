@@ -12,6 +12,7 @@
 #                                             KETO_FR_GENTIME: the line and the median time of each generation
 #   tools/gpu_round.sh OUT sq [wl]            SQ / TCC counters per kernel of the check path (two --pmc passes,
 #                                             tools/pmc_split.py): issue vs wait, instructions per batch
+#   tools/gpu_round.sh OUT sqlds [wl]         per-generation LDS / wait / instruction-mix counters of fr_expand (pmc_gens.py)
 #   tools/gpu_round.sh OUT patch              the store probe alone, the patcher's phase times (KETO_PATCH_VERBOSE)
 #   tools/gpu_round.sh OUT c5 [scale]         tests/test_gpu_c5.py (8 gloo ranks sharing the GPU) and the C5
 #                                             bench rehearsal at that scale (default 40 / 10)
@@ -63,6 +64,13 @@ sq)
   timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY TCC_HIT_sum TCC_MISS_sum \
     -d $OUT/sq2 -o pmc --output-format csv -- python3 bench.py $A > $OUT/sq2.log 2>&1 || exit 1
   python3 tools/pmc_split.py $OUT/sq_$WL.json $OUT/sq1 $OUT/sq2 | cut -c1-400 | head -12 ;;
+sqlds)
+  WL=${1:-c4}; A="--workload $WL --steps 3 --warmup 0 $QUIET"
+  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS \
+    -d $OUT/lds1 -o pmc --output-format csv -- python3 bench.py $A > $OUT/lds1.log 2>&1 || exit 1
+  timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA \
+    -d $OUT/lds2 -o pmc --output-format csv -- python3 bench.py $A > $OUT/lds2.log 2>&1 || exit 1
+  python3 tools/pmc_gens.py $OUT/lds1 $OUT/lds2 | cut -c1-400 ;;
 patch)
   KETO_PATCH_VERBOSE=1 timeout -k 10 400 python3 -u tools/patch_probe.py 10 > $OUT/patch.log 2>&1 || { tail -5 $OUT/patch.log; exit 1; }
   grep -E "keto (patch|advance)|advance_ms" $OUT/patch.log | cut -c1-900 | head -60 ;;
