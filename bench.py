@@ -318,13 +318,26 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
         nodes, offs, err = xe.build_trees(r, out=pin)
     dt = (time.perf_counter() - t0) / reps
     nodes = nodes.copy()
-    pin.free()
     c = stream.counters(reset=True)
     ms, nb = stream.expand_time(reset=True)
     kms = ms / max(1, nb)
+    # keto_expand_batch_spans into the same pinned buffer: each tree written as its walk ends, the
+    # copy-out overlapping the other walks; the same trees (checked root by root)
+    xe.build_trees_spans(r, out=pin)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sn, first, count, serr = xe.build_trees_spans(r, out=pin)
+    dt_spans = (time.perf_counter() - t0) / reps
+    stream.counters(reset=True)
+    stream.expand_time(reset=True)
+    spans_mis = int((serr != err).sum()) + sum(
+        0 if np.array_equal(sn[int(first[i]):int(first[i]) + int(count[i])], nodes[int(offs[i]):int(offs[i + 1])]) else 1
+        for i in range(n))
+    pin.free()
     # algorithmic bytes: 8*rows + 4*edges + 12*out_nodes per batch
     xbytes = (8 * c["rows"] + 4 * c["edges"] + 12 * c["out_nodes"]) / reps
     return {"roots_per_batch": n, "ms_per_batch": dt * 1e3, "ms_per_batch_pageable_out": dt_pageable * 1e3,
+            "ms_per_batch_spans": dt_spans * 1e3, "spans_tree_mismatches": spans_mis,
             "trees_per_s": n / dt, "nodes_per_batch": int(offs[n]),
             "errors": int((err != 0).sum()), "max_read_depth": wl.max_depth,
             "traversal_kernel_ms": kms,
@@ -334,7 +347,9 @@ def expand_probe(km, snap, wl, stream, n: int = 4096, reps: int = 5):
                          "bytes_model": "8*rows + 4*edges + 12*out_nodes (SURVEY.md 8.1 (d))",
                          "kernel": "expand_wave (wave per root, one traversal) + fallback count pass if any"},
             "note": "ms_per_batch: host roots in, trees out into pinned host memory (API form, root order) incl. "
-                    "PCIe; ms_per_batch_pageable_out: the same into pageable memory; traversal_kernel_ms: HIP events "
+                    "PCIe; ms_per_batch_spans: keto_expand_batch_spans into the same pinned memory (completion "
+                    "order, each tree written over PCIe as its walk ends; trees compared root by root with "
+                    "ms_per_batch's); ms_per_batch_pageable_out: the same into pageable memory; traversal_kernel_ms: HIP events "
                     "around the traversal on the engine stream; roots: Group#members and Folder#viewers"}
 
 

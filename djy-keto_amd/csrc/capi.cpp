@@ -435,6 +435,32 @@ int keto_expand_batch(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_
     return g != KETO_OK ? g : rc;
 }
 
+int keto_expand_batch_spans(keto_snapshot *hsnap, keto_stream *hs, const keto_subject_set *roots, uint64_t n,
+                            const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_first,
+                            uint32_t *out_count, int32_t *out_err, uint64_t *out_total) {
+    keto::Snapshot *snap = SN(hsnap);
+    keto::Stream *s = ST(hs);
+    if (!snap || !s) return fail(KETO_E_INVALID, "null snapshot or stream");
+    if (snap->broken) return fail(KETO_E_INVALID, BROKEN);
+    if (!out_total || (n && (!roots || !out_first || !out_count || !out_err))) return fail(KETO_E_INVALID, "null buffer");
+    keto_limits lim = limits ? *limits : keto_limits{5, 100};
+    if (lim.max_read_depth < 1 || lim.max_read_depth > 65535) return fail(KETO_E_INVALID, "max_read_depth out of range");
+    if (s->device != snap->device) return fail(KETO_E_INVALID, "stream and snapshot are on different devices");
+    int rc = KETO_OK;
+    int g = guarded([&] {
+        KETO_HIP(hipSetDevice(s->device));
+        *out_total = 0;
+        if (n == 0) return;
+        grow(s->qbuf, s->qbuf_bytes, n * sizeof(keto_subject_set));
+        auto *d_roots = static_cast<keto_subject_set *>(s->qbuf);
+        KETO_HIP(hipMemcpyAsync(d_roots, roots, n * sizeof(keto_subject_set), hipMemcpyHostToDevice, s->stream));
+        if (!keto::expand_batch_spans(*snap, *s, d_roots, n, lim.max_read_depth, out_nodes, out_cap, out_first, out_count, out_err,
+                                      out_total))
+            rc = fail(KETO_E_CAPACITY, "expand output needs " + std::to_string(*out_total) + " nodes");
+    });
+    return g != KETO_OK ? g : rc;
+}
+
 int keto_host_alloc(uint64_t bytes, void **out) {
     if (!out) return fail(KETO_E_INVALID, "null output pointer");
     *out = nullptr;

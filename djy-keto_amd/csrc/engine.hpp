@@ -265,6 +265,7 @@ struct Stream {
         uint2 *priv = nullptr, *stage = nullptr;  // walk records {subject key, n_children | union} (expand.hip)
         keto_tree_node *outbuf = nullptr;
         uint64_t out_cap = 0;
+        uint64_t span_hint = 0;  // keto_expand_batch_spans into pageable memory: the device buffer it wants
         unsigned long long *sizes = nullptr, *soff = nullptr, *ctrl = nullptr;
         uint64_t *offsets = nullptr;
         int32_t *err = nullptr;
@@ -375,6 +376,12 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L);
 // offsets filled) when out_cap is too small
 bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth,
                   keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets, int32_t *out_err);
+
+// keto_expand_batch_spans' device path: root i's tree at out_nodes[out_first[i]], out_count[i]
+// nodes, written as the walks finish; false (*out_total = the nodes required) when out_cap is too small
+bool expand_batch_spans(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth,
+                        keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_first, uint32_t *out_count,
+                        int32_t *out_err, uint64_t *out_total);
 
 // treefmt.cpp: Expand trees -> API form (Mapper.ToTree + JSON / Tree.ToProto), host only
 void trees_to_json(const keto_tree_node *nodes, const uint64_t *offsets, uint64_t n_trees,

@@ -236,6 +236,12 @@ struct ExpandWaveParams {
     const uint32_t *order;          // queue position -> root (expand_order: heavy roots first); null: batch order
     uint32_t *fb_list, *fb_count;   // roots for expand_kernel
     unsigned long long *counters;   // rows, edges, -, out nodes
+    // span output (keto_expand_batch_spans): a finished tree goes straight to dout (the caller's
+    // pinned buffer, mapped, or a device buffer) at the run dtop hands it, in API form -- root i at
+    // first[i] -- while the other roots still walk; null: the stage, placed in root order later
+    keto_tree_node *dout;
+    unsigned long long dcap, *dtop;
+    uint64_t *first;
 };
 
 // A walk record is what the DFS decides about a node: {subject key, n_children | XR_UNION}.  The
@@ -411,6 +417,35 @@ __global__ __launch_bounds__(64) void expand_wave(ExpandWaveParams P) {
         }
         __syncthreads();  // (the wave's LDS writes before the next root clears them)
         unsigned long long off = 0;
+        if (P.dout && !fail) {  // span output: the tree's run of the output, written now
+            if (lane == 0 && cnt) off = atomicAdd(P.dtop, (unsigned long long)cnt);
+            off = __shfl(off, 0);
+            if (off + cnt <= P.dcap)  // (past the capacity: only counted -- the caller learns the size it needs)
+                for (uint32_t i0 = 0; i0 < cnt; i0 += 4 * XWW) {  // four records per lane in flight
+                    uint2 r[4];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; u++) {
+                        const uint32_t i = i0 + u * XWW + lane;
+                        r[u] = i < cnt ? priv[i] : make_uint2(0, 0);
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; u++) {
+                        const uint32_t i = i0 + u * XWW + lane;
+                        const bool un = (r[u].y & XR_UNION) != 0u;
+                        if (i < cnt) P.dout[off + i] = api_node(s, un ? 1u : 4u, r[u].x, un ? r[u].y & ~XR_UNION : 0u);
+                    }
+                }
+            if (lane == 0) {
+                P.sizes[q] = cnt;
+                P.first[q] = off;
+                P.soff[q] = 0;
+                P.err[q] = 0;
+            }
+            c_rows += rows;
+            c_edges += edges;
+            c_out += cnt;
+            continue;
+        }
         if (!fail && cnt) {
             if (lane == 0) off = atomicAdd(P.stage_top, (unsigned long long)cnt);
             off = __shfl(off, 0);
@@ -455,6 +490,17 @@ __global__ __launch_bounds__(256) void expand_place(DevSnapshot s, const uint2 *
             out[offsets[q] + i] = api_node(s, un ? 1u : 4u, r.x, un ? r.y & ~XR_UNION : 0u);
         }
     }
+}
+
+// span output: the runs of the fallback roots (expand_kernel's count pass sized them), taken from
+// the same counter as the wave kernel's trees; an errored root gets none
+__global__ __launch_bounds__(256) void expand_fb_spans(const uint32_t *fb_list, const uint32_t *fb_count, uint32_t n,
+                                                       const unsigned long long *sizes, const int32_t *err, unsigned long long *dtop,
+                                                       uint64_t *first) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (fb_list ? j >= *fb_count : j >= n) return;  // (no list: every root is a fallback root)
+    const uint32_t q = fb_list ? fb_list[j] : j;
+    first[q] = err[q] ? 0ull : atomicAdd(dtop, sizes[q]);
 }
 
 // root-order offsets of the trees on the device: offsets[i + 1] = offsets[i] + (err[i] ? 0 :
@@ -557,10 +603,15 @@ void run_expand(const Snapshot &s, Stream &st, const ExpandLaunch &L) {
 
 static size_t xal(size_t b) { return (b + 255) / 256 * 256; }
 
-bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth,
-                  keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets, int32_t *out_err) {
-    out_offsets[0] = 0;
-    if (n == 0) return true;
+namespace {
+// the wave kernel's buffers for n roots (grown as needed), its parameters, the heavy-first queue,
+// and the fallback pass's launch: what both output forms share
+struct XwRun {
+    ExpandWaveParams P;
+    ExpandLaunch F;
+    bool wave;
+};
+XwRun xw_prepare(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth, size_t host_extra) {
     if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "batch too large");
     auto &X = st.xw;
     const uint32_t cus = (uint32_t)num_cus(s.device);
@@ -604,7 +655,7 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         X.ncap = nc;
     }
     // pinned read-back: ctrl (stage top, fallback count), offsets[n + 1], errors[n]
-    const size_t hb = 64 + (n + 1) * 8 + n * 4;
+    const size_t hb = 64 + (n + 1) * 8 + n * 4 + host_extra;
     if (X.hpin_bytes < hb) {
         if (X.hpin) KETO_HIP(hipHostFree(X.hpin));
         X.hpin = nullptr;
@@ -647,26 +698,44 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
         KETO_HIP(hipGetLastError());
         P.order = X.order;
     }
-    if (wave) {
-        hipLaunchKernelGGL(expand_wave, dim3((uint32_t)std::min<uint64_t>(grid, n)), dim3(XWW), 0, st.stream, P);
-        KETO_HIP(hipGetLastError());
-    } else {
-        KETO_HIP(hipMemsetAsync(X.soff, 0xFF, n * 8, st.stream));
-    }
-    // the roots past the wave kernel's LDS / staging space: the lane kernel counts them, reading
-    // their count from the device (no host round trip; with none its launches end at once)
     ExpandLaunch F{};
     F.roots = d_roots;
     F.n = n;
     F.max_depth = max_depth;
     F.sizes = reinterpret_cast<uint64_t *>(X.sizes);
-    F.offsets = X.offsets;  // (root i's first node: offsets[i], read by the emit pass below)
+    F.offsets = X.offsets;  // (root i's first node: offsets[i], read by the emit pass)
     F.err = X.err;
     F.list = wave ? X.fb_list : nullptr;
     F.list_count = wave ? P.fb_count : nullptr;
     F.nl = n;
     F.emit = false;
-    run_expand(s, st, F);
+    return XwRun{P, F, wave};
+}
+// the wave kernel (or, KETO_EXPAND_WAVE=0, a memset sending every root to the fallback), then the
+// fallback's count pass over the roots it left -- reading their count from the device (no host
+// round trip; with none its launches end at once)
+void xw_walk(const Snapshot &s, Stream &st, XwRun &R, uint64_t n) {
+    auto &X = st.xw;
+    if (R.wave) {
+        hipLaunchKernelGGL(expand_wave, dim3((uint32_t)std::min<uint64_t>(X.grid, n)), dim3(XWW), 0, st.stream, R.P);
+        KETO_HIP(hipGetLastError());
+    } else {
+        KETO_HIP(hipMemsetAsync(X.soff, 0xFF, n * 8, st.stream));
+    }
+    run_expand(s, st, R.F);
+}
+}  // namespace
+
+bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth,
+                  keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_offsets, int32_t *out_err) {
+    out_offsets[0] = 0;
+    if (n == 0) return true;
+    auto &X = st.xw;
+    const uint32_t cus = (uint32_t)num_cus(s.device);
+    XwRun R = xw_prepare(s, st, d_roots, n, max_depth, 0);
+    ExpandLaunch &F = R.F;
+    const bool wave = R.wave;
+    xw_walk(s, st, R, n);
     KETO_HIP(hipEventRecord(X.ev[1], st.stream));
     hipLaunchKernelGGL(expand_offsets, dim3(1), dim3(XO_BLOCK), 0, st.stream, X.sizes, X.err, (uint32_t)n,
                        reinterpret_cast<unsigned long long *>(X.offsets));
@@ -711,6 +780,97 @@ bool expand_batch(const Snapshot &s, Stream &st, const keto_subject_set *d_roots
     // (Writing them from expand_place straight into mapped pinned memory instead, over PCIe,
     // measured the same: 1.38 / 1.40 vs 1.37 / 1.38 ms API -- the copy runs at PCIe speed either way.)
     KETO_HIP(hipMemcpyAsync(out_nodes, X.outbuf, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipStreamSynchronize(st.stream));
+    return true;
+}
+
+// keto_expand_batch_spans: every tree written the moment its wave finishes it, at the run the
+// output's counter hands it -- straight into the caller's buffer over PCIe when it is pinned
+// (keto_host_alloc), so the copy-out overlaps the other roots' walks; else into a device buffer
+// copied once at the end.  The fallback roots follow (count pass, runs, emit pass).  false with
+// *out_total = the nodes required when out_cap is too small (nothing of the batch is usable then).
+bool expand_batch_spans(const Snapshot &s, Stream &st, const keto_subject_set *d_roots, uint64_t n, int32_t max_depth,
+                        keto_tree_node *out_nodes, uint64_t out_cap, uint64_t *out_first, uint32_t *out_count,
+                        int32_t *out_err, uint64_t *out_total) {
+    *out_total = 0;
+    if (n == 0) return true;
+    auto &X = st.xw;
+    // the caller's buffer, as the device sees it: pinned host memory is written in place
+    keto_tree_node *dout = nullptr;
+    hipPointerAttribute_t pa{};
+    if (out_nodes && out_cap && hipPointerGetAttributes(&pa, out_nodes) == hipSuccess && pa.type == hipMemoryTypeHost &&
+        pa.devicePointer && pa.hostPointer)
+        dout = reinterpret_cast<keto_tree_node *>(static_cast<char *>(pa.devicePointer) +
+                                                  (reinterpret_cast<char *>(out_nodes) - static_cast<char *>(pa.hostPointer)));
+    else
+        (void)hipGetLastError();  // (pageable memory: not a HIP allocation)
+    uint64_t dcap = out_cap;
+    if (!dout) {  // a device buffer of the last batch's size (at least 1Mi nodes); a larger batch runs again
+        const uint64_t want = std::min<uint64_t>(out_cap, std::max<uint64_t>({X.out_cap, X.span_hint, 1ull << 20}));
+        if (X.out_cap < want) {
+            if (X.outbuf) KETO_HIP(hipFree(X.outbuf));
+            X.outbuf = nullptr;
+            X.out_cap = 0;
+            KETO_HIP(hipMalloc(&X.outbuf, std::max<uint64_t>(1, want) * sizeof(keto_tree_node)));
+            X.out_cap = want;
+        }
+        dout = X.outbuf;
+        dcap = std::min<uint64_t>(out_cap, X.out_cap);
+    }
+    XwRun R = xw_prepare(s, st, d_roots, n, max_depth, n * 8);
+    unsigned long long *dtop = X.ctrl + 4;
+    R.P.dout = dout;
+    R.P.dcap = dcap;
+    R.P.dtop = dtop;
+    R.P.first = X.offsets;
+    R.F.offsets = X.offsets;  // (the emit pass writes root q at first[q])
+    xw_walk(s, st, R, n);
+    KETO_HIP(hipEventRecord(X.ev[1], st.stream));
+    if (R.wave) {
+        hipLaunchKernelGGL(expand_fb_spans, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st.stream, X.fb_list, R.P.fb_count,
+                           (uint32_t)n, X.sizes, X.err, dtop, X.offsets);
+    } else {
+        hipLaunchKernelGGL(expand_fb_spans, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st.stream, nullptr, nullptr,
+                           (uint32_t)n, X.sizes, X.err, dtop, X.offsets);
+    }
+    KETO_HIP(hipGetLastError());
+    char *hp = static_cast<char *>(X.hpin);
+    unsigned long long *h = reinterpret_cast<unsigned long long *>(hp);
+    uint64_t *hfirst = reinterpret_cast<uint64_t *>(hp + 64);
+    int32_t *herr = reinterpret_cast<int32_t *>(hp + 64 + (n + 1) * 8);
+    unsigned long long *hsize = reinterpret_cast<unsigned long long *>(hp + 64 + (n + 1) * 8 + ((n * 4 + 7) & ~7ull));
+    KETO_HIP(hipMemcpyAsync(h, X.ctrl, 40, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipMemcpyAsync(hfirst, X.offsets, n * 8, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipMemcpyAsync(herr, X.err, n * 4, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipMemcpyAsync(hsize, X.sizes, n * 8, hipMemcpyDeviceToHost, st.stream));
+    KETO_HIP(hipStreamSynchronize(st.stream));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, X.ev[0], X.ev[1]) == hipSuccess) {
+        X.ms_sum += ms;
+        X.batches++;
+    }
+    const uint64_t total = h[4];
+    const uint32_t nfb = R.wave ? (uint32_t)h[2] : (uint32_t)n;
+    *out_total = total;
+    X.span_hint = std::max<uint64_t>(X.span_hint, total + total / 4);
+    if (total > out_cap || (total && !out_nodes)) return false;
+    if (total > dcap) {  // past the device buffer (pageable output): once more into one of the right size
+        X.span_hint = total + total / 4;
+        return expand_batch_spans(s, st, d_roots, n, max_depth, out_nodes, out_cap, out_first, out_count, out_err, out_total);
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        out_err[i] = herr[i];
+        out_first[i] = herr[i] ? 0 : hfirst[i];
+        out_count[i] = herr[i] ? 0u : (uint32_t)hsize[i];
+    }
+    if (nfb) {  // the fallback roots' trees at their runs
+        R.F.emit = true;
+        R.F.nl = nfb;
+        R.F.out = dout;
+        run_expand(s, st, R.F);
+    }
+    if (dout == X.outbuf && total)
+        KETO_HIP(hipMemcpyAsync(out_nodes, X.outbuf, total * sizeof(keto_tree_node), hipMemcpyDeviceToHost, st.stream));
     KETO_HIP(hipStreamSynchronize(st.stream));
     return true;
 }

@@ -146,6 +146,8 @@ SIGNATURES = {
     "keto_check_batch16": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _VP, _U32]),
     "keto_pack_query16": (ctypes.c_int, [_VP, _U64, _VP]),
     "keto_expand_batch": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _U64, _VP, _VP]),
+    "keto_expand_batch_spans": (ctypes.c_int, [_VP, _VP, _VP, _U64, ctypes.POINTER(Limits), _VP, _U64, _VP, _VP, _VP,
+                                               ctypes.POINTER(ctypes.c_uint64)]),
     "keto_device_alloc": (ctypes.c_int, [_I32, _U64, ctypes.POINTER(_VP)]),
     "keto_device_free": (ctypes.c_int, [_VP]),
     "keto_memcpy_h2d": (ctypes.c_int, [_VP, _VP, _VP, _U64]),

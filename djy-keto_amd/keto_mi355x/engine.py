@@ -375,6 +375,32 @@ class ExpandEngine:
             check(rc)
             return nodes[: int(offs[n])], offs, err[:n]
 
+    def build_trees_spans(self, roots: np.ndarray, out: "PinnedArray | None" = None):
+        """keto_expand_batch_spans: the same trees in completion order -> (nodes TREE_DT, first
+        uint64[n], count uint32[n], err int32[n]); root i's tree is nodes[first[i]:first[i] + count[i]].
+        With out (a PinnedArray, keto_host_alloc) the library writes each tree into it as its walk
+        ends, over PCIe, while the other roots still walk."""
+        r = np.ascontiguousarray(roots, dtype=_abi.SUBJSET_DT)
+        n = len(r)
+        first = np.zeros(max(1, n), dtype=np.uint64)
+        count = np.zeros(max(1, n), dtype=np.uint32)
+        err = np.zeros(max(1, n), dtype=np.int32)
+        total = ctypes.c_uint64(0)
+        cap = max(64, 16 * n, self._cap)
+        while True:
+            if out is not None and len(out.array) >= cap:
+                nodes, cap = out.array, len(out.array)
+            else:
+                nodes = np.empty(cap, dtype=_abi.TREE_DT)
+            rc = lib().keto_expand_batch_spans(self.snapshot.handle, self.stream.handle, r.ctypes.data, n,
+                                               ctypes.byref(self.limits), nodes.ctypes.data, cap, first.ctypes.data,
+                                               count.ctypes.data, err.ctypes.data, ctypes.byref(total))
+            if rc == _abi.KETO_E_CAPACITY:
+                cap = self._cap = int(total.value) + 1
+                continue
+            check(rc)
+            return nodes[: int(total.value)], first[:n], count[:n], err[:n]
+
     def build_tree(self, ns: int, obj: int, rel: int, rest_depth: int = 0):
         """expand.Engine.BuildTree (expand/engine.go:43-52) for one subject-set root:
         the pre-order TREE_DT nodes, or None for a nil tree."""

@@ -241,6 +241,15 @@ int keto_pack_query16(const keto_query *in, uint64_t n, keto_query16 *out);
 int keto_expand_batch(keto_snapshot *snap, keto_stream *s, const keto_subject_set *roots, uint64_t n,
                       const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap,
                       uint64_t *out_offsets, int32_t *out_err);
+/* ABI 7: keto_expand_batch with the trees in completion order instead of root order: root i's
+ * tree is out_nodes[out_first[i] .. out_first[i] + out_count[i]) (count 0: nil tree, or out_err[i]
+ * set), and *out_total = the nodes written.  Each tree is written the moment its walk ends -- into
+ * out_nodes directly, over PCIe, when it is pinned (keto_host_alloc) -- so the copy-out overlaps
+ * the other roots' walks.  If out_cap is too small returns KETO_E_CAPACITY with *out_total =
+ * required (nothing of the batch is usable then).  Same trees as keto_expand_batch. */
+int keto_expand_batch_spans(keto_snapshot *snap, keto_stream *s, const keto_subject_set *roots, uint64_t n,
+                            const keto_limits *limits, keto_tree_node *out_nodes, uint64_t out_cap,
+                            uint64_t *out_first, uint32_t *out_count, int32_t *out_err, uint64_t *out_total);
 
 /* Incremental snapshots: a device-resident tuple store of one network that applies
  * TransactRelationTuples deltas (persistence/sql/relationtuples.go:277-287: insert every row

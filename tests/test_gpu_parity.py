@@ -445,6 +445,17 @@ def test_expand_drive_trees_wave_and_fallback(stream, mode, output):
         nodes, offs, err = km.ExpandEngine(snap, stream, max_read_depth=6).build_trees(roots, out=pin)
         if pin is not None:
             assert int(offs[-1]) <= len(pin.array) and nodes.ctypes.data == pin.array.ctypes.data
+            nodes = nodes.copy()
+        # keto_expand_batch_spans: the same trees in completion order (pinned: written in place
+        # by the walks, over PCIe)
+        pin2 = km.PinnedArray(1 << 19, km.TREE_DT) if output == "pinned" else None
+        sn, first, count, serr = km.ExpandEngine(snap, stream, max_read_depth=6).build_trees_spans(roots, out=pin2)
+        np.testing.assert_array_equal(serr, err)
+        assert int(count.sum()) == len(sn) == int(offs[-1])
+        for i in range(n):
+            np.testing.assert_array_equal(sn[int(first[i]):int(first[i]) + int(count[i])], nodes[int(offs[i]):int(offs[i + 1])])
+        runs = sorted((int(first[i]), int(count[i])) for i in range(n) if count[i])
+        assert all(a + c <= b for (a, c), (b, _) in zip(runs, runs[1:]))  # disjoint runs
     finally:
         for k, v in old.items():
             if v is None:
@@ -503,6 +514,47 @@ def test_expand_pinned_output_capacity(stream):
 C1_OBJECTS = ["/cats", "/cats/1.mp4", "/cats/2.mp4"]
 C1_RELATIONS = ["owner", "view"]
 C1_SUBJECTS = ["cat lady", "*", "nobody"]
+
+
+
+def test_expand_spans_capacity(stream):
+    """keto_expand_batch_spans one node too small (pinned and pageable output): KETO_E_CAPACITY with
+    the nodes needed in *out_total; then the exact capacity: every root's run holds its tree as
+    keto_expand_batch gives it"""
+    import ctypes
+    from keto_mi355x import _abi, synth
+    wl = synth.drive(depth=4, n_groups=200, members_per_group=5, n_users=1000, seed=6)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids, strict=wl.strict)
+    eng = km.ExpandEngine(snap, stream, max_read_depth=5)
+    n = 96
+    rng = np.random.default_rng(2)
+    roots = np.zeros(n, dtype=km.SUBJSET_DT)
+    roots["ns"], roots["rel"] = wl.ns_names.index("Group"), wl.rel_names.index("members")
+    roots["obj"] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], n)
+    roots["obj"][:8] = 0  # (a few nil or tiny trees)
+    ref, ref_offs, ref_err = eng.build_trees(roots)
+    total = int(ref_offs[-1])
+    assert total > n
+    for pinned in (True, False):
+        for cap in (total - 1, total):
+            pin = km.PinnedArray(cap, km.TREE_DT) if pinned else None
+            buf = pin.array if pinned else np.zeros(cap, km.TREE_DT)
+            first, count = np.zeros(n, np.uint64), np.zeros(n, np.uint32)
+            err, tot = np.zeros(n, np.int32), ctypes.c_uint64(0)
+            rc = _abi.lib().keto_expand_batch_spans(snap.handle, stream.handle, roots.ctypes.data, n, ctypes.byref(eng.limits),
+                                                    buf.ctypes.data, cap, first.ctypes.data, count.ctypes.data,
+                                                    err.ctypes.data, ctypes.byref(tot))
+            assert tot.value == total
+            if cap < total:
+                assert rc == _abi.KETO_E_CAPACITY
+            else:
+                assert rc == 0
+                np.testing.assert_array_equal(err, ref_err)
+                for i in range(n):
+                    np.testing.assert_array_equal(buf[int(first[i]):int(first[i]) + int(count[i])],
+                                                  ref[int(ref_offs[i]):int(ref_offs[i + 1])])
+            if pin is not None:
+                pin.free()
 
 
 def c1_queries(n: int = 10_000, seed: int = 42) -> list:

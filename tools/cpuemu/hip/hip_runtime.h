@@ -59,6 +59,17 @@ inline hipError_t hipHostMalloc(void **p, size_t n, unsigned) { return hipMalloc
 inline hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
 inline hipError_t hipMemGetInfo(size_t *f, size_t *t) { *f = *t = (size_t)64 << 30; return hipSuccess; }
 inline hipError_t hipHostFree(void *p) { std::free(p); return hipSuccess; }
+// (every emulated allocation is host memory the "device" reaches: pinned-buffer paths run as on the GPU)
+enum hipMemoryType { hipMemoryTypeUnregistered = 0, hipMemoryTypeHost = 1, hipMemoryTypeDevice = 2 };
+struct hipPointerAttribute_t {
+    hipMemoryType type;
+    int device;
+    void *devicePointer, *hostPointer;
+};
+inline hipError_t hipPointerGetAttributes(hipPointerAttribute_t *a, const void *p) {
+    *a = hipPointerAttribute_t{hipMemoryTypeHost, 0, const_cast<void *>(p), const_cast<void *>(p)};
+    return hipSuccess;
+}
 inline hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) { std::memcpy(d, s, n); return hipSuccess; }
 inline hipError_t hipMemcpyToSymbol(void *sym, const void *s, size_t n, size_t off = 0, hipMemcpyKind = hipMemcpyHostToDevice) { std::memcpy(static_cast<char *>(sym) + off, s, n); return hipSuccess; }
 #define HIP_SYMBOL(x) (&(x))
