@@ -68,9 +68,12 @@ struct Slot {
     void *dq = nullptr, *da = nullptr, *de = nullptr;
     std::thread th;
 
-    // Expand: host node buffer grown on demand
-    std::vector<keto_tree_node> xnodes;
-    std::vector<uint64_t> xoffs;
+    // Expand: pinned node buffer grown on demand (keto_expand_batch_spans writes the trees into it
+    // as their walks end), each root's run and error
+    keto_tree_node *xnodes = nullptr;
+    uint64_t xcap = 0;
+    std::vector<uint64_t> xfirst;
+    std::vector<uint32_t> xcount;
     std::vector<int32_t> xerr;
 
     void run();
@@ -125,8 +128,9 @@ int Slot::launch(keto_snapshot *snap, uint64_t n, std::string &msg) {
     return rc;
 }
 
-// Expand batch for every taken request: one keto_expand_batch over all roots, then each
-// caller's trees are copied to its buffer with offsets rebased to it
+// Expand batch for every taken request: one keto_expand_batch_spans over all roots (each tree
+// lands in the pinned buffer as its walk ends), then each caller's trees are copied to its
+// buffer in its roots' order, with offsets from 0
 void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t n = 0;
@@ -136,15 +140,26 @@ void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
     std::vector<keto_subject_set> roots;
     roots.reserve(n);
     for (auto *r : take) roots.insert(roots.end(), r->roots, r->roots + r->n);
-    xoffs.assign(n + 1, 0);
+    xfirst.assign(n, 0);
+    xcount.assign(n, 0);
     xerr.assign(n, 0);
-    if (xnodes.empty()) xnodes.resize(1u << 16);
-    for (int attempt = 0; attempt < 2; attempt++) {
+    uint64_t total = 1u << 16;
+    for (int attempt = 0; attempt < 3; attempt++) {
+        if (xcap < total) {  // (first call, or the size the last attempt reported)
+            if (xnodes) (void)hipHostFree(xnodes);
+            xnodes = nullptr;
+            xcap = 0;
+            const uint64_t want = std::max<uint64_t>(total + total / 4, 1u << 16);
+            if (keto_host_alloc(want * sizeof(keto_tree_node), reinterpret_cast<void **>(&xnodes)) != KETO_OK) {
+                rc = KETO_E_DEVICE;
+                break;
+            }
+            xcap = want;
+        }
         keto_stream_expand_time(stream, nullptr, nullptr, 1);
-        rc = keto_expand_batch(snap, stream, roots.data(), n, &d->limits, xnodes.data(), xnodes.size(), xoffs.data(),
-                               xerr.data());
+        rc = keto_expand_batch_spans(snap, stream, roots.data(), n, &d->limits, xnodes, xcap, xfirst.data(), xcount.data(),
+                                     xerr.data(), &total);
         if (rc != KETO_E_CAPACITY) break;
-        xnodes.resize(xoffs[n]);  // the count pass reported the exact size
     }
     if (rc != KETO_OK) {
         char buf[512];
@@ -160,14 +175,16 @@ void Slot::run_expand(keto_snapshot *snap, std::vector<Request *> &take) {
         int rrc = rc;
         std::string rmsg = msg;
         if (rc == KETO_OK) {
-            const uint64_t base = xoffs[o], need = xoffs[o + r->n] - base;
-            for (uint64_t i = 0; i <= r->n; i++) r->offsets[i] = xoffs[o + i] - base;
+            uint64_t need = 0;
+            r->offsets[0] = 0;
+            for (uint64_t i = 0; i < r->n; i++) r->offsets[i + 1] = need += xcount[o + i];
             std::memcpy(r->err, xerr.data() + o, r->n * sizeof(int32_t));
             if (need > r->cap || (need && !r->nodes)) {
                 rrc = KETO_E_CAPACITY;
                 rmsg = "expand output needs " + std::to_string(need) + " nodes";
-            } else if (need) {
-                std::memcpy(r->nodes, xnodes.data() + base, need * sizeof(keto_tree_node));
+            } else {
+                for (uint64_t i = 0; i < r->n; i++)
+                    if (xcount[o + i]) std::memcpy(r->nodes + r->offsets[i], xnodes + xfirst[o + i], xcount[o + i] * sizeof(keto_tree_node));
             }
         }
         o += r->n;
@@ -283,6 +300,7 @@ void release_slot(Slot *x) {
     if (x->hq) (void)hipHostFree(x->hq);
     if (x->ha) (void)hipHostFree(x->ha);
     if (x->he) (void)hipHostFree(x->he);
+    if (x->xnodes) (void)hipHostFree(x->xnodes);
     if (x->dq) (void)hipFree(x->dq);
     if (x->da) (void)hipFree(x->da);
     if (x->de) (void)hipFree(x->de);
