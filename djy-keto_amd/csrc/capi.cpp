@@ -45,6 +45,17 @@ void grow(void *&p, size_t &cap, size_t need) {
 }  // namespace
 
 namespace keto {
+void Stream::flush_d2h() {
+    if (!pend.on) return;
+    pend.on = false;
+    Slot &sl = slot[pend.slot];
+    const char *o = static_cast<const char *>(pend.src);
+    KETO_HIP(hipStreamWaitEvent(h2d, sl.out, 0));
+    KETO_HIP(hipMemcpyAsync(pend.allowed, o, pend.n, hipMemcpyDeviceToHost, h2d));
+    KETO_HIP(hipMemcpyAsync(pend.err, o + ((pend.n + 63) / 64) * 64, pend.n * sizeof(int32_t), hipMemcpyDeviceToHost, h2d));
+    KETO_HIP(hipEventRecord(sl.free, h2d));
+}
+
 Stream::~Stream() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (check_scratch.mem) (void)hipFree(check_scratch.mem);
@@ -224,8 +235,10 @@ int keto_stream_sync(keto_stream *hs) {
     if (!s) return fail(KETO_E_INVALID, "null stream");
     return guarded([&] {
         KETO_HIP(hipSetDevice(s->device));
+        s->flush_d2h();  // (an asynchronous batch's last copy)
         KETO_HIP(hipStreamSynchronize(s->stream));
-        if (s->d2h) KETO_HIP(hipStreamSynchronize(s->d2h));  // (an asynchronous batch's last copy)
+        if (s->h2d) KETO_HIP(hipStreamSynchronize(s->h2d));
+        if (s->d2h) KETO_HIP(hipStreamSynchronize(s->d2h));
         s->harvest();
     });
 }
@@ -322,6 +335,7 @@ static int check_batch(keto_snapshot *hsnap, keto_stream *hs, const void *querie
         L.budget = s->fr_budget;
         L.async = (flags & KETO_F_ASYNC) != 0 && !L.count;
         L.q16 = rec == sizeof(keto_query16);
+        if (!(flags & KETO_F_ASYNC) || (flags & KETO_F_DEVICE_PTRS)) s->flush_d2h();  // (an earlier async batch's copy first)
         if (flags & KETO_F_DEVICE_PTRS) {
             L.queries = queries;
             L.out_allowed = out_allowed;
@@ -344,9 +358,14 @@ static int check_batch(keto_snapshot *hsnap, keto_stream *hs, const void *querie
                 KETO_HIP(hipStreamCreateWithFlags(&s->d2h, hipStreamNonBlocking));
                 for (auto &sl : s->slot)
                     for (hipEvent_t *e : {&sl.in, &sl.out, &sl.free}) KETO_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+                const char *cs = getenv("KETO_COPY_STREAMS");
+                s->one_copy = !(cs && cs[0] == '2');
             }
-            keto::Stream::Slot &sl = s->slot[s->slot_seq++ & 1];
+            const uint32_t si = (uint32_t)(s->slot_seq++ & 1);
+            keto::Stream::Slot &sl = s->slot[si];
             if (sl.qb < qb || sl.ob < ob + 64) {  // (growing a slot: wait until its last batch is done)
+                s->flush_d2h();
+                KETO_HIP(hipStreamSynchronize(s->h2d));
                 KETO_HIP(hipStreamSynchronize(s->d2h));
                 grow(sl.q, sl.qb, std::max<size_t>(qb, 64));
                 grow(sl.o, sl.ob, std::max<size_t>(ob + 64, 64));
@@ -356,12 +375,17 @@ static int check_batch(keto_snapshot *hsnap, keto_stream *hs, const void *querie
             KETO_HIP(hipStreamWaitEvent(s->h2d, sl.free, 0));
             KETO_HIP(hipMemcpyAsync(sl.q, queries, qb, hipMemcpyHostToDevice, s->h2d));
             KETO_HIP(hipEventRecord(sl.in, s->h2d));
+            s->flush_d2h();  // (one copy stream: the previous batch's D2H behind this H2D)
             KETO_HIP(hipStreamWaitEvent(s->stream, sl.in, 0));
             L.queries = sl.q;
             L.out_allowed = d_allowed;
             L.out_err = d_err;
             keto::run_check(*snap, *s, L);
             KETO_HIP(hipEventRecord(sl.out, s->stream));
+            if (s->one_copy) {  // enqueued by the next batch, or keto_stream_sync
+                s->pend = keto::Stream::PendingD2H{true, out_allowed, out_err, sl.o, n, si};
+                return;
+            }
             KETO_HIP(hipStreamWaitEvent(s->d2h, sl.out, 0));
             KETO_HIP(hipMemcpyAsync(out_allowed, d_allowed, n, hipMemcpyDeviceToHost, s->d2h));
             KETO_HIP(hipMemcpyAsync(out_err, d_err, n * sizeof(int32_t), hipMemcpyDeviceToHost, s->d2h));

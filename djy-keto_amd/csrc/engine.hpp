@@ -296,6 +296,20 @@ struct Stream {
         hipEvent_t in = nullptr, out = nullptr, free = nullptr;
     } slot[2];
     uint64_t slot_seq = 0;
+    // One copy stream (default; KETO_COPY_STREAMS=2: the two above): batch k's D2H is enqueued
+    // behind batch k+1's H2D -- or by keto_stream_sync -- on the h2d stream, so the two directions
+    // never run at once.  Concurrent H2D + D2H moved 17 GB/s together on the box, against 54-55 GB/s
+    // for either alone (tools/pcie_probe.py, round 6).
+    bool one_copy = true;
+    struct PendingD2H {
+        bool on = false;
+        uint8_t *allowed = nullptr;
+        int32_t *err = nullptr;
+        const void *src = nullptr;  // the slot's outputs: n decisions, then (64-aligned) n errors
+        uint64_t n = 0;
+        uint32_t slot = 0;
+    } pend;
+    void flush_d2h();  // (capi.cpp) enqueue the pending D2H, if any
     unsigned long long *counters = nullptr;  // device [3 tiers][8]
     keto_work_counters host_counters{};
     double last_kernel_ms = 0;
