@@ -68,3 +68,36 @@ def test_check_batch16_equals_check_batch():
     np.testing.assert_array_equal(pa.array, a32)
     np.testing.assert_array_equal(pe.array & 0xFF, e32 & 0xFF)
     snap.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("copy_streams", ["1", "2"])
+def test_async_batches_interleaved_with_synchronous_ones(monkeypatch, copy_streams):
+    """KETO_F_ASYNC host batches on one copy stream (default: each batch's D2H enqueued behind the
+    next batch's H2D, or by keto_stream_sync) and on two (KETO_COPY_STREAMS=2): five async batches
+    of different sizes in a row, a synchronous batch on the same stream between them, then one
+    sync -- every batch's outputs equal its synchronous answers (no D2H lost, none written into
+    another batch's buffers)"""
+    monkeypatch.setenv("KETO_COPY_STREAMS", copy_streams)
+    wl = synth.drive(depth=5, n_groups=800, n_users=5000, seed=23)
+    snap = km.Snapshot(wl.namespaces, wl.tuples, wl.ns_names, wl.rel_names, wl.n_uuids)
+    eng = km.CheckEngine(snap, km.Stream(0), max_read_depth=wl.max_depth, max_read_width=wl.max_width)
+    sizes = [30_000, 4_096, 77_000, 1, 12_345]
+    qs = [synth.drive_queries(wl, n, seed=40 + k) for k, n in enumerate(sizes)]
+    ref = [eng.check_batch(q) for q in qs]
+    pins = []
+    for k, q in enumerate(qs):
+        pq = km.PinnedArray(len(q), km.QUERY16_DT)
+        pq.array[:] = km.pack_queries16(q)
+        pa, pe = km.PinnedArray(len(q), np.uint8), km.PinnedArray(len(q), np.int32)
+        pa.array[:] = 0xEE
+        pins.append((pq, pa, pe))
+        eng.check_batch_async(pq.array, pa.array, pe.array)
+        if k == 2:  # a synchronous batch on the same stream, between async ones
+            a, e = eng.check_batch(qs[0])
+            np.testing.assert_array_equal(a, ref[0][0])
+    eng.stream.sync()
+    for (pq, pa, pe), (a, e) in zip(pins, ref):
+        np.testing.assert_array_equal(pa.array, a)
+        np.testing.assert_array_equal(pe.array, e)
+    snap.close()
