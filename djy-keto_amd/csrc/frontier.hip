@@ -366,7 +366,7 @@ uint32_t run_frontier(const Snapshot &s, Stream &st, const CheckLaunch &L, uint6
     f.stats.goals += top;
     f.stats.generations += gens;
     f.stats.max_generations = std::max<uint64_t>(f.stats.max_generations, gens);
-#ifdef KETO_FR_KINDSTAT
+#if defined(KETO_FR_KINDSTAT) || defined(KETO_FR_LVSTAT)
     {
         unsigned long long ks[64 * 8];
         KETO_HIP(hipMemcpyFromSymbol(ks, HIP_SYMBOL(g_kstat), sizeof ks));
