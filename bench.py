@@ -537,11 +537,12 @@ def run_c5(args, rank, world, device, dist_on):
     eng, n_part = None, 0
     for r in range(world if (dist_on and shared) else 1):
         if not (dist_on and shared) or r == rank:
-            part = synth.drive_partition(wl, world, rank)
+            place = synth.drive_placement(wl) if args.placement == "tree" else None
+            part = synth.drive_partition(wl, world, rank, placement=place)
             n_part = len(part)
             eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
                                               device=device, max_read_depth=wl.max_depth,
-                                              max_read_width=wl.max_width, collective=coll)
+                                              max_read_width=wl.max_width, collective=coll, placement=place)
             del part
         if dist_on and shared:
             import torch.distributed as dist
@@ -624,7 +625,7 @@ def run_c5(args, rank, world, device, dist_on):
         "data": "synthetic (seeded Drive-style folder forest, BASELINE config 5; generated per partition)",
         "config": {"workload": f"C5 Drive-style x{args.scale}: {wl.meta['n_tuples']} tuples partitioned by "
                                f"object over {world} rank(s), {args.batch} checks/batch/GPU, {how}",
-                   "tuples": int(wl.meta["n_tuples"]), "batch_per_gpu": args.batch,
+                   "tuples": int(wl.meta["n_tuples"]), "batch_per_gpu": args.batch, "placement": args.placement,
                    "parallelism": f"object partition x{world} (" + ("RCCL all-to-all of goal records per generation" if distributed
                                                                       else "RCCL all-to-all closure exchange per level") + ")"},
         "allowed_fraction": float(allowed.mean()),
@@ -779,6 +780,8 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c4")
     ap.add_argument("--scale", type=int, default=40, help="C5 graph = C3 x scale (40: ~4.2B tuples)")
+    ap.add_argument("--placement", choices=["hash", "tree"], default="hash",
+                    help="C5 owner rule: keto_object_owner's hash, or every root folder tree on one rank (keto_placement)")
     ap.add_argument("--tuples", type=int, default=10_000_000, help="C2 graph size")
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--engine-streams", type=int, default=int(os.environ.get("KETO_BENCH_STREAMS", "1")),

@@ -200,10 +200,10 @@ __global__ __launch_bounds__(BLK) void k_validate(const keto_tuple *t, uint64_t 
 // an entity of the ghost namespace n_ns + s_ns (keto_object_owner)
 struct Ghosts {
     uint32_t n_ns, rank, world;
+    Placement pl;
     __device__ __forceinline__ uint32_t ns_of_set(uint32_t s_ns, uint32_t s_obj) const {
         if (world <= 1) return s_ns;
-        const uint64_t h = ((((uint64_t)s_ns) << 32) | s_obj) * 0x9E3779B97F4A7C15ull;
-        return (uint32_t)((h >> 32) % world) == rank ? s_ns : n_ns + s_ns;
+        return place_owner(pl, s_ns, s_obj, world) == rank ? s_ns : n_ns + s_ns;
     }
 };
 __global__ __launch_bounds__(BLK) void k_entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride,
@@ -544,8 +544,8 @@ void validate(const keto_tuple *t, uint64_t n, uint32_t n_ns, uint32_t n_rel_cal
 }
 
 void entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride, unsigned long long *bits, uint64_t nblk,
-                 uint32_t *rank, uint32_t n_ns, uint32_t part_rank, uint32_t part_world) {
-    hipLaunchKernelGGL(k_entity_bits, grid_for(n), dim3(BLK), 0, 0, t, n, stride, bits, Ghosts{n_ns, part_rank, part_world});
+                 uint32_t *rank, uint32_t n_ns, uint32_t part_rank, uint32_t part_world, const Placement &place) {
+    hipLaunchKernelGGL(k_entity_bits, grid_for(n), dim3(BLK), 0, 0, t, n, stride, bits, Ghosts{n_ns, part_rank, part_world, place});
     hipLaunchKernelGGL(k_popc, grid_for(nblk), dim3(BLK), 0, 0, bits, nblk, rank);
     KETO_HIP(hipGetLastError());
     scan_excl(rank, nblk);
@@ -570,7 +570,7 @@ void rows(const RowsIn &in, RowsOut &out) {
         fprintf(stderr, "[keto build]   rows/%-12s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
         tp = now;
     };
-    NodeMap map{in.bits, in.rank, in.ns, in.slot_of, in.stride, in.n_rel, in.n_uuids, Ghosts{in.n_ns, in.part_rank, in.part_world}};
+    NodeMap map{in.bits, in.rank, in.ns, in.slot_of, in.stride, in.n_rel, in.n_uuids, Ghosts{in.n_ns, in.part_rank, in.part_world, in.place}};
     DevBuf src(4 * n), dst(4 * n), skey(8 * n);
     KETO_HIP(hipMemset(out.all_off, 0, 4 * (N + 1)));
     KETO_HIP(hipMemset(out.rev_off, 0, 4 * (M + 1)));

@@ -580,14 +580,23 @@ int keto_dispatcher_stats_get(keto_dispatcher *d, keto_dispatcher_stats *out) {
     return guarded([&] { keto::dispatcher_stats(d, out); });
 }
 
-int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
-                          const keto_collective *coll, const keto_limits *limits, keto_partition **out) {
+int keto_partition_create_placed(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
+                                 const keto_collective *coll, const keto_limits *limits, const keto_placement *placement,
+                                 keto_partition **out) {
     if (!out) return fail(KETO_E_INVALID, "null output pointer");
     *out = nullptr;
     return guarded([&] {
-        *out = reinterpret_cast<keto_partition *>(
-            keto::partition_create(cfg, tuples, n, (flags & KETO_F_DEVICE_PTRS) != 0, coll, limits, (flags & KETO_F_PART_DIST) != 0));
+        keto::Placement pl{};
+        if (placement)
+            for (uint32_t i = 0; i < keto::PLACE_NS; i++) pl.block[i] = placement->block[i];
+        *out = reinterpret_cast<keto_partition *>(keto::partition_create(cfg, tuples, n, (flags & KETO_F_DEVICE_PTRS) != 0, coll,
+                                                                         limits, (flags & KETO_F_PART_DIST) != 0, pl));
     });
+}
+
+int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
+                          const keto_collective *coll, const keto_limits *limits, keto_partition **out) {
+    return keto_partition_create_placed(cfg, tuples, n, flags, coll, limits, nullptr, out);
 }
 
 int keto_partition_check(keto_partition *p, const keto_query *queries, uint64_t n, uint8_t *out_allowed,

@@ -47,6 +47,7 @@ struct BuildOpts {
     // rank `part_rank` of a job of part_world > 1 ranks: subject-set objects another rank owns
     // (keto_object_owner) are entities of ghost namespaces -- every row array stops at them
     uint32_t part_rank = 0, part_world = 1;
+    Placement place{};  // (which objects are this rank's: keto_placement; zeros: the hash)
 };
 
 // Host mirror of the snapshot + its device buffers.
@@ -153,7 +154,8 @@ uint32_t read_u32(const uint32_t *d, uint64_t i);
 void validate(const keto_tuple *t, uint64_t n, uint32_t n_ns, uint32_t n_rel_caller, uint32_t n_uuids, uint32_t n_rel,
               uint32_t *used, unsigned long long *bad);
 void entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride, unsigned long long *bits, uint64_t nblk,
-                 uint32_t *rank, uint32_t n_ns = 0, uint32_t part_rank = 0, uint32_t part_world = 1);
+                 uint32_t *rank, uint32_t n_ns = 0, uint32_t part_rank = 0, uint32_t part_world = 1,
+                 const Placement &place = Placement{});
 void entity_ids(const unsigned long long *bits, uint32_t *rank, uint64_t nblk, uint64_t bpn, uint64_t stride,
                 const uint32_t *ent_base, const uint32_t *rank0, uint32_t *ent_obj, uint4 *table);
 struct RowsIn {
@@ -168,6 +170,7 @@ struct RowsIn {
     uint32_t n_rel, n_uuids;
     bool weights = true;            // scheduling weights (false: all 1, e.g. per-batch closure snapshots)
     uint32_t n_ns = 0, part_rank = 0, part_world = 1;  // (ghost namespaces: BuildOpts::part_world > 1)
+    Placement place{};
 };
 struct RowsOut {
     uint32_t *all_off, *rev_off, *all_subj, *rev_nodes, *weight;  // caller-allocated
@@ -453,7 +456,7 @@ void sum_u32(const uint32_t *v, uint64_t n, unsigned long long *out, hipStream_t
 struct PartitionHandle;
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
                                   bool device_ptrs, const keto_collective *coll, const keto_limits *limits,
-                                  bool force_dist = false);
+                                  bool force_dist = false, const Placement &place = Placement{});
 void partition_check(PartitionHandle *p, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, uint32_t flags);
 void partition_check_many(PartitionHandle *p, uint32_t nb, const keto_query *const *q, const uint64_t *n,
                           uint8_t *const *allowed, int32_t *const *err, uint32_t flags);

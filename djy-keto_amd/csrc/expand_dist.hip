@@ -42,10 +42,8 @@ __device__ __forceinline__ uint64_t xstride() { return (uint64_t)gridDim.x * blo
 __host__ __device__ __forceinline__ uint64_t nkey(uint32_t ns, uint32_t obj, uint32_t rel) {
     return ((uint64_t)(std::min(ns, 0x7FFFu) | (std::min(rel, 0xFFFFu) << 15)) << 32) | obj;
 }
-__device__ __forceinline__ uint32_t key_owner(uint64_t k, uint32_t world) {
-    const uint32_t ns = (uint32_t)(k >> 32) & 0x7FFFu, obj = (uint32_t)k;
-    const uint64_t h = ((((uint64_t)ns) << 32) | obj) * 0x9E3779B97F4A7C15ull;  // keto_object_owner
-    return (uint32_t)((h >> 32) % world);
+__device__ __forceinline__ uint32_t key_owner(uint64_t k, const Dest &D) {  // keto_object_owner / keto_placement
+    return D.owner((uint32_t)(k >> 32) & 0x7FFFu, (uint32_t)k);
 }
 // a row entry: {object or subject id, 1 << 31 | ns | rel << 15 for a subject set, else 0}
 constexpr uint32_t XE_SET = 1u << 31;
@@ -53,11 +51,11 @@ constexpr uint32_t XE_SET = 1u << 31;
 // ---- 1. fetching rows
 
 // keys per owner, then grouped by owner (order within an owner free)
-__global__ __launch_bounds__(XB) void kx_hist(const uint64_t *k, uint32_t n, uint32_t world, uint32_t *hist) {
-    for (uint64_t i = xgid(); i < n; i += xstride()) atomicAdd(&hist[key_owner(k[i], world)], 1u);
+__global__ __launch_bounds__(XB) void kx_hist(const uint64_t *k, uint32_t n, Dest D, uint32_t *hist) {
+    for (uint64_t i = xgid(); i < n; i += xstride()) atomicAdd(&hist[key_owner(k[i], D)], 1u);
 }
-__global__ __launch_bounds__(XB) void kx_scatter(const uint64_t *k, uint32_t n, uint32_t world, uint32_t *cur, uint64_t *out) {
-    for (uint64_t i = xgid(); i < n; i += xstride()) out[atomicAdd(&cur[key_owner(k[i], world)], 1u)] = k[i];
+__global__ __launch_bounds__(XB) void kx_scatter(const uint64_t *k, uint32_t n, Dest D, uint32_t *cur, uint64_t *out) {
+    for (uint64_t i = xgid(); i < n; i += xstride()) out[atomicAdd(&cur[key_owner(k[i], D)], 1u)] = k[i];
 }
 // owner side: the Expand row of a requested node (its object is this rank's): every tuple of it
 __device__ __forceinline__ void row_of(const DevSnapshot &s, const Tables &T, uint64_t k, uint32_t &b, uint32_t &e) {
@@ -379,7 +377,7 @@ void dist_expand(DistEngine &E, const keto_subject_set *roots, uint64_t n, std::
         hist.need((size_t)W * 4 + 16, s);
         uint32_t *h = hist.as<uint32_t>();
         KETO_HIP(hipMemsetAsync(h, 0, (size_t)W * 4, s));
-        if (ncur) hipLaunchKernelGGL(kx_hist, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, W, h);
+        if (ncur) hipLaunchKernelGGL(kx_hist, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, Dest{W, V.place}, h);
         std::vector<uint32_t> cnt(W);
         KETO_HIP(hipMemcpyAsync(cnt.data(), h, (size_t)W * 4, hipMemcpyDeviceToHost, s));
         KETO_HIP(hipStreamSynchronize(s));
@@ -404,7 +402,7 @@ void dist_expand(DistEngine &E, const keto_subject_set *roots, uint64_t n, std::
             std::vector<uint32_t> cu(W, 0);
             for (uint32_t r = 1; r < W; r++) cu[r] = cu[r - 1] + cnt[r - 1];
             KETO_HIP(hipMemcpyAsync(h, cu.data(), (size_t)W * 4, hipMemcpyHostToDevice, s));
-            hipLaunchKernelGGL(kx_scatter, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, W, h, sendk.as<uint64_t>());
+            hipLaunchKernelGGL(kx_scatter, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, Dest{W, V.place}, h, sendk.as<uint64_t>());
         }
         std::vector<uint64_t> sb(W), rb(W);
         for (uint32_t r = 0; r < W; r++) {

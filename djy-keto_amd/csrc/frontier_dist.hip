@@ -82,11 +82,8 @@ inline dim3 dgrid(uint64_t n, uint64_t cap = 1u << 16) {
 }
 __device__ __forceinline__ uint64_t dgid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t dstride() { return (uint64_t)gridDim.x * blockDim.x; }
-__device__ __forceinline__ uint32_t owner(uint32_t ns, uint32_t obj, uint32_t world) {
-    const uint64_t h = ((((uint64_t)ns) << 32) | obj) * 0x9E3779B97F4A7C15ull;  // keto_object_owner
-    return (uint32_t)((h >> 32) % world);
-}
-__device__ __forceinline__ uint32_t rec_owner(const uint4 &r0, uint32_t world) { return owner(r0.y & 0x7FFFu, r0.x, world); }
+// a record's destination: its node's owner (keto_object_owner, or the job's keto_placement)
+__device__ __forceinline__ uint32_t rec_owner(const uint4 &r0, const Dest &D) { return D.owner(r0.y & 0x7FFFu, r0.x); }
 
 // ------------------------------------------------------------------------------ kernels
 
@@ -116,21 +113,23 @@ __global__ __launch_bounds__(DBLK) void k_subjects(const uint4 *rec, uint32_t n,
 
 // records per destination rank (word 0: a null record, never sent); a block's counts in LDS
 constexpr uint32_t LDS_W = 2048;  // DIST_MAX_WORLD
-__global__ __launch_bounds__(DBLK) void k_dest_count(const uint4 *rec, uint32_t n, uint32_t world, uint32_t *hist) {
+__global__ __launch_bounds__(DBLK) void k_dest_count(const uint4 *rec, uint32_t n, Dest D, uint32_t *hist) {
     __shared__ uint32_t h[LDS_W];
+    const uint32_t world = D.world;
     for (uint32_t t = threadIdx.x; t < world; t += blockDim.x) h[t] = 0;
     __syncthreads();
     for (uint64_t i = dgid(); i < n; i += dstride())
-        if (rec[2 * i + 1].x) atomicAdd(&h[rec_owner(rec[2 * i], world)], 1u);
+        if (rec[2 * i + 1].x) atomicAdd(&h[rec_owner(rec[2 * i], D)], 1u);
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < world; t += blockDim.x)
         if (h[t]) atomicAdd(&hist[t], h[t]);
 }
 // records grouped by destination (cursor[r] = r's first slot, advanced); the sender's proxy of
 // each sent record, in send order, for the returns
-__global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_t n, uint32_t world, uint32_t *cursor,
+__global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_t n, Dest D, uint32_t *cursor,
                                                        uint32_t *out, uint32_t *sent_px) {
     __shared__ uint32_t h[LDS_W], base[LDS_W];
+    const uint32_t world = D.world;
     for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += dstride()) {
         for (uint32_t t = threadIdx.x; t < world; t += blockDim.x) h[t] = 0;
         __syncthreads();
@@ -140,7 +139,7 @@ __global__ __launch_bounds__(DBLK) void k_dest_scatter(const uint4 *rec, uint32_
         const bool live = i < n && (r1 = rec[2 * i + 1]).x != 0;
         if (live) {
             r0 = rec[2 * i];
-            dst = rec_owner(r0, world);
+            dst = rec_owner(r0, D);
             at = atomicAdd(&h[dst], 1u);
         }
         __syncthreads();
@@ -399,6 +398,7 @@ struct Level {  // one generation's exchange (records that arrive as goals of th
 struct DistEngine {
     int device = 0;
     uint32_t rank = 0, world = 1;
+    Placement place{};  // which objects each rank owns (keto_placement; zeros: the hash)
     keto_collective coll{};
     keto_limits limits{5, 100};
     std::unique_ptr<Snapshot> snap;
@@ -510,9 +510,10 @@ void agree_flags(DistEngine &D) {
 }  // namespace
 
 DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_ptrs,
-                        const keto_collective &coll, const keto_limits &limits) {
+                        const keto_collective &coll, const keto_limits &limits, const Placement &place) {
     auto E = std::make_unique<DistEngine>();
     E->device = cfg->device;
+    E->place = place;
     E->coll = coll;
     E->rank = (uint32_t)coll.rank;
     E->world = (uint32_t)coll.world;
@@ -532,6 +533,7 @@ DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuple
     o.no_weights = true;
     o.part_rank = E->rank;  // ghost namespaces for other ranks' subject sets
     o.part_world = E->world;
+    o.place = E->place;
     // KETO_PART_STAGED (ranks that share one device and so create their partitions one after
     // another, tests/test_gpu_c5.py): no collective here -- each rank lays out the slots its own
     // tuples use, and the first batch checks that every rank's layout is the same (an error
@@ -576,7 +578,7 @@ DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuple
 void dist_free(DistEngine *E) { delete E; }
 DistView dist_view(DistEngine &E) {
     if (!E.agreed) agree_flags(E);  // (collective: every dist_view caller is)
-    return DistView{E.device, E.rank, E.world, &E.coll, E.hs, E.snap.get(), E.limits};
+    return DistView{E.device, E.rank, E.world, &E.coll, E.hs, E.snap.get(), E.limits, E.place};
 }
 std::vector<uint64_t> dist_alltoall(const DistView &V, const std::vector<uint64_t> &send, double &wait_s) {
     std::vector<uint64_t> recv(V.world, 0);
@@ -729,7 +731,7 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
     E.dsend.reserve((size_t)W * 8 + 64, 0, s);
     uint32_t *h = E.dsend.as<uint32_t>();
     KETO_HIP(hipMemsetAsync(h, 0, (size_t)W * 4, s));
-    if (n) hipLaunchKernelGGL(k_dest_count, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, W, h);
+    if (n) hipLaunchKernelGGL(k_dest_count, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, Dest{W, E.place}, h);
     KETO_HIP(hipGetLastError());
     std::vector<uint32_t> cnt(W);
     KETO_HIP(hipMemcpyAsync(cnt.data(), h, (size_t)W * 4, hipMemcpyDeviceToHost, s));
@@ -746,7 +748,7 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
         std::vector<uint32_t> cur(W, 0);
         for (uint32_t r = 1; r < W; r++) cur[r] = cur[r - 1] + cnt[r - 1];
         KETO_HIP(hipMemcpyAsync(h, cur.data(), (size_t)W * 4, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_dest_scatter, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, W, h, E.sbuf.as<uint32_t>(),
+        hipLaunchKernelGGL(k_dest_scatter, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, Dest{W, E.place}, h, E.sbuf.as<uint32_t>(),
                            E.sent_px.as<uint32_t>() + L.sent_off);
         KETO_HIP(hipGetLastError());
     }

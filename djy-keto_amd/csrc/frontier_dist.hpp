@@ -12,10 +12,11 @@ struct DistStats {
     uint64_t generations = 0, goals = 0, positions = 0, routed = 0, records_sent = 0, bytes_exchanged = 0, decisive = 0;
     double device_s = 0, exchange_s = 0, wall_s = 0;
 };
-// this rank's partition (the tuples keto_object_owner gives it) as a resident snapshot whose node
-// arithmetic, relation flags and uuid ids agree with every other rank's (collective)
+// this rank's partition (the tuples keto_object_owner -- or the job's placement -- gives it) as a
+// resident snapshot whose node arithmetic, relation flags and uuid ids agree with every other
+// rank's (collective)
 DistEngine *dist_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_ptrs,
-                        const keto_collective &coll, const keto_limits &limits);
+                        const keto_collective &coll, const keto_limits &limits, const Placement &place);
 // collective: this rank's n queries (host) -> decisions (host); `routed` = the queries the
 // caller's exact path must answer (their outputs here are placeholders)
 void dist_check(DistEngine &E, const keto_query *q, uint64_t n, uint8_t *allowed, int32_t *err, bool err_detail,
@@ -34,6 +35,7 @@ struct DistView {
     hipStream_t hs;
     const Snapshot *snap;
     keto_limits limits;
+    Placement place;
 };
 DistView dist_view(DistEngine &E);
 // the collective (all ranks call in the same order): one u64 per rank; all-to-all-v of device

@@ -63,9 +63,9 @@ inline dim3 grid_for(uint64_t n) {
 __device__ __forceinline__ uint64_t gid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
 __device__ __forceinline__ uint64_t okey(uint32_t ns, uint32_t obj) { return ((uint64_t)ns << 32) | obj; }
-// keto_object_owner (include/keto_mi355x.h) on the device: the same hash of (ns << 32 | obj)
-__host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
-    return (uint32_t)(((key * 0x9E3779B97F4A7C15ull) >> 32) % world);
+// keto_object_owner (include/keto_mi355x.h) on the device -- or the job's keto_placement
+__host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, const Dest &D) {
+    return D.owner((uint32_t)(key >> 32), (uint32_t)key);
 }
 
 // ------------------------------------------------------------------ kernels
@@ -223,13 +223,12 @@ __global__ __launch_bounds__(BLK) void k_rehash(const uint64_t *keys, uint64_t n
     }
 }
 // routing: destination histogram, then a counting scatter (order within a destination is free)
-__global__ __launch_bounds__(BLK) void k_dest_hist(const uint64_t *keys, uint64_t n, uint32_t world,
-                                                    unsigned long long *hist) {
-    for (uint64_t i = gid(); i < n; i += gstride()) atomicAdd(&hist[owner_of(keys[i], world)], 1ull);
+__global__ __launch_bounds__(BLK) void k_dest_hist(const uint64_t *keys, uint64_t n, Dest D, unsigned long long *hist) {
+    for (uint64_t i = gid(); i < n; i += gstride()) atomicAdd(&hist[owner_of(keys[i], D)], 1ull);
 }
-__global__ __launch_bounds__(BLK) void k_dest_scatter(const uint64_t *keys, uint64_t n, uint32_t world,
-                                                       unsigned long long *cursor, uint64_t *out) {
-    for (uint64_t i = gid(); i < n; i += gstride()) out[atomicAdd(&cursor[owner_of(keys[i], world)], 1ull)] = keys[i];
+__global__ __launch_bounds__(BLK) void k_dest_scatter(const uint64_t *keys, uint64_t n, Dest D, unsigned long long *cursor,
+                                                       uint64_t *out) {
+    for (uint64_t i = gid(); i < n; i += gstride()) out[atomicAdd(&cursor[owner_of(keys[i], D)], 1ull)] = keys[i];
 }
 // object-key index of the partition: open addressing, {key lo, key hi, run, 0} per slot
 __global__ __launch_bounds__(BLK) void k_index_fill(const uint64_t *ukeys, uint64_t m, uint4 *slots, uint64_t mask) {
@@ -619,6 +618,7 @@ struct Partition {
     bool have_coll = false;
     keto_collective coll{};
     uint32_t rank = 0, world = 1;
+    Placement place{};  // which objects each rank owns (keto_placement; zeros: keto_object_owner's hash)
     keto_limits limits{5, 100};
     // snapshot configuration for the per-batch closure builds
     std::vector<std::string> ns_names, rel_names;
@@ -950,8 +950,8 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             ensure(hist, W * 8);
             KETO_HIP(hipMemsetAsync(hist.p, 0, W * 8, P.hs));
             if (n_new)
-                hipLaunchKernelGGL(k_dest_hist, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new, W,
-                                   dptr<unsigned long long>(hist));
+                hipLaunchKernelGGL(k_dest_hist, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new,
+                                   Dest{W, P.place}, dptr<unsigned long long>(hist));
             KETO_HIP(hipMemcpyAsync(send.data(), hist.p, W * 8, hipMemcpyDeviceToHost, P.hs));
             sync(P);
             std::vector<uint64_t> cur(W, 0);
@@ -959,7 +959,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             KETO_HIP(hipMemcpyAsync(hist.p, cur.data(), W * 8, hipMemcpyHostToDevice, P.hs));
             if (n_new)
                 hipLaunchKernelGGL(k_dest_scatter, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new,
-                                   W, dptr<unsigned long long>(hist), dptr<uint64_t>(P.routed));
+                                   Dest{W, P.place}, dptr<unsigned long long>(hist), dptr<uint64_t>(P.routed));
         }
         std::vector<uint64_t> from = exchange(P, P.routed.p, send, 8, P.req, st.bytes_sent);
         lv_req = st.bytes_sent - lv_b0;
@@ -1066,7 +1066,8 @@ double secs(std::chrono::steady_clock::time_point a) {
 struct PartitionHandle : Partition {};
 
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n,
-                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits, bool force_dist) {
+                                  bool device_ptrs, const keto_collective *coll, const keto_limits *limits, bool force_dist,
+                                  const Placement &place) {
     if (!cfg) throw Error(KETO_E_INVALID, "null config");
     if (n && !tuples) throw Error(KETO_E_INVALID, "null tuples");
     if (n >= (1ull << 31)) throw Error(KETO_E_LIMIT, "a partition holds at most 2^31 - 1 tuples");
@@ -1074,6 +1075,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
         throw Error(KETO_E_LIMIT, "a partitioned snapshot holds at most 1024 relation names and 2048 namespaces");
     auto P = std::make_unique<PartitionHandle>();
     P->device = cfg->device;
+    P->place = place;
     KETO_HIP(hipSetDevice(P->device));
     if (coll) {
         if (coll->world < 1 || (uint32_t)coll->world > MAX_WORLD || coll->rank < 0 || coll->rank >= coll->world)
@@ -1109,7 +1111,7 @@ PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tu
     if ((P->world > 1 || force_dist) && !getenv("KETO_PART_CLOSURE")) {
         // several ranks (or KETO_F_PART_DIST): the partition resident, the distributed frontier over it
         auto t0 = std::chrono::steady_clock::now();
-        P->dist = dist_create(&P->cfg, tuples, n, device_ptrs, P->coll, P->limits);
+        P->dist = dist_create(&P->cfg, tuples, n, device_ptrs, P->coll, P->limits, P->place);
         if (P->verbose)
             fprintf(stderr, "[keto partition] rank %u: %llu tuples as a resident partition, %.2f s\n", P->rank,
                     (unsigned long long)n, secs(t0));

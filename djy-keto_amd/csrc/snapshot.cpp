@@ -393,7 +393,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
     DevBuf d_bits(8 * nblk), d_rank(4 * (nblk + 1));
     KETO_HIP(hipMemset(d_bits.p, 0, 8 * nblk));
     build::entity_bits(dt, n, stride, static_cast<unsigned long long *>(d_bits.p), nblk, d_rank.u32(), s.n_ns,
-                       ghosts ? opts->part_rank : 0, ghosts ? opts->part_world : 1);
+                       ghosts ? opts->part_rank : 0, ghosts ? opts->part_world : 1, ghosts ? opts->place : Placement{});
     std::vector<uint32_t> n_real(NX, 0), rank0(NX + 1);
     for (uint32_t ns = 0; ns <= NX; ns++) rank0[ns] = build::read_u32(d_rank.u32(), ns * bpn);
     uint64_t ent_total = 0, node_total = 0;
@@ -501,6 +501,7 @@ Snapshot *build_snapshot(const keto_snapshot_config *cfg, const keto_tuple *tupl
         ri.n_ns = s.n_ns;
         ri.part_rank = ghosts ? opts->part_rank : 0;
         ri.part_world = ghosts ? opts->part_world : 1;
+        if (ghosts) ri.place = opts->place;
         build::rows(ri, ro);
         if (total_slots) {
             DevBuf flag(4ull * total_slots);

@@ -168,8 +168,15 @@ int ks_drive_tuples(const ks_drive_params *pp, keto_tuple *out, uint64_t n, int 
 // once per object and only the partition's own tuples are generated (every rank of an 8-way
 // job scans the object space, not the 4.2B-tuple index space); two passes (count per chunk,
 // then fill at exact offsets), so no partition ever needs the whole graph in host memory.
+int ks_drive_tuples_part_placed(const ks_drive_params *pp, uint32_t nparts, uint32_t part, const keto_placement *pl,
+                                keto_tuple *out, uint64_t cap, int threads, uint64_t *count);
 int ks_drive_tuples_part(const ks_drive_params *pp, uint32_t nparts, uint32_t part, keto_tuple *out, uint64_t cap,
                          int threads, uint64_t *count) {
+    return ks_drive_tuples_part_placed(pp, nparts, part, nullptr, out, cap, threads, count);
+}
+// the same under a placement (keto_object_owner_placed; null: keto_object_owner)
+int ks_drive_tuples_part_placed(const ks_drive_params *pp, uint32_t nparts, uint32_t part, const keto_placement *pl,
+                                keto_tuple *out, uint64_t cap, int threads, uint64_t *count) {
     ks_drive_layout L;
     if (ks_drive_layout_get(pp, &L) != 0 || nparts == 0 || part >= nparts || !count) return -1;
     const ks_drive_params p = *pp;
@@ -188,13 +195,13 @@ int ks_drive_tuples_part(const ks_drive_params *pp, uint32_t nparts, uint32_t pa
                 };
                 for (uint64_t x = b; x < e; x++) {
                     if (x < L.n_nodes) {
-                        if (keto_object_owner(node_ns(L, x), (uint32_t)x, nparts) != part) continue;
+                        if (keto_object_owner_placed(pl, node_ns(L, x), (uint32_t)x, nparts) != part) continue;
                         const uint64_t r = x / L.nodes_per_root, cc = x % L.nodes_per_root;
                         if (cc) emit(r * (L.nodes_per_root - 1) + cc - 1);
                         for (uint64_t a = 0; a < p.acl_per_node; a++) emit(L.n_parent_tuples + x * p.acl_per_node + a);
                     } else {
                         const uint64_t g = x - L.n_nodes;
-                        if (keto_object_owner(NS_GROUP, (uint32_t)(L.gbase + g), nparts) != part) continue;
+                        if (keto_object_owner_placed(pl, NS_GROUP, (uint32_t)(L.gbase + g), nparts) != part) continue;
                         for (uint64_t m = 0; m < p.members_per_group; m++)
                             emit(L.n_parent_tuples + L.n_acl_tuples + g * p.members_per_group + m);
                     }

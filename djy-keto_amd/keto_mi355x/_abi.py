@@ -48,6 +48,11 @@ class SnapshotInfo(ctypes.Structure):
                 ("n_reach", ctypes.c_uint64)]
 
 
+class Placement(ctypes.Structure):
+    """keto_placement (ABI 7): block[ns] > 0 puts object obj of namespace ns on rank (obj / block[ns]) % world"""
+    _fields_ = [("block", ctypes.c_uint32 * 16)]
+
+
 class Limits(ctypes.Structure):
     _fields_ = [("max_read_depth", ctypes.c_int32), ("max_read_width", ctypes.c_int32)]
 
@@ -169,6 +174,8 @@ SIGNATURES = {
     "keto_dispatcher_stats_get": (ctypes.c_int, [_VP, ctypes.POINTER(DispatcherStats)]),
     "keto_partition_create": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, _U32, _VP,
                                              ctypes.POINTER(Limits), ctypes.POINTER(_VP)]),
+    "keto_partition_create_placed": (ctypes.c_int, [ctypes.POINTER(SnapshotConfig), _VP, _U64, _U32, _VP,
+                                                    ctypes.POINTER(Limits), ctypes.POINTER(Placement), ctypes.POINTER(_VP)]),
     "keto_partition_check": (ctypes.c_int, [_VP, _VP, _U64, _VP, _VP, _U32]),
     "keto_partition_check_many": (ctypes.c_int, [_VP, _U32, _VP, _VP, _VP, _VP, _U32]),
     "keto_partition_expand": (ctypes.c_int, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),

@@ -32,12 +32,21 @@ from ._abi import check, lib
 _MULT = 0x9E3779B97F4A7C15
 
 
-def object_owner(ns: np.ndarray, obj: np.ndarray, nparts: int) -> np.ndarray:
-    """keto_object_owner (include/keto_mi355x.h) over numpy arrays."""
-    k = (np.asarray(ns).astype(np.uint64) << np.uint64(32)) | np.asarray(obj).astype(np.uint64)
+def object_owner(ns: np.ndarray, obj: np.ndarray, nparts: int, placement=None) -> np.ndarray:
+    """keto_object_owner (include/keto_mi355x.h) over numpy arrays; with placement (16 block
+    sizes per namespace, keto_placement) keto_object_owner_placed."""
+    ns, obj = np.asarray(ns).astype(np.uint64), np.asarray(obj).astype(np.uint64)
+    k = (ns << np.uint64(32)) | obj
     with np.errstate(over="ignore"):
         h = k * np.uint64(_MULT)
-    return ((h >> np.uint64(32)) % np.uint64(nparts)).astype(np.uint32)
+    own = ((h >> np.uint64(32)) % np.uint64(nparts)).astype(np.uint32)
+    if placement is not None:
+        blk = np.zeros(2 ** 16, np.uint64)
+        blk[:16] = np.asarray(placement, dtype=np.uint64)[:16]
+        b = blk[np.minimum(ns, 2 ** 16 - 1).astype(np.int64)]
+        placed = b > 0
+        own[placed] = ((obj[placed] // b[placed]) % np.uint64(nparts)).astype(np.uint32)
+    return own
 
 
 class _CCollective(ctypes.Structure):
@@ -102,7 +111,7 @@ class PartitionedEngine:
 
     def __init__(self, namespaces, ns_names, rel_names, n_uuids: int, part_tuples=None, *, strict: bool = False,
                  device: int = 0, max_read_depth: int = 5, max_read_width: int = 100, collective=None,
-                 device_tuples: tuple | None = None, distributed: bool = False):
+                 device_tuples: tuple | None = None, distributed: bool = False, placement=None):
         import json
         if isinstance(namespaces, dict):
             namespaces = json.dumps(namespaces)
@@ -119,17 +128,22 @@ class PartitionedEngine:
         if collective is not None and (int(collective.world) > 1 or distributed):
             self._coll = _c_collective(collective)
         flags = _abi.F_PART_DIST if distributed else 0
+        # placement: 16 block sizes per namespace (keto_placement; None: keto_object_owner)
+        pl = None
+        if placement is not None:
+            self._pl = _abi.Placement((ctypes.c_uint32 * 16)(*[int(b) for b in list(placement)[:16]]))
+            pl = ctypes.byref(self._pl)
         h = ctypes.c_void_p()
         if device_tuples is not None:
             ptr, count = device_tuples
-            check(lib().keto_partition_create(ctypes.byref(cfg), ptr, count, _abi.F_DEVICE_PTRS | flags,
-                                              ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
-                                              ctypes.byref(h)))
+            check(lib().keto_partition_create_placed(ctypes.byref(cfg), ptr, count, _abi.F_DEVICE_PTRS | flags,
+                                                     ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
+                                                     pl, ctypes.byref(h)))
         else:
             t = np.ascontiguousarray(part_tuples, dtype=_abi.TUPLE_DT)
-            check(lib().keto_partition_create(ctypes.byref(cfg), t.ctypes.data if len(t) else None, len(t), flags,
-                                              ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
-                                              ctypes.byref(h)))
+            check(lib().keto_partition_create_placed(ctypes.byref(cfg), t.ctypes.data if len(t) else None, len(t), flags,
+                                                     ctypes.byref(self._coll[0]) if self._coll else None, ctypes.byref(lim),
+                                                     pl, ctypes.byref(h)))
         self.handle = h
         self.last = {}
         _abi.track(self)

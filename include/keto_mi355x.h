@@ -434,6 +434,23 @@ typedef struct keto_partition keto_partition;
  * by value. */
 int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
                           const keto_collective *coll, const keto_limits *limits, keto_partition **out);
+/* ABI 7: where the job's objects live, beside keto_object_owner's hash.  block[ns] > 0 puts
+ * object obj of namespace ns (ns < 16) on rank (obj / block[ns]) % world: whole id ranges on one
+ * rank -- a deployment whose objects of a hierarchy are numbered together (a folder tree under
+ * its root) keeps a tuple-to-userset chain on one rank, so the distributed frontier walks it in
+ * one goal instead of a record and a generation per hop.  0: the hash.  Every rank passes the
+ * same placement, and loads the tuples keto_object_owner_placed gives it. */
+typedef struct keto_placement {
+    uint32_t block[16];
+} keto_placement;
+static inline uint32_t keto_object_owner_placed(const keto_placement *p, uint32_t ns, uint32_t obj, uint32_t nparts) {
+    if (p && ns < 16 && p->block[ns]) return (obj / p->block[ns]) % nparts;
+    return keto_object_owner(ns, obj, nparts);
+}
+/* keto_partition_create with a placement (NULL: keto_object_owner) */
+int keto_partition_create_placed(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, uint32_t flags,
+                                 const keto_collective *coll, const keto_limits *limits, const keto_placement *placement,
+                                 keto_partition **out);
 /* collective: this rank's queries (host) -> decisions, as keto_check_batch (flags: COUNT_WORK,
  * ERR_DETAIL).  Check closures ship subject-set tuples plus only the subject-id tuples that
  * name one of the batch's subjects: no other subject-id tuple is ever read by these queries. */

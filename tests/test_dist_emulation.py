@@ -77,7 +77,7 @@ def _worker(rank, world, port, lib, case, seeds, out):
                 oq = q_rs
             else:
                 wl = synth.drive(depth=4, fanout=3, acl_per_node=6, n_groups=200, members_per_group=6, n_users=600,
-                                 seed=seed)
+                                 seed=seed, roots=6 if case == "drive_placed" else 1)
                 tup = wl.tuples
                 q = synth.drive_queries(wl, 3000 - 500 * rank * (case == "drive_chunked"), seed=seed + 7)
                 ns_cfg, ns_names, rel_names = wl.namespaces, wl.ns_names, wl.rel_names
@@ -92,11 +92,13 @@ def _worker(rank, world, port, lib, case, seeds, out):
                 roots["obj"][:12] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], 12)
                 roots["ns"][12:], roots["rel"][12:] = wl.ns_names.index("Folder"), wl.rel_names.index("viewers")
                 roots["obj"][12:] = rng.integers(0, wl.meta["folders_per_root"], 12)
-            own = partition.object_owner(tup["ns"], tup["obj"], world) == rank
+            # drive_placed: every root's folder tree on one rank (keto_placement), groups hashed
+            place = synth.drive_placement(wl) if case == "drive_placed" else None
+            own = partition.object_owner(tup["ns"], tup["obj"], world, place) == rank
             # (world 1: KETO_F_PART_DIST, the distributed frontier with every exchange to this rank)
             eng = partition.PartitionedEngine(ns_cfg, ns_names, rel_names, n_uuids, tup[own], strict=strict,
                                               max_read_depth=depth, max_read_width=width, collective=coll,
-                                              distributed=world == 1)
+                                              distributed=world == 1, placement=place)
             allowed, err = eng.check_batch(q)  # every rank checks the whole batch: each root at its owner
             st = dict(eng.last)
             lv = eng.generation_stats()
@@ -147,7 +149,8 @@ def test_random_worlds_match_oracle(emu_lib, world):
     assert routed < 0.25 * total, (routed, total)
 
 
-@pytest.mark.parametrize("world,case", [(2, "drive"), (3, "drive"), (3, "drive_chunked")])
+@pytest.mark.parametrize("world,case", [(2, "drive"), (3, "drive"), (3, "drive_chunked"), (2, "drive_placed"),
+                                        (3, "drive_placed")])
 def test_small_drive_matches_oracle(emu_lib, world, case):
     res = _run(emu_lib, world, case, [5])
     for r in range(world):

@@ -40,6 +40,10 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1100)]
 
 WORLD = 8
 SCALE = int(os.environ.get("KETO_C5_SCALE", "40"))
+# KETO_C5_PLACED=1: every root's folder tree on one rank (keto_placement, synth.drive_placement),
+# groups and users hashed -- the same graph and queries, another owner rule
+PLACED = os.environ.get("KETO_C5_PLACED") == "1"
+PHASES = f"c5x{SCALE}{'_placed' if PLACED else ''}_phases.json"
 N = 1 << 20
 SAMPLE = 1 << 16
 ROOTS = 512  # Expand roots per rank
@@ -124,12 +128,13 @@ def _worker(rank, world, port, out):
         for r in range(world):
             if r == rank:
                 t0 = time.perf_counter()
-                part = synth.drive_partition(wl, world, rank)
+                place = synth.drive_placement(wl) if PLACED else None
+                part = synth.drive_partition(wl, world, rank, placement=place)
                 n_part = len(part)
                 t1 = time.perf_counter()
                 eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
                                                   max_read_depth=wl.max_depth, max_read_width=wl.max_width,
-                                                  collective=TorchCollective(device_buffers=True))
+                                                  collective=TorchCollective(device_buffers=True), placement=place)
                 del part
                 _log(rank, f"partition {n_part} tuples: generated {t1 - t0:.1f} s, resident snapshot "
                            f"{time.perf_counter() - t1:.1f} s, {_free_gib()}")
@@ -209,8 +214,9 @@ def test_c5_x40_eight_ranks_matches_oracle():
         res = dict(out)
     assert sorted(res) == list(range(WORLD))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "c5x40_phases.json"), "w") as f:
-        json.dump({"what": f"tests/test_gpu_c5.py: C3 x{SCALE} over 8 gloo ranks sharing one MI355X, resident partitions; "
+    with open(os.path.join(ROOT, "gpurun_out", PHASES), "w") as f:
+        json.dump({"what": f"tests/test_gpu_c5.py: C3 x{SCALE} over 8 gloo ranks sharing one MI355X, resident partitions "
+                           f"({'each root folder tree on one rank (keto_placement), groups hashed' if PLACED else 'keto_object_owner'}); "
                            "per rank the second (warm) 2^20-query check batch through the distributed frontier "
                            "(keto_partition_stats_get: generations, goals, routed, bytes of goal records + values sent to "
                            "other ranks, device time of the generations' kernels, time inside the collective; "

@@ -58,6 +58,28 @@ def test_partitions_cover_the_graph_exactly():
     np.testing.assert_array_equal(_rows_sorted(np.concatenate(parts)), _rows_sorted(w.tuples))
 
 
+def test_placed_partitions_keep_each_tree_on_one_rank():
+    """keto_placement (keto_object_owner_placed): a placed namespace's owner is (obj / block) %
+    world, every other namespace keeps the hash; synth.drive_placement puts each root's Folder and
+    File objects on one rank, and the placed partitions still cover the graph exactly once"""
+    w = synth.drive(depth=3, fanout=3, acl_per_node=3, n_groups=80, members_per_group=4, n_users=300, seed=4, roots=5)
+    pl = synth.drive_placement(w)
+    ns = np.array([0, 1, 2, 3, 17, 2], np.uint32)
+    obj = np.array([5, 9, 130, 41, 7, 2**32 - 1], np.uint32)
+    own = partition.object_owner(ns, obj, 3, pl)
+    hashed = partition.object_owner(ns, obj, 3)
+    for i in range(len(ns)):
+        b = int(pl[ns[i]]) if ns[i] < 16 else 0
+        assert own[i] == ((int(obj[i]) // b) % 3 if b else hashed[i])
+    parts = [synth.drive_partition(w, 3, r, placement=pl) for r in range(3)]
+    np.testing.assert_array_equal(_rows_sorted(np.concatenate(parts)), _rows_sorted(w.tuples))
+    per = w.meta["nodes_per_root"]
+    for r, p in enumerate(parts):
+        assert (partition.object_owner(p["ns"], p["obj"], 3, pl) == r).all()
+        tree = np.isin(p["ns"], [w.ns_names.index("Folder"), w.ns_names.index("File")])
+        assert ((p["obj"][tree] // per) % 3 == r).all()  # whole trees
+
+
 @pytest.mark.parametrize("depth", [2, 3, 16])
 def test_closure_decides_like_the_whole_graph(depth):
     """the exactness claim, Check (with the subject filter) and Expand; fewer levels than

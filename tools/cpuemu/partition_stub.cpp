@@ -26,11 +26,11 @@ struct PartitionHandle {
 };
 [[noreturn]] static void unavailable() { throw Error(KETO_E_DEVICE, "the closure path of keto_partition_* is not part of the CPU emulation"); }
 PartitionHandle *partition_create(const keto_snapshot_config *cfg, const keto_tuple *tuples, uint64_t n, bool device_ptrs,
-                                  const keto_collective *coll, const keto_limits *limits, bool force_dist) {
+                                  const keto_collective *coll, const keto_limits *limits, bool force_dist, const Placement &place) {
     if (!coll || (coll->world < 2 && !force_dist)) unavailable();
     auto P = std::make_unique<PartitionHandle>();
     keto_limits lim = limits ? *limits : keto_limits{5, 100};
-    P->dist = dist_create(cfg, tuples, n, device_ptrs, *coll, lim);
+    P->dist = dist_create(cfg, tuples, n, device_ptrs, *coll, lim, place);
     return P.release();
 }
 void partition_check_many(PartitionHandle *P, uint32_t nb, const keto_query *const *q, const uint64_t *n, uint8_t *const *allowed,

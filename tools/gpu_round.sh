@@ -78,7 +78,7 @@ c5)
   S=${1:-40}; B=${2:-10}
   KETO_C5_SCALE=$S timeout -k 10 1100 python3 -u -m pytest -x -v -s --timeout 1080 --timeout-method thread tests/test_gpu_c5.py \
     > $OUT/c5test.log 2>&1 || { grep -E "failed|Error" $OUT/c5test.log | head; exit 1; }
-  cp gpurun_out/c5x40_phases.json $OUT/c5_phases_x$S.json
+  cp gpurun_out/c5x${S}*_phases.json $OUT/ 2>/dev/null; true
   KETO_BENCH_BACKEND=gloo KETO_POOL_CAP_MB=1 KETO_SCRATCH_CAP_MB=1 KETO_PART_TRIM=1 timeout -k 10 900 \
     python3 -u bench.py --workload c5 --scale $B --gpus 8 --steps 4 --warmup 1 --no-cpu-baseline > $OUT/c5bench.log 2>&1 \
     || { tail -5 $OUT/c5bench.log; exit 1; }
