@@ -21,9 +21,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
-def _wl():
+def _wl(roots=1):
     return synth.drive(depth=6, fanout=4, acl_per_node=6, n_groups=3000, members_per_group=10, n_users=20_000,
-                       seed=12)
+                       seed=12, roots=roots)
 
 
 def _roots(wl, rng, n):
@@ -182,16 +182,19 @@ def _worker(rank, world, port, out, device_buffers=False, mode="dist"):
         if p not in sys.path:
             sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    placed = mode.endswith("_placed")  # every root's folder tree on one rank (keto_placement)
+    mode = mode.replace("_placed", "")
     if mode == "closure":
         os.environ["KETO_PART_CLOSURE"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from torch_collective import TorchCollective
-        wl = _wl()
+        wl = _wl(3 if placed else 1)
+        place = synth.drive_placement(wl) if placed else None
         eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids,
-                                          synth.drive_partition(wl, world, rank), max_read_depth=wl.max_depth,
-                                          max_read_width=wl.max_width,
-                                          collective=TorchCollective(device_buffers=device_buffers))
+                                          synth.drive_partition(wl, world, rank, placement=place),
+                                          max_read_depth=wl.max_depth, max_read_width=wl.max_width,
+                                          collective=TorchCollective(device_buffers=device_buffers), placement=place)
         q = synth.drive_queries(wl, 8192, seed=40 + rank)
         allowed, err = eng.check_batch(q)
         st = dict(eng.last)
@@ -231,7 +234,7 @@ def _worker(rank, world, port, out, device_buffers=False, mode="dist"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["dist", "closure"])
+@pytest.mark.parametrize("mode", ["dist", "closure", "dist_placed", "closure_placed"])
 @pytest.mark.parametrize("device_buffers", [False, True])
 def test_two_rank_partitioned_matches_oracle(device_buffers, mode):
     """two ranks sharing the GPU: the exchange over host copies (keto_collective.alltoallv), and
