@@ -537,7 +537,8 @@ def run_c5(args, rank, world, device, dist_on):
     eng, n_part = None, 0
     for r in range(world if (dist_on and shared) else 1):
         if not (dist_on and shared) or r == rank:
-            place = synth.drive_placement(wl) if args.placement == "tree" else None
+            place = (synth.drive_placement(wl, replicate_groups=args.placement == "tree_repl")
+                     if args.placement != "hash" else None)
             part = synth.drive_partition(wl, world, rank, placement=place)
             n_part = len(part)
             eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids, part,
@@ -780,8 +781,9 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c4")
     ap.add_argument("--scale", type=int, default=40, help="C5 graph = C3 x scale (40: ~4.2B tuples)")
-    ap.add_argument("--placement", choices=["hash", "tree"], default="hash",
-                    help="C5 owner rule: keto_object_owner's hash, or every root folder tree on one rank (keto_placement)")
+    ap.add_argument("--placement", choices=["hash", "tree", "tree_repl"], default="hash",
+                    help="C5 owner rule: keto_object_owner's hash, every root folder tree on one rank (keto_placement), "
+                         "or that with the groups replicated on every rank")
     ap.add_argument("--tuples", type=int, default=10_000_000, help="C2 graph size")
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--engine-streams", type=int, default=int(os.environ.get("KETO_BENCH_STREAMS", "1")),

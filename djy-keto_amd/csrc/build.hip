@@ -203,7 +203,8 @@ struct Ghosts {
     Placement pl;
     __device__ __forceinline__ uint32_t ns_of_set(uint32_t s_ns, uint32_t s_obj) const {
         if (world <= 1) return s_ns;
-        return place_owner(pl, s_ns, s_obj, world) == rank ? s_ns : n_ns + s_ns;
+        const uint32_t o = place_owner(pl, s_ns, s_obj, world);
+        return o == rank || o == PLACE_ALL ? s_ns : n_ns + s_ns;
     }
 };
 __global__ __launch_bounds__(BLK) void k_entity_bits(const keto_tuple *t, uint64_t n, uint64_t stride,

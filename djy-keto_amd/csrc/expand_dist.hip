@@ -377,7 +377,7 @@ void dist_expand(DistEngine &E, const keto_subject_set *roots, uint64_t n, std::
         hist.need((size_t)W * 4 + 16, s);
         uint32_t *h = hist.as<uint32_t>();
         KETO_HIP(hipMemsetAsync(h, 0, (size_t)W * 4, s));
-        if (ncur) hipLaunchKernelGGL(kx_hist, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, Dest{W, V.place}, h);
+        if (ncur) hipLaunchKernelGGL(kx_hist, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, Dest{W, V.rank, V.place}, h);
         std::vector<uint32_t> cnt(W);
         KETO_HIP(hipMemcpyAsync(cnt.data(), h, (size_t)W * 4, hipMemcpyDeviceToHost, s));
         KETO_HIP(hipStreamSynchronize(s));
@@ -402,7 +402,7 @@ void dist_expand(DistEngine &E, const keto_subject_set *roots, uint64_t n, std::
             std::vector<uint32_t> cu(W, 0);
             for (uint32_t r = 1; r < W; r++) cu[r] = cu[r - 1] + cnt[r - 1];
             KETO_HIP(hipMemcpyAsync(h, cu.data(), (size_t)W * 4, hipMemcpyHostToDevice, s));
-            hipLaunchKernelGGL(kx_scatter, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, Dest{W, V.place}, h, sendk.as<uint64_t>());
+            hipLaunchKernelGGL(kx_scatter, xgrid(ncur), dim3(XB), 0, s, cur.as<uint64_t>(), ncur, Dest{W, V.rank, V.place}, h, sendk.as<uint64_t>());
         }
         std::vector<uint64_t> sb(W), rb(W);
         for (uint32_t r = 0; r < W; r++) {

@@ -731,7 +731,7 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
     E.dsend.reserve((size_t)W * 8 + 64, 0, s);
     uint32_t *h = E.dsend.as<uint32_t>();
     KETO_HIP(hipMemsetAsync(h, 0, (size_t)W * 4, s));
-    if (n) hipLaunchKernelGGL(k_dest_count, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, Dest{W, E.place}, h);
+    if (n) hipLaunchKernelGGL(k_dest_count, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, Dest{W, E.rank, E.place}, h);
     KETO_HIP(hipGetLastError());
     std::vector<uint32_t> cnt(W);
     KETO_HIP(hipMemcpyAsync(cnt.data(), h, (size_t)W * 4, hipMemcpyDeviceToHost, s));
@@ -748,7 +748,7 @@ uint64_t send_level(DistEngine &E, const uint4 *src, uint64_t n, Level &L, bool 
         std::vector<uint32_t> cur(W, 0);
         for (uint32_t r = 1; r < W; r++) cur[r] = cur[r - 1] + cnt[r - 1];
         KETO_HIP(hipMemcpyAsync(h, cur.data(), (size_t)W * 4, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_dest_scatter, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, Dest{W, E.place}, h, E.sbuf.as<uint32_t>(),
+        hipLaunchKernelGGL(k_dest_scatter, dgrid(n, 4096), dim3(DBLK), 0, s, src, (uint32_t)n, Dest{W, E.rank, E.place}, h, E.sbuf.as<uint32_t>(),
                            E.sent_px.as<uint32_t>() + L.sent_off);
         KETO_HIP(hipGetLastError());
     }

@@ -21,22 +21,29 @@ constexpr uint32_t VIRT_BIT = 0x80000000u;  // frame node id: virtual node
 
 // Where a partitioned graph's objects live (keto_placement, include/keto_mi355x.h): block[ns] > 0
 // puts object obj of namespace ns on rank (obj / block[ns]) % world -- whole id ranges on one
-// rank, e.g. a folder tree on its root's; 0 (and every ns >= PLACE_NS) hashes (keto_object_owner)
-constexpr uint32_t PLACE_NS = 16;
+// rank, e.g. a folder tree on its root's; PLACE_ALL replicates the namespace (every rank holds all
+// of its tuples: each owns it); 0 (and every ns >= PLACE_NS) hashes (keto_object_owner)
+constexpr uint32_t PLACE_NS = 16, PLACE_ALL = 0xFFFFFFFFu;
 struct Placement {
     uint32_t block[PLACE_NS];
 };
+// the owner rank, or PLACE_ALL for a replicated namespace
 __host__ __device__ inline uint32_t place_owner(const Placement &p, uint32_t ns, uint32_t obj, uint32_t world) {
     const uint32_t b = ns < PLACE_NS ? p.block[ns] : 0u;
+    if (b == PLACE_ALL) return PLACE_ALL;
     if (b) return (obj / b) % world;
     const uint64_t h = ((((uint64_t)ns) << 32) | obj) * 0x9E3779B97F4A7C15ull;
     return (uint32_t)((h >> 32) % world);
 }
-// an owner lookup's arguments, passed by value to the routing kernels
+// an owner lookup's arguments, passed by value to the routing kernels (a replicated object is the
+// asking rank's own)
 struct Dest {
-    uint32_t world;
+    uint32_t world, rank;
     Placement pl;
-    __host__ __device__ uint32_t owner(uint32_t ns, uint32_t obj) const { return place_owner(pl, ns, obj, world); }
+    __host__ __device__ uint32_t owner(uint32_t ns, uint32_t obj) const {
+        const uint32_t o = place_owner(pl, ns, obj, world);
+        return o == PLACE_ALL ? rank : o;
+    }
 };
 constexpr uint32_t EDGE_ALIAS = 0x80000000u; // set_dst entry: visited key != node id
 // set_dst entry (snapshots of < 2^30 nodes, DevSnapshot::edge_leaf): the child node holds no

@@ -951,7 +951,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             KETO_HIP(hipMemsetAsync(hist.p, 0, W * 8, P.hs));
             if (n_new)
                 hipLaunchKernelGGL(k_dest_hist, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new,
-                                   Dest{W, P.place}, dptr<unsigned long long>(hist));
+                                   Dest{W, P.rank, P.place}, dptr<unsigned long long>(hist));
             KETO_HIP(hipMemcpyAsync(send.data(), hist.p, W * 8, hipMemcpyDeviceToHost, P.hs));
             sync(P);
             std::vector<uint64_t> cur(W, 0);
@@ -959,7 +959,7 @@ uint64_t closure(Partition &P, const uint64_t *keys, uint64_t n_keys, const uint
             KETO_HIP(hipMemcpyAsync(hist.p, cur.data(), W * 8, hipMemcpyHostToDevice, P.hs));
             if (n_new)
                 hipLaunchKernelGGL(k_dest_scatter, grid_for(n_new), dim3(BLK), 0, P.hs, dptr<uint64_t>(P.fresh), n_new,
-                                   Dest{W, P.place}, dptr<unsigned long long>(hist), dptr<uint64_t>(P.routed));
+                                   Dest{W, P.rank, P.place}, dptr<unsigned long long>(hist), dptr<uint64_t>(P.routed));
         }
         std::vector<uint64_t> from = exchange(P, P.routed.p, send, 8, P.req, st.bytes_sent);
         lv_req = st.bytes_sent - lv_b0;

@@ -9,8 +9,8 @@
 // Tabled slot: pure (no rewrite, no ASTRelationFor error: definitions.go:37-62), some row holds a
 // subject set (RI_SETROWS) and some tuple's subject set names it (an expand-subject child can be
 // one of its nodes).  Tabled node: every node of its reach is pure and |Reach| <= REACH_CAP.
-// Snapshots whose visited keys alias (D.vkey) and partitions (ghost rows live elsewhere) carry
-// none.  Layout: reach_base[global slot] = first entry of the slot in reach_idx (NONE32: not
+// Snapshots whose visited keys alias (D.vkey) carry none; in a partition's snapshot a reach that
+// meets a ghost node (another rank's object: its rows live there) leaves its node untabled.  Layout: reach_base[global slot] = first entry of the slot in reach_idx (NONE32: not
 // tabled), reach_idx[base + entity - ent_base] = {offset, count} (count NONE32: not tabled) into
 // reach_pool, the reach without the node itself (its own row is what the caller tested).
 #include <hip/hip_runtime.h>
@@ -39,7 +39,8 @@ struct ReachIn {
     const uint4 *tslots;  // {first candidate, ns, slot in ns, 0} per tabled slot, ascending
     uint32_t n_tslots;
     uint64_t n_cand;
-    uint32_t cap;  // REACH_CAP, or KETO_REACH_CAP (A/B)
+    uint32_t cap;      // REACH_CAP, or KETO_REACH_CAP (A/B)
+    uint32_t n_owned;  // the first ghost node (a partition's snapshot; else every node)
 };
 
 __device__ __forceinline__ uint32_t ns_of_node(const NsDev *ns, uint32_t n_ns, uint32_t node) {
@@ -115,7 +116,7 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
         L[0] = g;
         while (ok && head < cnt) {
             const uint32_t n = L[head++];
-            if (!node_pure(R, n)) {
+            if (n >= R.n_owned || !node_pure(R, n)) {  // (a ghost: its row is another rank's)
                 ok = false;
                 break;
             }
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(RB) void k_reach(ReachIn R, const uint32_t *list, u
         while (ok && head < cnt) {
             const uint32_t n = __shfl(head < 64 ? e0 : e1, (int)(head & 63u));
             head++;
-            if (!node_pure(R, n)) {
+            if (n >= R.n_owned || !node_pure(R, n)) {  // (a ghost: its row is another rank's)
                 ok = false;
                 break;
             }
@@ -335,7 +336,7 @@ void build_reach(Snapshot &s) {
         return e && *e == '1';
     }();
     const uint32_t n_slots = (uint32_t)s.relinfo.size();
-    if (off || D.vkey || D.n_ns_x != D.n_ns || !n_slots || !s.info.n_set_edges) return;
+    if (off || D.vkey || !n_slots || !s.info.n_set_edges) return;
     std::vector<uint32_t> base;
     std::vector<uint4> ts;
     const uint64_t n_cand = tabled_slots(s, base, ts);
@@ -351,7 +352,7 @@ void build_reach(Snapshot &s) {
         return c >= 1 && c <= REACH_CAP_MAX ? c : REACH_CAP;
     }();
     ReachIn R{D.set_row, D.set_dst, D.edge_mask, D.ns, D.n_ns, D.relinfo, static_cast<const uint4 *>(d_ts.p), (uint32_t)ts.size(),
-              n_cand, cap};
+              n_cand, cap, D.n_ns_x != D.n_ns ? D.n_owned : NONE32};
     const dim3 grid((uint32_t)std::min<uint64_t>(65536, (n_cand + RB / 64 - 1) / (RB / 64)));  // (4 waves a block)
     hipLaunchKernelGGL(k_reach<false>, grid, dim3(RB), 0, 0, R, nullptr, n_cand, idx, lens.u32(), nullptr, 0u,
                        static_cast<unsigned long long *>(tot.p));
@@ -455,7 +456,7 @@ void patch_reach(Snapshot &s, const Snapshot &B, const std::vector<uint32_t> &to
     uint32_t nc = 0;
     KETO_HIP(hipMemcpy(&nc, cnt.p, 4, hipMemcpyDeviceToHost));
     ReachIn R{D.set_row, D.set_dst, D.edge_mask, D.ns, D.n_ns, D.relinfo, static_cast<const uint4 *>(d_ts.p), (uint32_t)ts.size(),
-              n_cand, cap};
+              n_cand, cap, NONE32};
     const dim3 grid((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, ((uint64_t)nc + RB / 64 - 1) / (RB / 64))));
     // a copy of the base's records, or (an advance) the snapshot's own, rewritten where they lie
     const bool in_place = &s == &B && s.sole(D.reach_idx) && s.sole(D.reach_pool);

@@ -195,13 +195,15 @@ int ks_drive_tuples_part_placed(const ks_drive_params *pp, uint32_t nparts, uint
                 };
                 for (uint64_t x = b; x < e; x++) {
                     if (x < L.n_nodes) {
-                        if (keto_object_owner_placed(pl, node_ns(L, x), (uint32_t)x, nparts) != part) continue;
+                        const uint32_t o = keto_object_owner_placed(pl, node_ns(L, x), (uint32_t)x, nparts);
+                        if (o != part && o != KETO_OWNER_ALL) continue;
                         const uint64_t r = x / L.nodes_per_root, cc = x % L.nodes_per_root;
                         if (cc) emit(r * (L.nodes_per_root - 1) + cc - 1);
                         for (uint64_t a = 0; a < p.acl_per_node; a++) emit(L.n_parent_tuples + x * p.acl_per_node + a);
                     } else {
                         const uint64_t g = x - L.n_nodes;
-                        if (keto_object_owner_placed(pl, NS_GROUP, (uint32_t)(L.gbase + g), nparts) != part) continue;
+                        const uint32_t o = keto_object_owner_placed(pl, NS_GROUP, (uint32_t)(L.gbase + g), nparts);
+                        if (o != part && o != KETO_OWNER_ALL) continue;
                         for (uint64_t m = 0; m < p.members_per_group; m++)
                             emit(L.n_parent_tuples + L.n_acl_tuples + g * p.members_per_group + m);
                     }

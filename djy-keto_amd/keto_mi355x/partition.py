@@ -32,9 +32,14 @@ from ._abi import check, lib
 _MULT = 0x9E3779B97F4A7C15
 
 
+OWNER_ALL = 0xFFFFFFFF  # KETO_OWNER_ALL: a replicated namespace's objects (placement block PLACE_ALL)
+PLACE_ALL = 0xFFFFFFFF
+
+
 def object_owner(ns: np.ndarray, obj: np.ndarray, nparts: int, placement=None) -> np.ndarray:
     """keto_object_owner (include/keto_mi355x.h) over numpy arrays; with placement (16 block
-    sizes per namespace, keto_placement) keto_object_owner_placed."""
+    sizes per namespace, keto_placement) keto_object_owner_placed: OWNER_ALL for a replicated
+    namespace (every rank holds its tuples)."""
     ns, obj = np.asarray(ns).astype(np.uint64), np.asarray(obj).astype(np.uint64)
     k = (ns << np.uint64(32)) | obj
     with np.errstate(over="ignore"):
@@ -44,8 +49,10 @@ def object_owner(ns: np.ndarray, obj: np.ndarray, nparts: int, placement=None) -
         blk = np.zeros(2 ** 16, np.uint64)
         blk[:16] = np.asarray(placement, dtype=np.uint64)[:16]
         b = blk[np.minimum(ns, 2 ** 16 - 1).astype(np.int64)]
-        placed = b > 0
+        repl = b == PLACE_ALL
+        placed = (b > 0) & ~repl
         own[placed] = ((obj[placed] // b[placed]) % np.uint64(nparts)).astype(np.uint32)
+        own[repl] = OWNER_ALL
     return own
 
 

@@ -438,12 +438,18 @@ int keto_partition_create(const keto_snapshot_config *cfg, const keto_tuple *tup
  * object obj of namespace ns (ns < 16) on rank (obj / block[ns]) % world: whole id ranges on one
  * rank -- a deployment whose objects of a hierarchy are numbered together (a folder tree under
  * its root) keeps a tuple-to-userset chain on one rank, so the distributed frontier walks it in
- * one goal instead of a record and a generation per hop.  0: the hash.  Every rank passes the
- * same placement, and loads the tuples keto_object_owner_placed gives it. */
+ * one goal instead of a record and a generation per hop.  KETO_PLACE_ALL replicates the
+ * namespace: every rank loads all of its tuples and owns all of its objects (a group graph small
+ * beside the rest: nested-group expand-subjects then run where they are spawned, with the
+ * reachability tables).  0: the hash.  Every rank passes the same placement, and loads the
+ * tuples whose keto_object_owner_placed is its rank or KETO_OWNER_ALL. */
+#define KETO_PLACE_ALL 0xFFFFFFFFu
+#define KETO_OWNER_ALL 0xFFFFFFFFu
 typedef struct keto_placement {
     uint32_t block[16];
 } keto_placement;
 static inline uint32_t keto_object_owner_placed(const keto_placement *p, uint32_t ns, uint32_t obj, uint32_t nparts) {
+    if (p && ns < 16 && p->block[ns] == KETO_PLACE_ALL) return KETO_OWNER_ALL;
     if (p && ns < 16 && p->block[ns]) return (obj / p->block[ns]) % nparts;
     return keto_object_owner(ns, obj, nparts);
 }

@@ -77,7 +77,7 @@ def _worker(rank, world, port, lib, case, seeds, out):
                 oq = q_rs
             else:
                 wl = synth.drive(depth=4, fanout=3, acl_per_node=6, n_groups=200, members_per_group=6, n_users=600,
-                                 seed=seed, roots=6 if case == "drive_placed" else 1)
+                                 seed=seed, roots=6 if case.startswith("drive_placed") else 1)
                 tup = wl.tuples
                 q = synth.drive_queries(wl, 3000 - 500 * rank * (case == "drive_chunked"), seed=seed + 7)
                 ns_cfg, ns_names, rel_names = wl.namespaces, wl.ns_names, wl.rel_names
@@ -92,9 +92,12 @@ def _worker(rank, world, port, lib, case, seeds, out):
                 roots["obj"][:12] = wl.meta["gbase"] + rng.integers(0, wl.meta["n_groups"], 12)
                 roots["ns"][12:], roots["rel"][12:] = wl.ns_names.index("Folder"), wl.rel_names.index("viewers")
                 roots["obj"][12:] = rng.integers(0, wl.meta["folders_per_root"], 12)
-            # drive_placed: every root's folder tree on one rank (keto_placement), groups hashed
-            place = synth.drive_placement(wl) if case == "drive_placed" else None
-            own = partition.object_owner(tup["ns"], tup["obj"], world, place) == rank
+            # drive_placed: every root's folder tree on one rank (keto_placement), groups hashed;
+            # drive_placed_repl: the same with the groups replicated on every rank (KETO_PLACE_ALL)
+            place = synth.drive_placement(wl, replicate_groups=case == "drive_placed_repl") \
+                if case.startswith("drive_placed") else None
+            o = partition.object_owner(tup["ns"], tup["obj"], world, place)
+            own = (o == rank) | (o == partition.OWNER_ALL)
             # (world 1: KETO_F_PART_DIST, the distributed frontier with every exchange to this rank)
             eng = partition.PartitionedEngine(ns_cfg, ns_names, rel_names, n_uuids, tup[own], strict=strict,
                                               max_read_depth=depth, max_read_width=width, collective=coll,
@@ -150,7 +153,7 @@ def test_random_worlds_match_oracle(emu_lib, world):
 
 
 @pytest.mark.parametrize("world,case", [(2, "drive"), (3, "drive"), (3, "drive_chunked"), (2, "drive_placed"),
-                                        (3, "drive_placed")])
+                                        (3, "drive_placed"), (2, "drive_placed_repl"), (3, "drive_placed_repl")])
 def test_small_drive_matches_oracle(emu_lib, world, case):
     res = _run(emu_lib, world, case, [5])
     for r in range(world):

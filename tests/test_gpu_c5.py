@@ -42,8 +42,9 @@ WORLD = 8
 SCALE = int(os.environ.get("KETO_C5_SCALE", "40"))
 # KETO_C5_PLACED=1: every root's folder tree on one rank (keto_placement, synth.drive_placement),
 # groups and users hashed -- the same graph and queries, another owner rule
-PLACED = os.environ.get("KETO_C5_PLACED") == "1"
-PHASES = f"c5x{SCALE}{'_placed' if PLACED else ''}_phases.json"
+PLACED = os.environ.get("KETO_C5_PLACED") in ("1", "repl")
+REPL = os.environ.get("KETO_C5_PLACED") == "repl"  # ... and the groups replicated on every rank
+PHASES = f"c5x{SCALE}{'_placed' if PLACED else ''}{'_repl' if REPL else ''}_phases.json"
 N = 1 << 20
 SAMPLE = 1 << 16
 ROOTS = 512  # Expand roots per rank
@@ -128,7 +129,7 @@ def _worker(rank, world, port, out):
         for r in range(world):
             if r == rank:
                 t0 = time.perf_counter()
-                place = synth.drive_placement(wl) if PLACED else None
+                place = synth.drive_placement(wl, replicate_groups=REPL) if PLACED else None
                 part = synth.drive_partition(wl, world, rank, placement=place)
                 n_part = len(part)
                 t1 = time.perf_counter()
@@ -207,6 +208,15 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
+def synth_meta(scale):
+    """the Drive layout of C3 x scale (no tuples generated)"""
+    for p in (ROOT, os.path.join(ROOT, "djy-keto_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from keto_mi355x import synth
+    return synth.drive_scaled(scale, materialize=False).meta
+
+
 def test_c5_x40_eight_ranks_matches_oracle():
     with mp.Manager() as m:
         out = m.dict()
@@ -216,7 +226,7 @@ def test_c5_x40_eight_ranks_matches_oracle():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", PHASES), "w") as f:
         json.dump({"what": f"tests/test_gpu_c5.py: C3 x{SCALE} over 8 gloo ranks sharing one MI355X, resident partitions "
-                           f"({'each root folder tree on one rank (keto_placement), groups hashed' if PLACED else 'keto_object_owner'}); "
+                           f"({('each root folder tree on one rank (keto_placement), groups ' + ('replicated on every rank' if REPL else 'hashed')) if PLACED else 'keto_object_owner'}); "
                            "per rank the second (warm) 2^20-query check batch through the distributed frontier "
                            "(keto_partition_stats_get: generations, goals, routed, bytes of goal records + values sent to "
                            "other ranks, device time of the generations' kernels, time inside the collective; "
@@ -227,7 +237,8 @@ def test_c5_x40_eight_ranks_matches_oracle():
     total = res[0]["total"]
     if SCALE == 40:
         assert total > 4_000_000_000  # configs[4]: C3 x40
-    assert sum(r["n_part"] for r in res.values()) == total  # the partitions cover the graph once
+    replicated = (WORLD - 1) * int(synth_meta(SCALE)["n_member_tuples"]) if REPL else 0
+    assert sum(r["n_part"] for r in res.values()) == total + replicated  # the partitions cover the graph once
     for rank, r in res.items():
         print(rank, {k: v for k, v in r.items() if k != "phases"})
         assert r["det_mis"] == 0, r
