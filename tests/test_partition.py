@@ -80,6 +80,24 @@ def test_placed_partitions_keep_each_tree_on_one_rank():
         assert ((p["obj"][tree] // per) % 3 == r).all()  # whole trees
 
 
+def test_replicated_groups_on_every_rank():
+    """KETO_PLACE_ALL: a replicated namespace's objects are OWNER_ALL (keto_object_owner_placed
+    returns KETO_OWNER_ALL), every rank's partition holds all of its tuples, the others are split
+    as before"""
+    w = synth.drive(depth=3, fanout=3, acl_per_node=3, n_groups=80, members_per_group=4, n_users=300, seed=4, roots=5)
+    pl = synth.drive_placement(w, replicate_groups=True)
+    g = w.ns_names.index("Group")
+    assert pl[g] == partition.PLACE_ALL
+    parts = [synth.drive_partition(w, 3, r, placement=pl) for r in range(3)]
+    groups = w.tuples[w.tuples["ns"] == g]
+    for r, p in enumerate(parts):
+        o = partition.object_owner(p["ns"], p["obj"], 3, pl)
+        assert ((o == r) | (o == partition.OWNER_ALL)).all()
+        np.testing.assert_array_equal(_rows_sorted(p[p["ns"] == g]), _rows_sorted(groups))
+    rest = np.concatenate([p[p["ns"] != g] for p in parts])
+    np.testing.assert_array_equal(_rows_sorted(rest), _rows_sorted(w.tuples[w.tuples["ns"] != g]))
+
+
 @pytest.mark.parametrize("depth", [2, 3, 16])
 def test_closure_decides_like_the_whole_graph(depth):
     """the exactness claim, Check (with the subject filter) and Expand; fewer levels than
