@@ -151,7 +151,9 @@ typedef struct keto_stream keto_stream;
 /* KETO_F_ASYNC: enqueue only, no host synchronisation inside the call; pair with
  * keto_stream_sync before reading the outputs.  With host buffers the copies in and out are
  * enqueued on the stream too (pinned memory, keto_host_alloc, makes them truly asynchronous);
- * the buffers must stay valid until the stream is synchronised.  The frontier engine launches
+ * the buffers must stay valid until the stream is synchronised.  (A host-buffer batch's copy
+ * out is enqueued behind the next batch's copy in, or by keto_stream_sync: synchronise before
+ * destroying the stream.)  The frontier engine launches
  * the generations the stream's last synchronous batch needed plus a margin; a query deeper than
  * that is answered by the DFS interpreter (same answers).  keto_frontier_stats counts these
  * batches in async_batches only. */
