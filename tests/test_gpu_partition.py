@@ -182,15 +182,16 @@ def _worker(rank, world, port, out, device_buffers=False, mode="dist"):
         if p not in sys.path:
             sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    placed = mode.endswith("_placed")  # every root's folder tree on one rank (keto_placement)
-    mode = mode.replace("_placed", "")
+    placed = "_placed" in mode  # every root's folder tree on one rank (keto_placement)
+    repl = mode.endswith("_repl")  # ... and the groups on every rank (KETO_PLACE_ALL)
+    mode = mode.replace("_placed", "").replace("_repl", "")
     if mode == "closure":
         os.environ["KETO_PART_CLOSURE"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from torch_collective import TorchCollective
         wl = _wl(3 if placed else 1)
-        place = synth.drive_placement(wl) if placed else None
+        place = synth.drive_placement(wl, replicate_groups=repl) if placed else None
         eng = partition.PartitionedEngine(wl.namespaces, wl.ns_names, wl.rel_names, wl.n_uuids,
                                           synth.drive_partition(wl, world, rank, placement=place),
                                           max_read_depth=wl.max_depth, max_read_width=wl.max_width,
@@ -234,7 +235,8 @@ def _worker(rank, world, port, out, device_buffers=False, mode="dist"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["dist", "closure", "dist_placed", "closure_placed"])
+@pytest.mark.parametrize("mode", ["dist", "closure", "dist_placed", "closure_placed", "dist_placed_repl",
+                                  "closure_placed_repl"])
 @pytest.mark.parametrize("device_buffers", [False, True])
 def test_two_rank_partitioned_matches_oracle(device_buffers, mode):
     """two ranks sharing the GPU: the exchange over host copies (keto_collective.alltoallv), and
